@@ -1,0 +1,272 @@
+/*
+ * murr_codec.h — C ABI of the MI355X (gfx950) row-blob codec.
+ *
+ * This is the drop-in boundary for murr's `src/io` encode/decode path.  Every
+ * entry point names the reference interface it replaces (paths are relative to
+ * the murrdb/murr source tree, v0.2.1).  Plain C: pointers, sizes and status
+ * codes only; no exceptions cross this boundary.
+ *
+ * Naming follows the north star, not the reference:
+ *   decode = row blobs -> Arrow buffers  (reference ColumnEncoder / ReadBatchBuilder)
+ *   encode = Arrow buffers -> row blobs  (reference ColumnDecoder / WriteRow)
+ * (src/io/codec/mod.rs:43-51; .memory/io_codec_design.md explains the inversion.)
+ *
+ * Row blob layout (src/io/row/write.rs:19-52, src/io/row/read.rs:22-56):
+ *   [bitset: bs = ceil(C/8) bytes, bit i set <=> column i NULL, init 0xFF]
+ *   [static region: capacity bytes, column i at offset_i, little endian]
+ *   [payloads: per non-null utf8 column in column order: u32 len, bytes]
+ * A utf8 static slot holds the payload offset relative to the static region.
+ *
+ * Threading: a murr_ctx_t owns one HIP stream and one workspace; calls on one
+ * context must be serialised by the caller (the reference reads under
+ * RwLock::read with one ReadBatchBuilder per request, src/io/table/mod.rs:127).
+ * Use one context per calling thread for concurrency.  Kernels are stateless.
+ */
+#ifndef MURR_CODEC_H
+#define MURR_CODEC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MURR_ABI_VERSION 1
+
+/* DTypeName, same members and order as src/core/schema.rs:6-19. */
+typedef enum {
+    MURR_UTF8 = 0,
+    MURR_BOOL = 1,
+    MURR_INT8 = 2,
+    MURR_INT16 = 3,
+    MURR_INT32 = 4,
+    MURR_INT64 = 5,
+    MURR_UINT8 = 6,
+    MURR_UINT16 = 7,
+    MURR_UINT32 = 8,
+    MURR_UINT64 = 9,
+    MURR_FLOAT32 = 10,
+    MURR_FLOAT64 = 11,
+    MURR_NUM_DTYPES = 12
+} murr_dtype_t;
+
+/* Status codes.  MurrError variants (src/core/error.rs:4-19) map as noted. */
+typedef enum {
+    MURR_OK = 0,
+    MURR_E_INVALID_UTF8 = 1,    /* SegmentError("invalid utf8: ..."), src/io/codec/utf8.rs:90-92 */
+    MURR_E_DTYPE = 2,           /* SegmentError("expected ..., got ..."), src/io/codec/mod.rs:78-85 */
+    MURR_E_BAD_COLUMN = 3,      /* SegmentError("column '...' not found"), src/io/table/mod.rs:115-123 */
+    MURR_E_OFFSET_OVERFLOW = 4, /* arrow-rs StringBuilder panics past i32::MAX; we report instead */
+    MURR_E_MALFORMED_ROW = 5,   /* reference panics on the out-of-bounds slice (read.rs:39-55) */
+    MURR_E_CAPACITY = 6,        /* caller-provided output buffer too small (required size reported) */
+    MURR_E_ARGUMENT = 7,        /* invalid argument (null pointer, bad dtype code, misaligned buffer) */
+    MURR_E_NULL_KEY = 8,        /* SegmentError("null in key column"), src/io/table/mod.rs:80-82 */
+    MURR_E_HIP = 9,             /* HIP runtime error; hip_error holds the hipError_t */
+    MURR_E_INTERNAL = 10,       /* device protocol failure (bounded spin expired) */
+    MURR_E_ARROW = 11,          /* ArrowError, e.g. RecordBatch with zero columns (read.rs:106-108) */
+    MURR_E_NO_DEVICE = 12       /* no HIP device visible */
+} murr_status_t;
+
+/* First error of a call, in the reference's own order (row-major, then
+ * projection order: ReadBatchBuilder::add_row loops encoders per row,
+ * src/io/row/read.rs:85-91). */
+typedef struct {
+    int32_t  status;     /* murr_status_t */
+    int32_t  hip_error;  /* hipError_t when status == MURR_E_HIP */
+    uint32_t block;      /* block index inside a batched call */
+    uint32_t column;     /* projected column position (decode) / segment column (encode) */
+    uint64_t row;        /* row inside the block */
+    uint64_t required;   /* MURR_E_CAPACITY: bytes required */
+} murr_error_t;
+
+/* SegmentColumnSchema (src/io/schema.rs:8-14), without the name. */
+typedef struct {
+    uint32_t index;   /* null-bit position = position among non-key columns */
+    uint32_t dtype;   /* murr_dtype_t */
+    uint32_t offset;  /* byte offset in the static region */
+    uint32_t size;    /* DType::size() */
+} murr_column_t;
+
+/* SegmentSchema (src/io/schema.rs:16-31). */
+typedef struct {
+    uint32_t ncols;
+    uint32_t bitset_size;  /* ceil(ncols / 8) */
+    uint32_t capacity;     /* sum of sizes */
+    uint32_t _pad;
+    const murr_column_t* cols;
+} murr_segment_t;
+
+/* ---- layout ------------------------------------------------------------ */
+
+/* DType::size() for each dtype (src/io/codec/<dtype>.rs `fn size`); -1 if unknown. */
+int murr_dtype_size(uint32_t dtype);
+
+/* From<&TableSchema> for SegmentSchema (src/io/schema.rs:33-54): `dtypes` are
+ * the non-key columns in TableSchema (IndexMap) order.  Fills `cols_out[ncols]`
+ * and `seg_out` (seg_out->cols = cols_out). */
+int murr_segment_init(const uint32_t* dtypes, uint32_t ncols,
+                      murr_column_t* cols_out, murr_segment_t* seg_out);
+
+/* Bytes a validity / bool bitmap of n rows occupies in murr's output buffers:
+ * ceil(n/8) rounded up to 8 (the kernels store whole 64-row words; bits past n
+ * are zero, as arrow-rs leaves them). */
+uint64_t murr_bitmap_bytes(uint64_t n_rows);
+
+/* ---- context / device memory -------------------------------------------- */
+
+typedef struct murr_ctx murr_ctx_t;
+
+int  murr_ctx_create(int device, murr_ctx_t** out);
+void murr_ctx_destroy(murr_ctx_t* ctx);
+/* hipStream_t the context enqueues on (opaque pointer). */
+void* murr_ctx_stream(murr_ctx_t* ctx);
+/* Device time of the last decode / encode kernel(s), HIP events recorded on
+ * the context stream around the kernel launches only (no copies). */
+int  murr_ctx_last_kernel_ms(murr_ctx_t* ctx, float* ms);
+int  murr_device_count(int* n);
+
+int murr_dev_alloc(murr_ctx_t* ctx, uint64_t bytes, void** p);
+int murr_dev_free(murr_ctx_t* ctx, void* p);
+int murr_host_alloc(murr_ctx_t* ctx, uint64_t bytes, void** p); /* pinned */
+int murr_host_free(murr_ctx_t* ctx, void* p);
+int murr_memcpy_h2d(murr_ctx_t* ctx, void* dst, const void* src, uint64_t bytes);
+int murr_memcpy_d2h(murr_ctx_t* ctx, void* dst, const void* src, uint64_t bytes);
+int murr_memset_dev(murr_ctx_t* ctx, void* dst, int value, uint64_t bytes);
+int murr_sync(murr_ctx_t* ctx);
+
+/* ---- device-resident decode (row blobs -> Arrow) ------------------------- */
+
+/* A block = one batch read: n_rows row blobs back to back in `data`.
+ * Row i is data[row_off[i] .. row_off[i+1]); an empty row is a missing key
+ * (ReadBatchBuilder::add_empty, src/io/row/read.rs:93-98; a present row is
+ * never empty when the segment has >= 1 column, write.rs:21).
+ * `data` must be 16-byte aligned; all pointers are device pointers. */
+typedef struct {
+    const uint8_t*  data;
+    const uint64_t* row_off;   /* n_rows + 1 entries, row_off[0] may be > 0 */
+    uint64_t        n_rows;
+} murr_block_t;
+
+/* One output Arrow array (device pointers), arrow-rs 58 builder layout:
+ *   fixed W:  values = n*W bytes, null slots zero
+ *   bool:     values = bitmap (murr_bitmap_bytes(n)), null -> 0 bit
+ *   utf8:     offsets = n+1 i32 starting at 0, values = string bytes (values_cap)
+ *   validity: bitmap (murr_bitmap_bytes(n)), 1 = valid; the caller drops it
+ *             when null_count == 0 (arrow-rs NullBufferBuilder materialises
+ *             validity only after the first null).
+ * null_count / data_len are outputs. */
+typedef struct {
+    void*    values;
+    uint8_t* validity;
+    int32_t* offsets;
+    uint64_t values_cap;
+    uint64_t null_count;  /* out */
+    uint64_t data_len;    /* out: utf8 string bytes; fixed: n*W; bool: ceil(n/8) */
+} murr_array_t;
+
+/* Batched ReadBatchBuilder::add_row/add_empty/build over device-resident
+ * blocks (src/io/row/read.rs:62-110, encoders src/io/codec/primitive.rs:38-61,
+ * bool_.rs:85-104, utf8.rs:85-105).  `proj[nproj]` are segment column indices
+ * in request order (duplicates allowed).  `outs[b*nproj + p]` is block b,
+ * projected column p.  Synchronous: returns after the stream drained and the
+ * output counts are filled. */
+int murr_decode_blocks(murr_ctx_t* ctx, const murr_segment_t* seg,
+                       const uint32_t* proj, uint32_t nproj,
+                       const murr_block_t* blocks, uint32_t nblocks,
+                       murr_array_t* outs, murr_error_t* err);
+
+/* Same as murr_decode_blocks but only enqueues; murr_decode_wait finishes it
+ * (fills counts, reports errors).  One pending decode per context. */
+int murr_decode_enqueue(murr_ctx_t* ctx, const murr_segment_t* seg,
+                        const uint32_t* proj, uint32_t nproj,
+                        const murr_block_t* blocks, uint32_t nblocks,
+                        murr_array_t* outs);
+int murr_decode_wait(murr_ctx_t* ctx, murr_error_t* err);
+
+/* ---- device-resident encode (Arrow -> row blobs) -------------------------- */
+
+/* One Arrow input column (device pointers).  `offset` is the Arrow array
+ * offset in elements (bits for bitmaps).  validity == NULL means no nulls. */
+typedef struct {
+    const void*    values;    /* fixed: values; bool: bitmap; utf8: string data */
+    const uint8_t* validity;
+    const int32_t* offsets;   /* utf8 only */
+    uint64_t       offset;
+} murr_col_in_t;
+
+/* Upper bound of the blob bytes murr_encode_batch writes for n_rows rows:
+ * n*(bs+cap) + sum over utf8 columns of (4*n + utf8_data_bytes[c]).
+ * utf8_data_bytes has one entry per segment column (ignored for non-utf8). */
+uint64_t murr_encode_bound(const murr_segment_t* seg, uint64_t n_rows,
+                           const uint64_t* utf8_data_bytes);
+
+/* Table::write's per-row loop (src/io/table/mod.rs:97-109) over device
+ * buffers: for every row, WriteRow::new (0xFF bitset, write.rs:20-28) then each
+ * column's ColumnDecoder::write_to_row (primitive.rs:85-95, bool_.rs:111-117,
+ * utf8.rs:113-119).  `cols[seg->ncols]` in segment order.  Writes the blobs
+ * back to back into out_blob and out_row_off[n_rows+1] (row i =
+ * out_blob[row_off[i]..row_off[i+1]), row_off[0] = 0).  *blob_len = bytes
+ * written.  Keys stay with the caller (they are RocksDB keys, never in the blob). */
+int murr_encode_batch(murr_ctx_t* ctx, const murr_segment_t* seg,
+                      const murr_col_in_t* cols, uint64_t n_rows,
+                      uint8_t* out_blob, uint64_t blob_cap,
+                      uint64_t* out_row_off, uint64_t* blob_len,
+                      murr_error_t* err);
+
+/* ---- host-memory path (pinned staging + hipMemcpyAsync both ways) -------- */
+
+/* Batched ReadBatchBuilder (src/io/row/read.rs:62-110) for the store-driven
+ * read (Store::read feeds rows in caller order, src/io/store/rocksdb/mod.rs:259-266,
+ * src/io/store/memory.rs:38-43).  add_row copies the pinned slice into a pinned
+ * host staging block; build() = H2D + one decode launch + D2H into host
+ * Arrow buffers owned by the builder (valid until murr_builder_free). */
+typedef struct murr_builder murr_builder_t;
+
+typedef struct {             /* host Arrow array produced by build() */
+    const uint8_t* values;
+    const uint8_t* validity; /* NULL when null_count == 0 */
+    const int32_t* offsets;  /* utf8 only */
+    uint64_t length;
+    uint64_t null_count;
+    uint64_t values_len;     /* bytes in values */
+    uint32_t dtype;
+    uint32_t _pad;
+} murr_host_array_t;
+
+int murr_builder_new(murr_ctx_t* ctx, const murr_segment_t* seg,
+                     const uint32_t* proj, uint32_t nproj, uint64_t capacity,
+                     murr_builder_t** out);
+int murr_builder_add_row(murr_builder_t* b, const uint8_t* bytes, uint64_t len);
+int murr_builder_add_empty(murr_builder_t* b);
+/* Many rows at once: ptrs[i] == NULL is a missing key. */
+int murr_builder_add_rows(murr_builder_t* b, const uint8_t* const* ptrs,
+                          const uint64_t* lens, uint64_t n);
+int murr_builder_build(murr_builder_t* b, murr_host_array_t* outs /* nproj */,
+                       murr_error_t* err);
+/* Milliseconds of the last build(): total, h2d copy, decode kernel, d2h copy. */
+int murr_builder_last_timing(murr_builder_t* b, double* total_ms, float* h2d_ms,
+                             float* kernel_ms, float* d2h_ms);
+void murr_builder_free(murr_builder_t* b);
+
+/* Host-memory encode: H2D of the Arrow buffers, murr_encode_batch, D2H of the
+ * blobs.  Host input columns use the same murr_col_in_t (host pointers) plus
+ * the per-column byte lengths of their buffers.  Output buffers are allocated
+ * by the library (pinned) and freed with murr_host_free. */
+typedef struct {
+    murr_col_in_t col;       /* host pointers */
+    uint64_t values_bytes;   /* bytes readable at values (from element 0) */
+} murr_host_col_in_t;
+
+int murr_encode_host(murr_ctx_t* ctx, const murr_segment_t* seg,
+                     const murr_host_col_in_t* cols, uint64_t n_rows,
+                     uint8_t** out_blob, uint64_t* blob_len,
+                     uint64_t** out_row_off, murr_error_t* err);
+
+/* Human-readable name of a status code. */
+const char* murr_status_str(int status);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MURR_CODEC_H */

@@ -1,0 +1,177 @@
+"""ctypes binding of the C restatement (TEST INFRASTRUCTURE ONLY).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import
+this module, and only as the checker / CPU baseline.  The product path
+(murr_amd, libmurr_codec.so) never imports it.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libmurr_oracle.so")
+
+DTYPE_CODES = {"utf8": 0, "bool": 1, "int8": 2, "int16": 3, "int32": 4, "int64": 5,
+               "uint8": 6, "uint16": 7, "uint32": 8, "uint64": 9, "float32": 10, "float64": 11}
+SIZES = {0: 4, 1: 1, 2: 1, 3: 2, 4: 4, 5: 8, 6: 1, 7: 2, 8: 4, 9: 8, 10: 4, 11: 8}
+
+
+class OcColumn(C.Structure):
+    _fields_ = [("index", C.c_uint32), ("dtype", C.c_uint32), ("offset", C.c_uint32),
+                ("size", C.c_uint32)]
+
+
+class OcSegment(C.Structure):
+    _fields_ = [("ncols", C.c_uint32), ("bitset_size", C.c_uint32), ("capacity", C.c_uint32),
+                ("_pad", C.c_uint32), ("cols", C.POINTER(OcColumn))]
+
+
+class OcArray(C.Structure):
+    _fields_ = [("values", C.POINTER(C.c_uint8)), ("validity", C.POINTER(C.c_uint8)),
+                ("offsets", C.POINTER(C.c_int32)), ("length", C.c_uint64),
+                ("null_count", C.c_uint64), ("values_len", C.c_uint64), ("dtype", C.c_uint32),
+                ("_pad", C.c_uint32)]
+
+
+class OcColIn(C.Structure):
+    _fields_ = [("values", C.c_void_p), ("validity", C.c_void_p), ("offsets", C.c_void_p),
+                ("offset", C.c_uint64)]
+
+
+class OcError(C.Structure):
+    _fields_ = [("status", C.c_int32), ("_pad", C.c_int32), ("row", C.c_uint64),
+                ("column", C.c_uint32), ("_pad2", C.c_uint32), ("message", C.c_char * 128)]
+
+
+_lib = None
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = C.CDLL(LIB_PATH)
+        L.oc_segment_init.argtypes = [C.POINTER(C.c_uint32), C.c_uint32, C.POINTER(OcColumn),
+                                      C.POINTER(OcSegment)]
+        L.oc_decode_block.argtypes = [C.POINTER(OcSegment), C.POINTER(C.c_uint32), C.c_uint32,
+                                      C.c_void_p, C.c_void_p, C.c_uint64, C.POINTER(OcArray),
+                                      C.POINTER(OcError)]
+        L.oc_encode_batch.argtypes = [C.POINTER(OcSegment), C.POINTER(OcColIn), C.c_uint64,
+                                      C.POINTER(C.POINTER(C.c_uint8)), C.POINTER(C.c_uint64),
+                                      C.c_void_p, C.POINTER(OcError)]
+        L.oc_array_free.argtypes = [C.POINTER(OcArray)]
+        L.oc_free.argtypes = [C.c_void_p]
+        L.oc_utf8_valid.argtypes = [C.c_char_p, C.c_uint64, C.POINTER(C.c_uint64),
+                                    C.POINTER(C.c_int)]
+        _lib = L
+    return _lib
+
+
+class Segment:
+    def __init__(self, dtypes):
+        codes = [DTYPE_CODES[d] if isinstance(d, str) else int(d) for d in dtypes]
+        self.codes = codes
+        n = len(codes)
+        self._dt = (C.c_uint32 * max(n, 1))(*codes)
+        self._cols = (OcColumn * max(n, 1))()
+        self.seg = OcSegment()
+        st = lib().oc_segment_init(self._dt, n, self._cols, C.byref(self.seg))
+        if st:
+            raise ValueError(f"oc_segment_init: {st}")
+
+    @property
+    def bitset_size(self):
+        return self.seg.bitset_size
+
+    @property
+    def capacity(self):
+        return self.seg.capacity
+
+
+class OracleError(Exception):
+    def __init__(self, status, row, column, message):
+        super().__init__(f"status={status} row={row} column={column}: {message}")
+        self.status, self.row, self.column, self.message = status, row, column, message
+
+
+def _take_array(a: OcArray):
+    n = a.length
+    out = {"dtype": a.dtype, "length": n, "null_count": a.null_count,
+           "values": C.string_at(a.values, a.values_len) if a.values_len else b"",
+           "validity": C.string_at(a.validity, (n + 7) // 8) if a.validity else None,
+           "offsets": None}
+    if a.dtype == 0:
+        out["offsets"] = np.ctypeslib.as_array(a.offsets, shape=(n + 1,)).copy()
+    return out
+
+
+def decode_block(seg: Segment, proj, data: bytes | np.ndarray, row_off: np.ndarray):
+    """Store::read-style decode of one block through the restated ReadBatchBuilder."""
+    proj = list(proj)
+    np_ = len(proj)
+    pj = (C.c_uint32 * max(np_, 1))(*proj)
+    outs = (OcArray * max(np_, 1))()
+    err = OcError()
+    data = np.frombuffer(data, dtype=np.uint8) if isinstance(data, (bytes, bytearray)) else data
+    data = np.ascontiguousarray(data, dtype=np.uint8)
+    if data.size == 0:
+        data = np.zeros(1, np.uint8)
+    row_off = np.ascontiguousarray(row_off, dtype=np.uint64)
+    n = row_off.size - 1
+    st = lib().oc_decode_block(C.byref(seg.seg), pj, np_, data.ctypes.data, row_off.ctypes.data,
+                               n, outs, C.byref(err))
+    if st:
+        raise OracleError(st, err.row, err.column, err.message.decode(errors="replace"))
+    res = []
+    for p in range(np_):
+        res.append(_take_array(outs[p]))
+        lib().oc_array_free(C.byref(outs[p]))
+    return res
+
+
+def encode_batch(seg: Segment, cols, n: int):
+    """cols: per segment column a dict of numpy/bytes buffers
+    {values, validity (or None), offsets (utf8), offset}.  Returns (blob, row_off)."""
+    keep = []
+    cin = (OcColIn * max(len(cols), 1))()
+    for i, c in enumerate(cols):
+        def ptr(b):
+            if b is None:
+                return None
+            a = np.frombuffer(b, dtype=np.uint8) if isinstance(b, (bytes, bytearray)) else b
+            a = np.ascontiguousarray(a)
+            if a.size == 0:
+                a = np.zeros(8, np.uint8)
+            keep.append(a)
+            return a.ctypes.data
+        cin[i].values = ptr(c.get("values"))
+        cin[i].validity = ptr(c.get("validity"))
+        cin[i].offsets = ptr(c.get("offsets"))
+        cin[i].offset = int(c.get("offset", 0))
+    blob = C.POINTER(C.c_uint8)()
+    blen = C.c_uint64()
+    row_off = np.zeros(n + 1, np.uint64)
+    err = OcError()
+    st = lib().oc_encode_batch(C.byref(seg.seg), cin, n, C.byref(blob), C.byref(blen),
+                               row_off.ctypes.data, C.byref(err))
+    if st:
+        raise OracleError(st, err.row, err.column, err.message.decode(errors="replace"))
+    out = np.frombuffer(C.string_at(blob, blen.value), dtype=np.uint8).copy()
+    lib().oc_free(blob)
+    return out, row_off
+
+
+def utf8_valid(b: bytes):
+    vut = C.c_uint64()
+    el = C.c_int()
+    ok = lib().oc_utf8_valid(b, len(b), C.byref(vut), C.byref(el))
+    return bool(ok), vut.value, el.value
