@@ -1,0 +1,314 @@
+#!/usr/bin/env python3
+"""Block-decode throughput of murr's row-blob codec on MI355X.
+
+Metric (BASELINE.json): block-decode GiB/s, device-resident, Arrow bytes out,
+at 1/2/4/8 GPUs.  One step = one murr_decode_blocks call (one kernel launch)
+over K blocks of configs[1]'s shape ("read_block shape: 100k-row
+FLOAT32+UTF8"), inputs already resident in HBM; the step includes the
+readback of null counts / string lengths the caller needs to assemble the
+Arrow arrays.  Multi-GPU (torchrun, one process per GPU): every rank decodes its
+own key-range shard (weak scaling), no data-path collective; torch.distributed
+(gloo, CPU) carries only the barrier and the max-over-ranks timing.
+
+Extra modes (not the headline line): --mode host (pinned H2D + decode + D2H
+through the batched ReadBatchBuilder), --mode encode (configs[4] write shape),
+--config C/D (16-col mixed nullable).
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+# Load the HIP library before torch so one HIP runtime serves the process.
+import murr_amd  # noqa: E402
+from murr_amd import _abi, synth  # noqa: E402
+from murr_amd.device import Context, DecodeOutputs, DeviceBlock, encode_batch  # noqa: E402
+from murr_amd.schema import SegmentSchema  # noqa: E402
+
+murr_amd.lib()
+
+METRIC = "block-decode GiB/s device-resident (Arrow bytes out) at 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec); no MFMA on this path
+GIB = float(1 << 30)
+
+
+def dist_init(args):
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    if ws <= 1:
+        return None, 0, 1, 0
+    import torch.distributed as dist
+    dist.init_process_group("gloo")
+    return dist, dist.get_rank(), ws, int(os.environ.get("LOCAL_RANK", "0"))
+
+
+def barrier(dist):
+    if dist is not None:
+        dist.barrier()
+
+
+def max_over_ranks(dist, x: float) -> float:
+    if dist is None:
+        return x
+    import torch
+    t = torch.tensor([x], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def sum_over_ranks(dist, x: float) -> float:
+    if dist is None:
+        return x
+    import torch
+    t = torch.tensor([x], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return float(t.item())
+
+
+def make_columns(config: str, rows: int, start: int):
+    if config == "B":
+        return synth.config_b(rows, start=start)
+    if config in ("C", "D"):
+        return synth.config_c(rows, start=start)
+    if config == "E":
+        return synth.config_e(rows, start=start)
+    raise SystemExit(f"unknown config {config}")
+
+
+def arrow_out_bytes(seg, proj, n, null_counts, utf8_lens):
+    """SURVEY.md §8(d) bytes_out: values + offsets + string bytes + validity of
+    columns that have nulls."""
+    tot = 0
+    for p, ci in enumerate(proj):
+        d = int(seg.columns[ci].dtype)
+        if d == 0:
+            tot += 4 * (n + 1) + utf8_lens[p]
+        elif d == 1:
+            tot += (n + 7) // 8
+        else:
+            tot += n * _abi.lib().murr_dtype_size(d)
+        if null_counts[p]:
+            tot += (n + 7) // 8
+    return tot
+
+
+def pmc_traffic(path):
+    """HBM bytes per decode launch from a rocprofv3 --pmc CSV (FETCH_SIZE x2 on
+    gfx950 per MI355X_MICROARCH.md §HBM, + WRITE_SIZE; KB units)."""
+    if not path or not os.path.exists(path):
+        return None
+    import csv
+    fetch, write, nf, nw = 0.0, 0.0, 0, 0
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            if "decode_kernel" not in r.get("Kernel_Name", ""):
+                continue
+            name, val = r.get("Counter_Name"), float(r.get("Counter_Value", 0))
+            if name == "FETCH_SIZE":
+                fetch += val; nf += 1
+            elif name == "WRITE_SIZE":
+                write += val; nw += 1
+    if not nf and not nw:
+        return None
+    per = (2.0 * fetch / max(nf, 1) + write / max(nw, 1)) * 1024.0
+    return per
+
+
+def cpu_baseline(seg, proj, host_blob, host_off, rows, target_s):
+    """The oracle (C restatement of ReadBatchBuilder, 1 thread) on this host."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    oseg = O.Segment([int(c.dtype) for c in seg.columns])
+    t = time.perf_counter()
+    res = O.decode_block(oseg, proj, host_blob, host_off)
+    one = time.perf_counter() - t
+    out_bytes = arrow_out_bytes(seg, proj, rows, [r["null_count"] for r in res],
+                                [len(r["values"]) if r["dtype"] == 0 else 0 for r in res])
+    reps = int(max(1, min(1000, target_s / max(one, 1e-6))))
+    t = time.perf_counter()
+    for _ in range(reps):
+        O.decode_block(oseg, proj, host_blob, host_off)
+    dt = time.perf_counter() - t
+    return {"value": round(out_bytes * reps / dt / GIB, 4), "unit": "GiB/s", "cores": 1,
+            "kind": "port",
+            "sample": f"{reps} blocks x {rows} rows of the same workload decoded by "
+                      f"oracle/libmurr_oracle.so (serial ReadBatchBuilder restatement), {dt:.1f} s"}
+
+
+def run_decode(args, dist, rank, world, local_rank):
+    ctx = Context(local_rank)
+    rows, K = args.rows, args.blocks
+    cols = make_columns(args.config, rows, start=rank * rows)
+    dtypes = [c["dtype"] for c in cols]
+    seg = SegmentSchema([(f"c{i}", d) for i, d in enumerate(dtypes)])
+    proj = list(range(len(cols)))
+    # One block's row blobs, produced by the device encoder, then K resident copies.
+    dblob, doff, blen = encode_batch(ctx, seg, synth.upload_columns(ctx, cols), rows)
+    host_blob = dblob.download(blen)
+    host_off = doff.download((rows + 1) * 8).view(np.uint64).copy()
+    del dblob, doff
+    blocks = [DeviceBlock.upload(ctx, host_blob, host_off) for _ in range(K)]
+    outs = DecodeOutputs(ctx, seg, proj, blocks)
+    cb = (_abi.Block * K)()
+    for i, b in enumerate(blocks):
+        cb[i].data, cb[i].row_off, cb[i].n_rows = b.data.ptr, b.row_off.ptr, b.n_rows
+    pj = (C.c_uint32 * len(proj))(*proj)
+    err = _abi.Error()
+    L = ctx.L
+
+    def step():
+        st = L.murr_decode_blocks(ctx.h, C.byref(seg.c), pj, len(proj), cb, K, outs.arrays, C.byref(err))
+        if st:
+            raise RuntimeError(f"decode failed: {_abi.status_str(st)} row {err.row} col {err.column}")
+
+    for _ in range(args.warmup):
+        step()
+    barrier(dist)
+    ctx.sync()
+    kms = []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+        kms.append(ctx.last_kernel_ms())
+    ctx.sync()
+    barrier(dist)
+    elapsed = time.perf_counter() - t0
+    elapsed = max_over_ranks(dist, elapsed)
+
+    a0 = [outs.array(0, p) for p in range(len(proj))]
+    out_block = arrow_out_bytes(seg, proj, rows, [a.null_count for a in a0],
+                                [a.data_len for a in a0])
+    in_block = int(host_blob.size) + 8 * (rows + 1)
+    out_step = out_block * K
+    total_out = sum_over_ranks(dist, out_step * args.steps)
+    value = total_out / elapsed / GIB
+    k_avg_ms = float(np.mean(kms))
+    achieved = (in_block + out_block) * K / (k_avg_ms * 1e-3) / 1e9
+    traffic = pmc_traffic(args.pmc_csv)
+    line = {
+        "metric": METRIC, "value": round(value, 3), "unit": "GiB/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
+        "config": {"workload": {"B": "configs[1] read_block shape: 100k-row FLOAT32+UTF8 blocks",
+                                "C": "configs[2] schema: 16-col mixed nullable blocks",
+                                "D": "configs[3] shard: 16-col mixed nullable, key-range shard per GPU"
+                                }.get(args.config, args.config),
+                   "rows_per_block": rows, "blocks_per_step": K, "columns": len(proj),
+                   "bytes_in_per_step": in_block * K, "bytes_out_per_step": out_step,
+                   "parallelism": f"{world} key-range shard(s), no collective"},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     "traffic": traffic, "kernel": "decode_kernel",
+                     "kernel_ms_avg": round(k_avg_ms, 5),
+                     "algorithmic_bytes_per_launch": (in_block + out_block) * K},
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu:
+        line["cpu_baseline"] = cpu_baseline(seg, proj, host_blob, host_off, rows, args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    ctx.close()
+
+
+def run_host(args):
+    """PCIe-inclusive rate: pinned staging -> H2D -> decode -> D2H."""
+    from murr_amd.row import ReadBatchBuilder
+    ctx = Context(0)
+    rows = args.rows
+    cols = make_columns(args.config, rows, 0)
+    seg = SegmentSchema([(f"c{i}", c["dtype"]) for i, c in enumerate(cols)])
+    dblob, doff, blen = encode_batch(ctx, seg, synth.upload_columns(ctx, cols), rows)
+    blob = dblob.download(blen).tobytes()
+    off = doff.download((rows + 1) * 8).view(np.uint64)
+    res = []
+    b = ReadBatchBuilder(seg, seg.columns, rows, ctx)
+    for it in range(args.warmup + args.steps):
+        b = ReadBatchBuilder(seg, seg.columns, rows, ctx)
+        L = ctx.L
+        # bulk append: all rows in one call (the store's pinned slices)
+        ptrs = (C.c_void_p * rows)()
+        lens = (C.c_uint64 * rows)()
+        base = C.cast(C.c_char_p(blob), C.c_void_p).value
+        for i in range(rows):
+            ptrs[i] = base + int(off[i])
+            lens[i] = int(off[i + 1] - off[i])
+        L.murr_builder_add_rows(b.h, ptrs, lens, rows)
+        rb = b.build()
+        if it >= args.warmup:
+            res.append(b.last_timing())
+    out_bytes = sum(sum(buf.size for buf in col.buffers() if buf is not None) for col in rb.columns)
+    tm = {k: float(np.median([r[k] for r in res])) for k in res[0]}
+    print(json.dumps({"mode": "host", "config": args.config, "rows": rows, "arrow_bytes_out": out_bytes,
+                      "blob_bytes_in": len(blob), "median_ms": tm,
+                      "GiB_s_pcie_inclusive": round(out_bytes / (tm["total_ms"] * 1e-3) / GIB, 3),
+                      "GiB_s_kernel_only": round(out_bytes / (tm["kernel_ms"] * 1e-3) / GIB, 3)}))
+
+
+def run_encode(args):
+    """configs[4] write shape: Arrow (10 x f32) -> row blobs, device-resident."""
+    ctx = Context(0)
+    n = args.rows
+    cols = synth.config_e(n)
+    seg = SegmentSchema([(f"col_{i}", c["dtype"]) for i, c in enumerate(cols)])
+    dcols = synth.upload_columns(ctx, cols)
+    for _ in range(args.warmup):
+        encode_batch(ctx, seg, dcols, n)
+    kms = []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        blob, off, blen = encode_batch(ctx, seg, dcols, n)
+        kms.append(ctx.last_kernel_ms())
+        del blob, off
+    el = time.perf_counter() - t0
+    bytes_in = sum(c["values"].nbytes for c in cols)
+    bytes_out = blen + 8 * (n + 1)
+    k = float(np.mean(kms))
+    print(json.dumps({"mode": "encode", "rows": n, "bytes_in": bytes_in, "bytes_out": bytes_out,
+                      "kernel_ms_avg": round(k, 4), "ms_per_step": round(el / args.steps * 1e3, 3),
+                      "GB_s_algorithmic": round((bytes_in + bytes_out) / (k * 1e-3) / 1e9, 1),
+                      "frac_of_8TBs": round((bytes_in + bytes_out) / (k * 1e-3) / 8e12, 4),
+                      "GiB_s_blob_out": round(bytes_out / (k * 1e-3) / GIB, 2)}))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="B", choices=["B", "C", "D", "E"])
+    ap.add_argument("--rows", type=int, default=None, help="rows per block")
+    ap.add_argument("--blocks", type=int, default=None, help="blocks per launch")
+    ap.add_argument("--mode", default="decode", choices=["decode", "host", "encode"])
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--pmc-csv", default=None)
+    args = ap.parse_args()
+    if args.rows is None:
+        args.rows = {"B": 100_000, "C": 1_000_000, "D": 1_250_000, "E": 20_000_000}[args.config]
+        if args.mode == "encode":
+            args.rows = 20_000_000
+    if args.blocks is None:
+        args.blocks = {"B": 1000, "C": 1, "D": 1, "E": 1}[args.config]
+    if args.mode == "host":
+        return run_host(args)
+    if args.mode == "encode":
+        return run_encode(args)
+    dist, rank, world, local_rank = dist_init(args)
+    if world != args.gpus and rank == 0:
+        print(f"note: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    run_decode(args, dist, rank, world, local_rank)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

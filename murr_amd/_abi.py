@@ -1,0 +1,132 @@
+"""ctypes binding of include/murr_codec.h (libmurr_codec.so, built in-tree).
+
+Loading fails loudly: there is no CPU fallback anywhere in this package.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import re
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+LIB_PATH = os.path.join(HERE, "libmurr_codec.so")
+HEADER = os.path.join(ROOT, "include", "murr_codec.h")
+
+# murr_status_t
+OK, E_INVALID_UTF8, E_DTYPE, E_BAD_COLUMN, E_OFFSET_OVERFLOW, E_MALFORMED_ROW, E_CAPACITY, \
+    E_ARGUMENT, E_NULL_KEY, E_HIP, E_INTERNAL, E_ARROW, E_NO_DEVICE = range(13)
+
+
+class Column(C.Structure):
+    _fields_ = [("index", C.c_uint32), ("dtype", C.c_uint32), ("offset", C.c_uint32),
+                ("size", C.c_uint32)]
+
+
+class Segment(C.Structure):
+    _fields_ = [("ncols", C.c_uint32), ("bitset_size", C.c_uint32), ("capacity", C.c_uint32),
+                ("_pad", C.c_uint32), ("cols", C.POINTER(Column))]
+
+
+class Error(C.Structure):
+    _fields_ = [("status", C.c_int32), ("hip_error", C.c_int32), ("block", C.c_uint32),
+                ("column", C.c_uint32), ("row", C.c_uint64), ("required", C.c_uint64)]
+
+
+class Block(C.Structure):
+    _fields_ = [("data", C.c_void_p), ("row_off", C.c_void_p), ("n_rows", C.c_uint64)]
+
+
+class Array(C.Structure):
+    _fields_ = [("values", C.c_void_p), ("validity", C.c_void_p), ("offsets", C.c_void_p),
+                ("values_cap", C.c_uint64), ("null_count", C.c_uint64), ("data_len", C.c_uint64)]
+
+
+class ColIn(C.Structure):
+    _fields_ = [("values", C.c_void_p), ("validity", C.c_void_p), ("offsets", C.c_void_p),
+                ("offset", C.c_uint64)]
+
+
+class HostArray(C.Structure):
+    _fields_ = [("values", C.c_void_p), ("validity", C.c_void_p), ("offsets", C.c_void_p),
+                ("length", C.c_uint64), ("null_count", C.c_uint64), ("values_len", C.c_uint64),
+                ("dtype", C.c_uint32), ("_pad", C.c_uint32)]
+
+
+class HostColIn(C.Structure):
+    _fields_ = [("col", ColIn), ("values_bytes", C.c_uint64)]
+
+
+P = C.c_void_p
+PP = C.POINTER(C.c_void_p)
+U32, U64, I32 = C.c_uint32, C.c_uint64, C.c_int
+
+# name -> (restype, argtypes); mirrors include/murr_codec.h one to one.
+SIGNATURES = {
+    "murr_dtype_size": (I32, [U32]),
+    "murr_segment_init": (I32, [C.POINTER(U32), U32, C.POINTER(Column), C.POINTER(Segment)]),
+    "murr_bitmap_bytes": (U64, [U64]),
+    "murr_ctx_create": (I32, [I32, PP]),
+    "murr_ctx_destroy": (None, [P]),
+    "murr_ctx_stream": (P, [P]),
+    "murr_ctx_last_kernel_ms": (I32, [P, C.POINTER(C.c_float)]),
+    "murr_device_count": (I32, [C.POINTER(I32)]),
+    "murr_dev_alloc": (I32, [P, U64, PP]),
+    "murr_dev_free": (I32, [P, P]),
+    "murr_host_alloc": (I32, [P, U64, PP]),
+    "murr_host_free": (I32, [P, P]),
+    "murr_memcpy_h2d": (I32, [P, P, P, U64]),
+    "murr_memcpy_d2h": (I32, [P, P, P, U64]),
+    "murr_memset_dev": (I32, [P, P, I32, U64]),
+    "murr_sync": (I32, [P]),
+    "murr_decode_blocks": (I32, [P, C.POINTER(Segment), C.POINTER(U32), U32, C.POINTER(Block), U32,
+                                 C.POINTER(Array), C.POINTER(Error)]),
+    "murr_decode_enqueue": (I32, [P, C.POINTER(Segment), C.POINTER(U32), U32, C.POINTER(Block), U32,
+                                  C.POINTER(Array)]),
+    "murr_decode_wait": (I32, [P, C.POINTER(Error)]),
+    "murr_encode_bound": (U64, [C.POINTER(Segment), U64, C.POINTER(U64)]),
+    "murr_encode_batch": (I32, [P, C.POINTER(Segment), C.POINTER(ColIn), U64, P, U64, P,
+                                C.POINTER(U64), C.POINTER(Error)]),
+    "murr_builder_new": (I32, [P, C.POINTER(Segment), C.POINTER(U32), U32, U64, PP]),
+    "murr_builder_add_row": (I32, [P, P, U64]),
+    "murr_builder_add_empty": (I32, [P]),
+    "murr_builder_add_rows": (I32, [P, C.POINTER(C.c_void_p), C.POINTER(U64), U64]),
+    "murr_builder_build": (I32, [P, C.POINTER(HostArray), C.POINTER(Error)]),
+    "murr_builder_last_timing": (I32, [P, C.POINTER(C.c_double), C.POINTER(C.c_float),
+                                       C.POINTER(C.c_float), C.POINTER(C.c_float)]),
+    "murr_builder_free": (None, [P]),
+    "murr_encode_host": (I32, [P, C.POINTER(Segment), C.POINTER(HostColIn), U64,
+                               C.POINTER(C.POINTER(C.c_uint8)), C.POINTER(U64),
+                               C.POINTER(C.POINTER(C.c_uint64)), C.POINTER(Error)]),
+    "murr_status_str": (C.c_char_p, [I32]),
+}
+
+_lib = None
+
+
+def header_symbols():
+    """Every function the public header declares."""
+    with open(HEADER) as f:
+        src = f.read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(murr_[a-z0-9_]+)\s*\(", src)))
+
+
+def lib():
+    """Load libmurr_codec.so; raises if it is missing (no fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"libmurr_codec.so not built at {LIB_PATH}; run "
+                              "`python -c 'import __graft_entry__ as g; g.build()'`")
+        L = C.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def status_str(st: int) -> str:
+    return lib().murr_status_str(st).decode()

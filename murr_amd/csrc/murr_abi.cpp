@@ -1,0 +1,819 @@
+// murr_abi.cpp — host side of the C ABI declared in include/murr_codec.h.
+//
+// Owns the per-context HIP stream, events and a grow-only device workspace
+// (zeroed counters + look-back granules + descriptor tables), validates
+// arguments the way the reference does, launches the kernels in
+// murr_kernels.hip and turns the packed device error word back into the
+// reference's first error.  No exceptions cross the boundary.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "../../include/murr_codec.h"
+#include "murr_internal.h"
+
+using namespace murr;
+
+namespace {
+
+constexpr uint64_t round_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
+
+int dtype_size(uint32_t d) {
+    static const int sz[MURR_NUM_DTYPES] = {4, 1, 1, 2, 4, 8, 1, 2, 4, 8, 4, 8};
+    return d < MURR_NUM_DTYPES ? sz[d] : -1;
+}
+
+int set_err(murr_error_t* err, int status, int hip = 0) {
+    if (err) {
+        std::memset(err, 0, sizeof *err);
+        err->status = status;
+        err->hip_error = hip;
+    }
+    return status;
+}
+
+bool valid_segment(const murr_segment_t* s) {
+    if (!s || (s->ncols && !s->cols)) return false;
+    uint32_t off = 0;
+    for (uint32_t i = 0; i < s->ncols; i++) {
+        const murr_column_t& c = s->cols[i];
+        if (dtype_size(c.dtype) < 0 || (int)c.size != dtype_size(c.dtype) || c.index >= s->ncols)
+            return false;
+        off = std::max(off, c.offset + c.size);
+    }
+    return s->bitset_size == (s->ncols + 7) / 8 && off <= s->capacity;
+}
+
+}  // namespace
+
+struct murr_ctx {
+    int device = 0;
+    int cus = 256;
+    int dec_grid_per_cu = 1, enc_grid_per_cu = 1;
+    hipStream_t stream = nullptr;
+    hipEvent_t k0 = nullptr, k1 = nullptr;
+    bool timed = false;
+    uint8_t* ws = nullptr;  // device workspace
+    uint64_t ws_cap = 0;
+    uint8_t* hs = nullptr;  // pinned host scratch
+    uint64_t hs_cap = 0;
+    // pending decode
+    bool pending = false;
+    murr_array_t* outs = nullptr;
+    std::vector<uint64_t> n_rows;
+    std::vector<uint32_t> dtypes;  // per projected column
+    uint32_t nblocks = 0, nproj = 0;
+    uint64_t rb_off = 0;           // readback offset in hs
+    int pending_status = MURR_OK;
+};
+
+namespace {
+
+int hip_fail(murr_error_t* err, hipError_t e) { return set_err(err, MURR_E_HIP, (int)e); }
+
+#define HIPC(expr)                                          \
+    do {                                                    \
+        hipError_t _e = (expr);                             \
+        if (_e != hipSuccess) return hip_fail(err, _e);     \
+    } while (0)
+
+int ensure_ws(murr_ctx* c, uint64_t bytes, murr_error_t* err) {
+    if (bytes <= c->ws_cap) return MURR_OK;
+    if (c->ws) HIPC(hipFree(c->ws));
+    c->ws = nullptr;
+    uint64_t cap = std::max<uint64_t>(round_up(bytes, 1 << 20), 4 << 20);
+    HIPC(hipMalloc(&c->ws, cap));
+    c->ws_cap = cap;
+    return MURR_OK;
+}
+
+int ensure_hs(murr_ctx* c, uint64_t bytes, murr_error_t* err) {
+    if (bytes <= c->hs_cap) return MURR_OK;
+    if (c->hs) HIPC(hipHostFree(c->hs));
+    c->hs = nullptr;
+    uint64_t cap = std::max<uint64_t>(round_up(bytes, 1 << 16), 1 << 20);
+    HIPC(hipHostMalloc(&c->hs, cap, hipHostMallocDefault));
+    c->hs_cap = cap;
+    return MURR_OK;
+}
+
+// Decode the packed device error word into murr_error_t.
+int unpack_err(unsigned long long word, murr_error_t* err) {
+    if (!word) return MURR_OK;
+    uint64_t key = ~(uint64_t)word;
+    int st = (int)(key & 0xF);
+    if (err) {
+        err->status = st;
+        err->block = (uint32_t)(key >> 46);
+        err->row = (key >> 14) & 0xFFFFFFFFull;
+        err->column = (uint32_t)((key >> 4) & 0x3FF);
+    }
+    return st;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* murr_status_str(int s) {
+    switch (s) {
+    case MURR_OK: return "ok";
+    case MURR_E_INVALID_UTF8: return "invalid utf8";
+    case MURR_E_DTYPE: return "dtype mismatch";
+    case MURR_E_BAD_COLUMN: return "column not found";
+    case MURR_E_OFFSET_OVERFLOW: return "byte array offset overflow";
+    case MURR_E_MALFORMED_ROW: return "malformed row blob";
+    case MURR_E_CAPACITY: return "output capacity too small";
+    case MURR_E_ARGUMENT: return "invalid argument";
+    case MURR_E_NULL_KEY: return "null in key column";
+    case MURR_E_HIP: return "HIP runtime error";
+    case MURR_E_INTERNAL: return "device protocol failure";
+    case MURR_E_ARROW: return "arrow error";
+    case MURR_E_NO_DEVICE: return "no HIP device";
+    default: return "unknown";
+    }
+}
+
+int murr_dtype_size(uint32_t dtype) { return dtype_size(dtype); }
+
+int murr_segment_init(const uint32_t* dtypes, uint32_t ncols, murr_column_t* cols_out,
+                      murr_segment_t* seg_out) {
+    if ((ncols && (!dtypes || !cols_out)) || !seg_out) return MURR_E_ARGUMENT;
+    uint32_t off = 0;
+    for (uint32_t i = 0; i < ncols; i++) {
+        int sz = dtype_size(dtypes[i]);
+        if (sz < 0) return MURR_E_DTYPE;
+        cols_out[i] = murr_column_t{i, dtypes[i], off, (uint32_t)sz};
+        off += (uint32_t)sz;
+    }
+    seg_out->ncols = ncols;
+    seg_out->bitset_size = (ncols + 7) / 8;
+    seg_out->capacity = off;
+    seg_out->_pad = 0;
+    seg_out->cols = cols_out;
+    return MURR_OK;
+}
+
+uint64_t murr_bitmap_bytes(uint64_t n) { return round_up((n + 7) / 8, 8); }
+
+int murr_device_count(int* n) {
+    int k = 0;
+    hipError_t e = hipGetDeviceCount(&k);
+    if (n) *n = (e == hipSuccess) ? k : 0;
+    return e == hipSuccess ? MURR_OK : MURR_E_NO_DEVICE;
+}
+
+int murr_ctx_create(int device, murr_ctx_t** out) {
+    if (!out) return MURR_E_ARGUMENT;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return MURR_E_NO_DEVICE;
+    if (device < 0 || device >= n) return MURR_E_ARGUMENT;
+    murr_ctx* c = new (std::nothrow) murr_ctx();
+    if (!c) return MURR_E_INTERNAL;
+    c->device = device;
+    murr_error_t* err = nullptr;
+    HIPC(hipSetDevice(device));
+    hipDeviceProp_t prop;
+    HIPC(hipGetDeviceProperties(&prop, device));
+    c->cus = prop.multiProcessorCount;
+    // Persistent grid: blocks that are certainly co-resident (one below the
+    // occupancy answer: MI355X_MICROARCH.md "Residency"), at least one per CU.
+    c->dec_grid_per_cu = std::max(1, std::min(8, decode_blocks_per_cu()) - 1);
+    c->enc_grid_per_cu = std::max(1, std::min(8, encode_blocks_per_cu()) - 1);
+    HIPC(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    HIPC(hipEventCreate(&c->k0));
+    HIPC(hipEventCreate(&c->k1));
+    *out = c;
+    return MURR_OK;
+}
+
+void murr_ctx_destroy(murr_ctx_t* c) {
+    if (!c) return;
+    hipSetDevice(c->device);
+    if (c->stream) hipStreamSynchronize(c->stream);
+    if (c->ws) hipFree(c->ws);
+    if (c->hs) hipHostFree(c->hs);
+    if (c->k0) hipEventDestroy(c->k0);
+    if (c->k1) hipEventDestroy(c->k1);
+    if (c->stream) hipStreamDestroy(c->stream);
+    delete c;
+}
+
+void* murr_ctx_stream(murr_ctx_t* c) { return c ? (void*)c->stream : nullptr; }
+
+int murr_ctx_last_kernel_ms(murr_ctx_t* c, float* ms) {
+    murr_error_t* err = nullptr;
+    if (!c || !ms) return MURR_E_ARGUMENT;
+    if (!c->timed) { *ms = 0.f; return MURR_OK; }
+    HIPC(hipEventSynchronize(c->k1));
+    HIPC(hipEventElapsedTime(ms, c->k0, c->k1));
+    return MURR_OK;
+}
+
+int murr_dev_alloc(murr_ctx_t* c, uint64_t bytes, void** p) {
+    murr_error_t* err = nullptr;
+    if (!c || !p) return MURR_E_ARGUMENT;
+    HIPC(hipSetDevice(c->device));
+    // Rounded up and padded so 16-B staging loads of the last chunk stay inside.
+    HIPC(hipMalloc(p, round_up(bytes ? bytes : 1, 16) + 16));
+    return MURR_OK;
+}
+
+int murr_dev_free(murr_ctx_t* c, void* p) {
+    murr_error_t* err = nullptr;
+    if (!c) return MURR_E_ARGUMENT;
+    if (p) HIPC(hipFree(p));
+    return MURR_OK;
+}
+
+int murr_host_alloc(murr_ctx_t* c, uint64_t bytes, void** p) {
+    murr_error_t* err = nullptr;
+    if (!c || !p) return MURR_E_ARGUMENT;
+    HIPC(hipHostMalloc(p, round_up(bytes ? bytes : 1, 16) + 16, hipHostMallocDefault));
+    return MURR_OK;
+}
+
+int murr_host_free(murr_ctx_t* c, void* p) {
+    murr_error_t* err = nullptr;
+    (void)c;
+    if (p) HIPC(hipHostFree(p));
+    return MURR_OK;
+}
+
+int murr_memcpy_h2d(murr_ctx_t* c, void* dst, const void* src, uint64_t n) {
+    murr_error_t* err = nullptr;
+    if (!c) return MURR_E_ARGUMENT;
+    if (!n) return MURR_OK;
+    HIPC(hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, c->stream));
+    HIPC(hipStreamSynchronize(c->stream));
+    return MURR_OK;
+}
+
+int murr_memcpy_d2h(murr_ctx_t* c, void* dst, const void* src, uint64_t n) {
+    murr_error_t* err = nullptr;
+    if (!c) return MURR_E_ARGUMENT;
+    if (!n) return MURR_OK;
+    HIPC(hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToHost, c->stream));
+    HIPC(hipStreamSynchronize(c->stream));
+    return MURR_OK;
+}
+
+int murr_memset_dev(murr_ctx_t* c, void* dst, int v, uint64_t n) {
+    murr_error_t* err = nullptr;
+    if (!c) return MURR_E_ARGUMENT;
+    if (!n) return MURR_OK;
+    HIPC(hipMemsetAsync(dst, v, n, c->stream));
+    HIPC(hipStreamSynchronize(c->stream));
+    return MURR_OK;
+}
+
+int murr_sync(murr_ctx_t* c) {
+    murr_error_t* err = nullptr;
+    if (!c) return MURR_E_ARGUMENT;
+    HIPC(hipStreamSynchronize(c->stream));
+    return MURR_OK;
+}
+
+// ---- decode ------------------------------------------------------------------
+
+int murr_decode_enqueue(murr_ctx_t* c, const murr_segment_t* seg, const uint32_t* proj,
+                        uint32_t nproj, const murr_block_t* blocks, uint32_t nblocks,
+                        murr_array_t* outs) {
+    murr_error_t* err = nullptr;
+    if (!c || !valid_segment(seg) || (nblocks && (!blocks || !outs)) || (nproj && !proj) ||
+        c->pending)
+        return MURR_E_ARGUMENT;
+    if (nproj == 0) return MURR_E_ARROW;  // RecordBatch::try_new, read.rs:106-108
+    if (nproj > kMaxProj || nblocks > 0x3FFFF) return MURR_E_ARGUMENT;
+    for (uint32_t p = 0; p < nproj; p++)
+        if (proj[p] >= seg->ncols) return MURR_E_BAD_COLUMN;
+    HIPC(hipSetDevice(c->device));
+
+    std::vector<DecProj> dp(nproj);
+    uint32_t nutf8 = 0;
+    for (uint32_t p = 0; p < nproj; p++) {
+        const murr_column_t& col = seg->cols[proj[p]];
+        dp[p] = DecProj{col.dtype, col.index, col.offset, col.size, col.dtype == MURR_UTF8, 0};
+        if (col.dtype == MURR_UTF8) dp[p].uslot = nutf8++;
+    }
+    std::vector<DecBlock> db(nblocks);
+    uint64_t tiles = 0;
+    for (uint32_t b = 0; b < nblocks; b++) {
+        const murr_block_t& bl = blocks[b];
+        if (bl.n_rows && (!bl.data || !bl.row_off || ((uintptr_t)bl.data & 15)))
+            return MURR_E_ARGUMENT;
+        db[b] = DecBlock{bl.data, bl.row_off, bl.n_rows, tiles};
+        tiles += (bl.n_rows + kTile - 1) / kTile;
+        for (uint32_t p = 0; p < nproj; p++) {
+            const murr_array_t& o = outs[(uint64_t)b * nproj + p];
+            if (bl.n_rows && (!o.validity || !o.values || (dp[p].is_utf8 && !o.offsets)))
+                return MURR_E_ARGUMENT;
+            if (dp[p].is_utf8 && !o.offsets) return MURR_E_ARGUMENT;
+            if (((uintptr_t)o.validity & 7) || (dp[p].dtype == MURR_BOOL && ((uintptr_t)o.values & 7)) ||
+                (!dp[p].is_utf8 && ((uintptr_t)o.values & (dp[p].width - 1))))
+                return MURR_E_ARGUMENT;
+        }
+    }
+    std::vector<DecOut> dout((uint64_t)nblocks * nproj);
+    for (uint64_t i = 0; i < dout.size(); i++)
+        dout[i] = DecOut{(uint8_t*)outs[i].values, outs[i].validity, outs[i].offsets, outs[i].values_cap};
+
+    const uint64_t nbp = (uint64_t)nblocks * nproj;
+    const uint64_t z_err = 0, z_nulls = 16, z_lens = z_nulls + 8 * nbp, z_lb = z_lens + 8 * nbp;
+    const uint64_t zbytes = round_up(z_lb + 8 * (uint64_t)nutf8 * tiles, 16);
+    const uint64_t d_blocks = zbytes, d_proj = round_up(d_blocks + sizeof(DecBlock) * nblocks, 16);
+    const uint64_t d_outs = round_up(d_proj + sizeof(DecProj) * nproj, 16);
+    const uint64_t dend = round_up(d_outs + sizeof(DecOut) * dout.size(), 16);
+    int st = ensure_ws(c, dend, err);
+    if (st) return st;
+    // host scratch: [descriptors (dend - zbytes)] [readback z_lb bytes]
+    const uint64_t hdesc = dend - zbytes, rb = round_up(hdesc, 64);
+    st = ensure_hs(c, rb + z_lb, err);
+    if (st) return st;
+    std::memcpy(c->hs + (d_blocks - zbytes), db.data(), sizeof(DecBlock) * nblocks);
+    std::memcpy(c->hs + (d_proj - zbytes), dp.data(), sizeof(DecProj) * nproj);
+    std::memcpy(c->hs + (d_outs - zbytes), dout.data(), sizeof(DecOut) * dout.size());
+
+    HIPC(hipMemsetAsync(c->ws, 0, zbytes, c->stream));
+    HIPC(hipMemcpyAsync(c->ws + zbytes, c->hs, hdesc, hipMemcpyHostToDevice, c->stream));
+    // Empty blocks: utf8 offsets = [0] (StringBuilder starts with offset 0).
+    for (uint32_t b = 0; b < nblocks; b++)
+        if (blocks[b].n_rows == 0)
+            for (uint32_t p = 0; p < nproj; p++)
+                if (dp[p].is_utf8 && outs[(uint64_t)b * nproj + p].offsets)
+                    HIPC(hipMemsetAsync(outs[(uint64_t)b * nproj + p].offsets, 0, 4, c->stream));
+
+    DecodeArgs a{};
+    a.blocks = (const DecBlock*)(c->ws + d_blocks);
+    a.proj = (const DecProj*)(c->ws + d_proj);
+    a.outs = (const DecOut*)(c->ws + d_outs);
+    a.lookback = (uint64_t*)(c->ws + z_lb);
+    a.nulls = (unsigned long long*)(c->ws + z_nulls);
+    a.lens = (unsigned long long*)(c->ws + z_lens);
+    a.err = (unsigned long long*)(c->ws + z_err);
+    a.total_tiles = tiles;
+    a.nblocks = nblocks;
+    a.nproj = nproj;
+    a.nutf8 = nutf8;
+    a.bs = seg->bitset_size;
+    a.cap = seg->capacity;
+    HIPC(hipEventRecord(c->k0, c->stream));
+    if (tiles) {
+        uint64_t grid = std::min<uint64_t>(tiles, (uint64_t)c->cus * c->dec_grid_per_cu);
+        HIPC(launch_decode(a, (uint32_t)grid, c->stream));
+    }
+    HIPC(hipEventRecord(c->k1, c->stream));
+    c->timed = true;
+    HIPC(hipMemcpyAsync(c->hs + rb, c->ws, z_lb, hipMemcpyDeviceToHost, c->stream));
+
+    c->pending = true;
+    c->outs = outs;
+    c->nblocks = nblocks;
+    c->nproj = nproj;
+    c->rb_off = rb;
+    c->n_rows.resize(nblocks);
+    for (uint32_t b = 0; b < nblocks; b++) c->n_rows[b] = blocks[b].n_rows;
+    c->dtypes.resize(nproj);
+    for (uint32_t p = 0; p < nproj; p++) c->dtypes[p] = dp[p].dtype;
+    return MURR_OK;
+}
+
+int murr_decode_wait(murr_ctx_t* c, murr_error_t* err) {
+    if (!c || !c->pending) return set_err(err, MURR_E_ARGUMENT);
+    c->pending = false;
+    HIPC(hipStreamSynchronize(c->stream));
+    const uint8_t* rb = c->hs + c->rb_off;
+    unsigned long long word;
+    std::memcpy(&word, rb, 8);
+    const uint64_t nbp = (uint64_t)c->nblocks * c->nproj;
+    const unsigned long long* nulls = (const unsigned long long*)(rb + 16);
+    const unsigned long long* lens = nulls + nbp;
+    for (uint32_t b = 0; b < c->nblocks; b++) {
+        for (uint32_t p = 0; p < c->nproj; p++) {
+            murr_array_t& o = c->outs[(uint64_t)b * c->nproj + p];
+            const uint64_t n = c->n_rows[b];
+            const uint32_t d = c->dtypes[p];
+            o.null_count = nulls[(uint64_t)b * c->nproj + p];
+            o.data_len = d == MURR_UTF8 ? lens[(uint64_t)b * c->nproj + p]
+                         : d == MURR_BOOL ? (n + 7) / 8 : n * (uint64_t)dtype_size(d);
+        }
+    }
+    if (err) std::memset(err, 0, sizeof *err);
+    int st = unpack_err(word, err);
+    if (st == MURR_E_CAPACITY && err)
+        err->required = c->outs[(uint64_t)err->block * c->nproj + err->column].data_len;
+    return st;
+}
+
+int murr_decode_blocks(murr_ctx_t* c, const murr_segment_t* seg, const uint32_t* proj,
+                       uint32_t nproj, const murr_block_t* blocks, uint32_t nblocks,
+                       murr_array_t* outs, murr_error_t* err) {
+    int st = murr_decode_enqueue(c, seg, proj, nproj, blocks, nblocks, outs);
+    if (st) {
+        if (err && st != MURR_E_HIP) set_err(err, st);
+        else if (err && st == MURR_E_HIP) set_err(err, st, (int)hipGetLastError());
+        return st;
+    }
+    return murr_decode_wait(c, err);
+}
+
+// ---- encode ------------------------------------------------------------------
+
+uint64_t murr_encode_bound(const murr_segment_t* seg, uint64_t n, const uint64_t* utf8_bytes) {
+    if (!seg) return 0;
+    uint64_t b = n * ((uint64_t)seg->bitset_size + seg->capacity);
+    for (uint32_t i = 0; i < seg->ncols; i++)
+        if (seg->cols[i].dtype == MURR_UTF8) b += 4 * n + (utf8_bytes ? utf8_bytes[i] : 0);
+    return b;
+}
+
+int murr_encode_batch(murr_ctx_t* c, const murr_segment_t* seg, const murr_col_in_t* cols,
+                      uint64_t n, uint8_t* out_blob, uint64_t blob_cap, uint64_t* out_row_off,
+                      uint64_t* blob_len, murr_error_t* err) {
+    if (!c || !valid_segment(seg) || (seg->ncols && !cols) || !out_row_off || c->pending)
+        return set_err(err, MURR_E_ARGUMENT);
+    if (n > 0xFFFFFFFFull * kTile) return set_err(err, MURR_E_ARGUMENT);
+    HIPC(hipSetDevice(c->device));
+    uint32_t nutf8 = 0;
+    std::vector<EncCol> ec(seg->ncols);
+    for (uint32_t i = 0; i < seg->ncols; i++) {
+        const murr_column_t& col = seg->cols[i];
+        if (n && (!cols[i].values || (col.dtype == MURR_UTF8 && !cols[i].offsets)))
+            return set_err(err, MURR_E_ARGUMENT);
+        ec[i] = EncCol{(const uint8_t*)cols[i].values, cols[i].validity, cols[i].offsets,
+                       cols[i].offset, col.dtype, col.index, col.offset, col.size};
+        nutf8 += col.dtype == MURR_UTF8;
+    }
+    const uint64_t fixed = (uint64_t)seg->bitset_size + seg->capacity;
+    if (nutf8 == 0 && n * fixed > blob_cap) {
+        set_err(err, MURR_E_CAPACITY);
+        if (err) err->required = n * fixed;
+        return MURR_E_CAPACITY;
+    }
+    if (n && !out_blob) return set_err(err, MURR_E_ARGUMENT);
+    const uint64_t tiles = (n + kTile - 1) / kTile;
+    const uint64_t z_lb = 16, zbytes = round_up(z_lb + 8 * (nutf8 ? tiles : 0), 16);
+    const uint64_t d_cols = zbytes, dend = round_up(d_cols + sizeof(EncCol) * ec.size(), 16);
+    int st = ensure_ws(c, dend, err);
+    if (st) return st;
+    st = ensure_hs(c, round_up(dend - zbytes, 64) + 64, err);
+    if (st) return st;
+    std::memcpy(c->hs, ec.data(), sizeof(EncCol) * ec.size());
+    const uint64_t rb = round_up(dend - zbytes, 64);
+    HIPC(hipMemsetAsync(c->ws, 0, zbytes, c->stream));
+    if (!ec.empty()) HIPC(hipMemcpyAsync(c->ws + d_cols, c->hs, sizeof(EncCol) * ec.size(),
+                                         hipMemcpyHostToDevice, c->stream));
+    if (n == 0) HIPC(hipMemsetAsync(out_row_off, 0, 8, c->stream));
+    EncodeArgs a{};
+    a.cols = (const EncCol*)(c->ws + d_cols);
+    a.out = out_blob;
+    a.row_off = out_row_off;
+    a.lookback = (uint64_t*)(c->ws + z_lb);
+    a.err = (unsigned long long*)c->ws;
+    a.n_rows = n;
+    a.out_cap = blob_cap;
+    a.total_tiles = tiles;
+    a.ncols = seg->ncols;
+    a.nutf8 = nutf8;
+    a.bs = seg->bitset_size;
+    a.cap = seg->capacity;
+    HIPC(hipEventRecord(c->k0, c->stream));
+    if (tiles) {
+        uint64_t grid = std::min<uint64_t>(tiles, (uint64_t)c->cus * c->enc_grid_per_cu);
+        HIPC(launch_encode(a, (uint32_t)grid, c->stream));
+    }
+    HIPC(hipEventRecord(c->k1, c->stream));
+    c->timed = true;
+    HIPC(hipMemcpyAsync(c->hs + rb, c->ws, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPC(hipMemcpyAsync(c->hs + rb + 8, out_row_off + n, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPC(hipStreamSynchronize(c->stream));
+    unsigned long long word;
+    uint64_t total;
+    std::memcpy(&word, c->hs + rb, 8);
+    std::memcpy(&total, c->hs + rb + 8, 8);
+    if (blob_len) *blob_len = total;
+    if (err) std::memset(err, 0, sizeof *err);
+    st = unpack_err(word, err);
+    if (err) err->block = 0;
+    if (st == MURR_E_CAPACITY && err) err->required = total;
+    return st;
+}
+
+}  // extern "C"
+
+// ---- host-memory path --------------------------------------------------------
+
+struct murr_builder {
+    murr_ctx* ctx = nullptr;
+    std::vector<murr_column_t> cols;
+    murr_segment_t seg{};
+    std::vector<uint32_t> proj;
+    // pinned staging of the blobs + row offsets (add_row appends here)
+    uint8_t* hdata = nullptr;
+    uint64_t hdata_len = 0, hdata_cap = 0;
+    uint64_t* hoff = nullptr;
+    uint64_t n = 0, hoff_cap = 0;
+    uint64_t present = 0;
+    // device buffers (grow-only)
+    uint8_t* ddata = nullptr;
+    uint64_t ddata_cap = 0;
+    uint8_t* dout = nullptr;
+    uint64_t dout_cap = 0;
+    // host outputs (pinned)
+    uint8_t* hout = nullptr;
+    uint64_t hout_cap = 0;
+    std::vector<murr_array_t> arr;
+    std::vector<uint64_t> out_off;  // per column: values, validity, offsets offsets in dout/hout
+    hipEvent_t e0 = nullptr, e1 = nullptr, e2 = nullptr, e3 = nullptr;
+    double total_ms = 0;
+    float h2d_ms = 0, k_ms = 0, d2h_ms = 0;
+};
+
+namespace {
+
+bool grow_pinned(uint8_t** p, uint64_t* cap, uint64_t need, uint64_t keep) {
+    if (need <= *cap) return true;
+    uint64_t nc = std::max<uint64_t>(need, std::max<uint64_t>(*cap * 2, 1 << 16));
+    uint8_t* q = nullptr;
+    if (hipHostMalloc(&q, nc, hipHostMallocDefault) != hipSuccess) return false;
+    if (*p) {
+        if (keep) std::memcpy(q, *p, keep);
+        hipHostFree(*p);
+    }
+    *p = q;
+    *cap = nc;
+    return true;
+}
+
+bool grow_dev(uint8_t** p, uint64_t* cap, uint64_t need) {
+    if (need <= *cap) return true;
+    if (*p) hipFree(*p);
+    *p = nullptr;
+    uint64_t nc = round_up(std::max<uint64_t>(need, 1 << 16), 1 << 16);
+    if (hipMalloc(p, nc) != hipSuccess) { *cap = 0; return false; }
+    *cap = nc;
+    return true;
+}
+
+bool push_off(murr_builder* b) {
+    if (b->n + 2 > b->hoff_cap) {
+        uint8_t* p = (uint8_t*)b->hoff;
+        uint64_t capb = b->hoff_cap * 8;
+        if (!grow_pinned(&p, &capb, (b->n + 2) * 8, (b->n + 1) * 8)) return false;
+        b->hoff = (uint64_t*)p;
+        b->hoff_cap = capb / 8;
+    }
+    b->hoff[++b->n] = b->hdata_len;
+    return true;
+}
+
+}  // namespace
+
+extern "C" {
+
+int murr_builder_new(murr_ctx_t* c, const murr_segment_t* seg, const uint32_t* proj,
+                     uint32_t nproj, uint64_t capacity, murr_builder_t** out) {
+    if (!c || !out || !valid_segment(seg) || (nproj && !proj)) return MURR_E_ARGUMENT;
+    for (uint32_t p = 0; p < nproj; p++)
+        if (proj[p] >= seg->ncols) return MURR_E_BAD_COLUMN;
+    murr_builder* b = new (std::nothrow) murr_builder();
+    if (!b) return MURR_E_INTERNAL;
+    b->ctx = c;
+    b->cols.assign(seg->cols, seg->cols + seg->ncols);
+    b->seg = *seg;
+    b->seg.cols = b->cols.data();
+    b->proj.assign(proj, proj + nproj);
+    hipSetDevice(c->device);
+    uint64_t cap = std::max<uint64_t>(capacity, 16);
+    uint64_t capb = 0;
+    uint8_t* p = nullptr;
+    if (!grow_pinned(&p, &capb, (cap + 2) * 8, 0)) { delete b; return MURR_E_HIP; }
+    b->hoff = (uint64_t*)p;
+    b->hoff_cap = capb / 8;
+    b->hoff[0] = 0;
+    if (!grow_pinned(&b->hdata, &b->hdata_cap, cap * ((uint64_t)seg->bitset_size + seg->capacity + 16), 0)) {
+        murr_builder_free(b);
+        return MURR_E_HIP;
+    }
+    hipEventCreate(&b->e0); hipEventCreate(&b->e1); hipEventCreate(&b->e2); hipEventCreate(&b->e3);
+    *out = b;
+    return MURR_OK;
+}
+
+// ReadBatchBuilder::add_row (read.rs:85-91): the row bytes are copied into the
+// pinned staging block; decoding happens once per batch in build().
+int murr_builder_add_row(murr_builder_t* b, const uint8_t* bytes, uint64_t len) {
+    if (!b || (len && !bytes)) return MURR_E_ARGUMENT;
+    if (len == 0) return MURR_E_MALFORMED_ROW;  // a present row is never empty (write.rs:21)
+    if (!grow_pinned(&b->hdata, &b->hdata_cap, b->hdata_len + len, b->hdata_len)) return MURR_E_HIP;
+    std::memcpy(b->hdata + b->hdata_len, bytes, len);
+    b->hdata_len += len;
+    b->present++;
+    return push_off(b) ? MURR_OK : MURR_E_HIP;
+}
+
+// ReadBatchBuilder::add_empty (read.rs:93-98): a zero-length row.
+int murr_builder_add_empty(murr_builder_t* b) {
+    if (!b) return MURR_E_ARGUMENT;
+    return push_off(b) ? MURR_OK : MURR_E_HIP;
+}
+
+int murr_builder_add_rows(murr_builder_t* b, const uint8_t* const* ptrs, const uint64_t* lens,
+                          uint64_t n) {
+    if (!b || (n && (!ptrs || !lens))) return MURR_E_ARGUMENT;
+    for (uint64_t i = 0; i < n; i++) {
+        int st = ptrs[i] ? murr_builder_add_row(b, ptrs[i], lens[i]) : murr_builder_add_empty(b);
+        if (st) return st;
+    }
+    return MURR_OK;
+}
+
+// ReadBatchBuilder::build (read.rs:100-109): H2D, one decode launch, D2H.
+int murr_builder_build(murr_builder_t* b, murr_host_array_t* outs, murr_error_t* err) {
+    if (!b || (!b->proj.empty() && !outs)) return set_err(err, MURR_E_ARGUMENT);
+    if (b->proj.empty()) return set_err(err, MURR_E_ARROW);
+    auto t0 = std::chrono::steady_clock::now();
+    murr_ctx* c = b->ctx;
+    HIPC(hipSetDevice(c->device));
+    const uint64_t n = b->n, np = b->proj.size();
+    const uint64_t dbytes = round_up(b->hdata_len, 16) + 16;
+    const uint64_t obytes = (n + 1) * 8;
+    // Output layout in one device (and one pinned host) buffer, 64-B aligned parts.
+    const uint64_t bm = murr_bitmap_bytes(n);
+    const uint64_t utf8_cap = b->hdata_len > b->present * ((uint64_t)b->seg.bitset_size + b->seg.capacity)
+                                  ? b->hdata_len - b->present * ((uint64_t)b->seg.bitset_size + b->seg.capacity)
+                                  : 0;
+    b->out_off.assign(np * 3, 0);
+    uint64_t off = 0;
+    for (uint64_t p = 0; p < np; p++) {
+        const murr_column_t& col = b->cols[b->proj[p]];
+        uint64_t vb = col.dtype == MURR_UTF8 ? utf8_cap : col.dtype == MURR_BOOL ? bm : n * col.size;
+        b->out_off[3 * p] = off;
+        off = round_up(off + std::max<uint64_t>(vb, 8), 64);
+        b->out_off[3 * p + 1] = off;
+        off = round_up(off + std::max<uint64_t>(bm, 8), 64);
+        b->out_off[3 * p + 2] = off;
+        if (col.dtype == MURR_UTF8) off = round_up(off + (n + 1) * 4, 64);
+    }
+    const uint64_t total_out = std::max<uint64_t>(off, 64);
+    if (!grow_dev(&b->ddata, &b->ddata_cap, dbytes + obytes + 64) ||
+        !grow_dev(&b->dout, &b->dout_cap, total_out) ||
+        !grow_pinned(&b->hout, &b->hout_cap, total_out, 0))
+        return set_err(err, MURR_E_HIP);
+    uint8_t* ddata = b->ddata;
+    uint64_t* doff = (uint64_t*)(b->ddata + round_up(dbytes, 64));
+    HIPC(hipEventRecord(b->e0, c->stream));
+    if (b->hdata_len) HIPC(hipMemcpyAsync(ddata, b->hdata, b->hdata_len, hipMemcpyHostToDevice, c->stream));
+    HIPC(hipMemcpyAsync(doff, b->hoff, obytes, hipMemcpyHostToDevice, c->stream));
+    HIPC(hipEventRecord(b->e1, c->stream));
+    murr_block_t blk{ddata, doff, n};
+    b->arr.assign(np, murr_array_t{});
+    for (uint64_t p = 0; p < np; p++) {
+        const murr_column_t& col = b->cols[b->proj[p]];
+        murr_array_t& a = b->arr[p];
+        a.values = b->dout + b->out_off[3 * p];
+        a.validity = b->dout + b->out_off[3 * p + 1];
+        a.offsets = col.dtype == MURR_UTF8 ? (int32_t*)(b->dout + b->out_off[3 * p + 2]) : nullptr;
+        a.values_cap = utf8_cap;
+    }
+    int st = murr_decode_blocks(c, &b->seg, b->proj.data(), (uint32_t)np, &blk, 1, b->arr.data(), err);
+    if (st) return st;
+    HIPC(hipEventRecord(b->e2, c->stream));
+    for (uint64_t p = 0; p < np; p++) {
+        const murr_column_t& col = b->cols[b->proj[p]];
+        const murr_array_t& a = b->arr[p];
+        uint64_t vlen = a.data_len;
+        if (vlen) HIPC(hipMemcpyAsync(b->hout + b->out_off[3 * p], a.values, vlen, hipMemcpyDeviceToHost, c->stream));
+        if (a.null_count)
+            HIPC(hipMemcpyAsync(b->hout + b->out_off[3 * p + 1], a.validity, (n + 7) / 8,
+                                hipMemcpyDeviceToHost, c->stream));
+        if (col.dtype == MURR_UTF8)
+            HIPC(hipMemcpyAsync(b->hout + b->out_off[3 * p + 2], a.offsets, (n + 1) * 4,
+                                hipMemcpyDeviceToHost, c->stream));
+    }
+    HIPC(hipEventRecord(b->e3, c->stream));
+    HIPC(hipStreamSynchronize(c->stream));
+    for (uint64_t p = 0; p < np; p++) {
+        const murr_column_t& col = b->cols[b->proj[p]];
+        const murr_array_t& a = b->arr[p];
+        murr_host_array_t& h = outs[p];
+        h.values = b->hout + b->out_off[3 * p];
+        h.validity = a.null_count ? b->hout + b->out_off[3 * p + 1] : nullptr;
+        h.offsets = col.dtype == MURR_UTF8 ? (const int32_t*)(b->hout + b->out_off[3 * p + 2]) : nullptr;
+        h.length = n;
+        h.null_count = a.null_count;
+        h.values_len = a.data_len;
+        h.dtype = col.dtype;
+        h._pad = 0;
+    }
+    hipEventElapsedTime(&b->h2d_ms, b->e0, b->e1);
+    murr_ctx_last_kernel_ms(c, &b->k_ms);
+    hipEventElapsedTime(&b->d2h_ms, b->e2, b->e3);
+    b->total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return MURR_OK;
+}
+
+int murr_builder_last_timing(murr_builder_t* b, double* total_ms, float* h2d_ms, float* kernel_ms,
+                             float* d2h_ms) {
+    if (!b) return MURR_E_ARGUMENT;
+    if (total_ms) *total_ms = b->total_ms;
+    if (h2d_ms) *h2d_ms = b->h2d_ms;
+    if (kernel_ms) *kernel_ms = b->k_ms;
+    if (d2h_ms) *d2h_ms = b->d2h_ms;
+    return MURR_OK;
+}
+
+void murr_builder_free(murr_builder_t* b) {
+    if (!b) return;
+    if (b->ctx) hipSetDevice(b->ctx->device);
+    if (b->hdata) hipHostFree(b->hdata);
+    if (b->hoff) hipHostFree(b->hoff);
+    if (b->hout) hipHostFree(b->hout);
+    if (b->ddata) hipFree(b->ddata);
+    if (b->dout) hipFree(b->dout);
+    if (b->e0) hipEventDestroy(b->e0);
+    if (b->e1) hipEventDestroy(b->e1);
+    if (b->e2) hipEventDestroy(b->e2);
+    if (b->e3) hipEventDestroy(b->e3);
+    delete b;
+}
+
+// Host-memory encode: H2D Arrow buffers, murr_encode_batch, D2H blobs + offsets.
+int murr_encode_host(murr_ctx_t* c, const murr_segment_t* seg, const murr_host_col_in_t* cols,
+                     uint64_t n, uint8_t** out_blob, uint64_t* blob_len, uint64_t** out_row_off,
+                     murr_error_t* err) {
+    if (!c || !valid_segment(seg) || (seg->ncols && !cols) || !out_blob || !blob_len || !out_row_off)
+        return set_err(err, MURR_E_ARGUMENT);
+    HIPC(hipSetDevice(c->device));
+    std::vector<void*> dbufs;
+    auto cleanup = [&]() { for (void* p : dbufs) hipFree(p); };
+    std::vector<murr_col_in_t> din(seg->ncols);
+    std::vector<uint64_t> utf8_bytes(seg->ncols, 0);
+    auto up = [&](const void* h, uint64_t bytes, const void** d) -> int {
+        *d = nullptr;
+        if (!h) return MURR_OK;
+        void* p = nullptr;
+        if (hipMalloc(&p, round_up(bytes ? bytes : 1, 16) + 16) != hipSuccess) return MURR_E_HIP;
+        dbufs.push_back(p);
+        if (bytes && hipMemcpyAsync(p, h, bytes, hipMemcpyHostToDevice, c->stream) != hipSuccess)
+            return MURR_E_HIP;
+        *d = p;
+        return MURR_OK;
+    };
+    for (uint32_t i = 0; i < seg->ncols; i++) {
+        const murr_host_col_in_t& hc = cols[i];
+        const uint32_t dt = seg->cols[i].dtype;
+        const uint64_t e = hc.col.offset + n;
+        int st = up(hc.col.values, hc.values_bytes, &din[i].values);
+        if (!st) st = up(hc.col.validity, (e + 7) / 8, (const void**)&din[i].validity);
+        if (!st && dt == MURR_UTF8) st = up(hc.col.offsets, (e + 1) * 4, (const void**)&din[i].offsets);
+        din[i].offset = hc.col.offset;
+        if (st) { cleanup(); return set_err(err, st); }
+        if (dt == MURR_UTF8 && hc.col.offsets && n)
+            utf8_bytes[i] = (uint64_t)(hc.col.offsets[e] - hc.col.offsets[hc.col.offset]);
+    }
+    const uint64_t cap = murr_encode_bound(seg, n, utf8_bytes.data());
+    uint8_t* dblob = nullptr;
+    uint64_t* doff = nullptr;
+    if (hipMalloc(&dblob, round_up(cap + 16, 16)) != hipSuccess ||
+        hipMalloc(&doff, (n + 1) * 8) != hipSuccess) {
+        if (dblob) hipFree(dblob);
+        cleanup();
+        return set_err(err, MURR_E_HIP);
+    }
+    dbufs.push_back(dblob);
+    dbufs.push_back(doff);
+    uint64_t len = 0;
+    int st = murr_encode_batch(c, seg, din.data(), n, dblob, cap, doff, &len, err);
+    if (st) { cleanup(); return st; }
+    uint8_t* hb = nullptr;
+    uint64_t* ho = nullptr;
+    if (hipHostMalloc(&hb, round_up(len + 16, 16), hipHostMallocDefault) != hipSuccess ||
+        hipHostMalloc(&ho, (n + 1) * 8, hipHostMallocDefault) != hipSuccess) {
+        if (hb) hipHostFree(hb);
+        cleanup();
+        return set_err(err, MURR_E_HIP);
+    }
+    hipError_t e1 = len ? hipMemcpyAsync(hb, dblob, len, hipMemcpyDeviceToHost, c->stream) : hipSuccess;
+    hipError_t e2 = hipMemcpyAsync(ho, doff, (n + 1) * 8, hipMemcpyDeviceToHost, c->stream);
+    hipError_t e3 = hipStreamSynchronize(c->stream);
+    cleanup();
+    if (e1 != hipSuccess || e2 != hipSuccess || e3 != hipSuccess) {
+        hipHostFree(hb);
+        hipHostFree(ho);
+        return set_err(err, MURR_E_HIP, (int)(e1 ? e1 : e2 ? e2 : e3));
+    }
+    *out_blob = hb;
+    *blob_len = len;
+    *out_row_off = ho;
+    return MURR_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,85 @@
+// murr_internal.h — device descriptors shared by the kernels (murr_kernels.hip)
+// and the host side of the C ABI (murr_abi.cpp).  Not part of the public ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace murr {
+
+// Rows per tile = threads per workgroup (thread-per-row), 4 waves.
+constexpr uint32_t kTile = 256;
+// Bytes of row blobs / assembled rows a tile stages through LDS.  Tiles whose
+// byte span exceeds this read / write HBM directly (the "global" path).
+constexpr uint32_t kStage = 32768;
+// Projected columns per decode call (10 bits in the packed error key).
+constexpr uint32_t kMaxProj = 1024;
+
+// Decoupled look-back granule: [63:62] flag, [61:0] value.
+constexpr uint64_t kFlagA = 1ull << 62;  // tile aggregate published
+constexpr uint64_t kFlagP = 2ull << 62;  // tile inclusive prefix published
+constexpr uint64_t kValMask = (1ull << 62) - 1;
+
+struct DecBlock {             // one block (batch read) of row blobs
+    const uint8_t* data;
+    const uint64_t* row_off;  // n_rows + 1
+    uint64_t n_rows;
+    uint64_t tile_base;       // first global tile of this block
+};
+
+struct DecProj {              // one projected column
+    uint32_t dtype, bit, offset, width;
+    uint32_t is_utf8, uslot;  // uslot = ordinal among projected utf8 columns
+};
+
+struct DecOut {               // one output Arrow array (block, column)
+    uint8_t* values;
+    uint8_t* validity;
+    int32_t* offsets;
+    uint64_t values_cap;
+};
+
+struct DecodeArgs {
+    const DecBlock* blocks;
+    const DecProj* proj;
+    const DecOut* outs;          // [nblocks * nproj]
+    uint64_t* lookback;          // [nutf8 * total_tiles]
+    unsigned long long* nulls;   // [nblocks * nproj]
+    unsigned long long* lens;    // [nblocks * nproj] utf8 data bytes
+    unsigned long long* err;     // max of ~key (0 = no error)
+    uint64_t total_tiles;
+    uint32_t nblocks, nproj, nutf8, bs, cap, _pad;
+};
+
+struct EncCol {               // one Arrow input column, segment order
+    const uint8_t* values;
+    const uint8_t* validity;
+    const int32_t* offsets;
+    uint64_t offset;
+    uint32_t dtype, index, soff, width;
+};
+
+struct EncodeArgs {
+    const EncCol* cols;
+    uint8_t* out;
+    uint64_t* row_off;           // n_rows + 1
+    uint64_t* lookback;          // [total_tiles]
+    unsigned long long* err;     // max of ~key
+    uint64_t n_rows, out_cap, total_tiles;
+    uint32_t ncols, nutf8, bs, cap;
+};
+
+// Packed first-error key: block(18) | row(32) | column(10) | status(4); the
+// smallest key is the reference's first error (row-major, then column).
+__host__ __device__ inline uint64_t err_key(uint64_t block, uint64_t row, uint32_t col,
+                                            uint32_t status) {
+    if (row > 0xFFFFFFFFull) row = 0xFFFFFFFFull;
+    if (block > 0x3FFFFull) block = 0x3FFFFull;
+    return (block << 46) | (row << 14) | ((uint64_t)(col & 0x3FF) << 4) | (status & 0xF);
+}
+
+hipError_t launch_decode(const DecodeArgs& a, uint32_t grid, hipStream_t s);
+hipError_t launch_encode(const EncodeArgs& a, uint32_t grid, hipStream_t s);
+int decode_blocks_per_cu();
+int encode_blocks_per_cu();
+
+}  // namespace murr

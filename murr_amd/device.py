@@ -1,0 +1,223 @@
+"""Device-resident path: a context (HIP stream + workspace), device buffers, and
+the batched decode / encode entry points of the C ABI.
+
+This is the seam the north star measures: blocks of row blobs already in HBM
+-> Arrow buffers in HBM (murr_decode_blocks), Arrow buffers in HBM -> row blobs
+in HBM (murr_encode_batch).  Buffers are plain device pointers; no torch.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _abi
+from .errors import DeviceError, raise_status
+from .schema import DTypeName, SegmentSchema
+
+
+def device_count() -> int:
+    n = C.c_int(0)
+    _abi.lib().murr_device_count(C.byref(n))
+    return n.value
+
+
+class Context:
+    """murr_ctx_t: one device, one stream, one workspace.  Not thread-safe."""
+
+    def __init__(self, device: int = 0):
+        self.L = _abi.lib()
+        h = C.c_void_p()
+        st = self.L.murr_ctx_create(device, C.byref(h))
+        if st:
+            raise DeviceError(f"murr_ctx_create(device={device}): {_abi.status_str(st)}")
+        self.h = h
+        self.device = device
+
+    def close(self):
+        if self.h:
+            self.L.murr_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    # -- memory -------------------------------------------------------------
+    def alloc(self, nbytes: int) -> "DeviceBuffer":
+        p = C.c_void_p()
+        raise_status(self.L.murr_dev_alloc(self.h, int(nbytes), C.byref(p)), what="murr_dev_alloc")
+        return DeviceBuffer(self, p.value, int(nbytes))
+
+    def upload(self, arr) -> "DeviceBuffer":
+        a = np.ascontiguousarray(arr)
+        buf = self.alloc(max(a.nbytes, 1))
+        if a.nbytes:
+            raise_status(self.L.murr_memcpy_h2d(self.h, buf.ptr, a.ctypes.data, a.nbytes), what="h2d")
+        return buf
+
+    def sync(self):
+        raise_status(self.L.murr_sync(self.h), what="sync")
+
+    def last_kernel_ms(self) -> float:
+        ms = C.c_float()
+        raise_status(self.L.murr_ctx_last_kernel_ms(self.h, C.byref(ms)), what="kernel time")
+        return ms.value
+
+
+class DeviceBuffer:
+    def __init__(self, ctx: Context, ptr: int, nbytes: int):
+        self.ctx, self.ptr, self.nbytes = ctx, ptr, nbytes
+
+    def free(self):
+        if self.ptr:
+            self.ctx.L.murr_dev_free(self.ctx.h, self.ptr)
+            self.ptr = 0
+
+    def __del__(self):
+        try:
+            if self.ctx.h:
+                self.free()
+        except Exception:
+            pass
+
+    def download(self, nbytes: int | None = None, offset: int = 0) -> np.ndarray:
+        n = self.nbytes - offset if nbytes is None else int(nbytes)
+        out = np.empty(max(n, 0), dtype=np.uint8)
+        if n:
+            raise_status(self.ctx.L.murr_memcpy_d2h(self.ctx.h, out.ctypes.data, self.ptr + offset, n),
+                         what="d2h")
+        return out
+
+    def memset(self, value: int = 0):
+        raise_status(self.ctx.L.murr_memset_dev(self.ctx.h, self.ptr, value, self.nbytes), what="memset")
+
+
+@dataclass
+class DeviceBlock:
+    """murr_block_t: row blobs back to back + row offsets (n_rows + 1)."""
+    data: DeviceBuffer
+    row_off: DeviceBuffer
+    n_rows: int
+    data_bytes: int
+
+    @classmethod
+    def upload(cls, ctx: Context, data: np.ndarray, row_off: np.ndarray) -> "DeviceBlock":
+        data = np.ascontiguousarray(data, dtype=np.uint8)
+        row_off = np.ascontiguousarray(row_off, dtype=np.uint64)
+        return cls(ctx.upload(data), ctx.upload(row_off), row_off.size - 1, data.nbytes)
+
+
+class DecodeOutputs:
+    """Device output buffers for nblocks x nproj Arrow arrays (murr_array_t)."""
+
+    def __init__(self, ctx: Context, segment: SegmentSchema, proj, blocks):
+        self.ctx = ctx
+        self.proj = list(proj)
+        self.blocks = blocks
+        np_ = len(self.proj)
+        self.arrays = (_abi.Array * max(len(blocks) * np_, 1))()
+        self.bufs = []
+        L = ctx.L
+        fixed = segment.bitset_size + segment.capacity
+        for b, blk in enumerate(blocks):
+            n = blk.n_rows
+            bm = int(L.murr_bitmap_bytes(n))
+            utf8_cap = max(blk.data_bytes - 0, 0)  # strings are a subset of the blob bytes
+            for p, ci in enumerate(self.proj):
+                col = segment.columns[ci]
+                a = self.arrays[b * np_ + p]
+                if col.dtype == DTypeName.Utf8:
+                    vb = max(utf8_cap, 8)
+                    offs = ctx.alloc((n + 1) * 4)
+                    self.bufs.append(offs)
+                    a.offsets = offs.ptr
+                    a.values_cap = vb
+                elif col.dtype == DTypeName.Bool:
+                    vb = bm
+                else:
+                    vb = n * col.dtype.size()
+                vals = ctx.alloc(max(vb, 8))
+                valid = ctx.alloc(max(bm, 8))
+                self.bufs += [vals, valid]
+                a.values = vals.ptr
+                a.validity = valid.ptr
+        del fixed
+
+    def array(self, b: int, p: int):
+        return self.arrays[b * len(self.proj) + p]
+
+
+def decode_blocks(ctx: Context, segment: SegmentSchema, proj, blocks, outs: DecodeOutputs | None = None):
+    """murr_decode_blocks over device-resident blocks.  Returns the outputs
+    object (null counts / data lengths filled)."""
+    proj = list(proj)
+    outs = outs or DecodeOutputs(ctx, segment, proj, blocks)
+    cb = (_abi.Block * max(len(blocks), 1))()
+    for i, blk in enumerate(blocks):
+        cb[i].data = blk.data.ptr
+        cb[i].row_off = blk.row_off.ptr
+        cb[i].n_rows = blk.n_rows
+    pj = (C.c_uint32 * max(len(proj), 1))(*proj)
+    err = _abi.Error()
+    st = ctx.L.murr_decode_blocks(ctx.h, C.byref(segment.c), pj, len(proj), cb, len(blocks),
+                                  outs.arrays, C.byref(err))
+    raise_status(st, err, "murr_decode_blocks")
+    return outs
+
+
+def download_array(ctx: Context, a, dtype: int, n: int) -> dict:
+    """Copy one decoded Arrow array (murr_array_t) back to host buffers."""
+    def d2h(ptr, nbytes):
+        out = np.empty(nbytes, dtype=np.uint8)
+        if nbytes:
+            raise_status(ctx.L.murr_memcpy_d2h(ctx.h, out.ctypes.data, ptr, nbytes), what="d2h")
+        return out
+    bm = int(ctx.L.murr_bitmap_bytes(n))
+    res = {"dtype": dtype, "length": n, "null_count": a.null_count,
+           "validity": d2h(a.validity, bm).tobytes() if a.null_count else None,
+           "validity_raw": d2h(a.validity, bm).tobytes() if n else b"",
+           "offsets": None}
+    if dtype == int(DTypeName.Utf8):
+        res["offsets"] = d2h(a.offsets, (n + 1) * 4).view(np.int32)
+        res["values"] = d2h(a.values, a.data_len).tobytes()
+    elif dtype == int(DTypeName.Bool):
+        res["values"] = d2h(a.values, bm).tobytes()
+    else:
+        res["values"] = d2h(a.values, a.data_len).tobytes()
+    return res
+
+
+def encode_batch(ctx: Context, segment: SegmentSchema, cols, n: int, blob_cap: int | None = None):
+    """murr_encode_batch over device-resident Arrow columns.
+
+    cols: per segment column dict {values: DeviceBuffer, validity: DeviceBuffer|None,
+    offsets: DeviceBuffer|None, offset: int, utf8_bytes: int}.
+    Returns (blob DeviceBuffer, row_off DeviceBuffer, blob_len)."""
+    cin = (_abi.ColIn * max(len(cols), 1))()
+    ub = (C.c_uint64 * max(len(cols), 1))()
+    for i, c in enumerate(cols):
+        cin[i].values = c["values"].ptr if c.get("values") is not None else None
+        cin[i].validity = c["validity"].ptr if c.get("validity") is not None else None
+        cin[i].offsets = c["offsets"].ptr if c.get("offsets") is not None else None
+        cin[i].offset = int(c.get("offset", 0))
+        ub[i] = int(c.get("utf8_bytes", 0))
+    if blob_cap is None:
+        blob_cap = int(ctx.L.murr_encode_bound(C.byref(segment.c), n, ub))
+    blob = ctx.alloc(max(blob_cap, 16))
+    row_off = ctx.alloc((n + 1) * 8)
+    blen = C.c_uint64()
+    err = _abi.Error()
+    st = ctx.L.murr_encode_batch(ctx.h, C.byref(segment.c), cin, n, blob.ptr, blob_cap, row_off.ptr,
+                                 C.byref(blen), C.byref(err))
+    raise_status(st, err, "murr_encode_batch")
+    return blob, row_off, blen.value

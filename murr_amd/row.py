@@ -1,0 +1,123 @@
+"""ReadBatchBuilder (src/io/row/read.rs:62-110), batched on the GPU.
+
+The store feeds rows exactly as in the reference (`add_row` / `add_empty` in
+caller order, src/io/store/memory.rs:38-43); rows are copied into a pinned host
+staging block by the C ABI, and `build()` runs H2D -> one decode launch -> D2H
+and returns a pyarrow RecordBatch whose fields are nullable and in request
+order (read.rs:100-109).
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+import pyarrow as pa
+
+from . import _abi
+from .errors import ArrowError, raise_status
+from .schema import DTypeName, SegmentColumnSchema, SegmentSchema
+
+_ctx = {}
+
+
+def default_context(device: int = 0):
+    from .device import Context
+    if device not in _ctx:
+        _ctx[device] = Context(device)
+    return _ctx[device]
+
+
+class ReadBatchBuilder:
+    def __init__(self, segment: SegmentSchema, columns, capacity: int, ctx=None):
+        """ReadBatchBuilder::new(segment, columns, capacity): one output column per
+        requested column, request order, duplicates allowed (read.rs:69-83)."""
+        self.segment = segment
+        self.columns = list(columns)
+        self.ctx = ctx or default_context()
+        self.L = self.ctx.L
+        proj = [c.index if isinstance(c, SegmentColumnSchema) else int(c) for c in self.columns]
+        self._proj = (C.c_uint32 * max(len(proj), 1))(*proj)
+        self._nproj = len(proj)
+        h = C.c_void_p()
+        raise_status(self.L.murr_builder_new(self.ctx.h, C.byref(segment.c), self._proj, self._nproj,
+                                             int(capacity), C.byref(h)), what="ReadBatchBuilder::new")
+        self.h = h
+
+    def __del__(self):
+        try:
+            if self.h:
+                self.L.murr_builder_free(self.h)
+                self.h = None
+        except Exception:
+            pass
+
+    def add_row(self, raw: bytes):
+        raise_status(self.L.murr_builder_add_row(self.h, raw, len(raw)), what="add_row")
+
+    def add_empty(self):
+        raise_status(self.L.murr_builder_add_empty(self.h), what="add_empty")
+
+    def add_rows(self, rows):
+        """Many rows at once; None = missing key."""
+        n = len(rows)
+        if not n:
+            return
+        keep = [r if r is not None else None for r in rows]
+        ptrs = (C.c_void_p * n)()
+        lens = (C.c_uint64 * n)()
+        bufs = []
+        for i, r in enumerate(keep):
+            if r is None:
+                ptrs[i] = None
+            else:
+                b = C.create_string_buffer(bytes(r), len(r))
+                bufs.append(b)
+                ptrs[i] = C.addressof(b)
+                lens[i] = len(r)
+        raise_status(self.L.murr_builder_add_rows(self.h, ptrs, lens, n), what="add_rows")
+
+    def build(self) -> pa.RecordBatch:
+        if self._nproj == 0:
+            raise ArrowError("Arrow error: must either specify a row count or at least one column")
+        outs = (_abi.HostArray * self._nproj)()
+        err = _abi.Error()
+        raise_status(self.L.murr_builder_build(self.h, outs, C.byref(err)), err, "ReadBatchBuilder::build")
+        arrays, fields = [], []
+        for p, col in enumerate(self.columns):
+            seg_col = col if isinstance(col, SegmentColumnSchema) else self.segment.columns[int(col)]
+            arrays.append(host_array_to_arrow(outs[p]))
+            fields.append(pa.field(seg_col.name, seg_col.dtype.arrow_dtype(), True))
+        return pa.RecordBatch.from_arrays(arrays, schema=pa.schema(fields))
+
+    def last_timing(self):
+        tot, h2d, k, d2h = C.c_double(), C.c_float(), C.c_float(), C.c_float()
+        self.L.murr_builder_last_timing(self.h, C.byref(tot), C.byref(h2d), C.byref(k), C.byref(d2h))
+        return {"total_ms": tot.value, "h2d_ms": h2d.value, "kernel_ms": k.value, "d2h_ms": d2h.value}
+
+
+def _copy(ptr, n) -> pa.Buffer:
+    return pa.py_buffer(C.string_at(ptr, n)) if n else pa.py_buffer(b"")
+
+
+def host_array_to_arrow(h) -> pa.Array:
+    """murr_host_array_t -> pyarrow Array (copies out of the builder's pinned memory)."""
+    n, dt = h.length, DTypeName(h.dtype)
+    validity = _copy(h.validity, (n + 7) // 8) if h.validity else None
+    if dt == DTypeName.Utf8:
+        offs = _copy(h.offsets, (n + 1) * 4)
+        data = _copy(h.values, h.values_len)
+        return pa.Array.from_buffers(pa.string(), n, [validity, offs, data], null_count=h.null_count)
+    vals = _copy(h.values, h.values_len)
+    return pa.Array.from_buffers(dt.arrow_dtype(), n, [validity, vals], null_count=h.null_count)
+
+
+def host_array_buffers(h) -> dict:
+    """murr_host_array_t -> raw buffer dict (for bit-exact parity checks)."""
+    n = h.length
+    out = {"dtype": h.dtype, "length": n, "null_count": h.null_count,
+           "validity": C.string_at(h.validity, (n + 7) // 8) if h.validity else None,
+           "values": C.string_at(h.values, h.values_len) if h.values_len else b"",
+           "offsets": None}
+    if h.dtype == int(DTypeName.Utf8):
+        out["offsets"] = np.frombuffer(C.string_at(h.offsets, (n + 1) * 4), dtype=np.int32).copy()
+    return out

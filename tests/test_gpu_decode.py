@@ -1,0 +1,166 @@
+"""HIP decode (murr_decode_blocks, through the C ABI) against the oracle and the
+golden fixtures: bit-exact Arrow buffers, first-error parity."""
+import numpy as np
+import pytest
+
+import oracle as O
+from golden_util import assert_array_equal, block_from_rows, expected_array, load_cases
+from randgen import ALL, drop_rows, random_columns
+from murr_amd import MurrError, SegmentError, synth
+from murr_amd.device import Context, DeviceBlock, decode_blocks, download_array
+from murr_amd.schema import DTypeName as D, SegmentSchema
+
+pytestmark = pytest.mark.gpu
+CASES = load_cases()
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    c = Context(0)
+    yield c
+    c.close()
+
+
+def seg_of(dtypes):
+    return SegmentSchema([(f"c{i}", D.parse(d)) for i, d in enumerate(dtypes)])
+
+
+def gpu_decode(ctx, seg, proj, blocks):
+    dblocks = [DeviceBlock.upload(ctx, d, o) for d, o in blocks]
+    outs = decode_blocks(ctx, seg, proj, dblocks)
+    res = []
+    for b, blk in enumerate(dblocks):
+        row = []
+        for p, ci in enumerate(proj):
+            row.append(download_array(ctx, outs.array(b, p), int(seg.columns[ci].dtype), blk.n_rows))
+        res.append(row)
+    return res
+
+
+def check_padding(got, n):
+    raw = got["validity_raw"]
+    nb = (n + 7) // 8
+    if n % 8 and got["validity"] is not None:
+        assert raw[nb - 1] >> (n % 8) == 0, "validity bits past n must be zero"
+    assert all(x == 0 for x in raw[nb:]), "validity padding must be zero"
+    if got["dtype"] == 1:
+        vals = got["values"]
+        if n % 8:
+            assert vals[nb - 1] >> (n % 8) == 0
+        assert all(x == 0 for x in vals[nb:])
+
+
+@pytest.mark.parametrize("case", CASES, ids=[c["name"] for c in CASES])
+def test_golden(ctx, case):
+    seg = seg_of(case["dtypes"])
+    data, row_off = block_from_rows(case["rows"])
+    if case["expect_error"]:
+        with pytest.raises(SegmentError, match="invalid utf8"):
+            gpu_decode(ctx, seg, case["proj"], [(data, row_off)])
+        return
+    got = gpu_decode(ctx, seg, case["proj"], [(data, row_off)])[0]
+    for p, e in enumerate(case["expected"]):
+        assert_array_equal(got[p], expected_array(e), f"{case['name']} col {p}")
+        check_padding(got[p], e["length"])
+
+
+def oracle_block(seg_dtypes, cols, n, missing=()):
+    oseg = O.Segment([int(d) for d in seg_dtypes])
+    data, off = O.encode_batch(oseg, synth.oracle_cols(cols), n)
+    if missing:
+        data, off = drop_rows(data, off, set(missing))
+    return oseg, data, off
+
+
+@pytest.mark.parametrize("seed,n", [(1, 1), (2, 63), (3, 64), (4, 65), (5, 255), (6, 256), (7, 257),
+                                    (8, 1000), (9, 4099), (10, 20000)])
+def test_random_all_dtypes_vs_oracle(ctx, seed, n):
+    rng = np.random.default_rng(seed)
+    dtypes = list(rng.choice(ALL, size=int(rng.integers(1, 20))))
+    dtypes = [D(int(d)) for d in dtypes]
+    cols = random_columns(rng, dtypes, n, null_p=float(rng.choice([0.0, 0.1, 0.5, 1.0])))
+    missing = set(rng.choice(n, size=n // 10, replace=False).tolist()) if n > 5 else set()
+    oseg, data, off = oracle_block(dtypes, cols, n, missing)
+    proj = list(rng.integers(0, len(dtypes), size=int(rng.integers(1, 2 * len(dtypes) + 1))))
+    seg = seg_of(dtypes)
+    got = gpu_decode(ctx, seg, proj, [(data, off)])[0]
+    want = O.decode_block(oseg, proj, data, off)
+    for p in range(len(proj)):
+        assert_array_equal(got[p], want[p], f"seed {seed} proj {p} ({dtypes[proj[p]].name})")
+        check_padding(got[p], n)
+
+
+def test_long_strings_take_the_hbm_path(ctx):
+    # tiles whose blob span exceeds the 32 KiB LDS stage read HBM directly
+    rng = np.random.default_rng(11)
+    dtypes = [D.Int32, D.Utf8, D.Float64, D.Utf8]
+    n = 700
+    cols = random_columns(rng, dtypes, n, null_p=0.2, long_every=37, long_len=50000)
+    oseg, data, off = oracle_block(dtypes, cols, n, missing={3, 100, 699})
+    proj = [1, 0, 3, 2, 1]
+    got = gpu_decode(ctx, seg_of(dtypes), proj, [(data, off)])[0]
+    want = O.decode_block(oseg, proj, data, off)
+    for p in range(len(proj)):
+        assert_array_equal(got[p], want[p], f"proj {p}")
+
+
+def test_multi_block_batch_with_empty_blocks(ctx):
+    rng = np.random.default_rng(12)
+    dtypes = [D.Float32, D.Utf8, D.Bool, D.UInt64]
+    blocks, wants = [], []
+    oseg = O.Segment([int(d) for d in dtypes])
+    for k, n in enumerate([1000, 0, 257, 1, 0, 3000, 64]):
+        cols = random_columns(rng, dtypes, n, null_p=0.1) if n else random_columns(rng, dtypes, 0)
+        _, data, off = oracle_block(dtypes, cols, n, missing={0} if n > 2 else set())
+        blocks.append((data, off))
+        wants.append(O.decode_block(oseg, [1, 0, 2, 3], data, off))
+    got = gpu_decode(ctx, seg_of(dtypes), [1, 0, 2, 3], blocks)
+    for b in range(len(blocks)):
+        for p in range(4):
+            assert_array_equal(got[b][p], wants[b][p], f"block {b} proj {p}")
+
+
+def test_all_rows_missing(ctx):
+    dtypes = [D.Utf8, D.Float32]
+    n = 300
+    data = np.zeros(0, np.uint8)
+    off = np.zeros(n + 1, np.uint64)
+    got = gpu_decode(ctx, seg_of(dtypes), [0, 1], [(data, off)])[0]
+    assert got[0]["null_count"] == n and got[1]["null_count"] == n
+    assert np.all(got[0]["offsets"] == 0)
+    assert got[1]["values"] == b"\0" * (4 * n)
+
+
+def test_first_invalid_utf8_error_is_row_major(ctx):
+    # ReadBatchBuilder stops at the first failing (row, encoder) pair (read.rs:85-91)
+    dtypes = [D.Utf8, D.Utf8]
+    n = 2000
+    rng = np.random.default_rng(13)
+    cols = random_columns(rng, dtypes, n, null_p=0.0, unicode=False)
+    oseg, data, off = oracle_block(dtypes, cols, n)
+    # corrupt the first non-empty cell at/after row 1500 col 1 and row 1700 col 0
+    data = data.copy()
+    lens = [np.diff(c["offsets"].astype(np.int64)) for c in cols]
+    for r0, c in ((1700, 0), (1500, 1)):
+        r = r0 + int(np.argmax(lens[c][r0:] > 0))
+        a = int(off[r])
+        slot = int.from_bytes(data[a + 1 + 4 * c: a + 5 + 4 * c].tobytes(), "little")
+        data[a + 1 + slot + 4] = 0xFF
+    with pytest.raises(O.OracleError) as oe:
+        O.decode_block(oseg, [0, 1], data, off)
+    with pytest.raises(SegmentError, match=r"row %d, column %d" % (oe.value.row, oe.value.column)):
+        gpu_decode(ctx, seg_of(dtypes), [0, 1], [(data, off)])
+
+
+def test_malformed_short_row_reports_instead_of_crashing(ctx):
+    dtypes = [D.Float64, D.Utf8]
+    data = np.frombuffer(bytes([0xFC, 1, 2, 3]), np.uint8).copy()  # far shorter than bs+cap
+    off = np.array([0, 4], np.uint64)
+    with pytest.raises(SegmentError, match="malformed"):
+        gpu_decode(ctx, seg_of(dtypes), [0], [(data, off)])
+
+
+def test_zero_projection_is_arrow_error(ctx):
+    from murr_amd import ArrowError
+    with pytest.raises(ArrowError):
+        gpu_decode(ctx, seg_of([D.Float32]), [], [(np.zeros(5, np.uint8), np.array([0, 5], np.uint64))])
