@@ -132,7 +132,7 @@ def cpu_baseline(seg, proj, host_blob, host_off, rows, target_s):
     one = time.perf_counter() - t
     out_bytes = arrow_out_bytes(seg, proj, rows, [r["null_count"] for r in res],
                                 [len(r["values"]) if r["dtype"] == 0 else 0 for r in res])
-    reps = int(max(1, min(1000, target_s / max(one, 1e-6))))
+    reps = int(max(1, min(100000, target_s / max(one, 1e-6))))
     t = time.perf_counter()
     for _ in range(reps):
         O.decode_block(oseg, proj, host_blob, host_off)
@@ -149,7 +149,7 @@ def run_decode(args, dist, rank, world, local_rank):
     cols = make_columns(args.config, rows, start=rank * rows)
     dtypes = [c["dtype"] for c in cols]
     seg = SegmentSchema([(f"c{i}", d) for i, d in enumerate(dtypes)])
-    proj = list(range(len(cols)))
+    proj = list(range(len(cols))) if args.proj is None else [int(x) for x in args.proj.split(",")]
     # One block's row blobs, produced by the device encoder, then K resident copies.
     dblob, doff, blen = encode_batch(ctx, seg, synth.upload_columns(ctx, cols), rows)
     host_blob = dblob.download(blen)
@@ -160,6 +160,7 @@ def run_decode(args, dist, rank, world, local_rank):
     cb = (_abi.Block * K)()
     for i, b in enumerate(blocks):
         cb[i].data, cb[i].row_off, cb[i].n_rows = b.data.ptr, b.row_off.ptr, b.n_rows
+        cb[i].data_bytes = b.data_bytes
     pj = (C.c_uint32 * len(proj))(*proj)
     err = _abi.Error()
     L = ctx.L
@@ -291,6 +292,7 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--pmc-csv", default=None)
+    ap.add_argument("--proj", default=None, help="comma-separated projected columns (default all)")
     args = ap.parse_args()
     if args.rows is None:
         args.rows = {"B": 100_000, "C": 1_000_000, "D": 1_250_000, "E": 20_000_000}[args.config]

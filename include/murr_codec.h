@@ -146,6 +146,8 @@ typedef struct {
     const uint8_t*  data;
     const uint64_t* row_off;   /* n_rows + 1 entries, row_off[0] may be > 0 */
     uint64_t        n_rows;
+    uint64_t        data_bytes; /* optional: row_off[n] - row_off[0] (0 = unknown);
+                                   sizes the tiles, never read past */
 } murr_block_t;
 
 /* One output Arrow array (device pointers), arrow-rs 58 builder layout:

@@ -34,7 +34,8 @@ class Error(C.Structure):
 
 
 class Block(C.Structure):
-    _fields_ = [("data", C.c_void_p), ("row_off", C.c_void_p), ("n_rows", C.c_uint64)]
+    _fields_ = [("data", C.c_void_p), ("row_off", C.c_void_p), ("n_rows", C.c_uint64),
+                ("data_bytes", C.c_uint64)]
 
 
 class Array(C.Structure):

@@ -55,7 +55,7 @@ bool valid_segment(const murr_segment_t* s) {
 struct murr_ctx {
     int device = 0;
     int cus = 256;
-    int dec_grid_per_cu = 1, enc_grid_per_cu = 1;
+    int enc_grid_per_cu = 1;
     hipStream_t stream = nullptr;
     hipEvent_t k0 = nullptr, k1 = nullptr;
     bool timed = false;
@@ -185,7 +185,6 @@ int murr_ctx_create(int device, murr_ctx_t** out) {
     c->cus = prop.multiProcessorCount;
     // Persistent grid: blocks that are certainly co-resident (one below the
     // occupancy answer: MI355X_MICROARCH.md "Residency"), at least one per CU.
-    c->dec_grid_per_cu = std::max(1, std::min(8, decode_blocks_per_cu()) - 1);
     c->enc_grid_per_cu = std::max(1, std::min(8, encode_blocks_per_cu()) - 1);
     HIPC(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     HIPC(hipEventCreate(&c->k0));
@@ -303,6 +302,29 @@ int murr_decode_enqueue(murr_ctx_t* c, const murr_segment_t* seg, const uint32_t
         dp[p] = DecProj{col.dtype, col.index, col.offset, col.size, col.dtype == MURR_UTF8, 0};
         if (col.dtype == MURR_UTF8) dp[p].uslot = nutf8++;
     }
+    // Tile shape: as many rows per thread (1..8) as keep a tile's blob bytes
+    // inside the LDS stage, from the data_bytes hints (or a schema estimate).
+    uint64_t hint_bytes = 0, hint_rows = 0, all_rows = 0;
+    bool hinted = true;
+    for (uint32_t b = 0; b < nblocks; b++) {
+        all_rows += blocks[b].n_rows;
+        if (blocks[b].n_rows && !blocks[b].data_bytes) hinted = false;
+        hint_bytes += blocks[b].data_bytes;
+        hint_rows += blocks[b].n_rows;
+    }
+    double est_row = (double)seg->bitset_size + seg->capacity;
+    for (uint32_t i = 0; i < seg->ncols; i++) est_row += seg->cols[i].dtype == MURR_UTF8 ? 20.0 : 0.0;
+    if (hinted && hint_rows) est_row = (double)hint_bytes / (double)hint_rows;
+    uint32_t stage = kDecStage;
+    int rpt = 8;
+    while (rpt > 1 && 256.0 * rpt * est_row * 1.15 > stage) rpt /= 2;
+    if (rpt == 1 && 256.0 * est_row * 1.15 > stage)
+        stage = (uint32_t)std::min<double>(65536.0, round_up((uint64_t)(256.0 * est_row * 1.2), 1024));
+    else  // no bigger than the tile needs (+25 % for row-size variance): more workgroups per CU
+        stage = std::min<uint32_t>(stage, std::max<uint32_t>(8192, (uint32_t)round_up(
+                    (uint64_t)(256.0 * rpt * est_row * 1.25), 1024)));
+    const uint32_t lds = decode_lds_bytes(stage, nproj, rpt);
+    const uint64_t R = (uint64_t)kTile * rpt;
     std::vector<DecBlock> db(nblocks);
     uint64_t tiles = 0;
     for (uint32_t b = 0; b < nblocks; b++) {
@@ -310,7 +332,7 @@ int murr_decode_enqueue(murr_ctx_t* c, const murr_segment_t* seg, const uint32_t
         if (bl.n_rows && (!bl.data || !bl.row_off || ((uintptr_t)bl.data & 15)))
             return MURR_E_ARGUMENT;
         db[b] = DecBlock{bl.data, bl.row_off, bl.n_rows, tiles};
-        tiles += (bl.n_rows + kTile - 1) / kTile;
+        tiles += (bl.n_rows + R - 1) / R;
         for (uint32_t p = 0; p < nproj; p++) {
             const murr_array_t& o = outs[(uint64_t)b * nproj + p];
             if (bl.n_rows && (!o.validity || !o.values || (dp[p].is_utf8 && !o.offsets)))
@@ -330,11 +352,17 @@ int murr_decode_enqueue(murr_ctx_t* c, const murr_segment_t* seg, const uint32_t
     const uint64_t zbytes = round_up(z_lb + 8 * (uint64_t)nutf8 * tiles, 16);
     const uint64_t d_blocks = zbytes, d_proj = round_up(d_blocks + sizeof(DecBlock) * nblocks, 16);
     const uint64_t d_outs = round_up(d_proj + sizeof(DecProj) * nproj, 16);
-    const uint64_t dend = round_up(d_outs + sizeof(DecOut) * dout.size(), 16);
+    // Persistent grid: workgroups that are certainly co-resident (the occupancy
+    // answer, one fewer when it is >= 4: MI355X_MICROARCH.md "Residency").
+    int bpc = decode_blocks_per_cu(rpt, lds);
+    bpc = std::max(1, bpc >= 4 ? std::min(bpc, 8) - 1 : bpc);
+    const uint64_t grid = std::min<uint64_t>(std::max<uint64_t>(tiles, 1), (uint64_t)c->cus * bpc);
+    const uint64_t d_prev = round_up(d_outs + sizeof(DecOut) * dout.size(), 16);
+    const uint64_t dend = round_up(d_prev + 8 * grid * nutf8, 16);
     int st = ensure_ws(c, dend, err);
     if (st) return st;
     // host scratch: [descriptors (dend - zbytes)] [readback z_lb bytes]
-    const uint64_t hdesc = dend - zbytes, rb = round_up(hdesc, 64);
+    const uint64_t hdesc = d_prev - zbytes, rb = round_up(dend - zbytes, 64);
     st = ensure_hs(c, rb + z_lb, err);
     if (st) return st;
     std::memcpy(c->hs + (d_blocks - zbytes), db.data(), sizeof(DecBlock) * nblocks);
@@ -355,6 +383,7 @@ int murr_decode_enqueue(murr_ctx_t* c, const murr_segment_t* seg, const uint32_t
     a.proj = (const DecProj*)(c->ws + d_proj);
     a.outs = (const DecOut*)(c->ws + d_outs);
     a.lookback = (uint64_t*)(c->ws + z_lb);
+    a.prev = (uint64_t*)(c->ws + d_prev);
     a.nulls = (unsigned long long*)(c->ws + z_nulls);
     a.lens = (unsigned long long*)(c->ws + z_lens);
     a.err = (unsigned long long*)(c->ws + z_err);
@@ -364,11 +393,9 @@ int murr_decode_enqueue(murr_ctx_t* c, const murr_segment_t* seg, const uint32_t
     a.nutf8 = nutf8;
     a.bs = seg->bitset_size;
     a.cap = seg->capacity;
+    a.stage = stage;
     HIPC(hipEventRecord(c->k0, c->stream));
-    if (tiles) {
-        uint64_t grid = std::min<uint64_t>(tiles, (uint64_t)c->cus * c->dec_grid_per_cu);
-        HIPC(launch_decode(a, (uint32_t)grid, c->stream));
-    }
+    if (tiles) HIPC(launch_decode(a, rpt, (uint32_t)grid, c->stream));
     HIPC(hipEventRecord(c->k1, c->stream));
     c->timed = true;
     HIPC(hipMemcpyAsync(c->hs + rb, c->ws, z_lb, hipMemcpyDeviceToHost, c->stream));
@@ -673,7 +700,7 @@ int murr_builder_build(murr_builder_t* b, murr_host_array_t* outs, murr_error_t*
     if (b->hdata_len) HIPC(hipMemcpyAsync(ddata, b->hdata, b->hdata_len, hipMemcpyHostToDevice, c->stream));
     HIPC(hipMemcpyAsync(doff, b->hoff, obytes, hipMemcpyHostToDevice, c->stream));
     HIPC(hipEventRecord(b->e1, c->stream));
-    murr_block_t blk{ddata, doff, n};
+    murr_block_t blk{ddata, doff, n, b->hdata_len};
     b->arr.assign(np, murr_array_t{});
     for (uint64_t p = 0; p < np; p++) {
         const murr_column_t& col = b->cols[b->proj[p]];

@@ -6,18 +6,16 @@
 
 namespace murr {
 
-// Rows per tile = threads per workgroup (thread-per-row), 4 waves.
+// Threads per workgroup (4 waves); a decode tile is kTile * RPT rows.
 constexpr uint32_t kTile = 256;
-// Bytes of row blobs / assembled rows a tile stages through LDS.  Tiles whose
-// byte span exceeds this read / write HBM directly (the "global" path).
+// Bytes of assembled rows an encode tile stages through LDS.  Tiles whose
+// byte span exceeds the stage read / write HBM directly (the "global" path).
 constexpr uint32_t kStage = 32768;
+// Default decode stage (bytes of row blobs per tile held in LDS).
+constexpr uint32_t kDecStage = 36864;
 // Projected columns per decode call (10 bits in the packed error key).
 constexpr uint32_t kMaxProj = 1024;
 
-// Decoupled look-back granule: [63:62] flag, [61:0] value.
-constexpr uint64_t kFlagA = 1ull << 62;  // tile aggregate published
-constexpr uint64_t kFlagP = 2ull << 62;  // tile inclusive prefix published
-constexpr uint64_t kValMask = (1ull << 62) - 1;
 
 struct DecBlock {             // one block (batch read) of row blobs
     const uint8_t* data;
@@ -42,12 +40,13 @@ struct DecodeArgs {
     const DecBlock* blocks;
     const DecProj* proj;
     const DecOut* outs;          // [nblocks * nproj]
-    uint64_t* lookback;          // [nutf8 * total_tiles]
+    uint64_t* lookback;          // [nutf8 * total_tiles] tile aggregates + 1
+    uint64_t* prev;              // [grid * nutf8] each workgroup's last inclusive prefix
     unsigned long long* nulls;   // [nblocks * nproj]
     unsigned long long* lens;    // [nblocks * nproj] utf8 data bytes
     unsigned long long* err;     // max of ~key (0 = no error)
     uint64_t total_tiles;
-    uint32_t nblocks, nproj, nutf8, bs, cap, _pad;
+    uint32_t nblocks, nproj, nutf8, bs, cap, stage;
 };
 
 struct EncCol {               // one Arrow input column, segment order
@@ -77,9 +76,10 @@ __host__ __device__ inline uint64_t err_key(uint64_t block, uint64_t row, uint32
     return (block << 46) | (row << 14) | ((uint64_t)(col & 0x3FF) << 4) | (status & 0xF);
 }
 
-hipError_t launch_decode(const DecodeArgs& a, uint32_t grid, hipStream_t s);
+uint32_t decode_lds_bytes(uint32_t stage, uint32_t nproj, int rpt);
+hipError_t launch_decode(const DecodeArgs& a, int rpt, uint32_t grid, hipStream_t s);
 hipError_t launch_encode(const EncodeArgs& a, uint32_t grid, hipStream_t s);
-int decode_blocks_per_cu();
+int decode_blocks_per_cu(int rpt, uint32_t lds);
 int encode_blocks_per_cu();
 
 }  // namespace murr

@@ -17,10 +17,9 @@
 // Validity and bool bitmaps come straight out of __ballot: one 64-bit word per
 // wave.  UTF-8 offsets (decode) and row offsets (encode) need a prefix sum
 // across tiles: a wave-level shuffle scan, an LDS combine across the 4 waves,
-// and a decoupled look-back across tiles (granule = {flag, value} in one
-// 8-byte agent-scope store; MI355X_MICROARCH.md R2 hand-off form).  Tiles are
+// and a one-hop window sum across tiles (see window_prefix).  Tiles are
 // assigned round-robin to a persistent grid that fits on the chip at once, so
-// every tile a look-back waits on is resident or finished.
+// every tile a prefix waits on is resident or finished.
 #include "murr_internal.h"
 
 namespace murr {
@@ -52,16 +51,16 @@ struct LdsSrc {
 };
 
 struct GlbSrc {
-    const uint8_t* g;  // HBM; never reads a dword that holds no requested byte
-    __device__ __forceinline__ uint32_t u32(uint64_t a) const {
-        const uint32_t* w = reinterpret_cast<const uint32_t*>(g + (a & ~3ull));
-        uint32_t sh = a & 3u;
+    const uint8_t* g;  // HBM (16-B aligned); never reads a dword holding no requested byte
+    __device__ __forceinline__ uint32_t u32(uint32_t a) const {
+        const uint32_t* w = reinterpret_cast<const uint32_t*>(g + (a & ~3u));
+        const uint32_t sh = a & 3u;
         return sh ? __builtin_amdgcn_alignbyte(w[1], w[0], sh) : w[0];
     }
-    __device__ __forceinline__ uint64_t u64(uint64_t a) const {
+    __device__ __forceinline__ uint64_t u64(uint32_t a) const {
         return (uint64_t)u32(a) | ((uint64_t)u32(a + 4) << 32);
     }
-    __device__ __forceinline__ uint32_t u8(uint64_t a) const { return g[a]; }
+    __device__ __forceinline__ uint32_t u8(uint32_t a) const { return g[a]; }
 };
 
 // Read W (1,2,4,8) little-endian bytes at a.
@@ -114,39 +113,38 @@ __device__ __forceinline__ uint64_t block_incl_scan(uint64_t x, uint64_t* s_w, u
     return pre + inc;
 }
 
-// Decoupled look-back by one wave: exclusive prefix of tile t among tiles
-// [tfirst, t).  Predecessor granules are polled with agent-scope relaxed loads
-// (sc1: bypass this CU's L1); bounded spin -> kStInternal.
-__device__ uint64_t lookback(uint64_t* st, uint64_t t, uint64_t tfirst, unsigned long long* err,
-                             uint64_t ekey_base) {
-    const uint32_t lane = threadIdx.x & 63;
-    uint64_t prefix = 0;
-    int64_t wend = (int64_t)t;
-    for (;;) {
-        int64_t j = wend - 1 - (int64_t)lane;
-        uint64_t v = kFlagP;  // before the block's first tile: inclusive prefix 0
-        if (j >= (int64_t)tfirst) {
+// Cross-tile prefix by a one-hop window sum.  Tiles are dealt round-robin to
+// a persistent grid of G workgroups, so tile t's workgroup processed tile t-G
+// itself and kept its inclusive prefix (`base`).  What lies between is the
+// aggregate of tiles (t-G, t): each tile publishes its aggregate (+1, so 0 =
+// not yet) in one 8-byte agent-scope store right after its length scan, and
+// the whole workgroup sums the <= G-1 granules in parallel (agent-scope relaxed
+// loads = sc1: bypass this CU's L1; MI355X_MICROARCH.md R2 hand-off form).
+// Only tiles that are resident or done are ever waited on; spins are bounded.
+__device__ uint64_t window_prefix(const uint64_t* st, uint64_t lo, uint64_t t, uint64_t base,
+                                  uint64_t* s_w, unsigned long long* err, uint64_t ekey) {
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    uint64_t sum = 0;
+    for (uint64_t j = lo + tid; j < t; j += 256) {
+        uint64_t v = __hip_atomic_load(st + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        uint32_t spins = 0;
+        while (v == 0) {
+            __builtin_amdgcn_s_sleep(2);
             v = __hip_atomic_load(st + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            uint32_t spins = 0;
-            while ((v >> 62) == 0) {
-                __builtin_amdgcn_s_sleep(2);
-                v = __hip_atomic_load(st + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (++spins > kSpinLimit) {
-                    report(err, ekey_base | kStInternal);
-                    v = kFlagP;
-                    break;
-                }
+            if (++spins > kSpinLimit) {
+                report(err, ekey | kStInternal);
+                v = 1;
+                break;
             }
         }
-        uint64_t pmask = __ballot((v >> 62) == 2);
-        uint64_t val = v & kValMask;
-        if (pmask) {
-            uint32_t k = __builtin_ctzll(pmask);
-            return prefix + wave_sum(lane <= k ? val : 0);
-        }
-        prefix += wave_sum(val);
-        wend -= 64;
+        sum += v - 1;
     }
+    sum = wave_sum(sum);
+    if (lane == 0) s_w[wave] = sum;
+    __syncthreads();
+    const uint64_t tot = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+    __syncthreads();
+    return base + tot;
 }
 
 __device__ __forceinline__ void publish(uint64_t* p, uint64_t v) {
@@ -176,156 +174,218 @@ struct Utf8Dfa {
     __device__ __forceinline__ bool ok() const { return !bad && need == 0; }
 };
 
-// ---- decode: one tile ---------------------------------------------------------
-template <class Src, class Addr>
-__device__ __forceinline__ void decode_tile_rows(
-    const DecodeArgs& A, const Src& src, uint32_t b, uint64_t t, uint64_t tfirst, uint64_t r0,
-    uint32_t nr, bool last_tile, Addr ra, uint64_t rowlen, uint32_t* s_nulls, uint64_t* s_w,
-    uint64_t* s_prefix) {
+// ---- decode -------------------------------------------------------------------
+// A tile is R = 256*RPT rows; thread tid owns rows r0 + k*256 + tid (k < RPT),
+// so every (k, wave) pair covers 64 consecutive rows: coalesced row_off loads
+// and value stores, and one ballot = one 64-bit bitmap word.  Row addresses are
+// u32 offsets from the tile's 16-B aligned blob start, in LDS or in HBM.
+struct DecTile {
+    uint32_t b;         // block
+    uint64_t t, tfirst; // global tile, first tile of the block
+    uint64_t r0;        // first row of the tile inside the block
+    uint32_t nr;        // rows in the tile
+    bool last;          // last tile of the block
+};
+
+template <int RPT, class Src>
+__device__ __forceinline__ void decode_tile(const DecodeArgs& A, const Src& src, const DecTile& T,
+                                            const uint32_t (&ra)[RPT], const uint32_t (&rl)[RPT],
+                                            uint32_t* s_nulls, uint64_t* s_tot, uint64_t* s_w) {
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const bool active = tid < nr;
-    const uint64_t row = r0 + tid;
-    const bool present = active && rowlen > 0;
     const uint32_t bs = A.bs;
-    const bool short_row = present && rowlen < bs;  // ReadRow::new split_at panics
-    if (short_row) report(A.err, err_key(b, row, 0, kStMalformed));
-    const bool rowok = present && !short_row;
-    // Null bitset (bit = 1 -> NULL); bs <= 8 covers 64 columns in one register.
-    uint64_t bits = ~0ull;
-    if (rowok && bs <= 8) {
-        bits = 0;
-        for (uint32_t k = 0; k < bs; k++) bits |= (uint64_t)src.u8(ra + k) << (8 * k);
+    const uint64_t nproj = A.nproj;
+    // Null bitsets of my rows (bit = 1 -> NULL), cached when bs <= 4.
+    uint32_t bits[RPT];
+    uint32_t okm = 0, actm = 0;  // bit k: row k present & well formed / row k in tile
+#pragma unroll
+    for (int k = 0; k < RPT; k++) {
+        const bool act = k * 256 + tid < T.nr;
+        const bool present = act && rl[k] > 0;
+        const bool short_row = present && rl[k] < bs;  // ReadRow::new split_at panics
+        if (short_row) report(A.err, err_key(T.b, T.r0 + k * 256 + tid, 0, kStMalformed));
+        actm |= (uint32_t)act << k;
+        okm |= (uint32_t)(present && !short_row) << k;
+        bits[k] = ~0u;
+        if (present && !short_row && bs <= 4) {
+            bits[k] = 0;
+            for (uint32_t j = 0; j < bs; j++) bits[k] |= src.u8(ra[k] + j) << (8 * j);
+        }
     }
-    const bool wave_live = wave * 64 < nr;
-    const uint64_t wword = (r0 >> 6) + wave;  // 64-row bitmap word of this wave
 
     for (uint32_t p = 0; p < A.nproj; p++) {
         const DecProj pc = A.proj[p];
-        const DecOut o = A.outs[(uint64_t)b * A.nproj + p];
-        bool isnull = true;
-        if (rowok) {
-            uint32_t byte = pc.bit >> 3;
-            uint32_t bv = (bs <= 8) ? (uint32_t)(bits >> (8 * byte)) : src.u8(ra + byte);
-            isnull = (bv >> (pc.bit & 7)) & 1;
+        const DecOut o = A.outs[(uint64_t)T.b * nproj + p];
+        const uint32_t fo = bs + pc.offset;
+        uint32_t nullm = 0, nnull = 0;
+#pragma unroll
+        for (int k = 0; k < RPT; k++) {
+            bool isnull = true;
+            if ((okm >> k) & 1) {
+                const uint32_t byte = pc.bit >> 3;
+                const uint32_t bv = (bs <= 4) ? (bits[k] >> (8 * byte)) : src.u8(ra[k] + byte);
+                isnull = (bv >> (pc.bit & 7)) & 1;
+            }
+            const bool act = (actm >> k) & 1;
+            nullm |= (uint32_t)isnull << k;
+            const uint64_t vm = __ballot(act && !isnull);
+            nnull += __popcll(__ballot(act && isnull));
+            if (lane == 0 && k * 256 + wave * 64 < T.nr)
+                reinterpret_cast<uint64_t*>(o.validity)[((T.r0 + k * 256) >> 6) + wave] = vm;
         }
-        const uint64_t valid_mask = __ballot(active && !isnull);
-        const uint32_t nnull = __popcll(__ballot(active && isnull));
         if (lane == 0 && nnull) atomicAdd(&s_nulls[p], nnull);
-        if (lane == 0 && wave_live) reinterpret_cast<uint64_t*>(o.validity)[wword] = valid_mask;
-        const uint64_t fo = (uint64_t)bs + pc.offset;  // field offset within the row
 
         if (!pc.is_utf8) {
-            bool fnull = isnull;
-            if (!isnull && fo + pc.width > rowlen) {
-                report(A.err, err_key(b, row, p, kStMalformed));
-                fnull = true;
-            }
-            if (pc.dtype == kBool) {
-                bool v = !fnull && src.u8(ra + fo) != 0;
-                uint64_t m = __ballot(active && v);
-                if (lane == 0 && wave_live) reinterpret_cast<uint64_t*>(o.values)[wword] = m;
-            } else if (active) {
-                uint64_t v = fnull ? 0 : read_w(src, ra + fo, pc.width);
-                uint8_t* dst = o.values + row * pc.width;
-                switch (pc.width) {
-                case 8: *reinterpret_cast<uint64_t*>(dst) = v; break;
-                case 4: *reinterpret_cast<uint32_t*>(dst) = (uint32_t)v; break;
-                case 2: *reinterpret_cast<uint16_t*>(dst) = (uint16_t)v; break;
-                default: *dst = (uint8_t)v; break;
+#pragma unroll
+            for (int k = 0; k < RPT; k++) {
+                const uint64_t row = T.r0 + k * 256 + tid;
+                const bool act = (actm >> k) & 1;
+                bool fnull = (nullm >> k) & 1;
+                if (!fnull && fo + pc.width > rl[k]) {
+                    report(A.err, err_key(T.b, row, p, kStMalformed));
+                    fnull = true;
+                }
+                if (pc.dtype == kBool) {
+                    const bool v = !fnull && src.u8(ra[k] + fo) != 0;
+                    const uint64_t m = __ballot(act && v);
+                    if (lane == 0 && k * 256 + wave * 64 < T.nr)
+                        reinterpret_cast<uint64_t*>(o.values)[((T.r0 + k * 256) >> 6) + wave] = m;
+                } else if (act) {
+                    const uint64_t v = fnull ? 0 : read_w(src, ra[k] + fo, pc.width);
+                    uint8_t* dst = o.values + row * pc.width;
+                    switch (pc.width) {
+                    case 8: *reinterpret_cast<uint64_t*>(dst) = v; break;
+                    case 4: *reinterpret_cast<uint32_t*>(dst) = (uint32_t)v; break;
+                    case 2: *reinterpret_cast<uint16_t*>(dst) = (uint16_t)v; break;
+                    default: *dst = (uint8_t)v; break;
+                    }
                 }
             }
             continue;
         }
 
-        // ---- utf8: read_dynamic (read.rs:45-55) -> length, scan, copy + validate
-        uint32_t slen = 0;
-        Addr pay = 0;
-        if (!isnull) {
-            const uint64_t vlen = rowlen - bs;  // static + payload region
-            if (fo + 4 > rowlen) {
-                report(A.err, err_key(b, row, p, kStMalformed));
-            } else {
-                uint32_t prel = src.u32(ra + fo);
-                if ((uint64_t)prel + 4 > vlen) {
-                    report(A.err, err_key(b, row, p, kStMalformed));
+        // ---- utf8: read_dynamic (read.rs:45-55) -> lengths, tile scan, window
+        //      prefix across tiles, offsets, copy + validate (utf8.rs:86-96)
+        uint32_t slen[RPT], pay[RPT];
+#pragma unroll
+        for (int k = 0; k < RPT; k++) {
+            slen[k] = 0;
+            pay[k] = 0;
+            if (!((nullm >> k) & 1)) {
+                const uint64_t row = T.r0 + k * 256 + tid;
+                const uint32_t vlen = rl[k] - bs;  // static + payload region
+                if (fo + 4 > rl[k]) {
+                    report(A.err, err_key(T.b, row, p, kStMalformed));
                 } else {
-                    uint32_t l = src.u32(ra + bs + prel);
-                    if ((uint64_t)prel + 4 + l > vlen) report(A.err, err_key(b, row, p, kStMalformed));
-                    else { slen = l; pay = ra + bs + prel + 4; }
+                    const uint32_t prel = src.u32(ra[k] + fo);
+                    if ((uint64_t)prel + 4 > vlen) {
+                        report(A.err, err_key(T.b, row, p, kStMalformed));
+                    } else {
+                        const uint32_t l = src.u32(ra[k] + bs + prel);
+                        if ((uint64_t)prel + 4 + l > vlen) report(A.err, err_key(T.b, row, p, kStMalformed));
+                        else { slen[k] = l; pay[k] = ra[k] + bs + prel + 4; }
+                    }
                 }
             }
+            const uint64_t inc = wave_incl_scan(slen[k], lane);
+            if (lane == 63) s_tot[k * 4 + wave] = inc;
         }
-        uint64_t agg;
-        const uint64_t incl = block_incl_scan(slen, s_w, &agg);
+        __syncthreads();
+        // exclusive prefix of each (k, wave) total, k-major (read after the
+        // barriers inside window_prefix)
+        uint64_t* s_pre = s_tot + 4 * RPT;
+        if (tid < 4 * RPT) {
+            uint64_t run = 0;
+            for (uint32_t j = 0; j < tid; j++) run += s_tot[j];
+            s_pre[tid] = run;
+        }
+        uint64_t agg = 0;
+#pragma unroll
+        for (int j = 0; j < 4 * RPT; j++) agg += s_tot[j];
         uint64_t* st = A.lookback + (uint64_t)pc.uslot * A.total_tiles;
-        if (wave == 0) {
-            uint64_t prefix = 0;
-            if (t == tfirst) {
-                if (lane == 0) publish(st + t, kFlagP | (agg & kValMask));
-            } else {
-                if (lane == 0) publish(st + t, kFlagA | (agg & kValMask));
-                prefix = lookback(st, t, tfirst, A.err, err_key(b, r0, p, 0));
-                if (lane == 0) publish(st + t, kFlagP | ((prefix + agg) & kValMask));
+        if (tid == 0) publish(st + T.t, agg + 1);
+        // this workgroup's own inclusive prefix of tile t - G (same block) or 0
+        uint64_t* mine = A.prev + (uint64_t)blockIdx.x * A.nutf8 + pc.uslot;
+        const uint64_t G = gridDim.x;
+        const bool have_prev = T.t >= T.tfirst + G;
+        const uint64_t lo = have_prev ? T.t - G + 1 : T.tfirst;
+        const uint64_t prefix = window_prefix(st, lo, T.t, have_prev ? *mine : 0, s_w, A.err,
+                                              err_key(T.b, T.r0, p, 0));
+        if (tid == 0) {
+            *mine = prefix + agg;
+            if (T.t == T.tfirst) o.offsets[0] = 0;
+            if (T.last) A.lens[(uint64_t)T.b * nproj + p] = prefix + agg;
+        }
+#pragma unroll
+        for (int k = 0; k < RPT; k++) {
+            const uint64_t inc = wave_incl_scan(slen[k], lane);
+            if (!((actm >> k) & 1)) continue;
+            const uint64_t row = T.r0 + k * 256 + tid;
+            const uint64_t end = prefix + s_pre[k * 4 + wave] + inc;
+            if (end > 0x7FFFFFFFull) {
+                report(A.err, err_key(T.b, row, p, kStOverflow));
+                continue;
             }
-            if (lane == 0) *s_prefix = prefix;
+            o.offsets[row + 1] = (int32_t)end;
+            if (slen[k] == 0) continue;
+            if (end > o.values_cap) {
+                report(A.err, err_key(T.b, row, p, kStCapacity));
+                continue;
+            }
+            uint8_t* dst = o.values + (end - slen[k]);
+            Utf8Dfa dfa;
+            for (uint32_t j = 0; j < slen[k]; j++) {
+                const uint32_t c = src.u8(pay[k] + j);
+                dst[j] = (uint8_t)c;
+                dfa.step(c);
+            }
+            if (!dfa.ok()) report(A.err, err_key(T.b, row, p, kStUtf8));
         }
-        __syncthreads();
-        const uint64_t prefix = *s_prefix;
-        __syncthreads();
-        if (tid == 0 && t == tfirst) o.offsets[0] = 0;
-        if (tid == 0 && last_tile) A.lens[(uint64_t)b * A.nproj + p] = prefix + agg;
-        if (!active) continue;
-        const uint64_t end = prefix + incl;
-        if (end > 0x7FFFFFFFull) {
-            report(A.err, err_key(b, row, p, kStOverflow));
-            continue;
-        }
-        o.offsets[row + 1] = (int32_t)end;
-        if (slen == 0) continue;
-        const uint64_t start = end - slen;
-        if (end > o.values_cap) {
-            report(A.err, err_key(b, row, p, kStCapacity));
-            continue;
-        }
-        uint8_t* dst = o.values + start;
-        Utf8Dfa dfa;
-        for (uint32_t k = 0; k < slen; k++) {
-            uint32_t c = src.u8(pay + k);
-            dst[k] = (uint8_t)c;
-            dfa.step(c);
-        }
-        if (!dfa.ok()) report(A.err, err_key(b, row, p, kStUtf8));
+        __syncthreads();  // s_tot / s_pre reused by the next utf8 column
     }
 }
 
+// LDS layout (dynamic): [stage: A.stage + 32][s_nulls: nproj u32][s_tot, s_pre: 4*RPT u64 each][s_w: 4 u64]
+template <int RPT>
 __global__ void __launch_bounds__(256) decode_kernel(DecodeArgs A) {
-    __shared__ __attribute__((aligned(16))) uint8_t stage[kStage + 32];
-    __shared__ uint32_t s_nulls[kMaxProj];
-    __shared__ uint64_t s_w[4];
-    __shared__ uint64_t s_prefix;
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    uint8_t* stage = lds;
+    uint32_t* s_nulls = reinterpret_cast<uint32_t*>(lds + A.stage + 32);
+    uint64_t* s_tot = reinterpret_cast<uint64_t*>(lds + A.stage + 32 + ((4 * A.nproj + 15) & ~15u));
+    uint64_t* s_w = s_tot + 8 * RPT;
+    constexpr uint32_t R = 256 * RPT;
     const uint32_t tid = threadIdx.x;
+    uint32_t b = 0;  // this workgroup visits tiles in increasing order
 
     for (uint64_t t = blockIdx.x; t < A.total_tiles; t += gridDim.x) {
-        // Block of this tile: last block with tile_base <= t (wave-uniform).
-        uint32_t lo = 0, hi = A.nblocks;
-        while (hi - lo > 1) {
-            uint32_t mid = (lo + hi) >> 1;
-            if (A.blocks[mid].tile_base <= t) lo = mid; else hi = mid;
-        }
-        const uint32_t b = lo;
+        while (b + 1 < A.nblocks && A.blocks[b + 1].tile_base <= t) b++;
         const DecBlock blk = A.blocks[b];
-        const uint64_t tfirst = blk.tile_base;
-        const uint64_t r0 = (t - tfirst) * kTile;
-        const uint32_t nr = (uint32_t)min((uint64_t)kTile, blk.n_rows - r0);
-        const bool last_tile = r0 + nr == blk.n_rows;
+        DecTile T;
+        T.b = b;
+        T.t = t;
+        T.tfirst = blk.tile_base;
+        T.r0 = (t - blk.tile_base) * R;
+        T.nr = (uint32_t)min((uint64_t)R, blk.n_rows - T.r0);
+        T.last = T.r0 + T.nr == blk.n_rows;
         for (uint32_t p = tid; p < A.nproj; p += 256) s_nulls[p] = 0;
 
-        const bool active = tid < nr;
-        const uint64_t ra = active ? blk.row_off[r0 + tid] : 0;
-        const uint64_t rb = active ? blk.row_off[r0 + tid + 1] : 0;
-        const uint64_t base = blk.row_off[r0], end = blk.row_off[r0 + nr];
+        const uint64_t base = blk.row_off[T.r0], end = blk.row_off[T.r0 + T.nr];
         const uint64_t abase = base & ~15ull;
-        const bool in_lds = end - abase <= kStage;
+        uint32_t ra[RPT], rl[RPT];
+#pragma unroll
+        for (int k = 0; k < RPT; k++) {
+            ra[k] = rl[k] = 0;
+            if (k * 256 + tid < T.nr) {
+                const uint64_t* ro = blk.row_off + T.r0 + k * 256 + tid;
+                const uint64_t a = ro[0], z = ro[1];
+                ra[k] = (uint32_t)(a - abase);
+                rl[k] = (uint32_t)(z - a);
+            }
+        }
+        const bool in_lds = end - abase <= A.stage;
+        if (end - abase > 0xFFFFFFF0ull) {  // one tile spanning > 4 GiB of blobs: unsupported
+            if (tid == 0) report(A.err, err_key(b, T.r0, 0, kStMalformed));
+            continue;
+        }
         if (in_lds) {
             // Coalesced 16-B loads of the tile's contiguous blob bytes into LDS.
             const uint64_t efull = end & ~15ull;
@@ -336,15 +396,8 @@ __global__ void __launch_bounds__(256) decode_kernel(DecodeArgs A) {
             if (tid < end - efull) stage[efull - abase + tid] = blk.data[efull + tid];
         }
         __syncthreads();
-        if (in_lds) {
-            LdsSrc s{stage};
-            decode_tile_rows(A, s, b, t, tfirst, r0, nr, last_tile, (uint32_t)(ra - abase), rb - ra,
-                             s_nulls, s_w, &s_prefix);
-        } else {
-            GlbSrc s{blk.data};
-            decode_tile_rows(A, s, b, t, tfirst, r0, nr, last_tile, ra, rb - ra, s_nulls, s_w,
-                             &s_prefix);
-        }
+        if (in_lds) decode_tile<RPT>(A, LdsSrc{stage}, T, ra, rl, s_nulls, s_tot, s_w);
+        else decode_tile<RPT>(A, GlbSrc{blk.data + abase}, T, ra, rl, s_nulls, s_tot, s_w);
         __syncthreads();
         for (uint32_t p = tid; p < A.nproj; p += 256)
             if (s_nulls[p]) atomicAdd(&A.nulls[(uint64_t)b * A.nproj + p], (unsigned long long)s_nulls[p]);
@@ -441,9 +494,9 @@ __device__ __forceinline__ void write_out(const uint8_t* stage, uint8_t* out, ui
 __global__ void __launch_bounds__(256) encode_kernel(EncodeArgs A) {
     __shared__ __attribute__((aligned(16))) uint8_t stage[kStage + 32];
     __shared__ uint64_t s_w[4];
-    __shared__ uint64_t s_prefix;
-    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t tid = threadIdx.x;
     const uint64_t fixed = (uint64_t)A.bs + A.cap;
+    uint64_t prev_incl = 0;
 
     for (uint64_t t = blockIdx.x; t < A.total_tiles; t += gridDim.x) {
         const uint64_t r0 = t * kTile;
@@ -469,20 +522,12 @@ __global__ void __launch_bounds__(256) encode_kernel(EncodeArgs A) {
         } else {
             uint64_t agg;
             const uint64_t incl = block_incl_scan(size, s_w, &agg);
-            if (wave == 0) {
-                uint64_t prefix = 0;
-                if (t == 0) {
-                    if (lane == 0) publish(A.lookback, kFlagP | (agg & kValMask));
-                } else {
-                    if (lane == 0) publish(A.lookback + t, kFlagA | (agg & kValMask));
-                    prefix = lookback(A.lookback, t, 0, A.err, err_key(0, r0, 0, 0));
-                    if (lane == 0) publish(A.lookback + t, kFlagP | ((prefix + agg) & kValMask));
-                }
-                if (lane == 0) s_prefix = prefix;
-            }
-            __syncthreads();
-            tstart = s_prefix;
-            __syncthreads();
+            if (tid == 0) publish(A.lookback + t, agg + 1);
+            const uint64_t G = gridDim.x;
+            const bool have_prev = t >= G;
+            tstart = window_prefix(A.lookback, have_prev ? t - G + 1 : 0, t, have_prev ? prev_incl : 0,
+                                   s_w, A.err, err_key(0, r0, 0, 0));
+            prev_incl = tstart + agg;  // this workgroup's next tile is t + G
             start = tstart + incl - size;
             span = agg;
         }
@@ -507,8 +552,18 @@ __global__ void __launch_bounds__(256) encode_kernel(EncodeArgs A) {
 
 }  // namespace
 
-hipError_t launch_decode(const DecodeArgs& a, uint32_t grid, hipStream_t s) {
-    hipLaunchKernelGGL(decode_kernel, dim3(grid), dim3(kTile), 0, s, a);
+uint32_t decode_lds_bytes(uint32_t stage, uint32_t nproj, int rpt) {
+    return stage + 32 + ((4 * nproj + 15) & ~15u) + 8 * (8 * rpt + 4);
+}
+
+hipError_t launch_decode(const DecodeArgs& a, int rpt, uint32_t grid, hipStream_t s) {
+    const uint32_t lds = decode_lds_bytes(a.stage, a.nproj, rpt);
+    switch (rpt) {
+    case 1: hipLaunchKernelGGL(decode_kernel<1>, dim3(grid), dim3(kTile), lds, s, a); break;
+    case 2: hipLaunchKernelGGL(decode_kernel<2>, dim3(grid), dim3(kTile), lds, s, a); break;
+    case 4: hipLaunchKernelGGL(decode_kernel<4>, dim3(grid), dim3(kTile), lds, s, a); break;
+    default: hipLaunchKernelGGL(decode_kernel<8>, dim3(grid), dim3(kTile), lds, s, a); break;
+    }
     return hipGetLastError();
 }
 
@@ -517,10 +572,16 @@ hipError_t launch_encode(const EncodeArgs& a, uint32_t grid, hipStream_t s) {
     return hipGetLastError();
 }
 
-int decode_blocks_per_cu() {
+int decode_blocks_per_cu(int rpt, uint32_t lds) {
     int n = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, decode_kernel, kTile, 0) != hipSuccess) return 1;
-    return n;
+    hipError_t e;
+    switch (rpt) {
+    case 1: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, decode_kernel<1>, kTile, lds); break;
+    case 2: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, decode_kernel<2>, kTile, lds); break;
+    case 4: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, decode_kernel<4>, kTile, lds); break;
+    default: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, decode_kernel<8>, kTile, lds); break;
+    }
+    return e == hipSuccess ? n : 1;
 }
 
 int encode_blocks_per_cu() {

@@ -167,6 +167,7 @@ def decode_blocks(ctx: Context, segment: SegmentSchema, proj, blocks, outs: Deco
         cb[i].data = blk.data.ptr
         cb[i].row_off = blk.row_off.ptr
         cb[i].n_rows = blk.n_rows
+        cb[i].data_bytes = blk.data_bytes
     pj = (C.c_uint32 * max(len(proj), 1))(*proj)
     err = _abi.Error()
     st = ctx.L.murr_decode_blocks(ctx.h, C.byref(segment.c), pj, len(proj), cb, len(blocks),
