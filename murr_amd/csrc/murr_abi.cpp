@@ -315,16 +315,18 @@ int murr_decode_enqueue(murr_ctx_t* c, const murr_segment_t* seg, const uint32_t
     double est_row = (double)seg->bitset_size + seg->capacity;
     for (uint32_t i = 0; i < seg->ncols; i++) est_row += seg->cols[i].dtype == MURR_UTF8 ? 20.0 : 0.0;
     if (hinted && hint_rows) est_row = (double)hint_bytes / (double)hint_rows;
-    uint32_t stage = kDecStage;
-    int rpt = 8;
-    while (rpt > 1 && 256.0 * rpt * est_row * 1.15 > stage) rpt /= 2;
-    if (rpt == 1 && 256.0 * est_row * 1.15 > stage)
-        stage = (uint32_t)std::min<double>(65536.0, round_up((uint64_t)(256.0 * est_row * 1.2), 1024));
-    else  // no bigger than the tile needs (+25 % for row-size variance): more workgroups per CU
-        stage = std::min<uint32_t>(stage, std::max<uint32_t>(8192, (uint32_t)round_up(
-                    (uint64_t)(256.0 * rpt * est_row * 1.25), 1024)));
-    const uint32_t lds = decode_lds_bytes(stage, nproj, rpt);
-    const uint64_t R = (uint64_t)kTile * rpt;
+    // Rows per tile (multiple of 256): the largest up to 2048 whose staged blob
+    // bytes (+25 % for row-size variance) and row offsets fit ~32 KiB; two such
+    // buffers per workgroup (loader one tile ahead).
+    const double per_row = est_row * 1.25 + 8.0;
+    uint32_t rows = 256;
+    double tile_bytes = 16384.0;
+    if (const char* e = std::getenv("MURR_DECODE_TILE_BYTES")) tile_bytes = std::atof(e);  // tuning
+    while (rows < 1024 && 2.0 * rows * per_row <= tile_bytes) rows *= 2;
+    uint32_t stage = (uint32_t)std::max<uint64_t>(4096, round_up((uint64_t)(rows * est_row * 1.25) + 64, 1024));
+    stage = std::min<uint32_t>(stage, 65536);
+    const uint32_t lds = decode_lds_bytes(stage, nproj, nutf8, rows);
+    const uint64_t R = rows;
     std::vector<DecBlock> db(nblocks);
     uint64_t tiles = 0;
     for (uint32_t b = 0; b < nblocks; b++) {
@@ -348,14 +350,14 @@ int murr_decode_enqueue(murr_ctx_t* c, const murr_segment_t* seg, const uint32_t
         dout[i] = DecOut{(uint8_t*)outs[i].values, outs[i].validity, outs[i].offsets, outs[i].values_cap};
 
     const uint64_t nbp = (uint64_t)nblocks * nproj;
-    const uint64_t z_err = 0, z_nulls = 16, z_lens = z_nulls + 8 * nbp, z_lb = z_lens + 8 * nbp;
+    const uint64_t z_err = 0, z_stamps = 16, z_nulls = 80, z_lens = z_nulls + 8 * nbp, z_lb = z_lens + 8 * nbp;
     const uint64_t zbytes = round_up(z_lb + 8 * (uint64_t)nutf8 * tiles, 16);
     const uint64_t d_blocks = zbytes, d_proj = round_up(d_blocks + sizeof(DecBlock) * nblocks, 16);
     const uint64_t d_outs = round_up(d_proj + sizeof(DecProj) * nproj, 16);
     // Persistent grid: workgroups that are certainly co-resident (the occupancy
     // answer, one fewer when it is >= 4: MI355X_MICROARCH.md "Residency").
-    int bpc = decode_blocks_per_cu(rpt, lds);
-    bpc = std::max(1, bpc >= 4 ? std::min(bpc, 8) - 1 : bpc);
+    // The occupancy API answer (LDS-limited here), capped at 6 per CU.
+    int bpc = std::max(1, std::min(decode_blocks_per_cu(lds, rows), 6));
     const uint64_t grid = std::min<uint64_t>(std::max<uint64_t>(tiles, 1), (uint64_t)c->cus * bpc);
     const uint64_t d_prev = round_up(d_outs + sizeof(DecOut) * dout.size(), 16);
     const uint64_t dend = round_up(d_prev + 8 * grid * nutf8, 16);
@@ -387,6 +389,7 @@ int murr_decode_enqueue(murr_ctx_t* c, const murr_segment_t* seg, const uint32_t
     a.nulls = (unsigned long long*)(c->ws + z_nulls);
     a.lens = (unsigned long long*)(c->ws + z_lens);
     a.err = (unsigned long long*)(c->ws + z_err);
+    a.stamps = (unsigned long long*)(c->ws + z_stamps);
     a.total_tiles = tiles;
     a.nblocks = nblocks;
     a.nproj = nproj;
@@ -394,8 +397,13 @@ int murr_decode_enqueue(murr_ctx_t* c, const murr_segment_t* seg, const uint32_t
     a.bs = seg->bitset_size;
     a.cap = seg->capacity;
     a.stage = stage;
+    a.rows_per_tile = rows;
+    {
+        const char* dbg = std::getenv("MURR_DEBUG_DECODE");  // ablation only
+        a.debug = dbg ? (uint32_t)std::atoi(dbg) : 0;
+    }
     HIPC(hipEventRecord(c->k0, c->stream));
-    if (tiles) HIPC(launch_decode(a, rpt, (uint32_t)grid, c->stream));
+    if (tiles) HIPC(launch_decode(a, (uint32_t)grid, c->stream));
     HIPC(hipEventRecord(c->k1, c->stream));
     c->timed = true;
     HIPC(hipMemcpyAsync(c->hs + rb, c->ws, z_lb, hipMemcpyDeviceToHost, c->stream));
@@ -420,7 +428,13 @@ int murr_decode_wait(murr_ctx_t* c, murr_error_t* err) {
     unsigned long long word;
     std::memcpy(&word, rb, 8);
     const uint64_t nbp = (uint64_t)c->nblocks * c->nproj;
-    const unsigned long long* nulls = (const unsigned long long*)(rb + 16);
+    const unsigned long long* nulls = (const unsigned long long*)(rb + 80);
+    if (const char* dbg = std::getenv("MURR_DEBUG_DECODE"))
+        if (std::atoi(dbg) & 8) {
+            const unsigned long long* stp = (const unsigned long long*)(rb + 16);
+            std::fprintf(stderr, "decode stamps (cycles, sum over workgroups): wait %llu issue %llu A %llu F %llu B %llu end %llu\n",
+                         stp[0], stp[1], stp[2], stp[3], stp[4], stp[5]);
+        }
     const unsigned long long* lens = nulls + nbp;
     for (uint32_t b = 0; b < c->nblocks; b++) {
         for (uint32_t p = 0; p < c->nproj; p++) {

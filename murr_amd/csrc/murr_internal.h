@@ -45,8 +45,11 @@ struct DecodeArgs {
     unsigned long long* nulls;   // [nblocks * nproj]
     unsigned long long* lens;    // [nblocks * nproj] utf8 data bytes
     unsigned long long* err;     // max of ~key (0 = no error)
+    unsigned long long* stamps;  // [8] cycle sums per phase (MURR_DEBUG_DECODE & 8 only)
     uint64_t total_tiles;
     uint32_t nblocks, nproj, nutf8, bs, cap, stage;
+    uint32_t debug;              // ablation switches (MURR_DEBUG_DECODE), 0 in production
+    uint32_t rows_per_tile;      // multiple of 256
 };
 
 struct EncCol {               // one Arrow input column, segment order
@@ -76,10 +79,10 @@ __host__ __device__ inline uint64_t err_key(uint64_t block, uint64_t row, uint32
     return (block << 46) | (row << 14) | ((uint64_t)(col & 0x3FF) << 4) | (status & 0xF);
 }
 
-uint32_t decode_lds_bytes(uint32_t stage, uint32_t nproj, int rpt);
-hipError_t launch_decode(const DecodeArgs& a, int rpt, uint32_t grid, hipStream_t s);
+uint32_t decode_lds_bytes(uint32_t stage, uint32_t nproj, uint32_t nutf8, uint32_t rows_per_tile);
+hipError_t launch_decode(const DecodeArgs& a, uint32_t grid, hipStream_t s);
 hipError_t launch_encode(const EncodeArgs& a, uint32_t grid, hipStream_t s);
-int decode_blocks_per_cu(int rpt, uint32_t lds);
+int decode_blocks_per_cu(uint32_t lds, uint32_t rows_per_tile);
 int encode_blocks_per_cu();
 
 }  // namespace murr
