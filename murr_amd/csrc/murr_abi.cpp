@@ -325,7 +325,9 @@ int murr_decode_enqueue(murr_ctx_t* c, const murr_segment_t* seg, const uint32_t
     while (rows < 1024 && 2.0 * rows * per_row <= tile_bytes) rows *= 2;
     uint32_t stage = (uint32_t)std::max<uint64_t>(4096, round_up((uint64_t)(rows * est_row * 1.25) + 64, 1024));
     stage = std::min<uint32_t>(stage, 65536);
-    const uint32_t lds = decode_lds_bytes(stage, nproj, nutf8, rows);
+    // phase-A cell cache: up to 8 KiB of (length, payload) pairs
+    const uint32_t cell_cols = std::min<uint32_t>(nutf8, 8192 / (8 * rows));
+    const uint32_t lds = decode_lds_bytes(stage, nproj, nutf8, rows, cell_cols);
     const uint64_t R = rows;
     std::vector<DecBlock> db(nblocks);
     uint64_t tiles = 0;
@@ -358,7 +360,13 @@ int murr_decode_enqueue(murr_ctx_t* c, const murr_segment_t* seg, const uint32_t
     // answer, one fewer when it is >= 4: MI355X_MICROARCH.md "Residency").
     // The occupancy API answer (LDS-limited here), capped at 6 per CU.
     int bpc = std::max(1, std::min(decode_blocks_per_cu(lds, rows), 6));
-    const uint64_t grid = std::min<uint64_t>(std::max<uint64_t>(tiles, 1), (uint64_t)c->cus * bpc);
+    uint64_t grid = std::min<uint64_t>(std::max<uint64_t>(tiles, 1), (uint64_t)c->cus * bpc);
+    // Block-local mode when every workgroup gets whole blocks: no cross-tile
+    // prefix protocol at all.  Otherwise tiles round-robin + window prefix.
+    uint32_t nonempty = 0;
+    for (uint32_t b = 0; b < nblocks; b++) nonempty += blocks[b].n_rows != 0;
+    const bool local = nonempty >= grid || std::getenv("MURR_DECODE_LOCAL") != nullptr;
+    if (local) grid = std::max<uint64_t>(1, std::min<uint64_t>(grid, nonempty));
     const uint64_t d_prev = round_up(d_outs + sizeof(DecOut) * dout.size(), 16);
     const uint64_t dend = round_up(d_prev + 8 * grid * nutf8, 16);
     int st = ensure_ws(c, dend, err);
@@ -398,9 +406,14 @@ int murr_decode_enqueue(murr_ctx_t* c, const murr_segment_t* seg, const uint32_t
     a.cap = seg->capacity;
     a.stage = stage;
     a.rows_per_tile = rows;
+    a.cell_cols = cell_cols;
+    a.local = local ? 1 : 0;
     {
         const char* dbg = std::getenv("MURR_DEBUG_DECODE");  // ablation only
         a.debug = dbg ? (uint32_t)std::atoi(dbg) : 0;
+        if (a.debug & 8)
+            std::fprintf(stderr, "decode launch: grid %llu (%d/CU) tiles %llu rows/tile %u stage %u lds %u cell_cols %u local %d\n",
+                         (unsigned long long)grid, bpc, (unsigned long long)tiles, rows, stage, lds, cell_cols, (int)local);
     }
     HIPC(hipEventRecord(c->k0, c->stream));
     if (tiles) HIPC(launch_decode(a, (uint32_t)grid, c->stream));

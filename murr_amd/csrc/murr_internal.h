@@ -50,6 +50,8 @@ struct DecodeArgs {
     uint32_t nblocks, nproj, nutf8, bs, cap, stage;
     uint32_t debug;              // ablation switches (MURR_DEBUG_DECODE), 0 in production
     uint32_t rows_per_tile;      // multiple of 256
+    uint32_t cell_cols;          // utf8 columns whose cells phase A caches in LDS
+    uint32_t local;              // 1: block-local mode (a workgroup owns whole blocks)
 };
 
 struct EncCol {               // one Arrow input column, segment order
@@ -79,7 +81,8 @@ __host__ __device__ inline uint64_t err_key(uint64_t block, uint64_t row, uint32
     return (block << 46) | (row << 14) | ((uint64_t)(col & 0x3FF) << 4) | (status & 0xF);
 }
 
-uint32_t decode_lds_bytes(uint32_t stage, uint32_t nproj, uint32_t nutf8, uint32_t rows_per_tile);
+uint32_t decode_lds_bytes(uint32_t stage, uint32_t nproj, uint32_t nutf8, uint32_t rows_per_tile,
+                          uint32_t cell_cols);
 hipError_t launch_decode(const DecodeArgs& a, uint32_t grid, hipStream_t s);
 hipError_t launch_encode(const EncodeArgs& a, uint32_t grid, hipStream_t s);
 int decode_blocks_per_cu(uint32_t lds, uint32_t rows_per_tile);

@@ -44,44 +44,6 @@ __device__ __forceinline__ void report(unsigned long long* err, uint64_t key) {
     __hip_atomic_fetch_max(gp(err), (unsigned long long)~key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// ---- byte sources: LDS stage (aligned dword reads, padded) or HBM ---------
-struct LdsSrc {
-    const uint8_t* s;  // LDS, 16-B aligned, >= 16 B of padding past the data
-    __device__ __forceinline__ uint32_t u32(uint32_t a) const {
-        const uint32_t* w = reinterpret_cast<const uint32_t*>(s + (a & ~3u));
-        return __builtin_amdgcn_alignbyte(w[1], w[0], a & 3u);
-    }
-    __device__ __forceinline__ uint64_t u64(uint32_t a) const {
-        const uint32_t* w = reinterpret_cast<const uint32_t*>(s + (a & ~3u));
-        uint32_t sh = a & 3u, w0 = w[0], w1 = w[1], w2 = w[2];
-        return (uint64_t)__builtin_amdgcn_alignbyte(w1, w0, sh) |
-               ((uint64_t)__builtin_amdgcn_alignbyte(w2, w1, sh) << 32);
-    }
-    __device__ __forceinline__ uint32_t u8(uint32_t a) const { return s[a]; }
-};
-
-struct GlbSrc {
-    const GAS uint8_t* g;  // HBM (16-B aligned); never reads a dword holding no requested byte
-    __device__ __forceinline__ uint32_t u32(uint32_t a) const {
-        const GAS uint32_t* w = reinterpret_cast<const GAS uint32_t*>(g + (a & ~3u));
-        const uint32_t sh = a & 3u;
-        return sh ? __builtin_amdgcn_alignbyte(w[1], w[0], sh) : w[0];
-    }
-    __device__ __forceinline__ uint64_t u64(uint32_t a) const {
-        return (uint64_t)u32(a) | ((uint64_t)u32(a + 4) << 32);
-    }
-    __device__ __forceinline__ uint32_t u8(uint32_t a) const { return g[a]; }
-};
-
-// Read W (1,2,4,8) little-endian bytes at a.
-template <class Src, class Addr>
-__device__ __forceinline__ uint64_t read_w(const Src& s, Addr a, uint32_t w) {
-    if (w == 8) return s.u64(a);
-    if (w == 4) return s.u32(a);
-    if (w == 2) return s.u8(a) | (s.u8(a + 1) << 8);
-    return s.u8(a);
-}
-
 // ---- wave / block scan helpers (wave64) --------------------------------------
 __device__ __forceinline__ uint64_t shfl_up64(uint64_t x, int d) {
     uint32_t lo = __shfl_up((uint32_t)x, d, 64), hi = __shfl_up((uint32_t)(x >> 32), d, 64);
@@ -143,14 +105,13 @@ __device__ __forceinline__ uint64_t block_incl_scan(uint64_t x, uint64_t* s_w, u
 // Workgroup barrier for LDS hand-offs only: waits for this wave's LDS ops,
 // not for its vector-memory ops, so LDS-DMA in flight survives it
 // (__syncthreads() emits s_waitcnt vmcnt(0) and would drain it).
-// Diagnostic phase stamps (MURR_DEBUG_DECODE & 8): thread 0 of each workgroup
-// adds s_memtime deltas into s_st[j]; s_st[7] holds the last stamp.
-__device__ __forceinline__ void dstamp(const DecodeArgs& A, uint64_t* s_st, int j) {
-    if ((A.debug & 8) && threadIdx.x == 0) {
-        const uint64_t t = __builtin_amdgcn_s_memtime();
-        s_st[j] += t - s_st[7];
-        s_st[7] = t;
-    }
+// threadIdx.x made opaque at each use: stops the compiler from hoisting the
+// many lane masks derived from it out of the tile loop into SGPR pairs, which
+// overflowed the SGPR file and spilled (recomputing a mask is one VALU op).
+__device__ __forceinline__ uint32_t tidx() {
+    uint32_t t = threadIdx.x;
+    asm volatile("" : "+v"(t));
+    return t;
 }
 
 __device__ __forceinline__ void lds_barrier() {
@@ -165,10 +126,10 @@ __device__ __forceinline__ void lds_barrier() {
 // the whole workgroup sums the <= G-1 granules in parallel (agent-scope relaxed
 // loads = sc1: bypass this CU's L1; MI355X_MICROARCH.md R2 hand-off form).
 // Only tiles that are resident or done are ever waited on; spins are bounded.
-__device__ uint64_t window_prefix(const uint64_t* st, uint64_t lo, uint64_t t, uint64_t base,
-                                  uint64_t* s_w, unsigned long long* err, uint64_t ekey) {
+__device__ __forceinline__ uint64_t window_prefix(const uint64_t* st, uint64_t lo, uint64_t t, uint64_t base,
+                                  LAS uint64_t* s_w, unsigned long long* err, uint64_t ekey) {
     constexpr int K = 4;  // granules per thread per pass: 1024 predecessors
-    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t tid = tidx(), lane = tid & 63, wave = tid >> 6;
     uint64_t sum = 0;
     for (uint64_t j0 = lo; j0 < t; j0 += 256 * K) {
         uint64_t v[K];
@@ -231,7 +192,7 @@ struct Utf8Dfa {
 // Copy buf[0..span) (LDS) to out[g0..g0+span) with aligned 16-B stores; the
 // unaligned head and tail bytes with byte stores.  `tid` / `nt`: the calling
 // lanes (a wave or the workgroup).
-__device__ __forceinline__ void write_out(const uint8_t* buf, GAS uint8_t* out, uint64_t g0,
+__device__ __forceinline__ void write_out(const LAS uint8_t* buf, GAS uint8_t* out, uint64_t g0,
                                           uint64_t span, uint32_t tid, uint32_t nt) {
     const uint64_t g1 = g0 + span;
     const uint64_t a0 = (g0 + 15) & ~15ull, a1 = g1 & ~15ull;
@@ -243,7 +204,7 @@ __device__ __forceinline__ void write_out(const uint8_t* buf, GAS uint8_t* out, 
     if (tid < g1 - a1) out[a1 + tid] = buf[a1 - g0 + tid];
     const uint32_t lb0 = (uint32_t)(a0 - g0);
     const uint32_t sh = lb0 & 3u;
-    const uint32_t* w = reinterpret_cast<const uint32_t*>(buf);
+    const LAS uint32_t* w = (const LAS uint32_t*)buf;
     const uint64_t nch = (a1 - a0) >> 4;
     GAS u32x4* o = reinterpret_cast<GAS u32x4*>(out + a0);
     for (uint64_t c = tid; c < nch; c += nt) {
@@ -262,17 +223,17 @@ __device__ __forceinline__ void write_out(const uint8_t* buf, GAS uint8_t* out, 
 // Persistent workgroups of 4 waves walk their tiles (t, t+G, t+2G, ...) with a
 // two-deep LDS pipeline: right after the barrier that makes tile i resident,
 // every wave issues its share of tile i+1's LDS-DMA (row-offset slice + blob
-// bytes, global_load_lds_dwordx4, 1 KiB per wave-instruction), and tile i+2's
-// blob span is loaded, so HBM stays busy while tile i is decoded from LDS:
-//   A: utf8 lengths per 64-row chunk -> chunk prefixes; tile aggregate published
+// bytes, global_load_lds_dwordx4, 1 KiB per wave-instruction), so HBM stays
+// busy while tile i is decoded from LDS:
+//   A: utf8 cells parsed (cached in LDS), 64-row chunk totals -> chunk
+//      prefixes, tile aggregate published for the cross-tile prefix
 //   F: validity of every column (__ballot words), fixed-width and bool values
 //   B: per utf8 column: cross-tile prefix (window_prefix), i32 offsets, string
-//      bytes assembled per wave in LDS and stored 16 B wide, UTF-8 validated.
-// Row state (offsets) is re-read from the staged slice, so the row loops stay
-// rolled and the register budget small.
-// Descriptor tables are wave-uniform: read them through the constant address
-// space so they become s_load (lgkmcnt) instead of vector loads whose vmcnt
-// waits would drain the LDS-DMA in flight (vmcnt retires in order).
+//      bytes assembled per wave in LDS and stored 16 B wide, UTF-8 checked.
+// Everything wave-uniform (descriptors, chunk prefixes, output bases) lives in
+// SGPRs: descriptor tables are read through the constant address space
+// (s_load, lgkmcnt: no vmcnt wait that would drain the LDS-DMA in flight), and
+// per-row arithmetic is 32-bit, relative to the tile.
 __device__ __forceinline__ DecBlock ldblk(const DecodeArgs& A, uint64_t i) {
     const CAS DecBlock* p = (const CAS DecBlock*)A.blocks + i;
     DecBlock r;
@@ -292,6 +253,10 @@ __device__ __forceinline__ DecOut ldout(const DecodeArgs& A, uint64_t i) {
     r.values = p->values; r.validity = p->validity; r.offsets = p->offsets; r.values_cap = p->values_cap;
     return r;
 }
+__device__ __forceinline__ uint32_t sgpr(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ uint64_t sgpr64(uint64_t v) {
+    return ((uint64_t)sgpr((uint32_t)(v >> 32)) << 32) | sgpr((uint32_t)v);
+}
 
 struct DecTile {
     uint64_t t, tfirst, r0;
@@ -305,59 +270,101 @@ struct DecLayout {     // byte offsets inside one LDS tile buffer
 
 __host__ __device__ inline DecLayout dec_layout(uint32_t R, uint32_t nutf8, uint32_t stage) {
     DecLayout L;
-    L.pre = 0;
-    L.rowoff = ((8 * nutf8 * (R / 64 + 1) + 15) & ~15u);
+    L.pre = 0;  // [nutf8][R/64 + 1] u32 chunk prefixes (+ tile aggregate)
+    L.rowoff = ((4 * nutf8 * (R / 64 + 1) + 15) & ~15u);
     L.stage = L.rowoff + ((8 * (R + 1) + 16 + 15) & ~15u);
     L.bytes = L.stage + stage + 32;
     return L;
 }
 
-// read_dynamic (read.rs:45-55) for one non-null cell: string length and
-// payload address; a slice the reference would panic on -> *bad.
-template <class Src>
-__device__ __forceinline__ uint32_t utf8_cell(const Src& src, uint32_t ra, uint32_t rl, uint32_t bs,
-                                              uint32_t fo, uint32_t* pay, bool* bad) {
-    *bad = false;
-    *pay = 0;
-    if (fo + 4 > rl) { *bad = true; return 0; }
-    const uint32_t vlen = rl - bs;  // static + payload region
-    const uint32_t prel = src.u32(ra + fo);
-    if ((uint64_t)prel + 4 > vlen) { *bad = true; return 0; }
-    const uint32_t l = src.u32(ra + bs + prel);
-    if ((uint64_t)prel + 4 + l > vlen) { *bad = true; return 0; }
-    *pay = ra + bs + prel + 4;
-    return l;
-}
+// What the pipeline carries per tile (few SGPRs): the tile, its block and its
+// blob span.  Everything else is re-derived from the block descriptor.
+struct TileRef {
+    uint64_t t, base, end;
+    uint32_t b, ok;
+};
 
-// Tile t's rows and blob span (b: this workgroup's current block, monotone).
-__device__ __forceinline__ DecTile tile_info(const DecodeArgs& A, uint64_t t, uint32_t* b) {
-    DecTile T;
-    T.t = t;
-    T.ok = 0;
-    if (t >= A.total_tiles) return T;
-    while (*b + 1 < A.nblocks && ldblk(A, *b + 1).tile_base <= t) (*b)++;
-    const DecBlock blk = ldblk(A, *b);
-    T.b = *b;
-    T.tfirst = blk.tile_base;
-    T.r0 = (t - blk.tile_base) * A.rows_per_tile;
-    T.nr = (uint32_t)min((uint64_t)A.rows_per_tile, blk.n_rows - T.r0);
-    T.last = T.r0 + T.nr == blk.n_rows;
+__device__ __forceinline__ TileRef make_ref(const DecodeArgs& A, uint64_t t, uint32_t b) {
+    const DecBlock blk = ldblk(A, b);
+    const uint64_t r0 = (t - blk.tile_base) * A.rows_per_tile;
+    const uint64_t nr = min((uint64_t)A.rows_per_tile, blk.n_rows - r0);
     // Scalar loads (constant address space -> s_load, counted by lgkmcnt): they
     // must not queue behind the LDS-DMA on vmcnt, which is in order.
-    const CAS uint64_t* ro = (const CAS uint64_t*)(blk.row_off + T.r0);
-    T.base = ro[0];
-    T.end = ro[T.nr];
-    T.abase = T.base & ~15ull;
-    T.ok = 1;
+    const CAS uint64_t* ro = (const CAS uint64_t*)(blk.row_off + r0);
+    TileRef r;
+    r.t = t;
+    r.b = b;
+    r.base = ro[0];
+    r.end = ro[nr];
+    r.ok = 1;
+    return r;
+}
+
+__device__ __forceinline__ uint64_t tiles_end(const DecodeArgs& A, uint32_t b) {
+    return b + 1 < A.nblocks ? ldblk(A, b + 1).tile_base : A.total_tiles;
+}
+
+// First tile of this workgroup.  Block-local mode: workgroup w owns blocks
+// w, w+G, ... whole, in tile order.  Window mode: tiles w, w+G, w+2G, ...
+__device__ __forceinline__ TileRef first_ref(const DecodeArgs& A) {
+    TileRef r;
+    r.ok = 0;
+    r.t = r.base = r.end = 0;
+    r.b = 0;
+    const uint32_t w = blockIdx.x, G = gridDim.x;
+    if (A.local) {
+        for (uint32_t b = w; b < A.nblocks; b += G)
+            if (tiles_end(A, b) > ldblk(A, b).tile_base) return make_ref(A, ldblk(A, b).tile_base, b);
+        return r;
+    }
+    if (w >= A.total_tiles) return r;
+    uint32_t b = 0;
+    while (b + 1 < A.nblocks && ldblk(A, b + 1).tile_base <= w) b++;
+    return make_ref(A, w, b);
+}
+
+__device__ __forceinline__ TileRef next_ref(const DecodeArgs& A, const TileRef& c) {
+    TileRef r;
+    r.ok = 0;
+    r.t = r.base = r.end = 0;
+    r.b = 0;
+    if (!c.ok) return r;
+    const uint32_t G = gridDim.x;
+    if (A.local) {
+        if (c.t + 1 < tiles_end(A, c.b)) return make_ref(A, c.t + 1, c.b);
+        for (uint32_t b = c.b + G; b < A.nblocks; b += G)
+            if (tiles_end(A, b) > ldblk(A, b).tile_base) return make_ref(A, ldblk(A, b).tile_base, b);
+        return r;
+    }
+    const uint64_t t = c.t + G;
+    if (t >= A.total_tiles) return r;
+    uint32_t b = c.b;
+    while (b + 1 < A.nblocks && ldblk(A, b + 1).tile_base <= t) b++;
+    return make_ref(A, t, b);
+}
+
+__device__ __forceinline__ DecTile tile_of(const DecodeArgs& A, const TileRef& r) {
+    const DecBlock blk = ldblk(A, r.b);
+    DecTile T;
+    T.t = r.t;
+    T.b = r.b;
+    T.tfirst = blk.tile_base;
+    T.r0 = (r.t - blk.tile_base) * A.rows_per_tile;
+    T.nr = (uint32_t)min((uint64_t)A.rows_per_tile, blk.n_rows - T.r0);
+    T.last = T.r0 + T.nr == blk.n_rows;
+    T.base = r.base;
+    T.end = r.end;
+    T.abase = r.base & ~15ull;
+    T.ok = r.ok;
     return T;
 }
 
 // Issue tile T's LDS-DMA: row-offset slice [r0, r0+nr] and, when it fits the
 // stage, the blob span rounded out to 16-B granules (never past the granule
 // holding the last byte, so never past the allocation).  No waits here.
-__device__ __forceinline__ void issue_stage(const DecodeArgs& A, const DecTile& T, uint8_t* buf,
+__device__ __forceinline__ void issue_stage(const DecodeArgs& A, const DecTile& T, LAS uint8_t* buf,
                                             const DecLayout& L) {
-    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t lane = tidx() & 63, wave = tidx() >> 6;
     const GAS uint64_t* ro = gp(ldblk(A, T.b).row_off) + T.r0;
     const uintptr_t s0 = (uintptr_t)ro & ~(uintptr_t)15;
     const uint32_t nb_off = (uint32_t)((((uintptr_t)ro - s0) + (uint64_t)(T.nr + 1) * 8 + 15) & ~15ull);
@@ -381,35 +388,59 @@ __device__ __forceinline__ void issue_stage(const DecodeArgs& A, const DecTile& 
     }
 }
 
-// Tile bytes live in LDS (staged) or, for a tile larger than the stage, in
-// HBM.  One decoder serves both through a wave-uniform branch per access, so
-// the kernel carries one copy of the tile code (code size is what bounds it:
-// two inlined copies of this decoder did not fit the instruction cache).
-struct TileSrc {
-    const uint8_t* l;      // LDS stage
-    const GAS uint8_t* g;  // HBM, 16-B aligned tile start
-    bool lds;
-    __device__ __forceinline__ uint32_t u8(uint32_t a) const { return lds ? (uint32_t)l[a] : (uint32_t)g[a]; }
+// Tile bytes: staged in LDS (the hot path) or, for the rare tile whose rows
+// outgrew the stage, read from HBM by an out-of-line copy of the decoder.
+struct StageSrc {
+    static constexpr bool kHbm = false;
+    const LAS uint8_t* s;  // 16-B aligned, >= 16 B of padding past the data
     __device__ __forceinline__ uint32_t u32(uint32_t a) const {
-        return lds ? LdsSrc{l}.u32(a) : GlbSrc{g}.u32(a);
+        const LAS uint32_t* w = (const LAS uint32_t*)(s + (a & ~3u));
+        return __builtin_amdgcn_alignbyte(w[1], w[0], a & 3u);
     }
     __device__ __forceinline__ uint64_t u64(uint32_t a) const {
-        return lds ? LdsSrc{l}.u64(a) : GlbSrc{g}.u64(a);
+        const LAS uint32_t* w = (const LAS uint32_t*)(s + (a & ~3u));
+        const uint32_t sh = a & 3u, w0 = w[0], w1 = w[1], w2 = w[2];
+        return (uint64_t)__builtin_amdgcn_alignbyte(w1, w0, sh) |
+               ((uint64_t)__builtin_amdgcn_alignbyte(w2, w1, sh) << 32);
+    }
+    __device__ __forceinline__ uint32_t u8(uint32_t a) const { return s[a]; }
+    // first n <= 4 bytes at a (padding makes the over-read safe)
+    __device__ __forceinline__ uint32_t head(uint32_t a, uint32_t n) const {
+        const uint32_t v = u32(a);
+        return n >= 4 ? v : v & ((1u << (8 * n)) - 1);
+    }
+};
+struct HbmSrc {
+    static constexpr bool kHbm = true;
+    const GAS uint8_t* g;  // 16-B aligned; never reads a dword holding no requested byte
+    __device__ __forceinline__ uint32_t u32(uint32_t a) const {
+        const GAS uint32_t* w = (const GAS uint32_t*)(g + (a & ~3u));
+        const uint32_t sh = a & 3u;
+        return sh ? __builtin_amdgcn_alignbyte(w[1], w[0], sh) : w[0];
+    }
+    __device__ __forceinline__ uint64_t u64(uint32_t a) const {
+        return (uint64_t)u32(a) | ((uint64_t)u32(a + 4) << 32);
+    }
+    __device__ __forceinline__ uint32_t u8(uint32_t a) const { return g[a]; }
+    __device__ __forceinline__ uint32_t head(uint32_t a, uint32_t n) const {
+        uint32_t v = 0;
+        for (uint32_t q = 0; q < n && q < 4; q++) v |= (uint32_t)g[a + q] << (8 * q);
+        return v;
     }
 };
 
-// UTF-8 validation of one string, out of line (rarely the hot path: the
-// caller skips strings whose bytes are all ASCII).
-__device__ __attribute__((noinline)) bool utf8_valid_slow(TileSrc src, uint32_t at, uint32_t n) {
+template <class Src>
+__device__ __forceinline__ bool utf8_valid_slow(Src src, uint32_t at, uint32_t n) {
     Utf8Dfa dfa;
     for (uint32_t q = 0; q < n; q++) dfa.step(src.u8(at + q));
     return dfa.ok();
 }
 
-// read_dynamic (read.rs:45-55) for one cell: string length (0 for NULL /
-// absent rows) and payload address; *bad = a slice the reference would panic on.
-__device__ __forceinline__ uint32_t utf8_cell_ts(const TileSrc& src, uint32_t ra, uint32_t rl, uint32_t bs,
-                                                 uint32_t fo, bool want, uint32_t* pay, bool* bad) {
+// read_dynamic (read.rs:45-55) for one non-null cell: string length and
+// payload address; *bad = a slice the reference would panic on.
+template <class Src>
+__device__ __forceinline__ uint32_t utf8_cell(const Src& src, uint32_t ra, uint32_t rl, uint32_t bs,
+                                              uint32_t fo, bool want, uint32_t* pay, bool* bad) {
     *pay = 0;
     *bad = false;
     if (!want) return 0;
@@ -423,273 +454,379 @@ __device__ __forceinline__ uint32_t utf8_cell_ts(const TileSrc& src, uint32_t ra
     return l;
 }
 
-__device__ __attribute__((noinline)) uint64_t window_prefix_ni(const uint64_t* st, uint64_t lo, uint64_t t,
-                                                              uint64_t base, uint64_t* s_w,
-                                                              unsigned long long* err, uint64_t ekey) {
-    return window_prefix(st, lo, t, base, s_w, err, ekey);
+
+struct DecLds {  // this workgroup's LDS regions besides the tile buffers
+    LAS uint32_t* nulls;  // [4][nproj] per-wave null counts of the current tile
+    LAS uint64_t* w;      // [4] scratch for window_prefix
+    LAS uint8_t* wbuf;    // 4 x (kWaveBuf + 32) string assembly buffers
+    LAS uint64_t* mine;   // [4][nutf8] per wave: the last inclusive prefix
+    LAS uint64_t* st;     // [8] diagnostic stamps
+    LAS uint64_t* cell;   // [cell_cols][R] (slen << 32 | payload address)
+};
+
+__device__ __forceinline__ void dstamp(const DecodeArgs& A, const DecLds& S, int j) {
+    if ((A.debug & 8) && tidx() == 0) {
+        const uint64_t t = __builtin_amdgcn_s_memtime();
+        S.st[j] += t - S.st[7];
+        S.st[7] = t;
+    }
 }
 
-__device__ __forceinline__ void decode_tile(const DecodeArgs& A, const TileSrc& src, const DecTile& T,
-                                            uint8_t* buf, const DecLayout& L, uint32_t* s_nulls,
-                                            uint64_t* s_w, uint8_t* s_wbuf, const DecProj* s_proj,
-                                            const DecOut* s_out, uint64_t* s_mine, uint64_t* s_st) {
-    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const uint32_t bs = A.bs, R = A.rows_per_tile;
-    const uint64_t* rowoff = reinterpret_cast<const uint64_t*>(
-        buf + L.rowoff + (((uintptr_t)(ldblk(A, T.b).row_off + T.r0)) & 15));
-    uint64_t* pre = reinterpret_cast<uint64_t*>(buf + L.pre);
-    const uint32_t nchunk = (T.nr + 63) / 64;
-    const uint32_t nk = (T.nr + 255) / 256;
-
-    // row i of the tile: blob offset (relative to abase), length (0 = absent),
-    // null bitset (cached when bs <= 4; ~0 when the row is absent / too short)
-    auto row_at = [&](uint32_t i, uint32_t* ra, uint32_t* rl, uint32_t* bits) {
-        const uint32_t ic = i < T.nr ? i : T.nr - 1;
-        const uint64_t a = rowoff[ic], z = rowoff[ic + 1];
-        *ra = (uint32_t)(a - T.abase);
-        *rl = i < T.nr ? (uint32_t)(z - a) : 0;
-        const bool ok = *rl >= bs && *rl > 0;
-        uint32_t bv = ~0u;
-        if (ok && bs <= 4) {
-            bv = 0;
-            for (uint32_t q = 0; q < bs; q++) bv |= src.u8(*ra + q) << (8 * q);
-        }
-        *bits = bv;
-    };
-    auto null_of = [&](uint32_t ra, uint32_t rl, uint32_t bits, uint32_t bit) -> bool {
-        if (bs <= 4) return (bits >> bit) & 1;
-        return !(rl >= bs && rl > 0) || ((src.u8(ra + (bit >> 3)) >> (bit & 7)) & 1);
-    };
-
-    // ---- phase A: utf8 chunk totals -> chunk prefixes, aggregate published ----
-    if (A.nutf8) {
-#pragma unroll 1
-        for (uint32_t k = 0; k < nk; k++) {
-            uint32_t ra, rl, bits;
-            row_at(k * 256 + tid, &ra, &rl, &bits);
-            const uint32_t c = k * 4 + wave;
-            for (uint32_t p = 0; p < A.nproj; p++) {
-                const DecProj pc = s_proj[p];
-                if (!pc.is_utf8) continue;
-                uint32_t pay;
-                bool bad;
-                const uint32_t slen = utf8_cell_ts(src, ra, rl, bs, bs + pc.offset, !null_of(ra, rl, bits, pc.bit),
-                                                   &pay, &bad);
-                const uint32_t tot = wave_total_u32(slen);  // < tile span < 4 GiB
-                if (lane == 0 && c < nchunk) pre[pc.uslot * (R / 64 + 1) + c] = tot;
-            }
-        }
-        lds_barrier();
-        if (tid < A.nutf8) {  // chunk totals -> exclusive prefixes (+ aggregate at [nchunk])
-            uint64_t* pu = pre + tid * (R / 64 + 1);
-            uint64_t run = 0;
-            for (uint32_t c = 0; c < nchunk; c++) {
-                const uint64_t v = pu[c];
-                pu[c] = run;
-                run += v;
-            }
-            pu[nchunk] = run;
-            publish(A.lookback + (uint64_t)tid * A.total_tiles + T.t, run + 1);
-        }
-    }
-    dstamp(A, s_st, 2);
-
-    // ---- phase F: validity of every column, fixed-width and bool values -----
+// One projected column of one tile, rows dealt as in the tile comment: this
+// wave's 64-row chunks k*4 + wave.  KIND: 0 utf8, 1 bool, 3 one-byte values,
+// else the value width in bytes.  Straight-line per row: row offsets from the staged slice,
+// null bit, value (or utf8 slot + length), ballot -> validity word.  Reads for
+// the LDS stage are unguarded (stale or out-of-range LDS reads are harmless
+// and masked); HBM reads are clamped to the tile start when not wanted.
+// Returns this wave's null count; sets bits k of *badk for malformed rows.
+template <int KIND, class Src>
+__device__ __forceinline__ uint32_t dec_column(const DecodeArgs& A, const Src& src, const DecTile& T,
+                                               const LAS uint32_t* ro, uint32_t nk, const DecProj& pc,
+                                               const DecOut& o, LAS uint64_t* cell, LAS uint32_t* pre_u,
+                                               uint32_t* badk) {
+    const uint32_t tid = tidx(), lane = tid & 63, wave = tid >> 6;
+    const uint32_t bs = A.bs, abase = (uint32_t)T.abase;
+    const uint32_t fo = bs + pc.offset, nbyte = pc.bit >> 3, nbit = pc.bit & 7;
+    GAS uint64_t* vwords = gp((uint64_t*)o.validity) + (T.r0 >> 6) + wave;
+    uint32_t nulls = 0;
 #pragma unroll 1
     for (uint32_t k = 0; k < nk; k++) {
         const uint32_t i = k * 256 + tid;
         const bool act = i < T.nr;
-        uint32_t ra, rl, bits;
-        row_at(i, &ra, &rl, &bits);
-        const uint64_t row = T.r0 + i;
-        if (rl && rl < bs) report(A.err, err_key(T.b, row, 0, kStMalformed));  // split_at panics
-        const bool live = k * 256 + wave * 64 < T.nr;
-        const uint64_t word = ((T.r0 + k * 256) >> 6) + wave;
-        for (uint32_t p = 0; p < A.nproj; p++) {
-            const DecProj pc = s_proj[p];
-            const DecOut o = s_out[p];
-            const bool isnull = null_of(ra, rl, bits, pc.bit);
-            const uint64_t vm = __ballot(act && !isnull);
-            const uint32_t nnull = __popcll(__ballot(act && isnull));
-            if (lane == 0 && nnull) atomicAdd(&s_nulls[p], nnull);  // LDS
-            if (lane == 0 && live) reinterpret_cast<GAS uint64_t*>(gp(o.validity))[word] = vm;
-            if (pc.is_utf8) continue;
-            const uint32_t fo = bs + pc.offset;
-            bool fnull = isnull;
-            if (!fnull && fo + pc.width > rl) {
-                report(A.err, err_key(T.b, row, p, kStMalformed));
-                fnull = true;
+        const uint32_t ra = ro[2 * i] - abase;
+        const uint32_t rl = act ? ro[2 * i + 2] - ro[2 * i] : 0;
+        const bool present = rl >= bs && rl != 0;
+        const uint32_t nb = src.u8(Src::kHbm && !present ? 0 : ra + nbyte);
+        const bool isnull = !present || ((nb >> nbit) & 1);
+        const uint64_t vm = __ballot(act && !isnull);
+        nulls += __popcll(__ballot(act && isnull));
+        const bool live = k * 256 + wave * 64 < T.nr;  // wave-uniform
+        if (live && lane == 0) vwords[4 * k] = vm;
+        bool bad = rl && !present;  // split_at panics on a row shorter than the bitset
+        if constexpr (KIND == 0) {
+            // read_dynamic (read.rs:45-55): slot -> payload offset p (relative to
+            // the static region), u32 length at p, bytes at p + 4
+            const uint32_t vlen = rl - bs;
+            const bool s_ok = !isnull && fo + 4 <= rl;
+            const uint32_t prel = src.u32(Src::kHbm && !s_ok ? 0 : ra + fo);
+            const bool p_ok = s_ok && prel <= vlen - 4;
+            const uint32_t l = src.u32(Src::kHbm && !p_ok ? 0 : ra + bs + prel);
+            const bool good = p_ok && l <= vlen - 4 - prel;
+            bad |= !isnull && !good;
+            const uint32_t slen = good ? l : 0;
+            if (cell) cell[i] = ((uint64_t)slen << 32) | (ra + bs + prel + 4);
+            const uint32_t tot = wave_total_u32(slen);  // < tile span < 4 GiB
+            if (live && lane == 0) pre_u[k * 4 + wave] = tot;
+        } else if constexpr (KIND == 1) {
+            const bool have = !isnull && fo + 1 <= rl;
+            bad |= !isnull && !have;
+            const uint32_t v = src.u8(Src::kHbm && !have ? 0 : ra + fo);
+            const uint64_t m = __ballot(act && have && v != 0);
+            if (live && lane == 0) gp((uint64_t*)o.values)[(T.r0 >> 6) + 4 * k + wave] = m;
+        } else {
+            constexpr uint32_t W = KIND == 3 ? 1 : KIND;  // KIND 3 = 1-byte values
+            const bool have = !isnull && fo + W <= rl;
+            bad |= !isnull && !have;
+            const uint32_t a = Src::kHbm && !have ? 0 : ra + fo;
+            if (act) {
+                if constexpr (KIND == 8) ((GAS uint64_t*)gp(o.values) + T.r0)[i] = have ? src.u64(a) : 0;
+                if constexpr (KIND == 4) ((GAS uint32_t*)gp(o.values) + T.r0)[i] = have ? src.u32(a) : 0;
+                if constexpr (KIND == 2) ((GAS uint16_t*)gp(o.values) + T.r0)[i] = have ? (uint16_t)src.head(a, 2) : 0;
+                if constexpr (KIND != 8 && KIND != 4 && KIND != 2)
+                    (gp((uint8_t*)o.values) + T.r0)[i] = have ? (uint8_t)src.u8(a) : 0;
             }
-            if (pc.dtype == kBool) {
-                const bool v = !fnull && src.u8(ra + fo) != 0;
-                const uint64_t m = __ballot(act && v);
-                if (lane == 0 && live) reinterpret_cast<GAS uint64_t*>(gp(o.values))[word] = m;
-            } else if (act) {
-                const uint64_t v = fnull ? 0 : read_w(src, ra + fo, pc.width);
-                GAS uint8_t* dst = gp(o.values) + row * pc.width;
-                switch (pc.width) {
-                case 8: *reinterpret_cast<GAS uint64_t*>(dst) = v; break;
-                case 4: *reinterpret_cast<GAS uint32_t*>(dst) = (uint32_t)v; break;
-                case 2: *reinterpret_cast<GAS uint16_t*>(dst) = (uint16_t)v; break;
-                default: *dst = (uint8_t)v; break;
+        }
+        *badk |= (uint32_t)bad << k;
+    }
+    return nulls;
+}
+
+template <class Src>
+__device__ __forceinline__ void decode_tile(const DecodeArgs& A, const Src& src, const DecTile& T,
+                                            LAS uint8_t* buf, const DecLayout& L, const DecLds& S) {
+    const uint32_t tid = tidx(), lane = tid & 63, wave = tid >> 6;
+    const uint32_t bs = A.bs, R = A.rows_per_tile, nproj = A.nproj;
+    // staged row offsets; their low dwords suffice (a tile spans < 4 GiB)
+    const LAS uint32_t* ro = (const LAS uint32_t*)(buf + L.rowoff +
+                                                   (((uintptr_t)(ldblk(A, T.b).row_off + T.r0)) & 15));
+    const uint32_t abase = (uint32_t)T.abase;
+    LAS uint32_t* pre = (LAS uint32_t*)(buf + L.pre);
+    const uint32_t PS = R / 64 + 1;  // pre stride per utf8 column
+    const uint32_t nchunk = (T.nr + 63) / 64;
+    const uint32_t nk = (T.nr + 255) / 256;
+    LAS uint32_t* wnull = S.nulls + wave * nproj;  // this wave's null counters
+
+    // ---- pass 1: column by column (descriptor loads and the dtype dispatch
+    // once per column, straight-line row loops inside).
+    uint32_t badk = 0;
+#pragma unroll 1
+    for (uint32_t p = 0; p < nproj; p++) {
+        const DecProj pc = ldproj(A, p);
+        const DecOut o = ldout(A, (uint64_t)T.b * nproj + p);
+        uint32_t nn;
+        if (pc.is_utf8) {
+            LAS uint64_t* cell = pc.uslot < A.cell_cols ? S.cell + pc.uslot * R : nullptr;
+            nn = dec_column<0>(A, src, T, ro, nk, pc, o, cell, pre + pc.uslot * PS, &badk);
+        } else if (pc.dtype == kBool) {
+            nn = dec_column<1>(A, src, T, ro, nk, pc, o, nullptr, nullptr, &badk);
+        } else if (pc.width == 4) {
+            nn = dec_column<4>(A, src, T, ro, nk, pc, o, nullptr, nullptr, &badk);
+        } else if (pc.width == 8) {
+            nn = dec_column<8>(A, src, T, ro, nk, pc, o, nullptr, nullptr, &badk);
+        } else if (pc.width == 2) {
+            nn = dec_column<2>(A, src, T, ro, nk, pc, o, nullptr, nullptr, &badk);
+        } else {
+            nn = dec_column<3>(A, src, T, ro, nk, pc, o, nullptr, nullptr, &badk);  // 1-byte values
+        }
+        if (lane == 0 && nn) wnull[p] += nn;
+    }
+    // Exact error reports, in the reference's order (projection order inside a
+    // row; the packed key orders rows).  Cold: only rows the fast pass flagged.
+    if (__ballot(badk != 0)) {
+        for (uint32_t k = 0; k < nk; k++) {
+            if (!((badk >> k) & 1)) continue;
+            const uint32_t i = k * 256 + tid;
+            const uint32_t ra = ro[2 * i] - abase, rl = ro[2 * i + 2] - ro[2 * i];
+            const uint64_t row = T.r0 + i;
+            if (rl < bs) { report(A.err, err_key(T.b, row, 0, kStMalformed)); continue; }
+            for (uint32_t p = 0; p < nproj; p++) {
+                const DecProj pc = ldproj(A, p);
+                if ((src.u8(ra + (pc.bit >> 3)) >> (pc.bit & 7)) & 1) continue;
+                const uint32_t fo = bs + pc.offset;
+                bool bad = false;
+                if (pc.is_utf8) {
+                    uint32_t pay;
+                    utf8_cell(src, ra, rl, bs, fo, true, &pay, &bad);
+                } else {
+                    bad = fo + pc.width > rl;
+                }
+                if (bad) { report(A.err, err_key(T.b, row, p, kStMalformed)); break; }
+            }
+        }
+    }
+    if (A.nutf8) {
+        lds_barrier();
+        if (wave == 0) {  // chunk totals -> exclusive prefixes, aggregate at [nchunk]
+#pragma unroll 1
+            for (uint32_t u = 0; u < A.nutf8; u++) {
+                LAS uint32_t* pu = pre + u * PS;
+                const uint32_t v = lane < nchunk ? pu[lane] : 0;  // nchunk <= 16
+                const uint32_t inc = wave_scan_u32(v);
+                if (lane < nchunk) pu[lane] = inc - v;
+                const uint32_t agg = __builtin_amdgcn_readlane(inc, 63);
+                if (lane == 0) {
+                    pu[nchunk] = agg;
+                    if (!A.local) publish(A.lookback + (uint64_t)u * A.total_tiles + T.t, (uint64_t)agg + 1);
                 }
             }
         }
     }
-    dstamp(A, s_st, 3);
+    dstamp(A, S, 2);
     if (!A.nutf8) return;
 
-    // ---- phase B: cross-tile prefix, offsets, string bytes -------------------
-    uint8_t* wb = s_wbuf + wave * (kWaveBuf + 32);
-    for (uint32_t p = 0; p < A.nproj; p++) {
-        const DecProj pc = s_proj[p];
+    // ---- pass 2: per utf8 column: cross-tile prefix, offsets, string bytes ----
+    LAS uint8_t* wb = S.wbuf + wave * (kWaveBuf + 32);
+#pragma unroll 1
+    for (uint32_t p = 0; p < nproj; p++) {
+        const DecProj pc = ldproj(A, p);
         if (!pc.is_utf8) continue;
-        const DecOut o = s_out[p];
-        const uint64_t* pu = pre + pc.uslot * (R / 64 + 1);
-        const uint64_t agg = pu[nchunk];
-        // this workgroup's own inclusive prefix of tile t - G (same block) or 0
-        uint64_t* mine = s_mine + pc.uslot;
-        const uint64_t G = gridDim.x;
-        const bool have_prev = T.t >= T.tfirst + G;
-        const uint64_t lo = have_prev ? T.t - G + 1 : T.tfirst;
-        const uint64_t* st = A.lookback + (uint64_t)pc.uslot * A.total_tiles;
-        const uint64_t prefix = (A.debug & 2) ? 0 : window_prefix_ni(st, lo, T.t, have_prev ? *mine : 0, s_w, A.err,
-                                                                  err_key(T.b, T.r0, p, 0));
-        if (tid == 0) {
-            *mine = prefix + agg;
-            if (T.t == T.tfirst) gp(o.offsets)[0] = 0;
-            if (T.last) gp(A.lens)[(uint64_t)T.b * A.nproj + p] = prefix + agg;
+        const DecOut o = ldout(A, (uint64_t)T.b * nproj + p);
+        const LAS uint32_t* pu = pre + pc.uslot * PS;
+        const uint32_t agg = sgpr(pu[nchunk]);
+        // Block-local mode: this workgroup decodes the whole block in tile
+        // order, so the prefix is its own running sum.  Window mode: its own
+        // inclusive prefix of tile t - G (same block) plus the aggregates of the
+        // tiles between (window_prefix).  Each wave keeps its own copy.
+        LAS uint64_t* mine = S.mine + wave * A.nutf8 + pc.uslot;
+        uint64_t prefix;
+        if (A.local) {
+            prefix = T.t == T.tfirst ? 0 : sgpr64(*mine);
+        } else {
+            const uint64_t G = gridDim.x;
+            const bool have_prev = T.t >= T.tfirst + G;
+            const uint64_t lo = have_prev ? T.t - G + 1 : T.tfirst;
+            const uint64_t* st = A.lookback + (uint64_t)pc.uslot * A.total_tiles;
+            prefix = sgpr64((A.debug & 2) ? 0 : window_prefix(st, lo, T.t, have_prev ? *mine : 0, S.w, A.err,
+                                                               err_key(T.b, T.r0, p, 0)));
         }
+        if (lane == 0) *mine = prefix + agg;
+        if (tid == 0) {
+            if (T.t == T.tfirst) gp(o.offsets)[0] = 0;
+            if (T.last) gp(A.lens)[(uint64_t)T.b * nproj + p] = prefix + agg;
+        }
+        GAS int32_t* ob = gp(o.offsets) + T.r0 + 1;  // uniform base
         const uint32_t fo = bs + pc.offset;
 #pragma unroll 1
         for (uint32_t k = 0; k < nk; k++) {
+            const uint32_t c = k * 4 + wave;
+            if (c >= nchunk) break;  // wave-uniform
             const uint32_t i = k * 256 + tid;
             const bool act = i < T.nr;
-            uint32_t ra, rl, bits, pay;
-            bool bad;
-            row_at(i, &ra, &rl, &bits);
-            const uint32_t slen = utf8_cell_ts(src, ra, rl, bs, fo, !null_of(ra, rl, bits, pc.bit), &pay, &bad);
-            const uint64_t row = T.r0 + i;
-            if (bad) report(A.err, err_key(T.b, row, p, kStMalformed));
-            const uint64_t inc = wave_scan_u32(slen);  // < tile span < 4 GiB
-            const uint32_t c = k * 4 + wave;
-            const bool live = c < nchunk;
-            const uint64_t ws = prefix + (live ? pu[c] : 0);      // this wave chunk's output start
-            const uint64_t wn = live ? pu[c + 1] - pu[c] : 0;      // and its byte count
-            const uint64_t end = ws + inc, d0 = end - slen;
-            if (act) {
-                if (end > 0x7FFFFFFFull) report(A.err, err_key(T.b, row, p, kStOverflow));
-                else gp(o.offsets)[row + 1] = (int32_t)end;
-                if (slen && end > o.values_cap) report(A.err, err_key(T.b, row, p, kStCapacity));
+            uint32_t slen, pay;
+            if (pc.uslot < A.cell_cols) {
+                const uint64_t cl = S.cell[pc.uslot * R + i];
+                slen = (uint32_t)(cl >> 32);
+                pay = (uint32_t)cl;
+            } else {  // re-parse (more utf8 columns than the cell cache holds)
+                const uint32_t ra = ro[2 * i] - abase;
+                const uint32_t rl = act ? ro[2 * i + 2] - ro[2 * i] : 0;
+                const bool present = rl >= bs && rl != 0;
+                const bool nul = !present || ((src.u8(ra + (pc.bit >> 3)) >> (pc.bit & 7)) & 1);
+                bool bad;
+                slen = utf8_cell(src, ra, rl, bs, fo, !nul, &pay, &bad);
             }
+            slen = act ? slen : 0;
+            const uint32_t inc = wave_scan_u32(slen);  // < tile span < 4 GiB
+            const uint64_t ws = prefix + sgpr(pu[c]);      // this wave chunk's output start
+            const uint32_t wn = sgpr(pu[c + 1] - pu[c]);   // and its byte count
+            const bool fits = ws + wn <= 0x7FFFFFFFull;    // every i32 offset representable
+            const bool room = ws + wn <= o.values_cap;
+            if (fits) {
+                if (act) ob[i] = (int32_t)((uint32_t)ws + inc);
+            } else if (act) {
+                const uint64_t end = ws + inc;
+                if (end > 0x7FFFFFFFull) report(A.err, err_key(T.b, T.r0 + i, p, kStOverflow));
+                else ob[i] = (int32_t)end;
+            }
+            if (!room && act && slen && ws + inc > o.values_cap)
+                report(A.err, err_key(T.b, T.r0 + i, p, kStCapacity));
             // The wave's 64 consecutive rows own one contiguous output range
-            // [ws, ws+wn): assemble it in LDS (kWaveBuf bytes at a time), note any
-            // non-ASCII byte on the way, and store it with aligned 16-B stores.
-            bool ascii = true;
-            const bool emit = wn && !(A.debug & 1) && ws + wn <= o.values_cap && ws + wn <= 0x7FFFFFFFull;
-            if (emit) {
+            // [ws, ws+wn): each lane moves its string into the wave's LDS buffer
+            // (aligned dword reads + alignbyte, unaligned ds_write_b32, then a
+            // 0-3 byte tail), noting any non-ASCII byte, kWaveBuf bytes per
+            // pass; the wave then stores the range with aligned 16-B stores.
+            uint32_t hi_bits = 0;
+            const uint32_t d0 = inc - slen;  // my string's start inside the wave range
+            if (wn && fits && room && !(A.debug & 1)) {
 #pragma unroll 1
-                for (uint64_t w0 = ws; w0 < ws + wn; w0 += kWaveBuf) {
-                    const uint64_t w1 = min(w0 + kWaveBuf, ws + wn);
-                    const uint64_t lo_b = max(d0, w0), hi_b = min(end, w1);
+                for (uint32_t w0 = 0; w0 < wn; w0 += kWaveBuf) {
+                    const uint32_t w1 = min(w0 + kWaveBuf, wn);
+                    const uint32_t lo_b = max(d0, w0), hi_b = max(min(d0 + slen, w1), lo_b);
+                    const uint32_t sa = pay - d0;  // source address of output byte 0
+                    uint32_t q = lo_b;
 #pragma unroll 1
-                    for (uint64_t q = lo_b; q < hi_b; q++) {
-                        const uint32_t ch = src.u8(pay + (uint32_t)(q - d0));
-                        ascii &= ch < 0x80;
-                        wb[q - w0] = (uint8_t)ch;
+                    for (; q + 4 <= hi_b; q += 4) {
+                        const uint32_t v = src.u32(sa + q);
+                        *(LAS uint32_t*)(wb + (q - w0)) = v;
+                        hi_bits |= v;
+                    }
+                    const uint32_t n = hi_b - q;  // 0..3 tail bytes
+                    if (n) {
+                        const uint32_t v = src.head(sa + q, n);
+                        hi_bits |= v;
+                        LAS uint8_t* dst = wb + (q - w0);
+                        if (n & 2) *(LAS uint16_t*)dst = (uint16_t)v;
+                        if (n & 1) dst[n & 2] = (uint8_t)(v >> (8 * (n & 2)));
                     }
                     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's LDS writes landed
-                    write_out(wb, gp(o.values), w0, w1 - w0, lane, 64);
+                    write_out(wb, gp(o.values), ws + w0, w1 - w0, lane, 64);
                     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done before reuse
                 }
             } else if (slen) {
 #pragma unroll 1
-                for (uint32_t q = 0; q < slen; q++) ascii &= src.u8(pay + q) < 0x80;
+                for (uint32_t q = 0; q < slen; q += 4) hi_bits |= src.head(pay + q, slen - q);
             }
-            if (!ascii && !utf8_valid_slow(src, pay, slen)) report(A.err, err_key(T.b, row, p, kStUtf8));
+            if ((hi_bits & 0x80808080u) && !utf8_valid_slow(src, pay, slen))
+                report(A.err, err_key(T.b, T.r0 + i, p, kStUtf8));
         }
     }
-    dstamp(A, s_st, 4);
+    dstamp(A, S, 4);
 }
 
-// LDS (dynamic): [buffer 0][buffer 1][s_nulls: nproj u32][s_w: 4 u64]
+// A tile whose rows outgrew the stage: the same decoder over HBM.
+__device__ __forceinline__ void decode_tile_hbm(const DecodeArgs& A, const DecTile& T, LAS uint8_t* buf,
+                                                          DecLayout L, DecLds S) {
+    decode_tile(A, HbmSrc{gp(ldblk(A, T.b).data) + T.abase}, T, buf, L, S);
+}
+
+// LDS (dynamic): [buffer 0][buffer 1][nulls: nproj u32][w: 4 u64]
 //                [wave string buffers: 4 x (kWaveBuf + 32) when utf8 is projected]
-//                [s_proj: nproj DecProj][s_out: nproj DecOut (current tile's block)][s_mine: nutf8 u64]
-__global__ void __launch_bounds__(256) decode_kernel(DecodeArgs A) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    const DecLayout L = dec_layout(A.rows_per_tile, A.nutf8, A.stage);
-    uint8_t* bufs[2] = {lds, lds + L.bytes};
-    const uint32_t np16 = (4 * A.nproj + 15) & ~15u;
-    uint32_t* s_nulls = reinterpret_cast<uint32_t*>(lds + 2 * L.bytes);
-    uint64_t* s_w = reinterpret_cast<uint64_t*>(lds + 2 * L.bytes + np16);
-    uint8_t* s_wbuf = lds + 2 * L.bytes + np16 + 32;
-    DecProj* s_proj = reinterpret_cast<DecProj*>(s_wbuf + (A.nutf8 ? 4 * (kWaveBuf + 32) : 0));
-    DecOut* s_out = reinterpret_cast<DecOut*>(s_proj + A.nproj);
-    uint64_t* s_mine = reinterpret_cast<uint64_t*>(s_out + A.nproj);
-    uint64_t* s_st = s_mine + A.nutf8;  // 8 diagnostic stamp slots
-    if (threadIdx.x < 8) s_st[threadIdx.x] = threadIdx.x == 7 ? __builtin_amdgcn_s_memtime() : 0;
-    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    // output descriptors of block b into LDS: uniform index -> s_load (no vmcnt)
-    auto fill_out = [&](uint32_t blk) {
-        if (wave == 0)
-            for (uint32_t p = 0; p < A.nproj; p++) {
-                const DecOut o = ldout(A, (uint64_t)blk * A.nproj + p);
-                if (lane == 0) s_out[p] = o;
-            }
-    };
-    const uint32_t tid = threadIdx.x;
-    const uint64_t G = gridDim.x;
-    for (uint32_t p = tid; p < A.nproj; p += 256) {
-        s_nulls[p] = 0;
-        s_proj[p] = ldproj(A, p);
+//                [mine: 4 x nutf8 u64][st: 8 u64][cell: cell_cols x R u64]
+// The arguments are re-read from the kernarg segment every tile (s_load, K$
+// hits) instead of being held in SGPRs across the loop: with ~30 argument
+// words live, the tile code ran out of SGPRs and spilled to VGPR lanes.
+__device__ __forceinline__ DecodeArgs load_args() {
+    const CAS DecodeArgs* ap = (const CAS DecodeArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(ap));  // opaque: no hoisting across the loop
+    DecodeArgs A;
+    A.blocks = ap->blocks; A.proj = ap->proj; A.outs = ap->outs; A.lookback = ap->lookback;
+    A.prev = ap->prev; A.nulls = ap->nulls; A.lens = ap->lens; A.err = ap->err; A.stamps = ap->stamps;
+    A.total_tiles = ap->total_tiles; A.nblocks = ap->nblocks; A.nproj = ap->nproj; A.nutf8 = ap->nutf8;
+    A.bs = ap->bs; A.cap = ap->cap; A.stage = ap->stage; A.debug = ap->debug;
+    A.rows_per_tile = ap->rows_per_tile; A.cell_cols = ap->cell_cols; A.local = ap->local;
+    return A;
+}
+
+__device__ __forceinline__ DecLds dec_lds(const DecodeArgs& A, LAS uint8_t* lds, const DecLayout& L) {
+    const uint32_t np16 = (16 * A.nproj + 15) & ~15u;
+    DecLds S;
+    S.nulls = (LAS uint32_t*)(lds + 2 * L.bytes);
+    S.w = (LAS uint64_t*)(lds + 2 * L.bytes + np16);
+    S.wbuf = lds + 2 * L.bytes + np16 + 32;
+    S.mine = (LAS uint64_t*)(S.wbuf + (A.nutf8 ? 4 * (kWaveBuf + 32) : 0));
+    S.st = S.mine + 4 * A.nutf8;
+    S.cell = S.st + 8;
+    return S;
+}
+
+__global__ void __launch_bounds__(256) decode_kernel(DecodeArgs A0) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds_[];
+    LAS uint8_t* lds = (LAS uint8_t*)lds_;
+    const uint32_t tid = tidx();
+    TileRef cur, nxt;
+    {
+        const DecodeArgs A = load_args();
+        const DecLayout L = dec_layout(A.rows_per_tile, A.nutf8, A.stage);
+        const DecLds S = dec_lds(A, lds, L);
+        if (tid < 8) S.st[tid] = tid == 7 ? __builtin_amdgcn_s_memtime() : 0;
+        for (uint32_t p = tid; p < 4 * A.nproj; p += 256) S.nulls[p] = 0;
+        cur = first_ref(A);
+        if (!cur.ok) return;  // uniform
+        issue_stage(A, tile_of(A, cur), lds, L);
+        nxt = next_ref(A, cur);
     }
-    uint32_t b = 0;
-    DecTile cur = tile_info(A, blockIdx.x, &b);
-    if (!cur.ok) return;  // uniform
-    fill_out(cur.b);
-    uint32_t out_b = cur.b;
-    issue_stage(A, cur, bufs[0], L);
-    DecTile nxt = tile_info(A, blockIdx.x + G, &b);
-    for (uint64_t i = 0; cur.ok; i++) {
+    for (uint32_t i = 0; cur.ok; i++) {
+        const DecodeArgs A = load_args();
+        const DecLayout L = dec_layout(A.rows_per_tile, A.nutf8, A.stage);
+        const DecLds S = dec_lds(A, lds, L);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA for `cur` landed
         __syncthreads();                                  // ... and every other wave's
-        dstamp(A, s_st, 0);
-        if (nxt.ok) issue_stage(A, nxt, bufs[(i + 1) & 1], L);
-        const DecTile nn = tile_info(A, cur.t + 2 * G, &b);
-        dstamp(A, s_st, 1);
-        uint8_t* buf = bufs[i & 1];
-        const bool span_ok = cur.end - cur.abase <= 0xFFFFFFF0ull;  // > 4 GiB tile: unsupported
-        if (!span_ok) {
+        dstamp(A, S, 0);
+        if (nxt.ok) issue_stage(A, tile_of(A, nxt), lds + ((i + 1) & 1) * L.bytes, L);
+        const TileRef nn = next_ref(A, nxt);
+        dstamp(A, S, 1);
+        LAS uint8_t* buf = lds + (i & 1) * L.bytes;
+        const DecTile T = tile_of(A, cur);
+        const uint64_t span = ((T.end + 15) & ~15ull) - T.abase;
+        if (T.end - T.abase > 0xFFFFFFF0ull) {  // > 4 GiB tile: unsupported
             if (tid == 0) {
-                report(A.err, err_key(cur.b, cur.r0, 0, kStMalformed));
-                for (uint32_t u = 0; u < A.nutf8; u++) publish(A.lookback + (uint64_t)u * A.total_tiles + cur.t, 1);
+                report(A.err, err_key(T.b, T.r0, 0, kStMalformed));
+                for (uint32_t u = 0; u < A.nutf8; u++) publish(A.lookback + (uint64_t)u * A.total_tiles + T.t, 1);
             }
         } else if (A.debug & 4) {
             // ablation: staging only
+        } else if (span <= A.stage) {
+            decode_tile(A, StageSrc{buf + L.stage}, T, buf, L, S);
         } else {
-            const TileSrc src{buf + L.stage, gp(ldblk(A, cur.b).data) + cur.abase,
-                              ((cur.end + 15) & ~15ull) - cur.abase <= A.stage};
-            decode_tile(A, src, cur, buf, L, s_nulls, s_w, s_wbuf, s_proj, s_out, s_mine, s_st);
+            decode_tile_hbm(A, T, buf, L, S);
         }
         lds_barrier();
         for (uint32_t p = tid; p < A.nproj; p += 256) {
-            const uint32_t v = s_nulls[p];
+            const uint32_t v = S.nulls[p] + S.nulls[A.nproj + p] + S.nulls[2 * A.nproj + p] + S.nulls[3 * A.nproj + p];
             if (v) {
-                __hip_atomic_fetch_add(gp(A.nulls) + (uint64_t)cur.b * A.nproj + p, (unsigned long long)v,
+                __hip_atomic_fetch_add(gp(A.nulls) + (uint64_t)T.b * A.nproj + p, (unsigned long long)v,
                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                s_nulls[p] = 0;
+                S.nulls[p] = S.nulls[A.nproj + p] = S.nulls[2 * A.nproj + p] = S.nulls[3 * A.nproj + p] = 0;
             }
         }
         cur = nxt;
         nxt = nn;
-        if (cur.ok && cur.b != out_b) {  // next tile's block outputs (read after the loop-top barrier)
-            fill_out(cur.b);
-            out_b = cur.b;
-        }
-        dstamp(A, s_st, 5);
+        dstamp(A, S, 5);
     }
-    if ((A.debug & 8) && threadIdx.x == 0)
-        for (int j = 0; j < 7; j++) __hip_atomic_fetch_add(gp(A.stamps) + j, (unsigned long long)s_st[j],
+    const DecodeArgs A = load_args();
+    const DecLds S = dec_lds(A, lds, dec_layout(A.rows_per_tile, A.nutf8, A.stage));
+    if ((A.debug & 8) && tid == 0)
+        for (int j = 0; j < 7; j++) __hip_atomic_fetch_add(gp(A.stamps) + j, (unsigned long long)S.st[j],
                                                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
@@ -785,7 +922,7 @@ __global__ void __launch_bounds__(256) encode_kernel(EncodeArgs A) {
             const uint64_t G = gridDim.x;
             const bool have_prev = t >= G;
             tstart = window_prefix(A.lookback, have_prev ? t - G + 1 : 0, t, have_prev ? prev_incl : 0,
-                                   s_w, A.err, err_key(0, r0, 0, 0));
+                                   (LAS uint64_t*)s_w, A.err, err_key(0, r0, 0, 0));
             prev_incl = tstart + agg;  // this workgroup's next tile is t + G
             start = tstart + incl - size;
             span = agg;
@@ -801,7 +938,7 @@ __global__ void __launch_bounds__(256) encode_kernel(EncodeArgs A) {
         if (span <= kStage) {
             if (active) encode_row(A, row, stage + (start - tstart));
             __syncthreads();
-            write_out(stage, gp(A.out), tstart, span, tid, 256);
+            write_out((const LAS uint8_t*)stage, gp(A.out), tstart, span, tid, 256);
             __syncthreads();
         } else if (active) {
             encode_row(A, row, A.out + start);
@@ -811,14 +948,15 @@ __global__ void __launch_bounds__(256) encode_kernel(EncodeArgs A) {
 
 }  // namespace
 
-uint32_t decode_lds_bytes(uint32_t stage, uint32_t nproj, uint32_t nutf8, uint32_t rows_per_tile) {
+uint32_t decode_lds_bytes(uint32_t stage, uint32_t nproj, uint32_t nutf8, uint32_t rows_per_tile,
+                          uint32_t cell_cols) {
     const DecLayout L = dec_layout(rows_per_tile, nutf8, stage);
-    return 2 * L.bytes + ((4 * nproj + 15) & ~15u) + 32 + (nutf8 ? 4 * (kWaveBuf + 32) : 0) +
-           nproj * (uint32_t)(sizeof(DecProj) + sizeof(DecOut)) + 8 * nutf8 + 64;
+    return 2 * L.bytes + ((16 * nproj + 15) & ~15u) + 32 + (nutf8 ? 4 * (kWaveBuf + 32) : 0) + 32 * nutf8 + 64 +
+           8 * rows_per_tile * cell_cols;
 }
 
 hipError_t launch_decode(const DecodeArgs& a, uint32_t grid, hipStream_t s) {
-    const uint32_t lds = decode_lds_bytes(a.stage, a.nproj, a.nutf8, a.rows_per_tile);
+    const uint32_t lds = decode_lds_bytes(a.stage, a.nproj, a.nutf8, a.rows_per_tile, a.cell_cols);
     hipLaunchKernelGGL(decode_kernel, dim3(grid), dim3(kTile), lds, s, a);
     return hipGetLastError();
 }
