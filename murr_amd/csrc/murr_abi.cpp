@@ -319,14 +319,14 @@ int murr_decode_enqueue(murr_ctx_t* c, const murr_segment_t* seg, const uint32_t
     // bytes (+25 % for row-size variance) and row offsets fit ~32 KiB; two such
     // buffers per workgroup (loader one tile ahead).
     const double per_row = est_row * 1.25 + 8.0;
-    uint32_t rows = 256;
-    double tile_bytes = 16384.0;
+    uint32_t rows = kDT;
+    double tile_bytes = 32768.0;
     if (const char* e = std::getenv("MURR_DECODE_TILE_BYTES")) tile_bytes = std::atof(e);  // tuning
-    while (rows < 1024 && 2.0 * rows * per_row <= tile_bytes) rows *= 2;
+    while (rows < 4 * kDT && 2.0 * rows * per_row <= tile_bytes) rows *= 2;
     uint32_t stage = (uint32_t)std::max<uint64_t>(4096, round_up((uint64_t)(rows * est_row * 1.25) + 64, 1024));
     stage = std::min<uint32_t>(stage, 65536);
-    // phase-A cell cache: up to 8 KiB of (length, payload) pairs
-    const uint32_t cell_cols = std::min<uint32_t>(nutf8, 8192 / (8 * rows));
+    // pass-1 cell cache: up to 16 KiB of (length, payload) pairs
+    const uint32_t cell_cols = std::min<uint32_t>(nutf8, 16384 / (8 * rows));
     const uint32_t lds = decode_lds_bytes(stage, nproj, nutf8, rows, cell_cols);
     const uint64_t R = rows;
     std::vector<DecBlock> db(nblocks);

@@ -6,8 +6,10 @@
 
 namespace murr {
 
-// Threads per workgroup (4 waves); a decode tile is kTile * RPT rows.
+// Threads per encode workgroup (4 waves).
 constexpr uint32_t kTile = 256;
+// Decode workgroup: kDW waves (kDT threads); a decode tile is kDT * KMAX rows.
+constexpr uint32_t kDW = 8, kDT = 64 * kDW;
 // Bytes of assembled rows an encode tile stages through LDS.  Tiles whose
 // byte span exceeds the stage read / write HBM directly (the "global" path).
 constexpr uint32_t kStage = 32768;

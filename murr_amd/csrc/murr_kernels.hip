@@ -36,7 +36,7 @@ template <class T> __device__ __forceinline__ const GAS T* gp(const T* p) { retu
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 constexpr uint32_t kUtf8 = 0, kBool = 1;
-constexpr uint32_t kWaveBuf = 2048;  // bytes of strings one wave assembles per 64-row chunk
+constexpr uint32_t kWaveBuf = 1024;  // bytes of strings one wave assembles per pass
 constexpr uint32_t kSpinLimit = 1u << 22;
 enum : uint32_t { kStUtf8 = 1, kStOverflow = 4, kStMalformed = 5, kStCapacity = 6, kStInternal = 10 };
 
@@ -126,21 +126,23 @@ __device__ __forceinline__ void lds_barrier() {
 // the whole workgroup sums the <= G-1 granules in parallel (agent-scope relaxed
 // loads = sc1: bypass this CU's L1; MI355X_MICROARCH.md R2 hand-off form).
 // Only tiles that are resident or done are ever waited on; spins are bounded.
+template <int NW>  // waves in the workgroup
 __device__ __forceinline__ uint64_t window_prefix(const uint64_t* st, uint64_t lo, uint64_t t, uint64_t base,
                                   LAS uint64_t* s_w, unsigned long long* err, uint64_t ekey) {
-    constexpr int K = 4;  // granules per thread per pass: 1024 predecessors
+    constexpr int K = 4;  // granules per thread per pass
+    constexpr uint32_t NT = 64 * NW;
     const uint32_t tid = tidx(), lane = tid & 63, wave = tid >> 6;
     uint64_t sum = 0;
-    for (uint64_t j0 = lo; j0 < t; j0 += 256 * K) {
+    for (uint64_t j0 = lo; j0 < t; j0 += NT * K) {
         uint64_t v[K];
 #pragma unroll
         for (int i = 0; i < K; i++) {  // every load in flight before the first check
-            const uint64_t j = j0 + i * 256 + tid;
+            const uint64_t j = j0 + i * NT + tid;
             v[i] = j < t ? __hip_atomic_load(gp(st) + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 1;
         }
 #pragma unroll
         for (int i = 0; i < K; i++) {
-            const uint64_t j = j0 + i * 256 + tid;
+            const uint64_t j = j0 + i * NT + tid;
             uint32_t spins = 0;
             while (v[i] == 0) {
                 __builtin_amdgcn_s_sleep(2);
@@ -157,7 +159,9 @@ __device__ __forceinline__ uint64_t window_prefix(const uint64_t* st, uint64_t l
     sum = wave_sum(sum);
     if (lane == 0) s_w[wave] = sum;
     lds_barrier();
-    const uint64_t tot = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+    uint64_t tot = 0;
+#pragma unroll
+    for (int w = 0; w < NW; w++) tot += s_w[w];
     lds_barrier();
     return base + tot;
 }
@@ -288,14 +292,16 @@ __device__ __forceinline__ TileRef make_ref(const DecodeArgs& A, uint64_t t, uin
     const DecBlock blk = ldblk(A, b);
     const uint64_t r0 = (t - blk.tile_base) * A.rows_per_tile;
     const uint64_t nr = min((uint64_t)A.rows_per_tile, blk.n_rows - r0);
-    // Scalar loads (constant address space -> s_load, counted by lgkmcnt): they
-    // must not queue behind the LDS-DMA on vmcnt, which is in order.
-    const CAS uint64_t* ro = (const CAS uint64_t*)(blk.row_off + r0);
+    // Vector loads (HBM latency): a tile's span is fetched one pipeline step
+    // before its DMA is issued, and the loop-top vmcnt(0) that waits for the
+    // DMA covers them, so they never stall.  (As scalar loads they shared
+    // lgkmcnt with LDS traffic, and the first LDS wait exposed their latency.)
+    const GAS uint64_t* ro = gp(blk.row_off) + r0;
     TileRef r;
     r.t = t;
     r.b = b;
-    r.base = ro[0];
-    r.end = ro[nr];
+    r.base = __builtin_nontemporal_load(ro);
+    r.end = __builtin_nontemporal_load(ro + nr);
     r.ok = 1;
     return r;
 }
@@ -352,9 +358,9 @@ __device__ __forceinline__ DecTile tile_of(const DecodeArgs& A, const TileRef& r
     T.r0 = (r.t - blk.tile_base) * A.rows_per_tile;
     T.nr = (uint32_t)min((uint64_t)A.rows_per_tile, blk.n_rows - T.r0);
     T.last = T.r0 + T.nr == blk.n_rows;
-    T.base = r.base;
-    T.end = r.end;
-    T.abase = r.base & ~15ull;
+    T.base = sgpr64(r.base);  // loaded by every lane (vector load), uniform
+    T.end = sgpr64(r.end);
+    T.abase = T.base & ~15ull;
     T.ok = r.ok;
     return T;
 }
@@ -369,7 +375,7 @@ __device__ __forceinline__ void issue_stage(const DecodeArgs& A, const DecTile& 
     const uintptr_t s0 = (uintptr_t)ro & ~(uintptr_t)15;
     const uint32_t nb_off = (uint32_t)((((uintptr_t)ro - s0) + (uint64_t)(T.nr + 1) * 8 + 15) & ~15ull);
     const GAS uint8_t* go = (const GAS uint8_t*)s0;
-    for (uint32_t c = wave; c * 1024 < nb_off; c += 4) {
+    for (uint32_t c = wave; c * 1024 < nb_off; c += kDW) {
         const uint32_t off = c * 1024 + lane * 16;
         if (off < nb_off)
             __builtin_amdgcn_global_load_lds((const GAS void*)(go + off), (LAS void*)(buf + L.rowoff + c * 1024),
@@ -379,7 +385,7 @@ __device__ __forceinline__ void issue_stage(const DecodeArgs& A, const DecTile& 
     if (span <= A.stage) {
         const GAS uint8_t* g = gp(ldblk(A, T.b).data) + T.abase;
         const uint32_t nb = (uint32_t)span;
-        for (uint32_t c = wave; c * 1024 < nb; c += 4) {
+        for (uint32_t c = wave; c * 1024 < nb; c += kDW) {
             const uint32_t off = c * 1024 + lane * 16;
             if (off < nb)
                 __builtin_amdgcn_global_load_lds((const GAS void*)(g + off), (LAS void*)(buf + L.stage + c * 1024),
@@ -479,7 +485,7 @@ __device__ __forceinline__ void dstamp(const DecodeArgs& A, const DecLds& S, int
 // the LDS stage are unguarded (stale or out-of-range LDS reads are harmless
 // and masked); HBM reads are clamped to the tile start when not wanted.
 // Returns this wave's null count; sets bits k of *badk for malformed rows.
-template <int KIND, class Src>
+template <int KIND, int KMAX, class Src>
 __device__ __forceinline__ uint32_t dec_column(const DecodeArgs& A, const Src& src, const DecTile& T,
                                                const LAS uint32_t* ro, uint32_t nk, const DecProj& pc,
                                                const DecOut& o, LAS uint64_t* cell, LAS uint32_t* pre_u,
@@ -489,9 +495,11 @@ __device__ __forceinline__ uint32_t dec_column(const DecodeArgs& A, const Src& s
     const uint32_t fo = bs + pc.offset, nbyte = pc.bit >> 3, nbit = pc.bit & 7;
     GAS uint64_t* vwords = gp((uint64_t*)o.validity) + (T.r0 >> 6) + wave;
     uint32_t nulls = 0;
-#pragma unroll 1
-    for (uint32_t k = 0; k < nk; k++) {
-        const uint32_t i = k * 256 + tid;
+    // All KMAX chunks unrolled, unguarded (chunks past the tile have no active
+    // lane): the LDS reads of the chunks overlap instead of forming one chain.
+#pragma unroll
+    for (uint32_t k = 0; k < KMAX; k++) {
+        const uint32_t i = k * kDT + tid;
         const bool act = i < T.nr;
         const uint32_t ra = ro[2 * i] - abase;
         const uint32_t rl = act ? ro[2 * i + 2] - ro[2 * i] : 0;
@@ -500,8 +508,8 @@ __device__ __forceinline__ uint32_t dec_column(const DecodeArgs& A, const Src& s
         const bool isnull = !present || ((nb >> nbit) & 1);
         const uint64_t vm = __ballot(act && !isnull);
         nulls += __popcll(__ballot(act && isnull));
-        const bool live = k * 256 + wave * 64 < T.nr;  // wave-uniform
-        if (live && lane == 0) vwords[4 * k] = vm;
+        const bool live = k * kDT + wave * 64 < T.nr;  // wave-uniform
+        if (live && lane == 0) vwords[kDW * k] = vm;
         bool bad = rl && !present;  // split_at panics on a row shorter than the bitset
         if constexpr (KIND == 0) {
             // read_dynamic (read.rs:45-55): slot -> payload offset p (relative to
@@ -516,13 +524,13 @@ __device__ __forceinline__ uint32_t dec_column(const DecodeArgs& A, const Src& s
             const uint32_t slen = good ? l : 0;
             if (cell) cell[i] = ((uint64_t)slen << 32) | (ra + bs + prel + 4);
             const uint32_t tot = wave_total_u32(slen);  // < tile span < 4 GiB
-            if (live && lane == 0) pre_u[k * 4 + wave] = tot;
+            if (live && lane == 0) pre_u[k * kDW + wave] = tot;
         } else if constexpr (KIND == 1) {
             const bool have = !isnull && fo + 1 <= rl;
             bad |= !isnull && !have;
             const uint32_t v = src.u8(Src::kHbm && !have ? 0 : ra + fo);
             const uint64_t m = __ballot(act && have && v != 0);
-            if (live && lane == 0) gp((uint64_t*)o.values)[(T.r0 >> 6) + 4 * k + wave] = m;
+            if (live && lane == 0) gp((uint64_t*)o.values)[(T.r0 >> 6) + kDW * k + wave] = m;
         } else {
             constexpr uint32_t W = KIND == 3 ? 1 : KIND;  // KIND 3 = 1-byte values
             const bool have = !isnull && fo + W <= rl;
@@ -541,7 +549,7 @@ __device__ __forceinline__ uint32_t dec_column(const DecodeArgs& A, const Src& s
     return nulls;
 }
 
-template <class Src>
+template <int KMAX, class Src>
 __device__ __forceinline__ void decode_tile(const DecodeArgs& A, const Src& src, const DecTile& T,
                                             LAS uint8_t* buf, const DecLayout& L, const DecLds& S) {
     const uint32_t tid = tidx(), lane = tid & 63, wave = tid >> 6;
@@ -553,7 +561,7 @@ __device__ __forceinline__ void decode_tile(const DecodeArgs& A, const Src& src,
     LAS uint32_t* pre = (LAS uint32_t*)(buf + L.pre);
     const uint32_t PS = R / 64 + 1;  // pre stride per utf8 column
     const uint32_t nchunk = (T.nr + 63) / 64;
-    const uint32_t nk = (T.nr + 255) / 256;
+    const uint32_t nk = (T.nr + kDT - 1) / kDT;
     LAS uint32_t* wnull = S.nulls + wave * nproj;  // this wave's null counters
 
     // ---- pass 1: column by column (descriptor loads and the dtype dispatch
@@ -566,17 +574,17 @@ __device__ __forceinline__ void decode_tile(const DecodeArgs& A, const Src& src,
         uint32_t nn;
         if (pc.is_utf8) {
             LAS uint64_t* cell = pc.uslot < A.cell_cols ? S.cell + pc.uslot * R : nullptr;
-            nn = dec_column<0>(A, src, T, ro, nk, pc, o, cell, pre + pc.uslot * PS, &badk);
+            nn = dec_column<0, KMAX>(A, src, T, ro, nk, pc, o, cell, pre + pc.uslot * PS, &badk);
         } else if (pc.dtype == kBool) {
-            nn = dec_column<1>(A, src, T, ro, nk, pc, o, nullptr, nullptr, &badk);
+            nn = dec_column<1, KMAX>(A, src, T, ro, nk, pc, o, nullptr, nullptr, &badk);
         } else if (pc.width == 4) {
-            nn = dec_column<4>(A, src, T, ro, nk, pc, o, nullptr, nullptr, &badk);
+            nn = dec_column<4, KMAX>(A, src, T, ro, nk, pc, o, nullptr, nullptr, &badk);
         } else if (pc.width == 8) {
-            nn = dec_column<8>(A, src, T, ro, nk, pc, o, nullptr, nullptr, &badk);
+            nn = dec_column<8, KMAX>(A, src, T, ro, nk, pc, o, nullptr, nullptr, &badk);
         } else if (pc.width == 2) {
-            nn = dec_column<2>(A, src, T, ro, nk, pc, o, nullptr, nullptr, &badk);
+            nn = dec_column<2, KMAX>(A, src, T, ro, nk, pc, o, nullptr, nullptr, &badk);
         } else {
-            nn = dec_column<3>(A, src, T, ro, nk, pc, o, nullptr, nullptr, &badk);  // 1-byte values
+            nn = dec_column<3, KMAX>(A, src, T, ro, nk, pc, o, nullptr, nullptr, &badk);  // 1-byte values
         }
         if (lane == 0 && nn) wnull[p] += nn;
     }
@@ -585,7 +593,7 @@ __device__ __forceinline__ void decode_tile(const DecodeArgs& A, const Src& src,
     if (__ballot(badk != 0)) {
         for (uint32_t k = 0; k < nk; k++) {
             if (!((badk >> k) & 1)) continue;
-            const uint32_t i = k * 256 + tid;
+            const uint32_t i = k * kDT + tid;
             const uint32_t ra = ro[2 * i] - abase, rl = ro[2 * i + 2] - ro[2 * i];
             const uint64_t row = T.r0 + i;
             if (rl < bs) { report(A.err, err_key(T.b, row, 0, kStMalformed)); continue; }
@@ -620,6 +628,7 @@ __device__ __forceinline__ void decode_tile(const DecodeArgs& A, const Src& src,
                 }
             }
         }
+        lds_barrier();  // every wave reads the prefixes in pass 2
     }
     dstamp(A, S, 2);
     if (!A.nutf8) return;
@@ -646,7 +655,7 @@ __device__ __forceinline__ void decode_tile(const DecodeArgs& A, const Src& src,
             const bool have_prev = T.t >= T.tfirst + G;
             const uint64_t lo = have_prev ? T.t - G + 1 : T.tfirst;
             const uint64_t* st = A.lookback + (uint64_t)pc.uslot * A.total_tiles;
-            prefix = sgpr64((A.debug & 2) ? 0 : window_prefix(st, lo, T.t, have_prev ? *mine : 0, S.w, A.err,
+            prefix = sgpr64((A.debug & 2) ? 0 : window_prefix<kDW>(st, lo, T.t, have_prev ? *mine : 0, S.w, A.err,
                                                                err_key(T.b, T.r0, p, 0)));
         }
         if (lane == 0) *mine = prefix + agg;
@@ -658,9 +667,9 @@ __device__ __forceinline__ void decode_tile(const DecodeArgs& A, const Src& src,
         const uint32_t fo = bs + pc.offset;
 #pragma unroll 1
         for (uint32_t k = 0; k < nk; k++) {
-            const uint32_t c = k * 4 + wave;
+            const uint32_t c = k * kDW + wave;
             if (c >= nchunk) break;  // wave-uniform
-            const uint32_t i = k * 256 + tid;
+            const uint32_t i = k * kDT + tid;
             const bool act = i < T.nr;
             uint32_t slen, pay;
             if (pc.uslot < A.cell_cols) {
@@ -734,9 +743,10 @@ __device__ __forceinline__ void decode_tile(const DecodeArgs& A, const Src& src,
 }
 
 // A tile whose rows outgrew the stage: the same decoder over HBM.
+template <int KMAX>
 __device__ __forceinline__ void decode_tile_hbm(const DecodeArgs& A, const DecTile& T, LAS uint8_t* buf,
                                                           DecLayout L, DecLds S) {
-    decode_tile(A, HbmSrc{gp(ldblk(A, T.b).data) + T.abase}, T, buf, L, S);
+    decode_tile<KMAX>(A, HbmSrc{gp(ldblk(A, T.b).data) + T.abase}, T, buf, L, S);
 }
 
 // LDS (dynamic): [buffer 0][buffer 1][nulls: nproj u32][w: 4 u64]
@@ -758,18 +768,20 @@ __device__ __forceinline__ DecodeArgs load_args() {
 }
 
 __device__ __forceinline__ DecLds dec_lds(const DecodeArgs& A, LAS uint8_t* lds, const DecLayout& L) {
-    const uint32_t np16 = (16 * A.nproj + 15) & ~15u;
+    const uint32_t np16 = (4 * kDW * A.nproj + 15) & ~15u;
     DecLds S;
     S.nulls = (LAS uint32_t*)(lds + 2 * L.bytes);
     S.w = (LAS uint64_t*)(lds + 2 * L.bytes + np16);
-    S.wbuf = lds + 2 * L.bytes + np16 + 32;
-    S.mine = (LAS uint64_t*)(S.wbuf + (A.nutf8 ? 4 * (kWaveBuf + 32) : 0));
-    S.st = S.mine + 4 * A.nutf8;
+    S.wbuf = lds + 2 * L.bytes + np16 + 8 * kDW;
+    S.mine = (LAS uint64_t*)(S.wbuf + (A.nutf8 ? kDW * (kWaveBuf + 32) : 0));
+    S.st = S.mine + kDW * A.nutf8;
     S.cell = S.st + 8;
     return S;
 }
 
-__global__ void __launch_bounds__(256) decode_kernel(DecodeArgs A0) {
+// KMAX = rows_per_tile / kDT: 64-row chunks per wave per tile.
+template <int KMAX>
+__global__ void __launch_bounds__(kDT) decode_kernel(DecodeArgs A0) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds_[];
     LAS uint8_t* lds = (LAS uint8_t*)lds_;
     const uint32_t tid = tidx();
@@ -779,7 +791,7 @@ __global__ void __launch_bounds__(256) decode_kernel(DecodeArgs A0) {
         const DecLayout L = dec_layout(A.rows_per_tile, A.nutf8, A.stage);
         const DecLds S = dec_lds(A, lds, L);
         if (tid < 8) S.st[tid] = tid == 7 ? __builtin_amdgcn_s_memtime() : 0;
-        for (uint32_t p = tid; p < 4 * A.nproj; p += 256) S.nulls[p] = 0;
+        for (uint32_t p = tid; p < kDW * A.nproj; p += kDT) S.nulls[p] = 0;
         cur = first_ref(A);
         if (!cur.ok) return;  // uniform
         issue_stage(A, tile_of(A, cur), lds, L);
@@ -806,17 +818,20 @@ __global__ void __launch_bounds__(256) decode_kernel(DecodeArgs A0) {
         } else if (A.debug & 4) {
             // ablation: staging only
         } else if (span <= A.stage) {
-            decode_tile(A, StageSrc{buf + L.stage}, T, buf, L, S);
+            decode_tile<KMAX>(A, StageSrc{buf + L.stage}, T, buf, L, S);
         } else {
-            decode_tile_hbm(A, T, buf, L, S);
+            decode_tile_hbm<KMAX>(A, T, buf, L, S);
         }
         lds_barrier();
-        for (uint32_t p = tid; p < A.nproj; p += 256) {
-            const uint32_t v = S.nulls[p] + S.nulls[A.nproj + p] + S.nulls[2 * A.nproj + p] + S.nulls[3 * A.nproj + p];
+        for (uint32_t p = tid; p < A.nproj; p += kDT) {
+            uint32_t v = 0;
+#pragma unroll
+            for (uint32_t w = 0; w < kDW; w++) v += S.nulls[w * A.nproj + p];
             if (v) {
                 __hip_atomic_fetch_add(gp(A.nulls) + (uint64_t)T.b * A.nproj + p, (unsigned long long)v,
                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                S.nulls[p] = S.nulls[A.nproj + p] = S.nulls[2 * A.nproj + p] = S.nulls[3 * A.nproj + p] = 0;
+#pragma unroll
+                for (uint32_t w = 0; w < kDW; w++) S.nulls[w * A.nproj + p] = 0;
             }
         }
         cur = nxt;
@@ -921,7 +936,7 @@ __global__ void __launch_bounds__(256) encode_kernel(EncodeArgs A) {
             if (tid == 0) publish(A.lookback + t, agg + 1);
             const uint64_t G = gridDim.x;
             const bool have_prev = t >= G;
-            tstart = window_prefix(A.lookback, have_prev ? t - G + 1 : 0, t, have_prev ? prev_incl : 0,
+            tstart = window_prefix<4>(A.lookback, have_prev ? t - G + 1 : 0, t, have_prev ? prev_incl : 0,
                                    (LAS uint64_t*)s_w, A.err, err_key(0, r0, 0, 0));
             prev_incl = tstart + agg;  // this workgroup's next tile is t + G
             start = tstart + incl - size;
@@ -951,13 +966,18 @@ __global__ void __launch_bounds__(256) encode_kernel(EncodeArgs A) {
 uint32_t decode_lds_bytes(uint32_t stage, uint32_t nproj, uint32_t nutf8, uint32_t rows_per_tile,
                           uint32_t cell_cols) {
     const DecLayout L = dec_layout(rows_per_tile, nutf8, stage);
-    return 2 * L.bytes + ((16 * nproj + 15) & ~15u) + 32 + (nutf8 ? 4 * (kWaveBuf + 32) : 0) + 32 * nutf8 + 64 +
+    return 2 * L.bytes + ((4 * kDW * nproj + 15) & ~15u) + 8 * kDW + (nutf8 ? kDW * (kWaveBuf + 32) : 0) +
+           8 * kDW * nutf8 + 64 +
            8 * rows_per_tile * cell_cols;
 }
 
 hipError_t launch_decode(const DecodeArgs& a, uint32_t grid, hipStream_t s) {
     const uint32_t lds = decode_lds_bytes(a.stage, a.nproj, a.nutf8, a.rows_per_tile, a.cell_cols);
-    hipLaunchKernelGGL(decode_kernel, dim3(grid), dim3(kTile), lds, s, a);
+    switch (a.rows_per_tile / kDT) {
+    case 1: hipLaunchKernelGGL(decode_kernel<1>, dim3(grid), dim3(kDT), lds, s, a); break;
+    case 2: hipLaunchKernelGGL(decode_kernel<2>, dim3(grid), dim3(kDT), lds, s, a); break;
+    default: hipLaunchKernelGGL(decode_kernel<4>, dim3(grid), dim3(kDT), lds, s, a); break;
+    }
     return hipGetLastError();
 }
 
@@ -969,8 +989,11 @@ hipError_t launch_encode(const EncodeArgs& a, uint32_t grid, hipStream_t s) {
 int decode_blocks_per_cu(uint32_t lds, uint32_t rows_per_tile) {
     int n = 0;
     hipError_t e;
-    (void)rows_per_tile;
-    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, decode_kernel, kTile, lds);
+    switch (rows_per_tile / kDT) {
+    case 1: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, decode_kernel<1>, kDT, lds); break;
+    case 2: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, decode_kernel<2>, kDT, lds); break;
+    default: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, decode_kernel<4>, kDT, lds); break;
+    }
     return e == hipSuccess ? n : 1;
 }
 
