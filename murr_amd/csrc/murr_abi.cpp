@@ -445,8 +445,9 @@ int murr_decode_wait(murr_ctx_t* c, murr_error_t* err) {
     if (const char* dbg = std::getenv("MURR_DEBUG_DECODE"))
         if (std::atoi(dbg) & 8) {
             const unsigned long long* stp = (const unsigned long long*)(rb + 16);
-            std::fprintf(stderr, "decode stamps (cycles, sum over workgroups): wait %llu issue %llu A %llu F %llu B %llu end %llu\n",
-                         stp[0], stp[1], stp[2], stp[3], stp[4], stp[5]);
+            std::fprintf(stderr, "decode stamps (cycles, sum over workgroups, wave 0): wait %llu issue %llu pass1 %llu "
+                         "pass2-scan/offsets %llu pass2-copy %llu pass2-other %llu end %llu\n",
+                         stp[0], stp[1], stp[2], stp[3], stp[6], stp[4], stp[5]);
         }
     const unsigned long long* lens = nulls + nbp;
     for (uint32_t b = 0; b < c->nblocks; b++) {

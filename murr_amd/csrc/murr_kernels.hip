@@ -494,54 +494,83 @@ __device__ __forceinline__ uint32_t dec_column(const DecodeArgs& A, const Src& s
     const uint32_t bs = A.bs, abase = (uint32_t)T.abase;
     const uint32_t fo = bs + pc.offset, nbyte = pc.bit >> 3, nbit = pc.bit & 7;
     GAS uint64_t* vwords = gp((uint64_t*)o.validity) + (T.r0 >> 6) + wave;
-    uint32_t nulls = 0;
-    // All KMAX chunks unrolled, unguarded (chunks past the tile have no active
-    // lane): the LDS reads of the chunks overlap instead of forming one chain.
+    // The KMAX chunks advance level by level (row offsets -> null byte and
+    // value / slot -> string length), so each level's LDS reads are all in
+    // flight before the first wait: KMAX independent chains, not one long one.
+    // Every read is unconditional and its use a select (a read inside a branch
+    // costs an exec-mask save/restore and a wait of its own; stage reads at
+    // stale or out-of-range LDS addresses are harmless; HBM reads are pointed
+    // at the tile start when not wanted).  Chunks past the tile have no
+    // active lane.
+    uint32_t ra[KMAX], rl[KMAX];
+    bool act[KMAX], present[KMAX];
 #pragma unroll
     for (uint32_t k = 0; k < KMAX; k++) {
         const uint32_t i = k * kDT + tid;
-        const bool act = i < T.nr;
-        const uint32_t ra = ro[2 * i] - abase;
-        const uint32_t rl = act ? ro[2 * i + 2] - ro[2 * i] : 0;
-        const bool present = rl >= bs && rl != 0;
-        const uint32_t nb = src.u8(Src::kHbm && !present ? 0 : ra + nbyte);
-        const bool isnull = !present || ((nb >> nbit) & 1);
-        const uint64_t vm = __ballot(act && !isnull);
-        nulls += __popcll(__ballot(act && isnull));
-        const bool live = k * kDT + wave * 64 < T.nr;  // wave-uniform
-        if (live && lane == 0) vwords[kDW * k] = vm;
-        bool bad = rl && !present;  // split_at panics on a row shorter than the bitset
-        if constexpr (KIND == 0) {
+        act[k] = i < T.nr;
+        const uint32_t a0 = ro[2 * i], a1 = ro[2 * i + 2];
+        ra[k] = a0 - abase;
+        rl[k] = act[k] ? a1 - a0 : 0;
+        present[k] = rl[k] >= bs && rl[k] != 0;
+    }
+    uint32_t nb[KMAX], v0[KMAX];
+    uint64_t v8[KMAX];
+#pragma unroll
+    for (uint32_t k = 0; k < KMAX; k++) {
+        nb[k] = src.u8(Src::kHbm && !present[k] ? 0 : ra[k] + nbyte);
+        constexpr uint32_t W = KIND == 0 ? 4 : KIND == 1 || KIND == 3 ? 1 : KIND;
+        const uint32_t a = Src::kHbm && !(present[k] && fo + W <= rl[k]) ? 0 : ra[k] + fo;
+        if constexpr (KIND == 8) v8[k] = src.u64(a);
+        else if constexpr (KIND == 4 || KIND == 0) v0[k] = src.u32(a);  // utf8: the slot
+        else if constexpr (KIND == 2) v0[k] = src.head(a, 2);
+        else v0[k] = src.u8(a);
+    }
+    uint32_t len[KMAX];
+    if constexpr (KIND == 0) {
+#pragma unroll
+        for (uint32_t k = 0; k < KMAX; k++) {
             // read_dynamic (read.rs:45-55): slot -> payload offset p (relative to
             // the static region), u32 length at p, bytes at p + 4
-            const uint32_t vlen = rl - bs;
-            const bool s_ok = !isnull && fo + 4 <= rl;
-            const uint32_t prel = src.u32(Src::kHbm && !s_ok ? 0 : ra + fo);
-            const bool p_ok = s_ok && prel <= vlen - 4;
-            const uint32_t l = src.u32(Src::kHbm && !p_ok ? 0 : ra + bs + prel);
-            const bool good = p_ok && l <= vlen - 4 - prel;
+            const bool p_ok = present[k] && fo + 4 <= rl[k] && v0[k] <= rl[k] - bs - 4;
+            len[k] = src.u32(Src::kHbm && !p_ok ? 0 : ra[k] + bs + v0[k]);
+        }
+    }
+    uint32_t nulls = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < KMAX; k++) {
+        const uint32_t i = k * kDT + tid;
+        const bool isnull = !present[k] || ((nb[k] >> nbit) & 1);
+        const uint64_t vm = __ballot(act[k] && !isnull);
+        nulls += __popcll(__ballot(act[k] && isnull));
+        const bool live = k * kDT + wave * 64 < T.nr;  // wave-uniform
+        if (live && lane == 0) vwords[kDW * k] = vm;
+        bool bad = rl[k] && !present[k];  // split_at panics on a row shorter than the bitset
+        if constexpr (KIND == 0) {
+            const uint32_t vlen = rl[k] - bs, prel = v0[k];
+            const bool p_ok = !isnull && fo + 4 <= rl[k] && prel <= vlen - 4;
+            const bool good = p_ok && len[k] <= vlen - 4 - prel;
             bad |= !isnull && !good;
-            const uint32_t slen = good ? l : 0;
-            if (cell) cell[i] = ((uint64_t)slen << 32) | (ra + bs + prel + 4);
+            const uint32_t slen = good ? len[k] : 0;
+            if (cell) cell[i] = ((uint64_t)slen << 32) | (ra[k] + bs + prel + 4);
             const uint32_t tot = wave_total_u32(slen);  // < tile span < 4 GiB
             if (live && lane == 0) pre_u[k * kDW + wave] = tot;
         } else if constexpr (KIND == 1) {
-            const bool have = !isnull && fo + 1 <= rl;
+            const bool have = !isnull && fo + 1 <= rl[k];
             bad |= !isnull && !have;
-            const uint32_t v = src.u8(Src::kHbm && !have ? 0 : ra + fo);
-            const uint64_t m = __ballot(act && have && v != 0);
+            const uint64_t m = __ballot(act[k] && have && v0[k] != 0);
             if (live && lane == 0) gp((uint64_t*)o.values)[(T.r0 >> 6) + kDW * k + wave] = m;
         } else {
             constexpr uint32_t W = KIND == 3 ? 1 : KIND;  // KIND 3 = 1-byte values
-            const bool have = !isnull && fo + W <= rl;
+            const bool have = !isnull && fo + W <= rl[k];
             bad |= !isnull && !have;
-            const uint32_t a = Src::kHbm && !have ? 0 : ra + fo;
-            if (act) {
-                if constexpr (KIND == 8) ((GAS uint64_t*)gp(o.values) + T.r0)[i] = have ? src.u64(a) : 0;
-                if constexpr (KIND == 4) ((GAS uint32_t*)gp(o.values) + T.r0)[i] = have ? src.u32(a) : 0;
-                if constexpr (KIND == 2) ((GAS uint16_t*)gp(o.values) + T.r0)[i] = have ? (uint16_t)src.head(a, 2) : 0;
-                if constexpr (KIND != 8 && KIND != 4 && KIND != 2)
-                    (gp((uint8_t*)o.values) + T.r0)[i] = have ? (uint8_t)src.u8(a) : 0;
+            if constexpr (KIND == 8) {
+                if (act[k]) ((GAS uint64_t*)gp(o.values) + T.r0)[i] = have ? v8[k] : 0;
+            } else if constexpr (KIND == 4) {
+                if (act[k]) ((GAS uint32_t*)gp(o.values) + T.r0)[i] = have ? v0[k] : 0;
+            } else if constexpr (KIND == 2) {
+                if (act[k]) ((GAS uint16_t*)gp(o.values) + T.r0)[i] = have ? (uint16_t)v0[k] : 0;
+            } else {
+                if (act[k]) (gp((uint8_t*)o.values) + T.r0)[i] = have ? (uint8_t)v0[k] : 0;
             }
         }
         *badk |= (uint32_t)bad << k;
@@ -704,6 +733,7 @@ __device__ __forceinline__ void decode_tile(const DecodeArgs& A, const Src& src,
             // (aligned dword reads + alignbyte, unaligned ds_write_b32, then a
             // 0-3 byte tail), noting any non-ASCII byte, kWaveBuf bytes per
             // pass; the wave then stores the range with aligned 16-B stores.
+            dstamp(A, S, 3);
             uint32_t hi_bits = 0;
             const uint32_t d0 = inc - slen;  // my string's start inside the wave range
             if (wn && fits && room && !(A.debug & 1)) {
@@ -735,6 +765,7 @@ __device__ __forceinline__ void decode_tile(const DecodeArgs& A, const Src& src,
 #pragma unroll 1
                 for (uint32_t q = 0; q < slen; q += 4) hi_bits |= src.head(pay + q, slen - q);
             }
+            dstamp(A, S, 6);
             if ((hi_bits & 0x80808080u) && !utf8_valid_slow(src, pay, slen))
                 report(A.err, err_key(T.b, T.r0 + i, p, kStUtf8));
         }
