@@ -1,0 +1,28 @@
+#!/usr/bin/env bash
+# Round profile on one MI355X: rocprofv3 kernel-trace stats of the headline
+# bench, FETCH_SIZE and WRITE_SIZE in separate --pmc passes (never combined with
+# trace domains), then the headline bench line with roofline.traffic filled,
+# plus the side measurements DESIGN.md quotes.  Everything under gpurun_out/$R.
+set -u
+export TMPDIR=/tmp
+R=${R:-r01}
+out=gpurun_out/$R
+mkdir -p $out
+run() {  # run <name> <timeout> <cmd...>
+  local name=$1 t=$2; shift 2
+  timeout -k 10 "$t" "$@" > "$out/$name.log" 2>&1
+  local rc=$?
+  echo "$name exit=$rc"; tail -n 2 "$out/$name.log"
+  [ $rc -eq 0 ] || exit $rc
+}
+run trace 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out/trace -o decode -- python3 bench.py --steps 20 --warmup 3 --no-cpu
+run fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $out/pmc -o fetch -- python3 bench.py --steps 3 --warmup 1 --no-cpu
+run write 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $out/pmc -o write -- python3 bench.py --steps 3 --warmup 1 --no-cpu
+run bench 400 python3 bench.py --pmc-csv "$out/pmc/fetch_counter_collection.csv,$out/pmc/write_counter_collection.csv"
+if [ -z "${QUICK:-}" ]; then
+  run host_B 300 python3 bench.py --mode host --config B --steps 10 --warmup 2
+  run encode_E 300 python3 bench.py --mode encode --steps 10 --warmup 2
+  run decode_C 300 python3 bench.py --config C --blocks 10 --steps 10 --warmup 2 --no-cpu
+  run decode_D 300 python3 bench.py --config D --rows 100000 --blocks 125 --steps 10 --warmup 2 --no-cpu
+  run host_C 300 python3 bench.py --mode host --config C --rows 1000 --steps 50 --warmup 5
+fi
