@@ -728,38 +728,27 @@ __device__ __forceinline__ void decode_tile(const DecodeArgs& A, const Src& src,
             }
             if (!room && act && slen && ws + inc > o.values_cap)
                 report(A.err, err_key(T.b, T.r0 + i, p, kStCapacity));
-            // The wave's 64 consecutive rows own one contiguous output range
-            // [ws, ws+wn): each lane moves its string into the wave's LDS buffer
-            // (aligned dword reads + alignbyte, unaligned ds_write_b32, then a
-            // 0-3 byte tail), noting any non-ASCII byte, kWaveBuf bytes per
-            // pass; the wave then stores the range with aligned 16-B stores.
+            // Each lane stores its own string straight to HBM: dword moves from
+            // the stage (aligned reads + alignbyte) as unaligned global_store_dword
+            // (gfx9 unaligned mode), then a 0-3 byte tail; the L2 merges the
+            // wave's partial lines.  Any non-ASCII byte is noted for the DFA.
             dstamp(A, S, 3);
             uint32_t hi_bits = 0;
-            const uint32_t d0 = inc - slen;  // my string's start inside the wave range
-            if (wn && fits && room && !(A.debug & 1)) {
+            if (fits && room && !(A.debug & 1)) {
+                GAS uint8_t* dst = gp(o.values) + ws + (inc - slen);
+                uint32_t q = 0;
 #pragma unroll 1
-                for (uint32_t w0 = 0; w0 < wn; w0 += kWaveBuf) {
-                    const uint32_t w1 = min(w0 + kWaveBuf, wn);
-                    const uint32_t lo_b = max(d0, w0), hi_b = max(min(d0 + slen, w1), lo_b);
-                    const uint32_t sa = pay - d0;  // source address of output byte 0
-                    uint32_t q = lo_b;
-#pragma unroll 1
-                    for (; q + 4 <= hi_b; q += 4) {
-                        const uint32_t v = src.u32(sa + q);
-                        *(LAS uint32_t*)(wb + (q - w0)) = v;
-                        hi_bits |= v;
-                    }
-                    const uint32_t n = hi_b - q;  // 0..3 tail bytes
-                    if (n) {
-                        const uint32_t v = src.head(sa + q, n);
-                        hi_bits |= v;
-                        LAS uint8_t* dst = wb + (q - w0);
-                        if (n & 2) *(LAS uint16_t*)dst = (uint16_t)v;
-                        if (n & 1) dst[n & 2] = (uint8_t)(v >> (8 * (n & 2)));
-                    }
-                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's LDS writes landed
-                    write_out(wb, gp(o.values), ws + w0, w1 - w0, lane, 64);
-                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done before reuse
+                for (; q + 4 <= slen; q += 4) {
+                    const uint32_t v = src.u32(pay + q);
+                    *(GAS uint32_t*)(dst + q) = v;
+                    hi_bits |= v;
+                }
+                const uint32_t n = slen - q;  // 0..3 tail bytes
+                if (n) {
+                    const uint32_t v = src.head(pay + q, n);
+                    hi_bits |= v;
+                    if (n & 2) *(GAS uint16_t*)(dst + q) = (uint16_t)v;
+                    if (n & 1) dst[q + (n & 2)] = (uint8_t)(v >> (8 * (n & 2)));
                 }
             } else if (slen) {
 #pragma unroll 1
