@@ -10,7 +10,8 @@ import re
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
-LIB_PATH = os.path.join(HERE, "libmurr_codec.so")
+# MURR_LIB: load another build of the same library (the ablation build, tools/)
+LIB_PATH = os.environ.get("MURR_LIB") or os.path.join(HERE, "libmurr_codec.so")
 HEADER = os.path.join(ROOT, "include", "murr_codec.h")
 
 # murr_status_t

@@ -446,7 +446,7 @@ int murr_decode_wait(murr_ctx_t* c, murr_error_t* err) {
         if (std::atoi(dbg) & 8) {
             const unsigned long long* stp = (const unsigned long long*)(rb + 16);
             std::fprintf(stderr, "decode stamps (cycles, sum over workgroups, wave 0): wait %llu issue %llu pass1 %llu "
-                         "pass2-scan/offsets %llu pass2-copy %llu pass2-other %llu end %llu\n",
+                         "pass2-scan/offsets %llu pass2-copy %llu pass2-other %llu pass1-barrier %llu\n",
                          stp[0], stp[1], stp[2], stp[3], stp[6], stp[4], stp[5]);
         }
     const unsigned long long* lens = nulls + nbp;

@@ -54,6 +54,10 @@ struct DecodeArgs {
     uint32_t rows_per_tile;      // multiple of 256
     uint32_t cell_cols;          // utf8 columns whose cells phase A caches in LDS
     uint32_t local;              // 1: block-local mode (a workgroup owns whole blocks)
+    // LDS plan (byte offsets), filled by launch_decode: buffer b of the two
+    // tile buffers starts at b * lds_buf; inside it the chunk prefixes at 0,
+    // the row-offset slice at lds_rowoff, the blob stage at lds_stage.
+    uint32_t lds_rowoff, lds_stage, lds_buf, lds_nulls, lds_w, lds_mine, lds_st, lds_cell, lds_total;
 };
 
 struct EncCol {               // one Arrow input column, segment order

@@ -36,8 +36,13 @@ template <class T> __device__ __forceinline__ const GAS T* gp(const T* p) { retu
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 constexpr uint32_t kUtf8 = 0, kBool = 1;
-constexpr uint32_t kWaveBuf = 1024;  // bytes of strings one wave assembles per pass
 constexpr uint32_t kSpinLimit = 1u << 22;
+// Ablation switches and phase stamps (MURR_DEBUG_DECODE) exist only in a
+// `make DEBUG=1` build; the production kernel carries none of their branches.
+#ifndef MURR_DECODE_DEBUG
+#define MURR_DECODE_DEBUG 0
+#endif
+constexpr bool kDbg = MURR_DECODE_DEBUG != 0;
 enum : uint32_t { kStUtf8 = 1, kStOverflow = 4, kStMalformed = 5, kStCapacity = 6, kStInternal = 10 };
 
 __device__ __forceinline__ void report(unsigned long long* err, uint64_t key) {
@@ -464,14 +469,13 @@ __device__ __forceinline__ uint32_t utf8_cell(const Src& src, uint32_t ra, uint3
 struct DecLds {  // this workgroup's LDS regions besides the tile buffers
     LAS uint32_t* nulls;  // [4][nproj] per-wave null counts of the current tile
     LAS uint64_t* w;      // [4] scratch for window_prefix
-    LAS uint8_t* wbuf;    // 4 x (kWaveBuf + 32) string assembly buffers
     LAS uint64_t* mine;   // [4][nutf8] per wave: the last inclusive prefix
     LAS uint64_t* st;     // [8] diagnostic stamps
     LAS uint64_t* cell;   // [cell_cols][R] (slen << 32 | payload address)
 };
 
 __device__ __forceinline__ void dstamp(const DecodeArgs& A, const DecLds& S, int j) {
-    if ((A.debug & 8) && tidx() == 0) {
+    if (kDbg && (A.debug & 8) && tidx() == 0) {
         const uint64_t t = __builtin_amdgcn_s_memtime();
         S.st[j] += t - S.st[7];
         S.st[7] = t;
@@ -641,36 +645,23 @@ __device__ __forceinline__ void decode_tile(const DecodeArgs& A, const Src& src,
             }
         }
     }
-    if (A.nutf8) {
-        lds_barrier();
-        if (wave == 0) {  // chunk totals -> exclusive prefixes, aggregate at [nchunk]
-#pragma unroll 1
-            for (uint32_t u = 0; u < A.nutf8; u++) {
-                LAS uint32_t* pu = pre + u * PS;
-                const uint32_t v = lane < nchunk ? pu[lane] : 0;  // nchunk <= 16
-                const uint32_t inc = wave_scan_u32(v);
-                if (lane < nchunk) pu[lane] = inc - v;
-                const uint32_t agg = __builtin_amdgcn_readlane(inc, 63);
-                if (lane == 0) {
-                    pu[nchunk] = agg;
-                    if (!A.local) publish(A.lookback + (uint64_t)u * A.total_tiles + T.t, (uint64_t)agg + 1);
-                }
-            }
-        }
-        lds_barrier();  // every wave reads the prefixes in pass 2
-    }
     dstamp(A, S, 2);
     if (!A.nutf8) return;
+    lds_barrier();  // every wave's chunk totals are in LDS
+    dstamp(A, S, 5);
 
     // ---- pass 2: per utf8 column: cross-tile prefix, offsets, string bytes ----
-    LAS uint8_t* wb = S.wbuf + wave * (kWaveBuf + 32);
 #pragma unroll 1
     for (uint32_t p = 0; p < nproj; p++) {
         const DecProj pc = ldproj(A, p);
         if (!pc.is_utf8) continue;
         const DecOut o = ldout(A, (uint64_t)T.b * nproj + p);
+        // Every wave scans the (<= 32) chunk totals itself: no further barrier.
         const LAS uint32_t* pu = pre + pc.uslot * PS;
-        const uint32_t agg = sgpr(pu[nchunk]);
+        const uint32_t ctot = lane < nchunk ? pu[lane] : 0;
+        const uint32_t cinc = wave_scan_u32(ctot);
+        const uint32_t agg = __builtin_amdgcn_readlane(cinc, 63);
+        if (!A.local && tid == 0) publish(A.lookback + (uint64_t)pc.uslot * A.total_tiles + T.t, (uint64_t)agg + 1);
         // Block-local mode: this workgroup decodes the whole block in tile
         // order, so the prefix is its own running sum.  Window mode: its own
         // inclusive prefix of tile t - G (same block) plus the aggregates of the
@@ -684,7 +675,7 @@ __device__ __forceinline__ void decode_tile(const DecodeArgs& A, const Src& src,
             const bool have_prev = T.t >= T.tfirst + G;
             const uint64_t lo = have_prev ? T.t - G + 1 : T.tfirst;
             const uint64_t* st = A.lookback + (uint64_t)pc.uslot * A.total_tiles;
-            prefix = sgpr64((A.debug & 2) ? 0 : window_prefix<kDW>(st, lo, T.t, have_prev ? *mine : 0, S.w, A.err,
+            prefix = sgpr64((kDbg && (A.debug & 2)) ? 0 : window_prefix<kDW>(st, lo, T.t, have_prev ? *mine : 0, S.w, A.err,
                                                                err_key(T.b, T.r0, p, 0)));
         }
         if (lane == 0) *mine = prefix + agg;
@@ -715,8 +706,8 @@ __device__ __forceinline__ void decode_tile(const DecodeArgs& A, const Src& src,
             }
             slen = act ? slen : 0;
             const uint32_t inc = wave_scan_u32(slen);  // < tile span < 4 GiB
-            const uint64_t ws = prefix + sgpr(pu[c]);      // this wave chunk's output start
-            const uint32_t wn = sgpr(pu[c + 1] - pu[c]);   // and its byte count
+            const uint32_t wn = __builtin_amdgcn_readlane(ctot, c);       // this chunk's bytes
+            const uint64_t ws = prefix + (__builtin_amdgcn_readlane(cinc, c) - wn);  // and output start
             const bool fits = ws + wn <= 0x7FFFFFFFull;    // every i32 offset representable
             const bool room = ws + wn <= o.values_cap;
             if (fits) {
@@ -734,7 +725,7 @@ __device__ __forceinline__ void decode_tile(const DecodeArgs& A, const Src& src,
             // wave's partial lines.  Any non-ASCII byte is noted for the DFA.
             dstamp(A, S, 3);
             uint32_t hi_bits = 0;
-            if (fits && room && !(A.debug & 1)) {
+            if (fits && room && !(kDbg && (A.debug & 1))) {
                 GAS uint8_t* dst = gp(o.values) + ws + (inc - slen);
                 uint32_t q = 0;
 #pragma unroll 1
@@ -770,7 +761,6 @@ __device__ __forceinline__ void decode_tile_hbm(const DecodeArgs& A, const DecTi
 }
 
 // LDS (dynamic): [buffer 0][buffer 1][nulls: nproj u32][w: 4 u64]
-//                [wave string buffers: 4 x (kWaveBuf + 32) when utf8 is projected]
 //                [mine: 4 x nutf8 u64][st: 8 u64][cell: cell_cols x R u64]
 // The arguments are re-read from the kernarg segment every tile (s_load, K$
 // hits) instead of being held in SGPRs across the loop: with ~30 argument
@@ -784,18 +774,30 @@ __device__ __forceinline__ DecodeArgs load_args() {
     A.total_tiles = ap->total_tiles; A.nblocks = ap->nblocks; A.nproj = ap->nproj; A.nutf8 = ap->nutf8;
     A.bs = ap->bs; A.cap = ap->cap; A.stage = ap->stage; A.debug = ap->debug;
     A.rows_per_tile = ap->rows_per_tile; A.cell_cols = ap->cell_cols; A.local = ap->local;
+    A.lds_rowoff = ap->lds_rowoff; A.lds_stage = ap->lds_stage; A.lds_buf = ap->lds_buf;
+    A.lds_nulls = ap->lds_nulls; A.lds_w = ap->lds_w; A.lds_mine = ap->lds_mine; A.lds_st = ap->lds_st;
+    A.lds_cell = ap->lds_cell; A.lds_total = ap->lds_total;
+    // every field above: a new DecodeArgs member must be copied here too
+    static_assert(sizeof(DecodeArgs) == 160, "load_args: copy every DecodeArgs field (10 x 8 B + 19 x 4 B)");
     return A;
 }
 
-__device__ __forceinline__ DecLds dec_lds(const DecodeArgs& A, LAS uint8_t* lds, const DecLayout& L) {
-    const uint32_t np16 = (4 * kDW * A.nproj + 15) & ~15u;
+__device__ __forceinline__ DecLayout dec_plan(const DecodeArgs& A) {
+    DecLayout L;
+    L.pre = 0;
+    L.rowoff = A.lds_rowoff;
+    L.stage = A.lds_stage;
+    L.bytes = A.lds_buf;
+    return L;
+}
+
+__device__ __forceinline__ DecLds dec_lds(const DecodeArgs& A, LAS uint8_t* lds, const DecLayout&) {
     DecLds S;
-    S.nulls = (LAS uint32_t*)(lds + 2 * L.bytes);
-    S.w = (LAS uint64_t*)(lds + 2 * L.bytes + np16);
-    S.wbuf = lds + 2 * L.bytes + np16 + 8 * kDW;
-    S.mine = (LAS uint64_t*)(S.wbuf + (A.nutf8 ? kDW * (kWaveBuf + 32) : 0));
-    S.st = S.mine + kDW * A.nutf8;
-    S.cell = S.st + 8;
+    S.nulls = (LAS uint32_t*)(lds + A.lds_nulls);
+    S.w = (LAS uint64_t*)(lds + A.lds_w);
+    S.mine = (LAS uint64_t*)(lds + A.lds_mine);
+    S.st = (LAS uint64_t*)(lds + A.lds_st);
+    S.cell = (LAS uint64_t*)(lds + A.lds_cell);
     return S;
 }
 
@@ -808,7 +810,7 @@ __global__ void __launch_bounds__(kDT) decode_kernel(DecodeArgs A0) {
     TileRef cur, nxt;
     {
         const DecodeArgs A = load_args();
-        const DecLayout L = dec_layout(A.rows_per_tile, A.nutf8, A.stage);
+        const DecLayout L = dec_plan(A);
         const DecLds S = dec_lds(A, lds, L);
         if (tid < 8) S.st[tid] = tid == 7 ? __builtin_amdgcn_s_memtime() : 0;
         for (uint32_t p = tid; p < kDW * A.nproj; p += kDT) S.nulls[p] = 0;
@@ -819,7 +821,7 @@ __global__ void __launch_bounds__(kDT) decode_kernel(DecodeArgs A0) {
     }
     for (uint32_t i = 0; cur.ok; i++) {
         const DecodeArgs A = load_args();
-        const DecLayout L = dec_layout(A.rows_per_tile, A.nutf8, A.stage);
+        const DecLayout L = dec_plan(A);
         const DecLds S = dec_lds(A, lds, L);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA for `cur` landed
         __syncthreads();                                  // ... and every other wave's
@@ -835,32 +837,32 @@ __global__ void __launch_bounds__(kDT) decode_kernel(DecodeArgs A0) {
                 report(A.err, err_key(T.b, T.r0, 0, kStMalformed));
                 for (uint32_t u = 0; u < A.nutf8; u++) publish(A.lookback + (uint64_t)u * A.total_tiles + T.t, 1);
             }
-        } else if (A.debug & 4) {
+        } else if (kDbg && (A.debug & 4)) {
             // ablation: staging only
         } else if (span <= A.stage) {
             decode_tile<KMAX>(A, StageSrc{buf + L.stage}, T, buf, L, S);
         } else {
             decode_tile_hbm<KMAX>(A, T, buf, L, S);
         }
-        lds_barrier();
-        for (uint32_t p = tid; p < A.nproj; p += kDT) {
-            uint32_t v = 0;
-#pragma unroll
-            for (uint32_t w = 0; w < kDW; w++) v += S.nulls[w * A.nproj + p];
-            if (v) {
-                __hip_atomic_fetch_add(gp(A.nulls) + (uint64_t)T.b * A.nproj + p, (unsigned long long)v,
-                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#pragma unroll
-                for (uint32_t w = 0; w < kDW; w++) S.nulls[w * A.nproj + p] = 0;
+        // Each wave flushes its own null counters when its block changes (or
+        // at the end): wave-private LDS, so no barrier.
+        if (!nxt.ok || nxt.b != cur.b) {
+            LAS uint32_t* wn = S.nulls + (tid >> 6) * A.nproj;
+            for (uint32_t p = tid & 63; p < A.nproj; p += 64) {
+                const uint32_t v = wn[p];
+                if (v) {
+                    __hip_atomic_fetch_add(gp(A.nulls) + (uint64_t)T.b * A.nproj + p, (unsigned long long)v,
+                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    wn[p] = 0;
+                }
             }
         }
         cur = nxt;
         nxt = nn;
-        dstamp(A, S, 5);
     }
     const DecodeArgs A = load_args();
-    const DecLds S = dec_lds(A, lds, dec_layout(A.rows_per_tile, A.nutf8, A.stage));
-    if ((A.debug & 8) && tid == 0)
+    const DecLds S = dec_lds(A, lds, dec_plan(A));
+    if (kDbg && (A.debug & 8) && tid == 0)
         for (int j = 0; j < 7; j++) __hip_atomic_fetch_add(gp(A.stamps) + j, (unsigned long long)S.st[j],
                                                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -983,16 +985,38 @@ __global__ void __launch_bounds__(256) encode_kernel(EncodeArgs A) {
 
 }  // namespace
 
-uint32_t decode_lds_bytes(uint32_t stage, uint32_t nproj, uint32_t nutf8, uint32_t rows_per_tile,
-                          uint32_t cell_cols) {
-    const DecLayout L = dec_layout(rows_per_tile, nutf8, stage);
-    return 2 * L.bytes + ((4 * kDW * nproj + 15) & ~15u) + 8 * kDW + (nutf8 ? kDW * (kWaveBuf + 32) : 0) +
-           8 * kDW * nutf8 + 64 +
-           8 * rows_per_tile * cell_cols;
+// The LDS plan of a launch (DecodeArgs::lds_*): two tile buffers, then the
+// per-wave null counters, the window scratch, the per-wave running prefixes,
+// the diagnostic stamps and the utf8 cell cache.
+void decode_lds_plan(DecodeArgs& a) {
+    const DecLayout L = dec_layout(a.rows_per_tile, a.nutf8, a.stage);
+    a.lds_rowoff = L.rowoff;
+    a.lds_stage = L.stage;
+    a.lds_buf = L.bytes;
+    a.lds_nulls = 2 * L.bytes;
+    a.lds_w = a.lds_nulls + ((4 * kDW * a.nproj + 15) & ~15u);
+    a.lds_mine = a.lds_w + 8 * kDW;
+    a.lds_st = a.lds_mine + 8 * kDW * a.nutf8;
+    a.lds_cell = a.lds_st + 64;
+    a.lds_total = a.lds_cell + 8 * a.rows_per_tile * a.cell_cols;
 }
 
-hipError_t launch_decode(const DecodeArgs& a, uint32_t grid, hipStream_t s) {
-    const uint32_t lds = decode_lds_bytes(a.stage, a.nproj, a.nutf8, a.rows_per_tile, a.cell_cols);
+uint32_t decode_lds_bytes(uint32_t stage, uint32_t nproj, uint32_t nutf8, uint32_t rows_per_tile,
+                          uint32_t cell_cols) {
+    DecodeArgs a{};
+    a.stage = stage;
+    a.nproj = nproj;
+    a.nutf8 = nutf8;
+    a.rows_per_tile = rows_per_tile;
+    a.cell_cols = cell_cols;
+    decode_lds_plan(a);
+    return a.lds_total;
+}
+
+hipError_t launch_decode(const DecodeArgs& a0, uint32_t grid, hipStream_t s) {
+    DecodeArgs a = a0;
+    decode_lds_plan(a);
+    const uint32_t lds = a.lds_total;
     switch (a.rows_per_tile / kDT) {
     case 1: hipLaunchKernelGGL(decode_kernel<1>, dim3(grid), dim3(kDT), lds, s, a); break;
     case 2: hipLaunchKernelGGL(decode_kernel<2>, dim3(grid), dim3(kDT), lds, s, a); break;
