@@ -302,12 +302,13 @@ int murr_decode_enqueue(murr_ctx_t* c, const murr_segment_t* seg, const uint32_t
         dp[p] = DecProj{col.dtype, col.index, col.offset, col.size, col.dtype == MURR_UTF8, 0};
         if (col.dtype == MURR_UTF8) dp[p].uslot = nutf8++;
     }
-    // Tile shape: as many rows per thread (1..8) as keep a tile's blob bytes
-    // inside the LDS stage, from the data_bytes hints (or a schema estimate).
-    uint64_t hint_bytes = 0, hint_rows = 0, all_rows = 0;
+    // Tile shape: NW waves x KC 64-row chunks per wave.  The largest tile whose
+    // two LDS buffers (row-offset slice + blob stage, +25 % for row-size
+    // variance) fit the per-workgroup budget, from the data_bytes hints (or a
+    // schema estimate); a tile that still outgrows its stage is decoded from HBM.
+    uint64_t hint_bytes = 0, hint_rows = 0;
     bool hinted = true;
     for (uint32_t b = 0; b < nblocks; b++) {
-        all_rows += blocks[b].n_rows;
         if (blocks[b].n_rows && !blocks[b].data_bytes) hinted = false;
         hint_bytes += blocks[b].data_bytes;
         hint_rows += blocks[b].n_rows;
@@ -315,19 +316,56 @@ int murr_decode_enqueue(murr_ctx_t* c, const murr_segment_t* seg, const uint32_t
     double est_row = (double)seg->bitset_size + seg->capacity;
     for (uint32_t i = 0; i < seg->ncols; i++) est_row += seg->cols[i].dtype == MURR_UTF8 ? 20.0 : 0.0;
     if (hinted && hint_rows) est_row = (double)hint_bytes / (double)hint_rows;
-    // Rows per tile (multiple of 256): the largest up to 2048 whose staged blob
-    // bytes (+25 % for row-size variance) and row offsets fit ~32 KiB; two such
-    // buffers per workgroup (loader one tile ahead).
-    const double per_row = est_row * 1.25 + 8.0;
-    uint32_t rows = kDT;
-    double tile_bytes = 32768.0;
-    if (const char* e = std::getenv("MURR_DECODE_TILE_BYTES")) tile_bytes = std::atof(e);  // tuning
-    while (rows < 4 * kDT && 2.0 * rows * per_row <= tile_bytes) rows *= 2;
-    uint32_t stage = (uint32_t)std::max<uint64_t>(4096, round_up((uint64_t)(rows * est_row * 1.25) + 64, 1024));
-    stage = std::min<uint32_t>(stage, 65536);
-    // pass-1 cell cache: up to 16 KiB of (length, payload) pairs
-    const uint32_t cell_cols = std::min<uint32_t>(nutf8, 16384 / (8 * rows));
-    const uint32_t lds = decode_lds_bytes(stage, nproj, nutf8, rows, cell_cols);
+    // Per workgroup (NW waves: NW-1 consumers + 1 loader) a ring of S slots of
+    // one fill each (F = 64 * KC * (NW-1) rows), P fills in flight:
+    // (P-1) * E <= 63 (the loader's vmcnt field), S = P + 2, and the look-back
+    // window (64 sub-tiles) must cover every sub-tile in flight:
+    // (NW-1) * S < 64.  Take the first shape whose ring fits the LDS budget
+    // with P >= 3 (else >= 2).
+    double budget = 81920.0;  // bytes of LDS per workgroup (2 workgroups per CU)
+    if (const char* e = std::getenv("MURR_DECODE_LDS")) budget = std::atof(e);  // tuning
+    static const uint32_t shapes[][2] = {{8, 1}, {4, 2}, {8, 2}, {4, 4}, {4, 1}};
+    uint32_t nw = 4, kc = 1, stage = 4096, depth = 2, slots = 4;
+    auto plan = [&](uint32_t w, uint32_t k, uint32_t want_p, uint32_t* p_out, uint32_t* s_out, uint32_t* st_out) {
+        const double f = 64.0 * k * (w - 1);
+        uint32_t st = (uint32_t)round_up((uint64_t)(f * est_row * 1.25) + 64, 1024);
+        st = std::min<uint32_t>(std::max<uint32_t>(st, 1024), 61440);
+        const uint32_t ro = (uint32_t)round_up(8 * (uint64_t)(f + 1) + 16, 16);
+        const uint32_t E = 1 + (ro + 1023) / 1024 + st / 1024;
+        if (E > 63) return false;
+        uint32_t p = std::min<uint32_t>(want_p, 1 + 63 / E);
+        const uint32_t slot = 64 + ro + st + 32;
+        for (; p >= 2; p--) {
+            const uint32_t s = p + 2;
+            if ((w - 1) * s >= 64) continue;
+            const double lds = (double)s * slot + 2048.0 + 2048.0 * nutf8 + 16.0 * s * nutf8 + 4.0 * w * nproj;
+            if (lds <= budget) { *p_out = p; *s_out = s; *st_out = st; return true; }
+        }
+        return false;
+    };
+    uint32_t want_p = 8;
+    if (const char* e = std::getenv("MURR_DECODE_DEPTH")) want_p = (uint32_t)std::max(2, std::atoi(e));
+    bool found = false;
+    for (uint32_t minp : {3u, 2u}) {
+        for (const auto& sh : shapes) {
+            uint32_t p, s, st;
+            if (plan(sh[0], sh[1], want_p, &p, &s, &st) && p >= minp) {
+                nw = sh[0]; kc = sh[1]; depth = p; slots = s; stage = st; found = true;
+                break;
+            }
+        }
+        if (found) break;
+    }
+    if (const char* e = std::getenv("MURR_DECODE_SHAPE")) {  // tuning: "NWxKC"
+        uint32_t w = 0, k = 0, p, s, st;
+        if (std::sscanf(e, "%ux%u", &w, &k) == 2 && decode_shape_ok(w, k) && plan(w, k, want_p, &p, &s, &st)) {
+            nw = w; kc = k; depth = p; slots = s; stage = st; found = true;
+        }
+    }
+    if (!found) {  // very wide rows: the smallest ring; fills past the stage go to HBM
+        nw = 4; kc = 1; depth = 2; slots = 4; stage = 16384;
+    }
+    const uint32_t rows = 64 * kc * (nw - 1);
     const uint64_t R = rows;
     std::vector<DecBlock> db(nblocks);
     uint64_t tiles = 0;
@@ -352,14 +390,18 @@ int murr_decode_enqueue(murr_ctx_t* c, const murr_segment_t* seg, const uint32_t
         dout[i] = DecOut{(uint8_t*)outs[i].values, outs[i].validity, outs[i].offsets, outs[i].values_cap};
 
     const uint64_t nbp = (uint64_t)nblocks * nproj;
-    const uint64_t z_err = 0, z_stamps = 16, z_nulls = 80, z_lens = z_nulls + 8 * nbp, z_lb = z_lens + 8 * nbp;
+    const uint64_t z_err = 0, z_nulls = 80, z_lens = z_nulls + 8 * nbp, z_lb = z_lens + 8 * nbp;
     const uint64_t zbytes = round_up(z_lb + 8 * (uint64_t)nutf8 * tiles, 16);
     const uint64_t d_blocks = zbytes, d_proj = round_up(d_blocks + sizeof(DecBlock) * nblocks, 16);
     const uint64_t d_outs = round_up(d_proj + sizeof(DecProj) * nproj, 16);
-    // Persistent grid: workgroups that are certainly co-resident (the occupancy
-    // answer, one fewer when it is >= 4: MI355X_MICROARCH.md "Residency").
-    // The occupancy API answer (LDS-limited here), capped at 6 per CU.
-    int bpc = std::max(1, std::min(decode_blocks_per_cu(lds, rows), 6));
+    DecodeArgs a{};
+    a.nproj = nproj;
+    a.nutf8 = nutf8;
+    a.stage = stage;
+    decode_lds_plan(a, nw, kc, slots, depth);
+    const uint32_t lds = a.lds_total;
+    // Persistent grid: the occupancy answer (LDS-limited here), capped at 6 per CU.
+    int bpc = std::max(1, std::min(decode_blocks_per_cu(nw, kc, lds), 6));
     uint64_t grid = std::min<uint64_t>(std::max<uint64_t>(tiles, 1), (uint64_t)c->cus * bpc);
     // Block-local mode when every workgroup gets whole blocks: no cross-tile
     // prefix protocol at all.  Otherwise tiles round-robin + window prefix.
@@ -367,12 +409,12 @@ int murr_decode_enqueue(murr_ctx_t* c, const murr_segment_t* seg, const uint32_t
     for (uint32_t b = 0; b < nblocks; b++) nonempty += blocks[b].n_rows != 0;
     const bool local = nonempty >= grid || std::getenv("MURR_DECODE_LOCAL") != nullptr;
     if (local) grid = std::max<uint64_t>(1, std::min<uint64_t>(grid, nonempty));
-    const uint64_t d_prev = round_up(d_outs + sizeof(DecOut) * dout.size(), 16);
-    const uint64_t dend = round_up(d_prev + 8 * grid * nutf8, 16);
+    const uint64_t d_end_desc = round_up(d_outs + sizeof(DecOut) * dout.size(), 16);
+    const uint64_t dend = d_end_desc;
     int st = ensure_ws(c, dend, err);
     if (st) return st;
     // host scratch: [descriptors (dend - zbytes)] [readback z_lb bytes]
-    const uint64_t hdesc = d_prev - zbytes, rb = round_up(dend - zbytes, 64);
+    const uint64_t hdesc = d_end_desc - zbytes, rb = round_up(dend - zbytes, 64);
     st = ensure_hs(c, rb + z_lb, err);
     if (st) return st;
     std::memcpy(c->hs + (d_blocks - zbytes), db.data(), sizeof(DecBlock) * nblocks);
@@ -388,35 +430,24 @@ int murr_decode_enqueue(murr_ctx_t* c, const murr_segment_t* seg, const uint32_t
                 if (dp[p].is_utf8 && outs[(uint64_t)b * nproj + p].offsets)
                     HIPC(hipMemsetAsync(outs[(uint64_t)b * nproj + p].offsets, 0, 4, c->stream));
 
-    DecodeArgs a{};
     a.blocks = (const DecBlock*)(c->ws + d_blocks);
     a.proj = (const DecProj*)(c->ws + d_proj);
     a.outs = (const DecOut*)(c->ws + d_outs);
     a.lookback = (uint64_t*)(c->ws + z_lb);
-    a.prev = (uint64_t*)(c->ws + d_prev);
     a.nulls = (unsigned long long*)(c->ws + z_nulls);
     a.lens = (unsigned long long*)(c->ws + z_lens);
     a.err = (unsigned long long*)(c->ws + z_err);
-    a.stamps = (unsigned long long*)(c->ws + z_stamps);
     a.total_tiles = tiles;
     a.nblocks = nblocks;
-    a.nproj = nproj;
-    a.nutf8 = nutf8;
     a.bs = seg->bitset_size;
-    a.cap = seg->capacity;
-    a.stage = stage;
-    a.rows_per_tile = rows;
-    a.cell_cols = cell_cols;
     a.local = local ? 1 : 0;
-    {
-        const char* dbg = std::getenv("MURR_DEBUG_DECODE");  // ablation only
-        a.debug = dbg ? (uint32_t)std::atoi(dbg) : 0;
-        if (a.debug & 8)
-            std::fprintf(stderr, "decode launch: grid %llu (%d/CU) tiles %llu rows/tile %u stage %u lds %u cell_cols %u local %d\n",
-                         (unsigned long long)grid, bpc, (unsigned long long)tiles, rows, stage, lds, cell_cols, (int)local);
-    }
+    for (uint32_t p = 0, u = 0; p < nproj; p++)
+        if (dp[p].is_utf8 && u < 2) a.ufix[u++] = p;
+    if (std::getenv("MURR_DECODE_VERBOSE"))
+        std::fprintf(stderr, "decode launch: grid %llu (%d/CU) tiles %llu shape %ux%u rows/tile %u stage %u slots %u depth %u lds %u local %d\n",
+                     (unsigned long long)grid, bpc, (unsigned long long)tiles, nw, kc, rows, a.stage, slots, depth, lds, (int)local);
     HIPC(hipEventRecord(c->k0, c->stream));
-    if (tiles) HIPC(launch_decode(a, (uint32_t)grid, c->stream));
+    if (tiles) HIPC(launch_decode(a, nw, kc, (uint32_t)grid, c->stream));
     HIPC(hipEventRecord(c->k1, c->stream));
     c->timed = true;
     HIPC(hipMemcpyAsync(c->hs + rb, c->ws, z_lb, hipMemcpyDeviceToHost, c->stream));
@@ -442,13 +473,14 @@ int murr_decode_wait(murr_ctx_t* c, murr_error_t* err) {
     std::memcpy(&word, rb, 8);
     const uint64_t nbp = (uint64_t)c->nblocks * c->nproj;
     const unsigned long long* nulls = (const unsigned long long*)(rb + 80);
-    if (const char* dbg = std::getenv("MURR_DEBUG_DECODE"))
-        if (std::atoi(dbg) & 8) {
-            const unsigned long long* stp = (const unsigned long long*)(rb + 16);
-            std::fprintf(stderr, "decode stamps (cycles, sum over workgroups, wave 0): wait %llu issue %llu pass1 %llu "
-                         "pass2-scan/offsets %llu pass2-copy %llu pass2-other %llu pass1-barrier %llu\n",
-                         stp[0], stp[1], stp[2], stp[3], stp[6], stp[4], stp[5]);
-        }
+    if (std::getenv("MURR_DECODE_VERBOSE")) {  // phase stamps of a MURR_ABLATE & 8 build
+        const unsigned long long* stp = (const unsigned long long*)(rb + 16);
+        if (stp[0] | stp[4])
+            std::fprintf(stderr, "stamps (Gcycles, sum over waves): loader free-spin %.3f issue %.3f vmcnt %.3f other %.3f | "
+                         "consumer ready-spin %.3f passA %.3f lookback %.3f passB+rest %.3f\n",
+                         stp[0] * 1e-9, stp[1] * 1e-9, stp[2] * 1e-9, stp[3] * 1e-9, stp[4] * 1e-9, stp[5] * 1e-9,
+                         stp[6] * 1e-9, stp[7] * 1e-9);
+    }
     const unsigned long long* lens = nulls + nbp;
     for (uint32_t b = 0; b < c->nblocks; b++) {
         for (uint32_t p = 0; p < c->nproj; p++) {

@@ -8,8 +8,6 @@ namespace murr {
 
 // Threads per encode workgroup (4 waves).
 constexpr uint32_t kTile = 256;
-// Decode workgroup: kDW waves (kDT threads); a decode tile is kDT * KMAX rows.
-constexpr uint32_t kDW = 8, kDT = 64 * kDW;
 // Bytes of assembled rows an encode tile stages through LDS.  Tiles whose
 // byte span exceeds the stage read / write HBM directly (the "global" path).
 constexpr uint32_t kStage = 32768;
@@ -42,22 +40,26 @@ struct DecodeArgs {
     const DecBlock* blocks;
     const DecProj* proj;
     const DecOut* outs;          // [nblocks * nproj]
-    uint64_t* lookback;          // [nutf8 * total_tiles] tile aggregates + 1
-    uint64_t* prev;              // [grid * nutf8] each workgroup's last inclusive prefix
+    uint64_t* lookback;          // [nutf8 * total_tiles] tile aggregates + 1 (window mode)
     unsigned long long* nulls;   // [nblocks * nproj]
     unsigned long long* lens;    // [nblocks * nproj] utf8 data bytes
     unsigned long long* err;     // max of ~key (0 = no error)
-    unsigned long long* stamps;  // [8] cycle sums per phase (MURR_DEBUG_DECODE & 8 only)
     uint64_t total_tiles;
-    uint32_t nblocks, nproj, nutf8, bs, cap, stage;
-    uint32_t debug;              // ablation switches (MURR_DEBUG_DECODE), 0 in production
-    uint32_t rows_per_tile;      // multiple of 256
-    uint32_t cell_cols;          // utf8 columns whose cells phase A caches in LDS
+    uint32_t nblocks, nproj, nutf8, bs;
+    uint32_t stage;              // blob bytes a slot stages (multiple of 1 KiB)
+    uint32_t rows_per_tile;      // rows per fill: 64 * chunks per sub-tile * consumer waves
     uint32_t local;              // 1: block-local mode (a workgroup owns whole blocks)
-    // LDS plan (byte offsets), filled by launch_decode: buffer b of the two
-    // tile buffers starts at b * lds_buf; inside it the chunk prefixes at 0,
-    // the row-offset slice at lds_rowoff, the blob stage at lds_stage.
-    uint32_t lds_rowoff, lds_stage, lds_buf, lds_nulls, lds_w, lds_mine, lds_st, lds_cell, lds_total;
+    uint32_t ufix[2];            // projection index of utf8 columns 0 and 1
+    // loader ring: slots, fills in flight, LDS-DMA instructions per fill
+    // (row offsets, blob stage), bytes per slot
+    uint32_t nslots, depth, dro, dst, slot_bytes;
+    // LDS plan (byte offsets), filled by decode_lds_plan: inside a slot the
+    // row-offset slice at lds_ro and the stage at lds_stage; after the slots
+    // the ready flags / free counters, span ring, look-back ring (flags,
+    // aggregates, inclusive prefixes), per-wave null counters, a DMA scratch
+    // and the per-slot fill aggregates of window mode (sums, counters).
+    uint32_t lds_ro, lds_stage, lds_ready, lds_free, lds_span, lds_lbf, lds_lba, lds_lbi, lds_nulls, lds_scratch,
+        lds_fa, lds_fc, lds_total;
 };
 
 struct EncCol {               // one Arrow input column, segment order
@@ -87,11 +89,11 @@ __host__ __device__ inline uint64_t err_key(uint64_t block, uint64_t row, uint32
     return (block << 46) | (row << 14) | ((uint64_t)(col & 0x3FF) << 4) | (status & 0xF);
 }
 
-uint32_t decode_lds_bytes(uint32_t stage, uint32_t nproj, uint32_t nutf8, uint32_t rows_per_tile,
-                          uint32_t cell_cols);
-hipError_t launch_decode(const DecodeArgs& a, uint32_t grid, hipStream_t s);
+void decode_lds_plan(DecodeArgs& a, uint32_t nw, uint32_t kc, uint32_t slots, uint32_t depth);
+bool decode_shape_ok(uint32_t nw, uint32_t kc);
+hipError_t launch_decode(const DecodeArgs& a, uint32_t nw, uint32_t kc, uint32_t grid, hipStream_t s);
+int decode_blocks_per_cu(uint32_t nw, uint32_t kc, uint32_t lds);
 hipError_t launch_encode(const EncodeArgs& a, uint32_t grid, hipStream_t s);
-int decode_blocks_per_cu(uint32_t lds, uint32_t rows_per_tile);
 int encode_blocks_per_cu();
 
 }  // namespace murr

@@ -1,7 +1,11 @@
+#!/usr/bin/env bash
+# Decode ablations (make -C murr_amd/csrc ablate): kernel ms of the headline
+# bench with parts of the work switched off (MURR_ABLATE in murr_decode.hip).
 set -u
 mkdir -p gpurun_out
-for cfg in "0 0" "1 0" "0,1 0" "1 1" "1 2" "1 3"; do
-  set -- $cfg
-  MURR_DEBUG_DECODE=$2 timeout -k 10 120 python bench.py --steps 5 --warmup 1 --no-cpu --proj $1 ${EXTRA:-} > gpurun_out/abl.log 2>&1 || exit $?
-  python -c "import json;d=json.load(open('gpurun_out/abl.log'));print('proj=$1 dbg=$2', d['roofline']['kernel_ms_avg'], d['roofline']['achieved'])"
+for v in ${VARIANTS:-prod 1 2 4 7}; do
+  lib=murr_amd/libmurr_codec.so; [ "$v" != prod ] && lib=murr_amd/libmurr_codec_abl$v.so
+  MURR_LIB=$(pwd)/$lib timeout -k 10 120 python bench.py --steps 5 --warmup 1 --no-cpu ${ARGS:-} \
+    > gpurun_out/ab.log 2> gpurun_out/ab.err || { echo "variant $v failed"; tail -5 gpurun_out/ab.err; exit 1; }
+  python3 -c "import json;d=json.load(open('gpurun_out/ab.log'));print('ablate=$v', d['roofline']['kernel_ms_avg'], 'ms', d['roofline']['achieved'], 'GB/s')"
 done

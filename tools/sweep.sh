@@ -1,11 +1,15 @@
+#!/usr/bin/env bash
+# Decode tile-shape / LDS-budget sweep on one MI355X: kernel ms and achieved
+# GB/s of the headline bench per setting.  SHAPES: "NWxKC" list ("auto" = the
+# host's choice); LDSB: per-workgroup LDS budgets; ARGS: extra bench.py args.
 set -u
 mkdir -p gpurun_out
-for tb in ${TBS:-16384 32768}; do
-for cfg in ${CFGS:-"0,1:0" "0:0" "0,1:4" "0,1:8"}; do
-  pj=${cfg%%:*}; dbg=${cfg##*:}
-  lib=murr_amd/libmurr_codec.so; [ "$dbg" != 0 ] && lib=murr_amd/libmurr_codec_dbg.so
-  MURR_LIB=$(pwd)/$lib MURR_DECODE_TILE_BYTES=$tb MURR_DEBUG_DECODE=$dbg timeout -k 10 120 python bench.py --steps 5 --warmup 1 --no-cpu --proj $pj > gpurun_out/abl.log 2>gpurun_out/abl.err || exit $?
-  python -c "import json;d=json.load(open('gpurun_out/abl.log'));print('tile=$tb proj=$pj dbg=$dbg', d['roofline']['kernel_ms_avg'], d['roofline']['achieved'])"
-  if [ "$dbg" = 8 ]; then tail -1 gpurun_out/abl.err; fi
+for lds in ${LDSB:-40960}; do
+for sh in ${SHAPES:-auto}; do
+  if [ "$sh" = auto ]; then unset MURR_DECODE_SHAPE; else export MURR_DECODE_SHAPE=$sh; fi
+  MURR_DECODE_LDS=$lds MURR_DECODE_VERBOSE=1 timeout -k 10 120 python bench.py --steps 5 --warmup 1 --no-cpu ${ARGS:-} \
+    > gpurun_out/sw.log 2> gpurun_out/sw.err || { echo "shape $sh lds $lds failed"; tail -5 gpurun_out/sw.err; exit 1; }
+  python3 -c "import json;d=json.load(open('gpurun_out/sw.log'));print('shape=$sh lds=$lds', d['roofline']['kernel_ms_avg'], 'ms', d['roofline']['achieved'], 'GB/s', d['value'], 'GiB/s')"
+  tail -1 gpurun_out/sw.err
 done; done
 true
