@@ -365,6 +365,39 @@ int murr_decode_enqueue(murr_ctx_t* c, const murr_segment_t* seg, const uint32_t
     if (!found) {  // very wide rows: the smallest ring; fills past the stage go to HBM
         nw = 4; kc = 1; depth = 2; slots = 4; stage = 16384;
     }
+    // Run-time specialised kernel (murr_jit.cpp): block-local, so it is chosen
+    // when the blocks alone fill the chip or are small enough for latency not
+    // to matter; MURR_DECODE_JIT=0 disables it, =1 forces it.
+    uint32_t nonempty = 0;
+    uint64_t max_rows = 0;
+    for (uint32_t b = 0; b < nblocks; b++) {
+        nonempty += blocks[b].n_rows != 0;
+        max_rows = std::max<uint64_t>(max_rows, blocks[b].n_rows);
+    }
+    const bool verbose = std::getenv("MURR_DECODE_VERBOSE") != nullptr;
+    const JitKernel* jk = nullptr;
+    {
+        const char* je = std::getenv("MURR_DECODE_JIT");
+        const int jmode = je ? std::atoi(je) : -1;
+        JitShape js{8, 1, 0, nutf8};
+        if (const char* e = std::getenv("MURR_JIT_SHAPE")) std::sscanf(e, "%ux%u", &js.nw, &js.r);  // tuning
+        if (js.nw != 4 && js.nw != 8) js.nw = 8;
+        if (js.r < 1 || js.r > 4) js.r = 1;
+        const uint32_t tr = 64 * js.nw * js.r;
+        const bool fits = nonempty >= (uint32_t)c->cus || max_rows <= 4ull * tr;
+        if (jmode != 0 && (fits || jmode == 1) && max_rows < 0x7FFFFFFFull) {
+            double st = tr * est_row * 1.25 + 64;
+            if (const char* e = std::getenv("MURR_JIT_STAGE")) st = std::atof(e);  // tuning
+            // two slots + wave totals within 64 KiB of LDS per workgroup
+            const uint32_t ro = ((tr + 1) * 8 + 16 + 15) & ~15u;
+            const uint32_t smax = ((65536 - 4 * std::max<uint32_t>(nutf8, 1) * js.nw) / 2 - ro - 64) & ~1023u;
+            js.stage = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(round_up((uint64_t)st, 1024), 1024), smax);
+            std::string why;
+            jk = jit_decode_kernel(c->device, seg->bitset_size, dp.data(), nproj, nutf8, js, &why);
+            if (!jk && (verbose || jmode == 1)) std::fprintf(stderr, "murr: JIT decode unavailable: %s\n", why.c_str());
+            if (!jk && jmode == 1) return MURR_E_INTERNAL;
+        }
+    }
     const uint32_t rows = 64 * kc * (nw - 1);
     const uint64_t R = rows;
     std::vector<DecBlock> db(nblocks);
@@ -391,7 +424,7 @@ int murr_decode_enqueue(murr_ctx_t* c, const murr_segment_t* seg, const uint32_t
 
     const uint64_t nbp = (uint64_t)nblocks * nproj;
     const uint64_t z_err = 0, z_nulls = 80, z_lens = z_nulls + 8 * nbp, z_lb = z_lens + 8 * nbp;
-    const uint64_t zbytes = round_up(z_lb + 8 * (uint64_t)nutf8 * tiles, 16);
+    const uint64_t zbytes = round_up(z_lb + (jk ? 0 : 8 * (uint64_t)nutf8 * tiles), 16);
     const uint64_t d_blocks = zbytes, d_proj = round_up(d_blocks + sizeof(DecBlock) * nblocks, 16);
     const uint64_t d_outs = round_up(d_proj + sizeof(DecProj) * nproj, 16);
     DecodeArgs a{};
@@ -405,11 +438,11 @@ int murr_decode_enqueue(murr_ctx_t* c, const murr_segment_t* seg, const uint32_t
     uint64_t grid = std::min<uint64_t>(std::max<uint64_t>(tiles, 1), (uint64_t)c->cus * bpc);
     // Block-local mode when every workgroup gets whole blocks: no cross-tile
     // prefix protocol at all.  Otherwise tiles round-robin + window prefix.
-    uint32_t nonempty = 0;
-    for (uint32_t b = 0; b < nblocks; b++) nonempty += blocks[b].n_rows != 0;
     const bool local = nonempty >= grid || std::getenv("MURR_DECODE_LOCAL") != nullptr;
     if (local) grid = std::max<uint64_t>(1, std::min<uint64_t>(grid, nonempty));
-    const uint64_t d_end_desc = round_up(d_outs + sizeof(DecOut) * dout.size(), 16);
+    if (jk) grid = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)c->cus * jk->bpc, nonempty));
+    const uint64_t d_order = round_up(d_outs + sizeof(DecOut) * dout.size(), 16);
+    const uint64_t d_end_desc = round_up(d_order + (jk ? 4ull * nonempty : 0), 16);
     const uint64_t dend = d_end_desc;
     int st = ensure_ws(c, dend, err);
     if (st) return st;
@@ -420,6 +453,11 @@ int murr_decode_enqueue(murr_ctx_t* c, const murr_segment_t* seg, const uint32_t
     std::memcpy(c->hs + (d_blocks - zbytes), db.data(), sizeof(DecBlock) * nblocks);
     std::memcpy(c->hs + (d_proj - zbytes), dp.data(), sizeof(DecProj) * nproj);
     std::memcpy(c->hs + (d_outs - zbytes), dout.data(), sizeof(DecOut) * dout.size());
+    if (jk) {
+        uint32_t* order = (uint32_t*)(c->hs + (d_order - zbytes));
+        for (uint32_t b = 0, k = 0; b < nblocks; b++)
+            if (blocks[b].n_rows) order[k++] = b;
+    }
 
     HIPC(hipMemsetAsync(c->ws, 0, zbytes, c->stream));
     HIPC(hipMemcpyAsync(c->ws + zbytes, c->hs, hdesc, hipMemcpyHostToDevice, c->stream));
@@ -443,11 +481,26 @@ int murr_decode_enqueue(murr_ctx_t* c, const murr_segment_t* seg, const uint32_t
     a.local = local ? 1 : 0;
     for (uint32_t p = 0, u = 0; p < nproj; p++)
         if (dp[p].is_utf8 && u < 2) a.ufix[u++] = p;
-    if (std::getenv("MURR_DECODE_VERBOSE"))
+    if (verbose && jk)
+        std::fprintf(stderr, "decode launch (jit): grid %llu (%d/CU) blocks %u rows/tile %u lds %u\n",
+                     (unsigned long long)grid, jk->bpc, nonempty, jk->tr, jk->lds);
+    else if (verbose)
         std::fprintf(stderr, "decode launch: grid %llu (%d/CU) tiles %llu shape %ux%u rows/tile %u stage %u slots %u depth %u lds %u local %d\n",
                      (unsigned long long)grid, bpc, (unsigned long long)tiles, nw, kc, rows, a.stage, slots, depth, lds, (int)local);
     HIPC(hipEventRecord(c->k0, c->stream));
-    if (tiles) HIPC(launch_decode(a, nw, kc, (uint32_t)grid, c->stream));
+    if (jk && nonempty) {
+        JitArgs ja{};
+        ja.blocks = a.blocks;
+        ja.outs = a.outs;
+        ja.order = (const uint32_t*)(c->ws + d_order);
+        ja.nulls = a.nulls;
+        ja.lens = a.lens;
+        ja.err = a.err;
+        ja.norder = nonempty;
+        HIPC(jit_decode_launch(jk, ja, (uint32_t)grid, c->stream));
+    } else if (tiles) {
+        HIPC(launch_decode(a, nw, kc, (uint32_t)grid, c->stream));
+    }
     HIPC(hipEventRecord(c->k1, c->stream));
     c->timed = true;
     HIPC(hipMemcpyAsync(c->hs + rb, c->ws, z_lb, hipMemcpyDeviceToHost, c->stream));

@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <string>
+
 namespace murr {
 
 // Threads per encode workgroup (4 waves).
@@ -88,6 +90,28 @@ __host__ __device__ inline uint64_t err_key(uint64_t block, uint64_t row, uint32
     if (block > 0x3FFFFull) block = 0x3FFFFull;
     return (block << 46) | (row << 14) | ((uint64_t)(col & 0x3FF) << 4) | (status & 0xF);
 }
+
+// Run-time specialised decode kernel (murr_jit.cpp, murr_jit_kernel.hip).
+struct JitShape {
+    uint32_t nw, r, stage, nutf8;  // waves, rows per lane per tile, blob stage bytes
+};
+struct JitKernel {
+    hipFunction_t fn;
+    uint32_t lds, tr, threads;     // LDS bytes, rows per tile, threads per workgroup
+    int bpc;                       // resident workgroups per CU
+};
+struct JitArgs {                   // = mj::Args in murr_jit_kernel.hip
+    const DecBlock* blocks;
+    const DecOut* outs;            // [nblocks * nproj]
+    const uint32_t* order;         // non-empty blocks
+    unsigned long long* nulls;
+    unsigned long long* lens;
+    unsigned long long* err;
+    uint32_t norder, pad;
+};
+const JitKernel* jit_decode_kernel(int device, uint32_t bs, const DecProj* dp, uint32_t nproj, uint32_t nutf8,
+                                   const JitShape& shape, std::string* why);
+hipError_t jit_decode_launch(const JitKernel* k, const JitArgs& a, uint32_t grid, hipStream_t s);
 
 void decode_lds_plan(DecodeArgs& a, uint32_t nw, uint32_t kc, uint32_t slots, uint32_t depth);
 bool decode_shape_ok(uint32_t nw, uint32_t kc);

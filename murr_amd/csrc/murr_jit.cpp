@@ -1,0 +1,143 @@
+// murr_jit.cpp — run-time specialisation of the decode kernel.
+//
+// A table's segment layout (SegmentSchema, src/io/schema.rs:8-54) and a read's
+// projection (Table::read, src/io/table/mod.rs:114-129) are fixed for the life
+// of many batch reads, so the decode kernel is compiled for them: the host
+// writes a prelude of #defines (bitset size, per projected column: kind, field
+// offset, null bit; tile shape) in front of murr_jit_kernel.hip (embedded in
+// this library) and compiles it with hiprtc for gfx950.  Code objects are
+// cached per (device, prelude) for the life of the process.  A layout that
+// cannot be compiled falls back to the generic kernel (murr_decode.hip).
+#include <hip/hip_runtime.h>
+#include <hip/hiprtc.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "../../include/murr_codec.h"
+#include "murr_internal.h"
+
+namespace murr {
+
+namespace {
+
+const char* const kJitSrc =
+#include "murr_jit_src.inc"
+    ;
+
+struct Entry {
+    hipModule_t mod = nullptr;
+    hipFunction_t fn = nullptr;
+    JitKernel k;
+    bool ok = false;
+    std::string why;
+};
+
+std::mutex g_mu;
+std::map<std::string, std::unique_ptr<Entry>> g_cache;
+
+std::string prelude(uint32_t bs, const DecProj* dp, uint32_t nproj, uint32_t nutf8, const JitShape& s) {
+    std::ostringstream o;
+    o << "#define MJ_NW " << s.nw << "\n#define MJ_R " << s.r << "\n#define MJ_STAGE " << s.stage
+      << "\n#define MJ_BS " << bs << "\n#define MJ_NPROJ " << nproj << "\n#define MJ_NUTF8 " << nutf8
+      << "\n#define MJ_FIXED(X)";
+    for (uint32_t p = 0; p < nproj; p++)
+        if (!dp[p].is_utf8)
+            o << " X(" << p << ", " << (dp[p].dtype == MURR_BOOL ? 0u : dp[p].width) << ", " << bs + dp[p].offset
+              << ", " << dp[p].bit << ")";
+    o << "\n#define MJ_UTF8(X)";
+    for (uint32_t p = 0, u = 0; p < nproj; p++)
+        if (dp[p].is_utf8) o << " X(" << p << ", " << u++ << ", " << bs + dp[p].offset << ", " << dp[p].bit << ")";
+    o << "\n#define MJ_COL_FO";
+    for (uint32_t p = 0; p < nproj; p++) o << (p ? ", " : " ") << bs + dp[p].offset;
+    o << "\n#define MJ_COL_BIT";
+    for (uint32_t p = 0; p < nproj; p++) o << (p ? ", " : " ") << dp[p].bit;
+    o << "\n#define MJ_COL_WID";
+    for (uint32_t p = 0; p < nproj; p++) o << (p ? ", " : " ") << (dp[p].is_utf8 ? 0u : dp[p].width);
+    o << "\n";
+    return o.str();
+}
+
+bool compile(Entry& e, const std::string& pre, int device, const JitShape& s) {
+    const std::string src = pre + kJitSrc;
+    hiprtcProgram prog;
+    if (hiprtcCreateProgram(&prog, src.c_str(), "murr_jit_decode.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS) {
+        e.why = "hiprtcCreateProgram failed";
+        return false;
+    }
+    const char* opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17"};
+    const hiprtcResult r = hiprtcCompileProgram(prog, 3, opts);
+    if (r != HIPRTC_SUCCESS) {
+        size_t n = 0;
+        hiprtcGetProgramLogSize(prog, &n);
+        std::string log(n + 1, '\0');
+        if (n) hiprtcGetProgramLog(prog, &log[0]);
+        e.why = std::string("hiprtc: ") + hiprtcGetErrorString(r) + "\n" + log;
+        hiprtcDestroyProgram(&prog);
+        return false;
+    }
+    size_t n = 0;
+    hiprtcGetCodeSize(prog, &n);
+    std::vector<char> code(n);
+    hiprtcGetCode(prog, code.data());
+    hiprtcDestroyProgram(&prog);
+    int cur = 0;
+    hipGetDevice(&cur);
+    hipSetDevice(device);
+    hipError_t he = hipModuleLoadData(&e.mod, code.data());
+    if (he == hipSuccess) he = hipModuleGetFunction(&e.fn, e.mod, "murr_jit_decode");
+    if (he != hipSuccess) {
+        e.why = std::string("module load: ") + hipGetErrorString(he);
+        hipSetDevice(cur);
+        return false;
+    }
+    // LDS: two slots + wave totals (murr_jit_kernel.hip LDS_TOTAL)
+    const uint32_t tr = 64 * s.nw * s.r;
+    const uint32_t ro = ((tr + 1) * 8 + 16 + 15) & ~15u;
+    const uint32_t slot = ro + s.stage + 64;
+    e.k.lds = 2 * slot + 4 * std::max<uint32_t>(s.nutf8, 1) * s.nw;
+    e.k.tr = tr;
+    e.k.threads = 64 * s.nw;
+    int bpc = 0;
+    if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, e.fn, e.k.threads, e.k.lds) != hipSuccess || bpc < 1)
+        bpc = 1;
+    e.k.bpc = bpc;
+    e.k.fn = e.fn;
+    hipSetDevice(cur);
+    return true;
+}
+
+}  // namespace
+
+const JitKernel* jit_decode_kernel(int device, uint32_t bs, const DecProj* dp, uint32_t nproj, uint32_t nutf8,
+                                   const JitShape& shape, std::string* why) {
+    const std::string pre = prelude(bs, dp, nproj, nutf8, shape);
+    const std::string key = std::to_string(device) + "\n" + pre;
+    std::lock_guard<std::mutex> lk(g_mu);
+    auto it = g_cache.find(key);
+    if (it == g_cache.end()) {
+        auto e = std::make_unique<Entry>();
+        e->ok = compile(*e, pre, device, shape);
+        it = g_cache.emplace(key, std::move(e)).first;
+    }
+    if (!it->second->ok) {
+        if (why) *why = it->second->why;
+        return nullptr;
+    }
+    return &it->second->k;
+}
+
+hipError_t jit_decode_launch(const JitKernel* k, const JitArgs& a, uint32_t grid, hipStream_t s) {
+    JitArgs args = a;
+    size_t sz = sizeof(args);
+    void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &args, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
+    return hipModuleLaunchKernel(k->fn, grid, 1, 1, k->threads, 1, 1, k->lds, s, nullptr, cfg);
+}
+
+}  // namespace murr
