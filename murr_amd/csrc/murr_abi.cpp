@@ -379,7 +379,7 @@ int murr_decode_enqueue(murr_ctx_t* c, const murr_segment_t* seg, const uint32_t
     {
         const char* je = std::getenv("MURR_DECODE_JIT");
         const int jmode = je ? std::atoi(je) : -1;
-        JitShape js{8, 1, 0, nutf8};
+        JitShape js{4, 2, 0, nutf8};
         if (const char* e = std::getenv("MURR_JIT_SHAPE")) std::sscanf(e, "%ux%u", &js.nw, &js.r);  // tuning
         if (js.nw != 4 && js.nw != 8) js.nw = 8;
         if (js.r < 1 || js.r > 4) js.r = 1;
@@ -390,7 +390,7 @@ int murr_decode_enqueue(murr_ctx_t* c, const murr_segment_t* seg, const uint32_t
             if (const char* e = std::getenv("MURR_JIT_STAGE")) st = std::atof(e);  // tuning
             // two slots + wave totals within 64 KiB of LDS per workgroup
             const uint32_t ro = ((tr + 1) * 8 + 16 + 15) & ~15u;
-            const uint32_t smax = ((65536 - 4 * std::max<uint32_t>(nutf8, 1) * js.nw) / 2 - ro - 64) & ~1023u;
+            const uint32_t smax = ((65536 - 64 - 4 * std::max<uint32_t>(nutf8, 1) * js.nw) / 2 - ro - 64) & ~1023u;
             js.stage = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(round_up((uint64_t)st, 1024), 1024), smax);
             std::string why;
             jk = jit_decode_kernel(c->device, seg->bitset_size, dp.data(), nproj, nutf8, js, &why);
@@ -440,7 +440,11 @@ int murr_decode_enqueue(murr_ctx_t* c, const murr_segment_t* seg, const uint32_t
     // prefix protocol at all.  Otherwise tiles round-robin + window prefix.
     const bool local = nonempty >= grid || std::getenv("MURR_DECODE_LOCAL") != nullptr;
     if (local) grid = std::max<uint64_t>(1, std::min<uint64_t>(grid, nonempty));
-    if (jk) grid = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)c->cus * jk->bpc, nonempty));
+    if (jk) {  // whole blocks per workgroup: equal rounds of blocks for every workgroup
+        const uint64_t slots = std::max<uint64_t>(1, (uint64_t)c->cus * jk->bpc);
+        const uint64_t rounds = std::max<uint64_t>(1, (nonempty + slots - 1) / slots);
+        grid = std::max<uint64_t>(1, (nonempty + rounds - 1) / rounds);
+    }
     const uint64_t d_order = round_up(d_outs + sizeof(DecOut) * dout.size(), 16);
     const uint64_t d_end_desc = round_up(d_order + (jk ? 4ull * nonempty : 0), 16);
     const uint64_t dend = d_end_desc;

@@ -101,7 +101,7 @@ bool compile(Entry& e, const std::string& pre, int device, const JitShape& s) {
     const uint32_t tr = 64 * s.nw * s.r;
     const uint32_t ro = ((tr + 1) * 8 + 16 + 15) & ~15u;
     const uint32_t slot = ro + s.stage + 64;
-    e.k.lds = 2 * slot + 4 * std::max<uint32_t>(s.nutf8, 1) * s.nw;
+    e.k.lds = 2 * slot + 64 + 4 * std::max<uint32_t>(s.nutf8, 1) * s.nw;
     e.k.tr = tr;
     e.k.threads = 64 * s.nw;
     int bpc = 0;

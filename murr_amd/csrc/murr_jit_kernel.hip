@@ -79,7 +79,8 @@ constexpr uint32_t RO_BYTES = ((TR + 1) * 8 + 16 + 15) & ~15u;
 constexpr uint32_t SLOT = RO_BYTES + STAGE + 64;
 constexpr uint32_t RO_PIECES = (RO_BYTES + 1023) / 1024;
 constexpr uint32_t ST_PIECES = STAGE / 1024;
-constexpr uint32_t LDS_WT = 2 * SLOT;                   // [NUTF8][NW] u32 wave totals
+constexpr uint32_t LDS_SPAN = 2 * SLOT;                 // [4][16 B] tile spans
+constexpr uint32_t LDS_WT = LDS_SPAN + 64;              // [NUTF8][NW] u32 wave totals
 constexpr uint32_t LDS_TOTAL = LDS_WT + 4 * (NUTF8 ? NUTF8 : 1) * NW;
 static_assert(STAGE % 1024 == 0, "stage is whole 1 KiB pieces");
 
@@ -202,15 +203,15 @@ DEV const Args* args() {
 }
 DEV void cur_load(Cur& c, uint32_t k) {
     const CAS Args* A = (const CAS Args*)args();
-    c.k = k;
+    c.k = sgpr(k);
     c.r0 = 0;
-    c.ok = k < A->norder;
+    c.ok = c.k < A->norder;
     if (!c.ok) return;
-    c.b = ((const CAS uint32_t*)A->order)[k];
+    c.b = sgpr(((const CAS uint32_t*)A->order)[c.k]);
     const CAS Blk* bp = (const CAS Blk*)A->blocks + c.b;
-    c.data = bp->data;
-    c.row_off = bp->row_off;
-    c.n_rows = bp->n_rows;
+    c.data = (const uint8_t*)sgpr64((uint64_t)bp->data);
+    c.row_off = (const uint64_t*)sgpr64((uint64_t)bp->row_off);
+    c.n_rows = sgpr64(bp->n_rows);
 }
 DEV void cur_next(Cur& c) {
     if (!c.ok) return;
@@ -220,11 +221,21 @@ DEV void cur_next(Cur& c) {
 }
 DEV uint32_t cur_nr(const Cur& c) { return (uint32_t)min((uint64_t)TR, c.n_rows - c.r0); }
 
-// Span of a tile: lanes 0 and 1 load row_off[r0] and row_off[r0 + nr].
-DEV uint64_t span_load(const Cur& c, uint32_t lane) {
-    uint64_t v = 0;
-    if (c.ok && lane < 2) v = gp(c.row_off)[c.r0 + (lane ? cur_nr(c) : 0u)];
-    return v;
+// Span of a tile (row_off[r0], row_off[r0 + nr]) into a 16-B LDS entry:
+// wave 0, lanes 0-3, one LDS-DMA dword each (no register results, so the
+// compiler never waits on it; the loop-top vmcnt(0) + barrier publish it).
+DEV void glds4(const GAS void* src, LAS void* dst) {
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(src), "s"(__builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)dst))
+                 : "memory");
+}
+DEV void span_issue(const Cur& c, LAS uint8_t* ent, uint32_t wave, uint32_t lane) {
+    if (wave == 0 && c.ok && lane < 4) {
+        const uint64_t r = c.r0 + (lane < 2 ? 0u : cur_nr(c));
+        glds4((const GAS uint8_t*)(c.row_off + r) + (lane & 1) * 4, ent);
+    }
 }
 
 // The staged tile: where its bytes are and how they map to LDS.
@@ -234,13 +245,12 @@ struct Tile {
     uint32_t b, nr, ro_shift, hbm, first, last;
 };
 
-// Issue the LDS-DMA of one tile (this wave's share of the 1 KiB pieces).
-DEV Tile tile_issue(const Cur& c, uint64_t span_v, LAS uint8_t* slot, uint32_t wave, uint32_t lane) {
+// Issue the LDS-DMA of one tile (this wave's share of the 1 KiB pieces); its
+// span is in LDS entry `ent`.
+DEV Tile tile_issue(const Cur& c, const LAS uint8_t* ent, LAS uint8_t* slot, uint32_t wave, uint32_t lane) {
     Tile T;
-    const uint64_t base = sgpr64(__builtin_amdgcn_readlane((uint32_t)span_v, 0) |
-                                 ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(span_v >> 32), 0) << 32));
-    const uint64_t end = sgpr64(__builtin_amdgcn_readlane((uint32_t)span_v, 1) |
-                                ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(span_v >> 32), 1) << 32));
+    const uint64_t base = sgpr64(((const LAS uint64_t*)ent)[0]);
+    const uint64_t end = sgpr64(((const LAS uint64_t*)ent)[1]);
     T.r0 = c.r0;
     T.nr = cur_nr(c);
     T.b = c.b;
@@ -585,16 +595,19 @@ extern "C" __global__ void __launch_bounds__(64 * MJ_NW) murr_jit_decode(mj::Arg
     const uint32_t wave = sgpr(threadIdx.x >> 6);
     LAS uint32_t* wt = (LAS uint32_t*)(lds + LDS_WT);
 
+    LAS uint8_t* spans = lds + LDS_SPAN;
+
     Cur cur;
     cur_load(cur, blockIdx.x);
     if (!cur.ok) return;
     Cur nxt = cur;
     cur_next(nxt);
     // prologue: tile 0's span, its DMA, tile 1's span in flight
-    uint64_t sv = span_load(cur, lane);
+    span_issue(cur, spans, wave, lane);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    Tile T = tile_issue(cur, sv, lds, wave, lane);
-    uint64_t sv_next = span_load(nxt, lane);
+    lds_barrier();
+    Tile T = tile_issue(cur, spans, lds, wave, lane);
+    span_issue(nxt, spans + 16, wave, lane);
 
     uint64_t run[NUTF8 ? NUTF8 : 1];
     for (uint32_t u = 0; u < (NUTF8 ? NUTF8 : 1); u++) run[u] = 0;
@@ -611,9 +624,9 @@ extern "C" __global__ void __launch_bounds__(64 * MJ_NW) murr_jit_decode(mj::Arg
         const uint32_t have_next = nxt.ok;
         Cur nn2 = nxt;
         if (have_next) {
-            Tn = tile_issue(nxt, sv_next, lds + ((it + 1) & 1) * SLOT, wave, lane);
+            Tn = tile_issue(nxt, spans + ((it + 1) & 3) * 16, lds + ((it + 1) & 1) * SLOT, wave, lane);
             cur_next(nn2);
-            sv_next = span_load(nn2, lane);
+            span_issue(nn2, spans + ((it + 2) & 3) * 16, wave, lane);
         }
         const LAS uint32_t* ro = (const LAS uint32_t*)(slot + T.ro_shift);
         if (T.hbm == 2) {  // a tile over 4 GiB of blob bytes (unsupported): report; prefixes undefined
