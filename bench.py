@@ -101,7 +101,7 @@ def pmc_traffic(paths):
         per = {}
         with open(path) as f:
             for r in csv.DictReader(f):
-                if "decode_kernel" not in r.get("Kernel_Name", ""):
+                if "decode" not in r.get("Kernel_Name", ""):
                     continue
                 key = (r.get("Counter_Name"), r.get("Dispatch_Id"))
                 per[key] = per.get(key, 0.0) + float(r.get("Counter_Value", 0))

@@ -1,7 +1,7 @@
 // Sample prelude (config B: f32 + utf8, bs 1) for `make jitcheck`; the real
 // prelude is generated per launch layout by murr_jit.cpp.
-#define MJ_NW 8
-#define MJ_R 1
+#define MJ_NW 5
+#define MJ_R 2
 #define MJ_STAGE 12288
 #define MJ_BS 1
 #define MJ_NPROJ 2

@@ -379,18 +379,18 @@ int murr_decode_enqueue(murr_ctx_t* c, const murr_segment_t* seg, const uint32_t
     {
         const char* je = std::getenv("MURR_DECODE_JIT");
         const int jmode = je ? std::atoi(je) : -1;
-        JitShape js{4, 2, 0, nutf8};
+        JitShape js{5, 2, 0, nutf8};
         if (const char* e = std::getenv("MURR_JIT_SHAPE")) std::sscanf(e, "%ux%u", &js.nw, &js.r);  // tuning
-        if (js.nw != 4 && js.nw != 8) js.nw = 8;
-        if (js.r < 1 || js.r > 4) js.r = 1;
-        const uint32_t tr = 64 * js.nw * js.r;
+        if (js.nw < 2 || js.nw > 16) js.nw = 5;
+        if (js.r < 1 || js.r > 4) js.r = 2;
+        const uint32_t tr = jit_tile_rows(js);
         const bool fits = nonempty >= (uint32_t)c->cus || max_rows <= 4ull * tr;
         if (jmode != 0 && (fits || jmode == 1) && max_rows < 0x7FFFFFFFull) {
             double st = tr * est_row * 1.25 + 64;
             if (const char* e = std::getenv("MURR_JIT_STAGE")) st = std::atof(e);  // tuning
-            // two slots + wave totals within 64 KiB of LDS per workgroup
-            const uint32_t ro = ((tr + 1) * 8 + 16 + 15) & ~15u;
-            const uint32_t smax = ((65536 - 64 - 4 * std::max<uint32_t>(nutf8, 1) * js.nw) / 2 - ro - 64) & ~1023u;
+            // both slots within 64 KiB of LDS per workgroup
+            js.stage = 0;
+            const uint32_t smax = ((65536 - jit_lds_bytes(js)) / 2) & ~1023u;
             js.stage = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(round_up((uint64_t)st, 1024), 1024), smax);
             std::string why;
             jk = jit_decode_kernel(c->device, seg->bitset_size, dp.data(), nproj, nutf8, js, &why);

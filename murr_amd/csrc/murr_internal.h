@@ -93,7 +93,7 @@ __host__ __device__ inline uint64_t err_key(uint64_t block, uint64_t row, uint32
 
 // Run-time specialised decode kernel (murr_jit.cpp, murr_jit_kernel.hip).
 struct JitShape {
-    uint32_t nw, r, stage, nutf8;  // waves, rows per lane per tile, blob stage bytes
+    uint32_t nw, r, stage, nutf8;  // waves (nw-1 decode, 1 loads), 64-row chunks per decoding wave, stage bytes
 };
 struct JitKernel {
     hipFunction_t fn;
@@ -111,6 +111,8 @@ struct JitArgs {                   // = mj::Args in murr_jit_kernel.hip
 };
 const JitKernel* jit_decode_kernel(int device, uint32_t bs, const DecProj* dp, uint32_t nproj, uint32_t nutf8,
                                    const JitShape& shape, std::string* why);
+uint32_t jit_tile_rows(const JitShape& s);
+uint32_t jit_lds_bytes(const JitShape& s);
 hipError_t jit_decode_launch(const JitKernel* k, const JitArgs& a, uint32_t grid, hipStream_t s);
 
 void decode_lds_plan(DecodeArgs& a, uint32_t nw, uint32_t kc, uint32_t slots, uint32_t depth);

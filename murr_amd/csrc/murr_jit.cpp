@@ -97,11 +97,8 @@ bool compile(Entry& e, const std::string& pre, int device, const JitShape& s) {
         hipSetDevice(cur);
         return false;
     }
-    // LDS: two slots + wave totals (murr_jit_kernel.hip LDS_TOTAL)
-    const uint32_t tr = 64 * s.nw * s.r;
-    const uint32_t ro = ((tr + 1) * 8 + 16 + 15) & ~15u;
-    const uint32_t slot = ro + s.stage + 64;
-    e.k.lds = 2 * slot + 64 + 4 * std::max<uint32_t>(s.nutf8, 1) * s.nw;
+    const uint32_t tr = jit_tile_rows(s);
+    e.k.lds = jit_lds_bytes(s);
     e.k.tr = tr;
     e.k.threads = 64 * s.nw;
     int bpc = 0;
@@ -114,6 +111,15 @@ bool compile(Entry& e, const std::string& pre, int device, const JitShape& s) {
 }
 
 }  // namespace
+
+// Rows per tile and LDS bytes of a shape (murr_jit_kernel.hip TR, LDS_TOTAL):
+// NW-1 consumer waves x R chunks of 64 rows; two slots [row offsets | stage],
+// the span ring and the consumers' utf8 wave totals.
+uint32_t jit_tile_rows(const JitShape& s) { return 64 * (s.nw - 1) * s.r; }
+uint32_t jit_lds_bytes(const JitShape& s) {
+    const uint32_t ro = ((jit_tile_rows(s) + 1) * 8 + 16 + 15) & ~15u;
+    return 2 * (ro + s.stage + 64) + 64 + 4 * std::max<uint32_t>(s.nutf8, 1) * (s.nw - 1);
+}
 
 const JitKernel* jit_decode_kernel(int device, uint32_t bs, const DecProj* dp, uint32_t nproj, uint32_t nutf8,
                                    const JitShape& shape, std::string* why) {

@@ -72,7 +72,8 @@ struct Args {
     uint32_t norder, pad;
 };
 
-constexpr uint32_t NW = MJ_NW, R = MJ_R, TR = 64 * MJ_NW * MJ_R, BS = MJ_BS, NPROJ = MJ_NPROJ,
+// MJ_NW waves: NC = MJ_NW - 1 consumers decode, the last wave only loads.
+constexpr uint32_t NW = MJ_NW, NC = MJ_NW - 1, R = MJ_R, TR = 64 * NC * MJ_R, BS = MJ_BS, NPROJ = MJ_NPROJ,
                    NUTF8 = MJ_NUTF8, STAGE = MJ_STAGE;
 // LDS slot: [row offsets (TR+1)*8 + 16][blob stage STAGE + 64 pad]
 constexpr uint32_t RO_BYTES = ((TR + 1) * 8 + 16 + 15) & ~15u;
@@ -80,8 +81,8 @@ constexpr uint32_t SLOT = RO_BYTES + STAGE + 64;
 constexpr uint32_t RO_PIECES = (RO_BYTES + 1023) / 1024;
 constexpr uint32_t ST_PIECES = STAGE / 1024;
 constexpr uint32_t LDS_SPAN = 2 * SLOT;                 // [4][16 B] tile spans
-constexpr uint32_t LDS_WT = LDS_SPAN + 64;              // [NUTF8][NW] u32 wave totals
-constexpr uint32_t LDS_TOTAL = LDS_WT + 4 * (NUTF8 ? NUTF8 : 1) * NW;
+constexpr uint32_t LDS_WT = LDS_SPAN + 64;              // [NUTF8][NC] u32 wave totals
+constexpr uint32_t LDS_TOTAL = LDS_WT + 4 * (NUTF8 ? NUTF8 : 1) * NC;
 static_assert(STAGE % 1024 == 0, "stage is whole 1 KiB pieces");
 
 enum : uint32_t { kStUtf8 = 1, kStOverflow = 4, kStMalformed = 5, kStCapacity = 6, kStInternal = 10 };
@@ -242,12 +243,11 @@ DEV void span_issue(const Cur& c, LAS uint8_t* ent, uint32_t wave, uint32_t lane
 struct Tile {
     uint64_t r0, abase;
     const uint8_t* data;
-    uint32_t b, nr, ro_shift, hbm, first, last;
+    uint32_t b, nr, ro_shift, hbm, first, last, span;  // span: staged blob bytes (16-B granules)
 };
 
-// Issue the LDS-DMA of one tile (this wave's share of the 1 KiB pieces); its
-// span is in LDS entry `ent`.
-DEV Tile tile_issue(const Cur& c, const LAS uint8_t* ent, LAS uint8_t* slot, uint32_t wave, uint32_t lane) {
+// A tile's placement, from the cursor and its span (LDS entry `ent`).
+DEV Tile tile_info(const Cur& c, const LAS uint8_t* ent) {
     Tile T;
     const uint64_t base = sgpr64(((const LAS uint64_t*)ent)[0]);
     const uint64_t end = sgpr64(((const LAS uint64_t*)ent)[1]);
@@ -260,20 +260,23 @@ DEV Tile tile_issue(const Cur& c, const LAS uint8_t* ent, LAS uint8_t* slot, uin
     T.last = c.r0 + T.nr == c.n_rows;
     const uint64_t span = ((end + 15) & ~15ull) - T.abase;
     T.hbm = end < base || end - T.abase > 0xFFFFFF00ull ? 2u : span > STAGE ? 1u : 0u;
-    const uintptr_t rp = (uintptr_t)(c.row_off + c.r0), s0 = rp & ~(uintptr_t)15;
-    T.ro_shift = (uint32_t)(rp - s0);
-    const uint32_t nb_ro = (T.ro_shift + (T.nr + 1) * 8 + 15) & ~15u;
-    const uint32_t nb_st = T.hbm ? 0u : (uint32_t)span;
-    const uint32_t np_ro = (nb_ro + 1023) / 1024, np = np_ro + (nb_st + 1023) / 1024;
-    for (uint32_t q = wave; q < np; q += NW) {
-        const bool ro = q < np_ro;
-        const uint32_t pc = ro ? q : q - np_ro, nb = ro ? nb_ro : nb_st;
-        const uint32_t off = pc * 1024 + lane * 16;
-        const GAS uint8_t* g = ro ? (const GAS uint8_t*)s0 : gp(c.data) + T.abase;
-        LAS uint8_t* d = slot + (ro ? 0u : RO_BYTES) + pc * 1024;
-        if (off < nb) glds16(g + off, d);
-    }
+    T.span = T.hbm ? 0u : (uint32_t)span;
+    const uintptr_t rp = (uintptr_t)(c.row_off + c.r0);
+    T.ro_shift = (uint32_t)(rp & 15);
     return T;
+}
+
+// The loader wave's LDS-DMA of one tile: its row-offset slice, then (unless
+// it outgrew the stage) its blob span, in 1 KiB pieces.
+DEV void tile_dma(const Tile& T, const Cur& c, LAS uint8_t* slot, uint32_t lane) {
+    const GAS uint8_t* s0 = (const GAS uint8_t*)((uintptr_t)(c.row_off + c.r0) & ~(uintptr_t)15);
+    const uint32_t nb_ro = (T.ro_shift + (T.nr + 1) * 8 + 15) & ~15u;
+    for (uint32_t q = 0; q * 1024 < nb_ro; q++)
+        if (q * 1024 + lane * 16 < nb_ro) glds16(s0 + q * 1024 + lane * 16, slot + q * 1024);
+    if (T.hbm) return;
+    const GAS uint8_t* g = gp(c.data) + T.abase;
+    for (uint32_t q = 0; q * 1024 < T.span; q++)
+        if (q * 1024 + lane * 16 < T.span) glds16(g + q * 1024 + lane * 16, slot + RO_BYTES + q * 1024);
 }
 
 // ---- per-row state of a wave's R chunks ----------------------------------------
@@ -547,15 +550,15 @@ DEV void decode_tile(const Src& src, const Tile& T, const LAS uint32_t* ro, LAS 
 #if MJ_NUTF8 > 0
     // wave totals -> LDS; every wave derives its prefix and the tile total
     if (lane == 0)
-        for (uint32_t u = 0; u < NUTF8; u++) wt[u * NW + wave] = utot[u];
+        for (uint32_t u = 0; u < NUTF8; u++) wt[u * NC + wave] = utot[u];
     lds_barrier();
     uint64_t pre[NUTF8];
 #pragma unroll
     for (uint32_t u = 0; u < NUTF8; u++) {
         uint64_t before = 0, all = 0;
 #pragma unroll
-        for (uint32_t w = 0; w < NW; w++) {
-            const uint32_t v = wt[u * NW + w];
+        for (uint32_t w = 0; w < NC; w++) {
+            const uint32_t v = wt[u * NC + w];
             before += w < wave ? v : 0u;
             all += v;
         }
@@ -600,39 +603,54 @@ extern "C" __global__ void __launch_bounds__(64 * MJ_NW) murr_jit_decode(mj::Arg
     Cur cur;
     cur_load(cur, blockIdx.x);
     if (!cur.ok) return;
-    Cur nxt = cur;
-    cur_next(nxt);
-    // prologue: tile 0's span, its DMA, tile 1's span in flight
-    span_issue(cur, spans, wave, lane);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    lds_barrier();
-    Tile T = tile_issue(cur, spans, lds, wave, lane);
-    span_issue(nxt, spans + 16, wave, lane);
 
+    if (wave == NC) {
+        // ---- loader: tile i+1's DMA and tile i+2's span while the consumers
+        // decode tile i; it issues no other vector-memory instruction, so its
+        // vmcnt(0) waits for exactly those, never for the consumers' stores.
+        span_issue(cur, spans, 0, lane);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        Tile T = tile_info(cur, spans);
+        tile_dma(T, cur, lds, lane);
+        Cur nxt = cur;
+        cur_next(nxt);
+        span_issue(nxt, spans + 16, 0, lane);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        lds_barrier();  // B_0: tile 0 and span 1 landed
+        for (uint32_t it = 0;; it++) {
+            const uint32_t more = nxt.ok;
+            if (more) {
+                const Tile Tn = tile_info(nxt, spans + ((it + 1) & 3) * 16);
+                tile_dma(Tn, nxt, lds + ((it + 1) & 1) * SLOT, lane);
+                cur_next(nxt);
+                span_issue(nxt, spans + ((it + 2) & 3) * 16, 0, lane);
+            }
+            if (NUTF8) lds_barrier();  // P_i: the consumers' prefix barrier
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            lds_barrier();  // B_i+1: tile i+1 landed, tile i decoded
+            if (!more) break;
+        }
+        return;
+    }
+
+    // ---- consumers ----
     uint64_t run[NUTF8 ? NUTF8 : 1];
     for (uint32_t u = 0; u < (NUTF8 ? NUTF8 : 1); u++) run[u] = 0;
     uint32_t nn[NPROJ];
     for (uint32_t p = 0; p < NPROJ; p++) nn[p] = 0;
-
+    lds_barrier();  // B_0
     for (uint32_t it = 0;; it++) {
-        // tile `it` landed (every wave's pieces), tile it+1's span landed, and
-        // every wave is done with the slot tile it+1 is about to overwrite
-        tile_barrier();
         LAS uint8_t* slot = lds + (it & 1) * SLOT;
-        Tile Tn;
-        Tn.nr = 0;
-        const uint32_t have_next = nxt.ok;
-        Cur nn2 = nxt;
-        if (have_next) {
-            Tn = tile_issue(nxt, spans + ((it + 1) & 3) * 16, lds + ((it + 1) & 1) * SLOT, wave, lane);
-            cur_next(nn2);
-            span_issue(nn2, spans + ((it + 2) & 3) * 16, wave, lane);
-        }
+        const Tile T = tile_info(cur, spans + (it & 3) * 16);
         const LAS uint32_t* ro = (const LAS uint32_t*)(slot + T.ro_shift);
         if (T.hbm == 2) {  // a tile over 4 GiB of blob bytes (unsupported): report; prefixes undefined
             if (wave == 0 && lane == 0) report(args()->err, err_key(T.b, T.r0, 0, kStMalformed));
+            if (NUTF8) lds_barrier();
         } else if (T.hbm) {
             decode_tile(HbmSrc{gp(T.data) + T.abase}, T, ro, wt, run, nn, wave, lane);
+            // drain the cold path's loads here (a compiler-visible vmcnt(0)),
+            // so none is pending into a register the hot path reuses
+            __builtin_amdgcn_s_waitcnt(0x0F70);
         } else {
             decode_tile(StageSrc{slot + RO_BYTES}, T, ro, wt, run, nn, wave, lane);
         }
@@ -640,8 +658,8 @@ extern "C" __global__ void __launch_bounds__(64 * MJ_NW) murr_jit_decode(mj::Arg
             flush_nulls(T.b, nn, lane);
             for (uint32_t u = 0; u < (NUTF8 ? NUTF8 : 1); u++) run[u] = 0;
         }
-        if (!have_next) break;
-        T = Tn;
-        nxt = nn2;
+        cur_next(cur);
+        lds_barrier();  // B_it+1
+        if (!cur.ok) break;
     }
 }
