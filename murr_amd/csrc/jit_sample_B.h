@@ -2,6 +2,7 @@
 // prelude is generated per launch layout by murr_jit.cpp.
 #define MJ_NW 5
 #define MJ_R 2
+#define MJ_SLOTS 2
 #define MJ_STAGE 12288
 #define MJ_BS 1
 #define MJ_NPROJ 2

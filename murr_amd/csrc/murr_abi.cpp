@@ -379,18 +379,23 @@ int murr_decode_enqueue(murr_ctx_t* c, const murr_segment_t* seg, const uint32_t
     {
         const char* je = std::getenv("MURR_DECODE_JIT");
         const int jmode = je ? std::atoi(je) : -1;
-        JitShape js{5, 2, 0, nutf8};
-        if (const char* e = std::getenv("MURR_JIT_SHAPE")) std::sscanf(e, "%ux%u", &js.nw, &js.r);  // tuning
+        JitShape js{5, 2, 0, nutf8, 2};
+        double slack = 1.25;  // stage bytes over the hinted mean row size
+        if (const char* e = std::getenv("MURR_JIT_SHAPE"))  // tuning: "NWxR[xSLOTS[xSLACK]]"
+            std::sscanf(e, "%ux%ux%ux%lf", &js.nw, &js.r, &js.slots, &slack);
         if (js.nw < 2 || js.nw > 16) js.nw = 5;
         if (js.r < 1 || js.r > 4) js.r = 2;
+        if (js.slots < 2 || js.slots > 4) js.slots = 2;
         const uint32_t tr = jit_tile_rows(js);
         const bool fits = nonempty >= (uint32_t)c->cus || max_rows <= 4ull * tr;
         if (jmode != 0 && (fits || jmode == 1) && max_rows < 0x7FFFFFFFull) {
-            double st = tr * est_row * 1.25 + 64;
+            double st = tr * est_row * slack + 64;
             if (const char* e = std::getenv("MURR_JIT_STAGE")) st = std::atof(e);  // tuning
-            // both slots within 64 KiB of LDS per workgroup
+            // every slot within the workgroup's LDS budget (64 KiB; tuning: MURR_JIT_LDS)
+            uint32_t budget = 65536;
+            if (const char* e = std::getenv("MURR_JIT_LDS")) budget = (uint32_t)std::atoi(e);
             js.stage = 0;
-            const uint32_t smax = ((65536 - jit_lds_bytes(js)) / 2) & ~1023u;
+            const uint32_t smax = ((budget - jit_lds_bytes(js)) / js.slots) & ~1023u;
             js.stage = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(round_up((uint64_t)st, 1024), 1024), smax);
             std::string why;
             jk = jit_decode_kernel(c->device, seg->bitset_size, dp.data(), nproj, nutf8, js, &why);
@@ -423,7 +428,7 @@ int murr_decode_enqueue(murr_ctx_t* c, const murr_segment_t* seg, const uint32_t
         dout[i] = DecOut{(uint8_t*)outs[i].values, outs[i].validity, outs[i].offsets, outs[i].values_cap};
 
     const uint64_t nbp = (uint64_t)nblocks * nproj;
-    const uint64_t z_err = 0, z_nulls = 80, z_lens = z_nulls + 8 * nbp, z_lb = z_lens + 8 * nbp;
+    const uint64_t z_err = 0, z_nulls = kErrBytes, z_lens = z_nulls + 8 * nbp, z_lb = z_lens + 8 * nbp;
     const uint64_t zbytes = round_up(z_lb + (jk ? 0 : 8 * (uint64_t)nutf8 * tiles), 16);
     const uint64_t d_blocks = zbytes, d_proj = round_up(d_blocks + sizeof(DecBlock) * nblocks, 16);
     const uint64_t d_outs = round_up(d_proj + sizeof(DecProj) * nproj, 16);
@@ -446,7 +451,8 @@ int murr_decode_enqueue(murr_ctx_t* c, const murr_segment_t* seg, const uint32_t
         grid = std::max<uint64_t>(1, (nonempty + rounds - 1) / rounds);
     }
     const uint64_t d_order = round_up(d_outs + sizeof(DecOut) * dout.size(), 16);
-    const uint64_t d_end_desc = round_up(d_order + (jk ? 4ull * nonempty : 0), 16);
+    const uint64_t d_sink = round_up(d_order + (jk ? 4ull * nonempty : 0), 256);
+    const uint64_t d_end_desc = d_sink + (jk ? 1024 : 0);
     const uint64_t dend = d_end_desc;
     int st = ensure_ws(c, dend, err);
     if (st) return st;
@@ -500,6 +506,7 @@ int murr_decode_enqueue(murr_ctx_t* c, const murr_segment_t* seg, const uint32_t
         ja.nulls = a.nulls;
         ja.lens = a.lens;
         ja.err = a.err;
+        ja.sink = c->ws + d_sink;
         ja.norder = nonempty;
         HIPC(jit_decode_launch(jk, ja, (uint32_t)grid, c->stream));
     } else if (tiles) {
@@ -529,14 +536,14 @@ int murr_decode_wait(murr_ctx_t* c, murr_error_t* err) {
     unsigned long long word;
     std::memcpy(&word, rb, 8);
     const uint64_t nbp = (uint64_t)c->nblocks * c->nproj;
-    const unsigned long long* nulls = (const unsigned long long*)(rb + 80);
+    const unsigned long long* nulls = (const unsigned long long*)(rb + kErrBytes);
     if (std::getenv("MURR_DECODE_VERBOSE")) {  // phase stamps of a MURR_ABLATE & 8 build
         const unsigned long long* stp = (const unsigned long long*)(rb + 16);
-        if (stp[0] | stp[4])
-            std::fprintf(stderr, "stamps (Gcycles, sum over waves): loader free-spin %.3f issue %.3f vmcnt %.3f other %.3f | "
-                         "consumer ready-spin %.3f passA %.3f lookback %.3f passB+rest %.3f\n",
-                         stp[0] * 1e-9, stp[1] * 1e-9, stp[2] * 1e-9, stp[3] * 1e-9, stp[4] * 1e-9, stp[5] * 1e-9,
-                         stp[6] * 1e-9, stp[7] * 1e-9);
+        if (stp[0] | stp[4]) {
+            std::fprintf(stderr, "stamps (Gcycles, sum over waves; murr_jit_kernel.hip / murr_decode.hip Stamps):");
+            for (int i = 0; i < kStampSlots; i++) std::fprintf(stderr, "%s %.3f", i == 4 ? " |" : "", stp[i] * 1e-9);
+            std::fprintf(stderr, "\n");
+        }
     }
     const unsigned long long* lens = nulls + nbp;
     for (uint32_t b = 0; b < c->nblocks; b++) {

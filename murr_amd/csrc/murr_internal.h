@@ -15,6 +15,10 @@ constexpr uint32_t kTile = 256;
 constexpr uint32_t kStage = 32768;
 // Default decode stage (bytes of row blobs per tile held in LDS).
 constexpr uint32_t kDecStage = 36864;
+// Workspace head: the error word, then phase-stamp slots of tuning builds
+// (err[2 .. 2 + kStampSlots)), then the per-(block, column) counters.
+constexpr uint32_t kStampSlots = 16;
+constexpr uint64_t kErrBytes = 8 * (2 + kStampSlots);
 // Projected columns per decode call (10 bits in the packed error key).
 constexpr uint32_t kMaxProj = 1024;
 
@@ -94,6 +98,7 @@ __host__ __device__ inline uint64_t err_key(uint64_t block, uint64_t row, uint32
 // Run-time specialised decode kernel (murr_jit.cpp, murr_jit_kernel.hip).
 struct JitShape {
     uint32_t nw, r, stage, nutf8;  // waves (nw-1 decode, 1 loads), 64-row chunks per decoding wave, stage bytes
+    uint32_t slots;                // LDS ring slots (tiles in flight + 1)
 };
 struct JitKernel {
     hipFunction_t fn;
@@ -107,6 +112,7 @@ struct JitArgs {                   // = mj::Args in murr_jit_kernel.hip
     unsigned long long* nulls;
     unsigned long long* lens;
     unsigned long long* err;
+    uint8_t* sink;                 // >= 1 KiB scratch for inactive lanes' stores
     uint32_t norder, pad;
 };
 const JitKernel* jit_decode_kernel(int device, uint32_t bs, const DecProj* dp, uint32_t nproj, uint32_t nutf8,

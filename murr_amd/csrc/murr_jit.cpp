@@ -44,9 +44,29 @@ std::map<std::string, std::unique_ptr<Entry>> g_cache;
 
 std::string prelude(uint32_t bs, const DecProj* dp, uint32_t nproj, uint32_t nutf8, const JitShape& s) {
     std::ostringstream o;
-    o << "#define MJ_NW " << s.nw << "\n#define MJ_R " << s.r << "\n#define MJ_STAGE " << s.stage
-      << "\n#define MJ_BS " << bs << "\n#define MJ_NPROJ " << nproj << "\n#define MJ_NUTF8 " << nutf8
-      << "\n#define MJ_FIXED(X)";
+    o << "#define MJ_NW " << s.nw << "\n#define MJ_R " << s.r << "\n#define MJ_SLOTS " << s.slots << "\n#define MJ_STAGE " << s.stage
+      << (std::getenv("MURR_JIT_STAMPS") ? "\n#define MJ_STAMPS 1" : "") << "\n#define MJ_BS " << bs << "\n#define MJ_NPROJ " << nproj << "\n#define MJ_NUTF8 " << nutf8
+      << "\n#define MJ_FIXED_GROUPS";
+    // fixed columns in groups of `group` (loads of a group precede its stores)
+    uint32_t group = 4;
+    if (const char* e = std::getenv("MURR_JIT_GROUP")) group = std::max(1, std::atoi(e));  // tuning
+    for (uint32_t p = 0, inq = 0, ng = 0; p < nproj; p++) {
+        if (dp[p].is_utf8) continue;
+        if (inq == 0) o << (ng++ ? ">, G<" : " G<");
+        else o << ", ";
+        o << "FC<" << p << ", " << (dp[p].dtype == MURR_BOOL ? 0u : dp[p].width) << ", " << bs + dp[p].offset << ", "
+          << dp[p].bit << ">";
+        if (++inq == group) inq = 0;
+    }
+    {
+        bool any = false;
+        for (uint32_t p = 0; p < nproj; p++) any |= !dp[p].is_utf8;
+        if (any) o << ">";
+    }
+    o << "\n#define MJ_UTF8_COLS";
+    for (uint32_t p = 0, u = 0; p < nproj; p++)
+        if (dp[p].is_utf8) o << (u ? ", " : " ") << "UC<" << p << ", " << u++ << ", " << bs + dp[p].offset << ", " << dp[p].bit << ">";
+    o << "\n#define MJ_FIXED(X)";
     for (uint32_t p = 0; p < nproj; p++)
         if (!dp[p].is_utf8)
             o << " X(" << p << ", " << (dp[p].dtype == MURR_BOOL ? 0u : dp[p].width) << ", " << bs + dp[p].offset
@@ -61,11 +81,39 @@ std::string prelude(uint32_t bs, const DecProj* dp, uint32_t nproj, uint32_t nut
     o << "\n#define MJ_COL_WID";
     for (uint32_t p = 0; p < nproj; p++) o << (p ? ", " : " ") << (dp[p].is_utf8 ? 0u : dp[p].width);
     o << "\n";
+    // tuning: MURR_JIT_DEFS="NAME=VALUE,..." extra #defines (ablation builds)
+    if (const char* e = std::getenv("MURR_JIT_DEFS")) {
+        std::string d(e);
+        size_t pos = 0;
+        while (pos < d.size()) {
+            size_t end = d.find(',', pos);
+            if (end == std::string::npos) end = d.size();
+            std::string kv = d.substr(pos, end - pos);
+            const size_t eq = kv.find('=');
+            if (!kv.empty()) o << "#define " << (eq == std::string::npos ? kv : kv.substr(0, eq) + " " + kv.substr(eq + 1)) << "\n";
+            pos = end + 1;
+        }
+    }
     return o.str();
 }
 
+// The kernel source: embedded, or (tuning) the file MURR_JIT_SRC names.
+std::string kernel_source() {
+    if (const char* f = std::getenv("MURR_JIT_SRC")) {
+        if (FILE* fp = std::fopen(f, "rb")) {
+            std::string t;
+            char buf[65536];
+            size_t n;
+            while ((n = std::fread(buf, 1, sizeof buf, fp)) > 0) t.append(buf, n);
+            std::fclose(fp);
+            return t;
+        }
+    }
+    return kJitSrc;
+}
+
 bool compile(Entry& e, const std::string& pre, int device, const JitShape& s) {
-    const std::string src = pre + kJitSrc;
+    const std::string src = pre + kernel_source();
     hiprtcProgram prog;
     if (hiprtcCreateProgram(&prog, src.c_str(), "murr_jit_decode.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS) {
         e.why = "hiprtcCreateProgram failed";
@@ -118,13 +166,14 @@ bool compile(Entry& e, const std::string& pre, int device, const JitShape& s) {
 uint32_t jit_tile_rows(const JitShape& s) { return 64 * (s.nw - 1) * s.r; }
 uint32_t jit_lds_bytes(const JitShape& s) {
     const uint32_t ro = ((jit_tile_rows(s) + 1) * 8 + 16 + 15) & ~15u;
-    return 2 * (ro + s.stage + 64) + 64 + 4 * std::max<uint32_t>(s.nutf8, 1) * (s.nw - 1);
+    return s.slots * (ro + s.stage + 64) + 128 + 16 + 4 * std::max<uint32_t>(s.nutf8, 1) * (s.nw - 1);
 }
 
 const JitKernel* jit_decode_kernel(int device, uint32_t bs, const DecProj* dp, uint32_t nproj, uint32_t nutf8,
                                    const JitShape& shape, std::string* why) {
     const std::string pre = prelude(bs, dp, nproj, nutf8, shape);
-    const std::string key = std::to_string(device) + "\n" + pre;
+    const char* srcf = std::getenv("MURR_JIT_SRC");
+    const std::string key = std::to_string(device) + "\n" + (srcf ? srcf : "") + "\n" + pre;
     std::lock_guard<std::mutex> lk(g_mu);
     auto it = g_cache.find(key);
     if (it == g_cache.end()) {

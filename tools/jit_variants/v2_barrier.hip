@@ -82,8 +82,7 @@ constexpr uint32_t SLOT = RO_BYTES + STAGE + 64;
 constexpr uint32_t RO_PIECES = (RO_BYTES + 1023) / 1024;
 constexpr uint32_t ST_PIECES = STAGE / 1024;
 constexpr uint32_t LDS_SPAN = 2 * SLOT;                 // [4][16 B] tile spans
-constexpr uint32_t LDS_CNT = LDS_SPAN + 64;
-constexpr uint32_t LDS_WT = LDS_CNT + 16;              // [NUTF8][NC] u32 wave totals
+constexpr uint32_t LDS_WT = LDS_SPAN + 64;              // [NUTF8][NC] u32 wave totals
 constexpr uint32_t LDS_TOTAL = LDS_WT + 4 * (NUTF8 ? NUTF8 : 1) * NC;
 static_assert(STAGE % 1024 == 0, "stage is whole 1 KiB pieces");
 
@@ -499,7 +498,7 @@ DEV Out ldout(const Out* base, uint32_t p) {
 // (updated to after it); nn[p]: this wave's null counts for the block.
 template <class Src>
 DEV void decode_tile(const Src& src, const Tile& T, const LAS uint32_t* ro, LAS uint32_t* wt, uint64_t (&run)[NUTF8 ? NUTF8 : 1],
-                     uint32_t (&nn)[NPROJ], uint32_t wave, uint32_t lane, LAS uint32_t* pcnt, uint32_t ptarget) {
+                     uint32_t (&nn)[NPROJ], uint32_t wave, uint32_t lane) {
     unsigned long long* err = args()->err;
     const uint32_t rbase = wave * 64 * R;
     const uint32_t abase = (uint32_t)T.abase;
@@ -551,17 +550,9 @@ DEV void decode_tile(const Src& src, const Tile& T, const LAS uint32_t* ro, LAS 
 
 #if MJ_NUTF8 > 0
     // wave totals -> LDS; every wave derives its prefix and the tile total
-    if (lane == 0) {
+    if (lane == 0)
         for (uint32_t u = 0; u < NUTF8; u++) wt[u * NC + wave] = utot[u];
-        __hip_atomic_fetch_add(pcnt, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
-    {
-        uint32_t spins = 0;
-        while (__hip_atomic_load(pcnt, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < ptarget) {
-            __builtin_amdgcn_s_sleep(1);
-            if (++spins > (1u << 24)) { report(err, err_key(T.b, T.r0, 0, kStInternal)); break; }
-        }
-    }
+    lds_barrier();
     uint64_t pre[NUTF8];
 #pragma unroll
     for (uint32_t u = 0; u < NUTF8; u++) {
@@ -607,8 +598,6 @@ extern "C" __global__ void __launch_bounds__(64 * MJ_NW) murr_jit_decode(mj::Arg
     const uint32_t lane = lane_id();
     const uint32_t wave = sgpr(threadIdx.x >> 6);
     LAS uint32_t* wt = (LAS uint32_t*)(lds + LDS_WT);
-    LAS uint32_t* pcnt = (LAS uint32_t*)(lds + LDS_CNT);
-    if (threadIdx.x == 0) *pcnt = 0;
 
     LAS uint8_t* spans = lds + LDS_SPAN;
 
@@ -637,6 +626,7 @@ extern "C" __global__ void __launch_bounds__(64 * MJ_NW) murr_jit_decode(mj::Arg
                 cur_next(nxt);
                 span_issue(nxt, spans + ((it + 2) & 3) * 16, 0, lane);
             }
+            if (NUTF8) lds_barrier();  // P_i: the consumers' prefix barrier
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             lds_barrier();  // B_i+1: tile i+1 landed, tile i decoded
             if (!more) break;
@@ -656,15 +646,14 @@ extern "C" __global__ void __launch_bounds__(64 * MJ_NW) murr_jit_decode(mj::Arg
         const LAS uint32_t* ro = (const LAS uint32_t*)(slot + T.ro_shift);
         if (T.hbm == 2) {  // a tile over 4 GiB of blob bytes (unsupported): report; prefixes undefined
             if (wave == 0 && lane == 0) report(args()->err, err_key(T.b, T.r0, 0, kStMalformed));
-            if (NUTF8 && lane == 0) __hip_atomic_fetch_add(pcnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (NUTF8) lds_barrier();
         } else if (T.hbm) {
-            decode_tile(HbmSrc{gp(T.data) + T.abase}, T, ro, wt, run, nn, wave, lane, pcnt, NC * (it + 1));
-            __builtin_amdgcn_s_waitcnt(0x0F70);
+            decode_tile(HbmSrc{gp(T.data) + T.abase}, T, ro, wt, run, nn, wave, lane);
             // drain the cold path's loads here (a compiler-visible vmcnt(0)),
             // so none is pending into a register the hot path reuses
             __builtin_amdgcn_s_waitcnt(0x0F70);
         } else {
-            decode_tile(StageSrc{slot + RO_BYTES}, T, ro, wt, run, nn, wave, lane, pcnt, NC * (it + 1));
+            decode_tile(StageSrc{slot + RO_BYTES}, T, ro, wt, run, nn, wave, lane);
         }
         if (T.last) {
             flush_nulls(T.b, nn, lane);

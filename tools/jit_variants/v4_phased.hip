@@ -69,7 +69,7 @@ struct Args {
     unsigned long long* nulls;  // [nblocks][MJ_NPROJ]
     unsigned long long* lens;   // [nblocks][MJ_NPROJ] utf8 data bytes
     unsigned long long* err;    // max of ~key
-    uint8_t* sink;
+    uint8_t* sink;              // 1 KiB the inactive lanes of unmasked stores write to
     uint32_t norder, pad;
 };
 
@@ -81,9 +81,14 @@ constexpr uint32_t RO_BYTES = ((TR + 1) * 8 + 16 + 15) & ~15u;
 constexpr uint32_t SLOT = RO_BYTES + STAGE + 64;
 constexpr uint32_t RO_PIECES = (RO_BYTES + 1023) / 1024;
 constexpr uint32_t ST_PIECES = STAGE / 1024;
-constexpr uint32_t LDS_SPAN = 2 * SLOT;                 // [4][16 B] tile spans
-constexpr uint32_t LDS_CNT = LDS_SPAN + 64;
-constexpr uint32_t LDS_WT = LDS_CNT + 16;              // [NUTF8][NC] u32 wave totals
+#ifndef MJ_SLOTS
+#define MJ_SLOTS 2
+#endif
+constexpr uint32_t NSLOT = MJ_SLOTS;                    // LDS ring slots (tiles in flight + 1)
+static_assert(NSLOT >= 2 && NSLOT <= 4, "2..4 slots");
+constexpr uint32_t LDS_SPAN = NSLOT * SLOT;             // [8][16 B] tile spans
+constexpr uint32_t LDS_CNT = LDS_SPAN + 128;            // u32 prefix arrival counter (+ pad)
+constexpr uint32_t LDS_WT = LDS_CNT + 16;               // [NUTF8][NC] u32 wave totals
 constexpr uint32_t LDS_TOTAL = LDS_WT + 4 * (NUTF8 ? NUTF8 : 1) * NC;
 static_assert(STAGE % 1024 == 0, "stage is whole 1 KiB pieces");
 
@@ -141,6 +146,14 @@ struct Utf8Dfa {
     DEV bool ok() const { return !bad && need == 0; }
 };
 
+// Tuning-only ablations (MURR_JIT_DEFS="MJ_ABLATE=n"; wrong outputs, never
+// in a production prelude): 1 no string stores, 2 string stores 4-B aligned,
+// 4 no fixed-width value stores, 8 no utf8 offset stores, 16 no validity
+// stores, 32 fixed 4-B values stored by 16 lanes x 16 B.
+#ifndef MJ_ABLATE
+#define MJ_ABLATE 0
+#endif
+
 // ---- byte sources ------------------------------------------------------------
 // Tile bytes staged in LDS (hot path).  Aligned dword reads + v_alignbyte (an
 // unaligned ds_read_b32 is correct on gfx950 but far slower).  Reads are
@@ -191,6 +204,27 @@ DEV void glds16(const GAS void* src, LAS void* dst) {
 }
 DEV void tile_barrier() { asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 DEV void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// Phase stamps (MJ_STAMPS builds only, MURR_JIT_STAMPS=1): cycles per phase
+// summed over waves into err[2..17].  Loader: issue, -, vmcnt wait, tile
+// barrier.  Consumers: tile barrier, prefix wait, fixed columns, utf8 emit,
+// row offsets, utf8 slots, utf8 lengths, windows, error check, tile setup.
+#ifndef MJ_STAMPS
+#define MJ_STAMPS 0
+#endif
+struct Stamps {
+    uint64_t t = 0, acc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    DEV void start() { if (MJ_STAMPS) t = __builtin_amdgcn_s_memtime(); }
+    DEV void lap(int i) {
+        if (MJ_STAMPS) { const uint64_t n = __builtin_amdgcn_s_memtime(); acc[i] += n - t; t = n; }
+    }
+    DEV void flush(unsigned long long* err, int base, int n, uint32_t lane) {
+        if (MJ_STAMPS && lane == 0)
+            for (int i = 0; i < n; i++)
+                __hip_atomic_fetch_add((GAS unsigned long long*)err + 2 + base + i, (unsigned long long)acc[i],
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+};
 
 // ---- the workgroup's tile cursor (wave-uniform, every wave keeps a copy) -----
 struct Cur {
@@ -270,15 +304,41 @@ DEV Tile tile_info(const Cur& c, const LAS uint8_t* ent) {
 
 // The loader wave's LDS-DMA of one tile: its row-offset slice, then (unless
 // it outgrew the stage) its blob span, in 1 KiB pieces.
-DEV void tile_dma(const Tile& T, const Cur& c, LAS uint8_t* slot, uint32_t lane) {
+DEV uint32_t tile_dma(const Tile& T, const Cur& c, LAS uint8_t* slot, uint32_t lane) {
     const GAS uint8_t* s0 = (const GAS uint8_t*)((uintptr_t)(c.row_off + c.r0) & ~(uintptr_t)15);
     const uint32_t nb_ro = (T.ro_shift + (T.nr + 1) * 8 + 15) & ~15u;
-    for (uint32_t q = 0; q * 1024 < nb_ro; q++)
+    uint32_t n = 0;
+    for (uint32_t q = 0; q * 1024 < nb_ro; q++, n++)  // lane 0 is always active: one instruction each
         if (q * 1024 + lane * 16 < nb_ro) glds16(s0 + q * 1024 + lane * 16, slot + q * 1024);
-    if (T.hbm) return;
+    if (T.hbm) return n;
     const GAS uint8_t* g = gp(c.data) + T.abase;
-    for (uint32_t q = 0; q * 1024 < T.span; q++)
+    for (uint32_t q = 0; q * 1024 < T.span; q++, n++)
         if (q * 1024 + lane * 16 < T.span) glds16(g + q * 1024 + lane * 16, slot + RO_BYTES + q * 1024);
+    return n;
+}
+
+// s_waitcnt vmcnt(n) for a wave-uniform run-time n (clamped to the 6-bit
+// field: a larger n waits for more than needed, never for less).
+DEV void wait_vmcnt(uint32_t n) {
+    switch (n < 63u ? n : 63u) {
+#define W(N) case N: asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory"); break;
+        W(0) W(1) W(2) W(3) W(4) W(5) W(6) W(7) W(8) W(9) W(10) W(11) W(12) W(13) W(14) W(15)
+        W(16) W(17) W(18) W(19) W(20) W(21) W(22) W(23) W(24) W(25) W(26) W(27) W(28) W(29) W(30) W(31)
+        W(32) W(33) W(34) W(35) W(36) W(37) W(38) W(39) W(40) W(41) W(42) W(43) W(44) W(45) W(46) W(47)
+        W(48) W(49) W(50) W(51) W(52) W(53) W(54) W(55) W(56) W(57) W(58) W(59) W(60) W(61) W(62) W(63)
+#undef W
+    }
+}
+
+DEV const Out* outs_of(uint32_t b) {
+    const Out* o = args()->outs + (uint64_t)sgpr(b) * NPROJ;
+    return (const Out*)sgpr64((uint64_t)o);
+}
+DEV Out ldout(const Out* base, uint32_t p) {
+    const CAS Out* q = (const CAS Out*)base + p;
+    Out r;
+    r.values = q->values; r.validity = q->validity; r.offsets = q->offsets; r.values_cap = q->values_cap;
+    return r;
 }
 
 // ---- per-row state of a wave's R chunks ----------------------------------------
@@ -292,112 +352,189 @@ template <class Src> DEV bool null_bit(const Rows& W, int k, uint32_t bit, const
     return W.rl[k] == 0 || ((b >> (bit & 7)) & 1);
 }
 
-// One fixed-width (KIND = 1/2/4/8 bytes) or bool (KIND = 0) column over the
-// wave's chunks.  Returns its nulls.
-template <int KIND, uint32_t FO, uint32_t BIT, class Src>
-DEV uint32_t fixed_col(const Src& src, const Rows& W, const Tile& T, uint32_t rbase, const Out& o,
-                       uint32_t* badk, uint32_t lane) {
-    constexpr uint32_t WID = KIND == 0 ? 1 : KIND;
-    uint32_t nn = 0;
-#pragma unroll
-    for (int k = 0; k < (int)R; k++) {
-        const uint32_t i = rbase + k * 64 + lane;
-        const uint32_t nk = i - lane < T.nr ? min(64u, T.nr - (i - lane)) : 0u;
-        const bool isnull = null_bit(W, k, BIT, src);
-        const bool have = !isnull && FO + WID <= W.rl[k];
-        *badk |= (uint32_t)(!isnull && !have) << k;
-        const uint32_t a = at<Src>(have, W.ra[k] + FO);
-        const uint64_t vm = __ballot(!isnull);
-        nn += nk - (uint32_t)__popcll(vm);
-        const uint64_t word = (T.r0 + i - lane) >> 6;
-        if (nk && lane == 0) gp((uint64_t*)o.validity)[word] = vm;
-        const bool act = lane < nk;
-        if constexpr (KIND == 0) {
-            const uint32_t v = src.u8(a);
-            const uint64_t m = __ballot(have && v != 0);
-            if (nk && lane == 0) gp((uint64_t*)o.values)[word] = m;
-        } else if constexpr (KIND == 8) {
-            const uint64_t v = src.u64(a);
-            if (act) gp((uint64_t*)o.values)[T.r0 + i] = have ? v : 0;
-        } else if constexpr (KIND == 4) {
-            const uint32_t v = src.u32(a);
-            if (act) gp((uint32_t*)o.values)[T.r0 + i] = have ? v : 0;
-        } else if constexpr (KIND == 2) {
-            const uint32_t v = src.u16(a);
-            if (act) gp((uint16_t*)o.values)[T.r0 + i] = have ? (uint16_t)v : 0;
-        } else {
-            const uint32_t v = src.u8(a);
-            if (act) gp(o.values)[T.r0 + i] = have ? (uint8_t)v : 0;
-        }
-    }
-    return nn;
+// Rows of chunk k of this wave (wave-uniform).
+DEV uint32_t chunk_rows(const Tile& T, uint32_t rbase, int k) {
+    const uint32_t c0 = rbase + k * 64;
+    return c0 < T.nr ? min(64u, T.nr - c0) : 0u;
 }
 
-// Cells of one utf8 column (ReadRow::read_dynamic, read.rs:45-55): payload
-// address and length per row (0 for null / missing / malformed), chunk
-// inclusive scans, validity words.  Returns its nulls; *tot = wave total.
-template <uint32_t FO, uint32_t BIT, class Src>
-DEV uint32_t utf8_cells(const Src& src, const Rows& W, const Tile& T, uint32_t rbase, const Out& o,
-                        uint32_t* badk, uint32_t lane, uint32_t (&pay)[R], uint32_t (&len)[R],
-                        uint32_t (&inc)[R], uint32_t* tot) {
-    uint32_t nn = 0, wt = 0;
+// Stores are never exec-masked for inactive lanes in the hot path: those lanes
+// write to a per-lane sink in the workspace instead, so no branch splits the
+// wave's straight-line code (and the scheduler can overlap LDS reads across
+// columns and chunks).
+DEV GAS uint8_t* sink(uint32_t lane) { return gp(args()->sink) + lane * 16; }
+
+// Validity / bool value words of the wave's chunks: lane k < R stores chunk
+// k's word (one instruction per column).
+DEV void store_words(uint8_t* base, const Tile& T, uint32_t rbase, const uint64_t (&w)[R], uint32_t lane) {
+    uint64_t v = w[0];
+#pragma unroll
+    for (int k = 1; k < (int)R; k++) v = lane == (uint32_t)k ? w[k] : v;
+    const bool act = lane < R && rbase + lane * 64 < T.nr;
+    GAS uint64_t* dst = act ? gp((uint64_t*)base) + ((T.r0 + rbase) >> 6) + lane : (GAS uint64_t*)sink(lane);
+    if (lane < R) *dst = v;
+}
+
+// ---- column descriptors (compile-time; the prelude lists them) ----------------
+template <uint32_t P_, uint32_t KIND_, uint32_t FO_, uint32_t BIT_> struct FC {  // fixed width / bool
+    static constexpr uint32_t P = P_, KIND = KIND_, FO = FO_, BIT = BIT_;
+};
+template <uint32_t P_, uint32_t U_, uint32_t FO_, uint32_t BIT_> struct UC {  // utf8
+    static constexpr uint32_t P = P_, U = U_, FO = FO_, BIT = BIT_;
+};
+template <class... Cs> struct G {};    // a group of fixed columns: loads, then stores
+template <class... Gs> struct GL {};   // the groups
+
+// One fixed-width (KIND = 1/2/4/8 bytes) or bool (KIND = 0) column's values
+// for the wave's chunks, loaded and masked (null / malformed -> 0).
+template <class C> struct FV {
+    uint32_t lo[R], hi[R];
+    uint64_t vm[R], bm[R];
+};
+
+template <class C, class Src>
+DEV void fixed_load(FV<C>& v, const Src& src, const Rows& W, const Tile& T, uint32_t rbase, uint32_t lane,
+                    uint32_t& nn, uint32_t* badk) {
+    constexpr uint32_t WID = C::KIND == 0 ? 1 : C::KIND;
+#pragma unroll
+    for (int k = 0; k < (int)R; k++) {
+        const bool isnull = null_bit(W, k, C::BIT, src);
+        const bool have = !isnull && C::FO + WID <= W.rl[k];
+        *badk |= (uint32_t)(!isnull && !have) << k;
+        const uint32_t a = at<Src>(have, W.ra[k] + C::FO);
+        v.vm[k] = __ballot(!isnull);  // lanes past the tile are null
+        nn += chunk_rows(T, rbase, k) - (uint32_t)__popcll(v.vm[k]);
+        v.hi[k] = 0;
+        if constexpr (C::KIND == 0) {
+            v.bm[k] = __ballot(have && src.u8(a) != 0);
+            v.lo[k] = 0;
+        } else if constexpr (C::KIND == 8) {
+            const uint64_t x = src.u64(a);
+            v.lo[k] = have ? (uint32_t)x : 0u;
+            v.hi[k] = have ? (uint32_t)(x >> 32) : 0u;
+        } else if constexpr (C::KIND == 4) {
+            const uint32_t x = src.u32(a);
+            v.lo[k] = have ? x : 0u;
+        } else if constexpr (C::KIND == 2) {
+            const uint32_t x = src.u16(a);
+            v.lo[k] = have ? x : 0u;
+        } else {
+            const uint32_t x = src.u8(a);
+            v.lo[k] = have ? x : 0u;
+        }
+    }
+}
+
+template <class C>
+DEV void fixed_store(const FV<C>& v, const Out& o, const Tile& T, uint32_t rbase, uint32_t lane) {
 #pragma unroll
     for (int k = 0; k < (int)R; k++) {
         const uint32_t i = rbase + k * 64 + lane;
-        const uint32_t nk = i - lane < T.nr ? min(64u, T.nr - (i - lane)) : 0u;
-        const bool isnull = null_bit(W, k, BIT, src);
-        const bool s_ok = !isnull && FO + 4 <= W.rl[k];
-        const uint32_t slot = src.u32(at<Src>(s_ok, W.ra[k] + FO));
+        const bool act = i < T.nr;
+        if constexpr (C::KIND == 8) {
+            GAS uint64_t* d = act ? gp((uint64_t*)o.values) + T.r0 + i : (GAS uint64_t*)sink(lane);
+            *d = (uint64_t)v.lo[k] | ((uint64_t)v.hi[k] << 32);
+        } else if constexpr (C::KIND == 4) {
+            if (MJ_ABLATE & 32) {  // tuning only: 16 lanes x 16 B (wrong data)
+                typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+                if (lane < 16)
+                    *(GAS u32x4*)(gp((uint32_t*)o.values) + T.r0 + (i - lane) + lane * 4) =
+                        u32x4{v.lo[k], v.lo[k], v.lo[k], v.lo[k]};
+                continue;
+            }
+            GAS uint32_t* d = act ? gp((uint32_t*)o.values) + T.r0 + i : (GAS uint32_t*)sink(lane);
+            *d = v.lo[k];
+        } else if constexpr (C::KIND == 2) {
+            GAS uint16_t* d = act ? gp((uint16_t*)o.values) + T.r0 + i : (GAS uint16_t*)sink(lane);
+            *d = (uint16_t)v.lo[k];
+        } else if constexpr (C::KIND == 1) {
+            GAS uint8_t* d = act ? gp(o.values) + T.r0 + i : sink(lane);
+            *d = (uint8_t)v.lo[k];
+        }
+    }
+    if constexpr (C::KIND == 0) store_words(o.values, T, rbase, v.bm, lane);
+    store_words(o.validity, T, rbase, v.vm, lane);
+}
+
+// A group's columns: every load (and its LDS latency) ahead of every store.
+template <class Src, class C, class... Rest>
+DEV void fixed_chain(const Src& src, const Rows& W, const Tile& T, const Out* ob, uint32_t rbase, uint32_t lane,
+                     uint32_t (&nn)[NPROJ], uint32_t* badk) {
+    FV<C> v;
+    fixed_load<C>(v, src, W, T, rbase, lane, nn[C::P], badk);
+    if constexpr (sizeof...(Rest) > 0) fixed_chain<Src, Rest...>(src, W, T, ob, rbase, lane, nn, badk);
+    fixed_store<C>(v, ldout(ob, C::P), T, rbase, lane);
+}
+template <class Src, class... Cs>
+DEV void fixed_group(G<Cs...>, const Src& src, const Rows& W, const Tile& T, const Out* ob, uint32_t rbase,
+                     uint32_t lane, uint32_t (&nn)[NPROJ], uint32_t* badk) {
+    if constexpr (sizeof...(Cs) > 0) fixed_chain<Src, Cs...>(src, W, T, ob, rbase, lane, nn, badk);
+}
+template <class Src, class... Gs>
+DEV void fixed_groups(GL<Gs...>, const Src& src, const Rows& W, const Tile& T, const Out* ob, uint32_t rbase,
+                      uint32_t lane, uint32_t (&nn)[NPROJ], uint32_t* badk) {
+    (fixed_group(Gs{}, src, W, T, ob, rbase, lane, nn, badk), ...);
+}
+
+// ---- utf8 columns ----------------------------------------------------------------
+constexpr uint32_t NU = NUTF8 ? NUTF8 : 1;
+struct UState {
+    uint32_t pay[NU][R], len[NU][R], inc[NU][R], w0[NU][R], w1[NU][R], w2[NU][R];
+    uint64_t vm[NU][R];
+    uint32_t tot[NU];
+};
+
+// read_dynamic (read.rs:45-55), step 1: the slot (payload offset) of each row.
+template <class C, class Src>
+DEV void utf8_slot(UState& S, const Src& src, const Rows& W, const Tile& T, uint32_t rbase, uint32_t (&nn)[NPROJ]) {
+#pragma unroll
+    for (int k = 0; k < (int)R; k++) {
+        const bool isnull = null_bit(W, k, C::BIT, src);
+        const bool s_ok = !isnull && C::FO + 4 <= W.rl[k];
+        S.pay[C::U][k] = src.u32(at<Src>(s_ok, W.ra[k] + C::FO));
+        S.vm[C::U][k] = __ballot(!isnull);
+        nn[C::P] += chunk_rows(T, rbase, k) - (uint32_t)__popcll(S.vm[C::U][k]);
+    }
+}
+// step 2: the length word, bounds (the reference would panic: flagged), the
+// payload address, and the chunk scans of the lengths.
+template <class C, class Src>
+DEV void utf8_len(UState& S, const Src& src, const Rows& W, uint32_t* badk) {
+    uint32_t wt = 0;
+#pragma unroll
+    for (int k = 0; k < (int)R; k++) {
+        const bool isnull = null_bit(W, k, C::BIT, src);
+        const bool s_ok = !isnull && C::FO + 4 <= W.rl[k];
+        const uint32_t slot = S.pay[C::U][k];
         const uint32_t vlen = W.rl[k] - BS;  // >= 4 when s_ok
         const bool p_ok = s_ok && slot <= vlen - 4;
         const uint32_t l = src.u32(at<Src>(p_ok, W.ra[k] + BS + slot));
         const bool good = p_ok && l <= vlen - 4 - slot;
         *badk |= (uint32_t)(!isnull && !good) << k;
-        pay[k] = W.ra[k] + BS + slot + 4;
-        len[k] = good ? l : 0u;
-        inc[k] = wave_scan(len[k]) + wt;
-        wt = __builtin_amdgcn_readlane(inc[k], 63);
-        const uint64_t vm = __ballot(!isnull);
-        nn += nk - (uint32_t)__popcll(vm);
-        if (nk && lane == 0) gp((uint64_t*)o.validity)[(T.r0 + i - lane) >> 6] = vm;
+        S.pay[C::U][k] = W.ra[k] + BS + slot + 4;
+        S.len[C::U][k] = good ? l : 0u;
+        S.inc[C::U][k] = wave_scan(S.len[C::U][k]) + wt;
+        wt = __builtin_amdgcn_readlane(S.inc[C::U][k], 63);
     }
-    *tot = wt;
-    return nn;
+    S.tot[C::U] = wt;
+}
+// step 3 (stage only): the three aligned dwords around each string's start,
+// which hold every string of up to 8 bytes.
+template <class C, class Src> DEV void utf8_win(UState& S, const Src& src) {
+    if constexpr (!Src::kHbm) {
+#pragma unroll
+        for (int k = 0; k < (int)R; k++) src.win3(S.pay[C::U][k], S.w0[C::U][k], S.w1[C::U][k], S.w2[C::U][k]);
+    }
 }
 
-// Copy one string from the stage to vb[d .. d+n): overlapping unaligned dword
-// stores of its own bytes (head and tail), short/byte stores below 4 bytes.
-// Returns the OR of its bytes (UTF-8 pre-check).
 DEV uint32_t pick(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t x) {  // dword at byte x in [0, 8)
     return x < 4 ? __builtin_amdgcn_alignbyte(w1, w0, x) : __builtin_amdgcn_alignbyte(w2, w1, x - 4);
 }
-template <class Src>
-DEV uint32_t copy_str(const Src& src, GAS uint8_t* vb, uint32_t pay, uint32_t n) {
-    if constexpr (!Src::kHbm) {
-        if (n <= 8) {
-            uint32_t w0, w1, w2;
-            src.win3(pay, w0, w1, w2);
-            const uint32_t sh = pay & 3u;
-            const uint32_t head = __builtin_amdgcn_alignbyte(w1, w0, sh);
-            if (n >= 4) {
-                const uint32_t tail = pick(w0, w1, w2, sh + n - 4);
-                *(GAS u32u*)vb = head;
-                *(GAS u32u*)(vb + n - 4) = tail;
-                return head | tail;
-            }
-            if (n >= 2) {
-                const uint32_t t2 = pick(w0, w1, w2, sh + n - 2) & 0xFFFFu;
-                *(GAS u16u*)vb = (uint16_t)head;
-                *(GAS u16u*)(vb + n - 2) = (uint16_t)t2;
-                return (head & 0xFFFFu) | t2;
-            }
-            if (n == 1) {
-                *vb = (uint8_t)head;
-                return head & 0xFFu;
-            }
-            return 0u;
-        }
-    }
+
+// Generic string copy (any length, stage or HBM): unaligned dword stores and a
+// last overlapping dword of its own bytes; bytes below 4.  Returns the OR of
+// its bytes (UTF-8 pre-check).
+template <class Src> DEV uint32_t copy_str(const Src& src, GAS uint8_t* vb, uint32_t pay, uint32_t n) {
     uint32_t hib = 0, q = 0;
     if (n >= 4) {
 #pragma unroll 1
@@ -427,35 +564,72 @@ template <class Src> DEV bool utf8_valid_slow(const Src& src, uint32_t a, uint32
     return dfa.ok();
 }
 
-// Offsets and string bytes of one utf8 column (projection index P) for the
-// wave's chunks, from the wave's prefix `base`.
-template <uint32_t P, class Src>
-DEV void utf8_emit(const Src& src, const Tile& T, uint32_t rbase, const Out& o, uint64_t base,
-                   const uint32_t (&pay)[R], const uint32_t (&len)[R], const uint32_t (&inc)[R], uint32_t lane,
-                   unsigned long long* err) {
+// step 4: offsets and string bytes of one utf8 column from the wave's prefix
+// `base`; then its validity words.
+template <class C, class Src>
+DEV void utf8_emit(const UState& S, const Src& src, const Tile& T, uint32_t rbase, const Out& o, uint64_t base,
+                   uint32_t lane, unsigned long long* err) {
     GAS int32_t* ob = gp(o.offsets) + T.r0 + 1;
 #pragma unroll
     for (int k = 0; k < (int)R; k++) {
         const uint32_t i = rbase + k * 64 + lane;
         const bool act = i < T.nr;
-        const uint32_t n = len[k];
-        const uint64_t e = base + inc[k];
-        const uint64_t cend = base + __builtin_amdgcn_readlane(inc[k], 63);
+        const uint32_t n = S.len[C::U][k], pay = S.pay[C::U][k];
+        const uint64_t e = base + S.inc[C::U][k];  // inc: inclusive over the wave's chunks
+        const uint64_t cend = base + __builtin_amdgcn_readlane(S.inc[C::U][k], 63);
         uint32_t hib = 0;
         if (cend <= 0x7FFFFFFFull && cend <= o.values_cap) {  // wave-uniform fast path
-            if (act) ob[i] = (int32_t)e;
-            if (n) hib = copy_str(src, gp(o.values) + (e - n), pay[k], n);
+            *(act ? ob + i : (GAS int32_t*)sink(lane)) = (int32_t)e;
+            GAS uint8_t* vb = gp(o.values) + (e - n);
+            bool slow = n != 0;
+            if constexpr (!Src::kHbm) {
+                // 4..8 bytes (the common case): head and tail dwords, unmasked
+                const uint32_t w0 = S.w0[C::U][k], w1 = S.w1[C::U][k], w2 = S.w2[C::U][k], sh = pay & 3u;
+                const uint32_t head = __builtin_amdgcn_alignbyte(w1, w0, sh);
+                const uint32_t tail = pick(w0, w1, w2, sh + (n >= 4 ? n : 4u) - 4);
+                const bool fast = n >= 4 && n <= 8;
+                *(GAS u32u*)(fast ? vb : sink(lane)) = head;
+                *(GAS u32u*)(fast ? vb + n - 4 : sink(lane) + 4) = tail;
+                hib = fast ? head | tail : 0u;
+                slow = n != 0 && !fast;
+            }
+            if (slow) hib = copy_str(src, vb, pay, n);
         } else {
             if (act) {
-                if (e > 0x7FFFFFFFull) report(err, err_key(T.b, T.r0 + i, P, kStOverflow));
+                if (e > 0x7FFFFFFFull) report(err, err_key(T.b, T.r0 + i, C::P, kStOverflow));
                 else ob[i] = (int32_t)e;
-                if (n && e > o.values_cap) report(err, err_key(T.b, T.r0 + i, P, kStCapacity));
+                if (n && e > o.values_cap) report(err, err_key(T.b, T.r0 + i, C::P, kStCapacity));
             }
-            for (uint32_t q = 0; q < n; q++) hib |= src.u8(pay[k] + q);
+            for (uint32_t q = 0; q < n; q++) hib |= src.u8(pay + q);
         }
-        if ((hib & 0x80808080u) && !utf8_valid_slow(src, pay[k], n))
-            report(err, err_key(T.b, T.r0 + i, P, kStUtf8));
+        if ((hib & 0x80808080u) && !utf8_valid_slow(src, pay, n)) report(err, err_key(T.b, T.r0 + i, C::P, kStUtf8));
     }
+    store_words(o.validity, T, rbase, S.vm[C::U], lane);
+}
+
+template <class Src, class... Cs>
+DEV void utf8_slots(G<Cs...>, UState& S, const Src& src, const Rows& W, const Tile& T, uint32_t rbase,
+                    uint32_t (&nn)[NPROJ]) {
+    (utf8_slot<Cs>(S, src, W, T, rbase, nn), ...);
+}
+template <class Src, class... Cs> DEV void utf8_lens(G<Cs...>, UState& S, const Src& src, const Rows& W, uint32_t* badk) {
+    (utf8_len<Cs>(S, src, W, badk), ...);
+}
+template <class Src, class... Cs> DEV void utf8_wins(G<Cs...>, UState& S, const Src& src) { (utf8_win<Cs>(S, src), ...); }
+// The block's first tile writes offsets[0] = 0 (StringBuilder); its last the
+// block's utf8 byte total.
+template <class C> DEV void firstlast(const Tile& T, const Out* ob, const uint64_t (&run)[NU]) {
+    const Out o = ldout(ob, C::P);
+    if (T.first) gp(o.offsets)[0] = 0;
+    if (T.last) gp(args()->lens)[(uint64_t)T.b * NPROJ + C::P] = run[C::U];
+}
+template <class... Cs> DEV void utf8_firstlast(G<Cs...>, const Tile& T, const Out* ob, const uint64_t (&run)[NU]) {
+    (firstlast<Cs>(T, ob, run), ...);
+}
+template <class Src, class... Cs>
+DEV void utf8_emits(G<Cs...>, const UState& S, const Src& src, const Tile& T, uint32_t rbase, const Out* ob,
+                    const uint64_t (&pre)[NU], uint32_t lane, unsigned long long* err) {
+    (utf8_emit<Cs>(S, src, T, rbase, ldout(ob, Cs::P), pre[Cs::U], lane, err), ...);
 }
 
 // Exact error of a flagged row: the first projected column (projection order)
@@ -484,28 +658,22 @@ DEV void report_row(const Src& src, uint32_t ra, uint32_t rl, uint64_t b, uint64
     }
 }
 
-DEV const Out* outs_of(uint32_t b) {
-    const Out* o = args()->outs + (uint64_t)sgpr(b) * NPROJ;
-    return (const Out*)sgpr64((uint64_t)o);
-}
-DEV Out ldout(const Out* base, uint32_t p) {
-    const CAS Out* q = (const CAS Out*)base + p;
-    Out r;
-    r.values = q->values; r.validity = q->validity; r.offsets = q->offsets; r.values_cap = q->values_cap;
-    return r;
-}
-
 // Decode one staged tile.  run[u]: the block's utf8 bytes before this tile
 // (updated to after it); nn[p]: this wave's null counts for the block.
+using FixedGroups = GL<MJ_FIXED_GROUPS>;
+using Utf8Cols = G<MJ_UTF8_COLS>;
+
 template <class Src>
-DEV void decode_tile(const Src& src, const Tile& T, const LAS uint32_t* ro, LAS uint32_t* wt, uint64_t (&run)[NUTF8 ? NUTF8 : 1],
-                     uint32_t (&nn)[NPROJ], uint32_t wave, uint32_t lane, LAS uint32_t* pcnt, uint32_t ptarget) {
+DEV void decode_tile(const Src& src, const Tile& T, const LAS uint32_t* ro, LAS uint32_t* wt, uint64_t (&run)[NU],
+                     uint32_t (&nn)[NPROJ], uint32_t wave, uint32_t lane, Stamps& St, LAS uint32_t* pcnt,
+                     uint32_t ptarget) {
     unsigned long long* err = args()->err;
     const uint32_t rbase = wave * 64 * R;
     const uint32_t abase = (uint32_t)T.abase;
     const Out* ob = outs_of(T.b);
     Rows W;
     uint32_t badk = 0;
+    St.lap(9);
 #pragma unroll
     for (int k = 0; k < (int)R; k++) {
         const uint32_t i = rbase + k * 64 + lane;
@@ -527,18 +695,31 @@ DEV void decode_tile(const Src& src, const Tile& T, const LAS uint32_t* ro, LAS 
         }
     }
 
-#define MJ_DO_FIXED(P, KIND, FO, BIT) \
-    nn[P] += fixed_col<KIND, FO, BIT>(src, W, T, rbase, ldout(ob, P), &badk, lane);
-    MJ_FIXED(MJ_DO_FIXED)
-#undef MJ_DO_FIXED
-
 #if MJ_NUTF8 > 0
-    uint32_t upay[NUTF8][R], ulen[NUTF8][R], uinc[NUTF8][R], utot[NUTF8];
-#define MJ_DO_CELLS(P, U, FO, BIT) \
-    nn[P] += utf8_cells<FO, BIT>(src, W, T, rbase, ldout(ob, P), &badk, lane, upay[U], ulen[U], uinc[U], &utot[U]);
-    MJ_UTF8(MJ_DO_CELLS)
-#undef MJ_DO_CELLS
+    // utf8 cells first: the wave totals go out before the fixed columns are
+    // decoded, so the prefix wait below overlaps with them.
+    UState U;
+    if (MJ_STAMPS) asm volatile("" ::"v"(W.bits[0]), "v"(W.bits[R - 1]), "v"(W.rl[R - 1]));
+    St.lap(4);
+    utf8_slots(Utf8Cols{}, U, src, W, T, rbase, nn);
+    if (MJ_STAMPS) asm volatile("" ::"v"(U.pay[0][0]), "v"(U.pay[NU - 1][R - 1]));
+    St.lap(5);
+    utf8_lens(Utf8Cols{}, U, src, W, &badk);
+    St.lap(6);
+    // Consumers only (the loader may still be issuing): each wave stores its
+    // totals, then counts itself in; LDS operations of one wave complete in
+    // order, so a count of NC * (tile + 1) means every total is in place.
+    if (lane == 0) {
+        for (uint32_t u = 0; u < NUTF8; u++) wt[u * NC + wave] = U.tot[u];
+        __hip_atomic_fetch_add(pcnt, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    utf8_wins(Utf8Cols{}, U, src);
+    if (MJ_STAMPS) asm volatile("" ::"v"(U.w0[0][0]), "v"(U.w2[NU - 1][R - 1]));
+    St.lap(7);
 #endif
+
+    fixed_groups(FixedGroups{}, src, W, T, ob, rbase, lane, nn, &badk);
+    St.lap(2);
 
     if (__ballot(badk != 0)) {  // cold: exact error reports
 #pragma unroll
@@ -548,13 +729,9 @@ DEV void decode_tile(const Src& src, const Tile& T, const LAS uint32_t* ro, LAS 
             report_row(src, W.ra[k], ro[2 * i + 2] - ro[2 * i], T.b, T.r0 + i, err);
         }
     }
+    St.lap(8);
 
 #if MJ_NUTF8 > 0
-    // wave totals -> LDS; every wave derives its prefix and the tile total
-    if (lane == 0) {
-        for (uint32_t u = 0; u < NUTF8; u++) wt[u * NC + wave] = utot[u];
-        __hip_atomic_fetch_add(pcnt, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
     {
         uint32_t spins = 0;
         while (__hip_atomic_load(pcnt, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < ptarget) {
@@ -562,7 +739,8 @@ DEV void decode_tile(const Src& src, const Tile& T, const LAS uint32_t* ro, LAS 
             if (++spins > (1u << 24)) { report(err, err_key(T.b, T.r0, 0, kStInternal)); break; }
         }
     }
-    uint64_t pre[NUTF8];
+    St.lap(1);
+    uint64_t pre[NU];
 #pragma unroll
     for (uint32_t u = 0; u < NUTF8; u++) {
         uint64_t before = 0, all = 0;
@@ -575,16 +753,10 @@ DEV void decode_tile(const Src& src, const Tile& T, const LAS uint32_t* ro, LAS 
         pre[u] = run[u] + sgpr64(before);
         run[u] += sgpr64(all);
     }
-#define MJ_DO_EMIT(P, U, FO, BIT)                                                                      \
-    {                                                                                                  \
-        const Out o = ldout(ob, P);                                                                    \
-        if (T.first && wave == 0 && lane == 0) gp(o.offsets)[0] = 0;                                   \
-        if (T.last && wave == 0 && lane == 0) gp(args()->lens)[(uint64_t)T.b * NPROJ + P] = run[U];    \
-        utf8_emit<P>(src, T, rbase, o, pre[U], upay[U], ulen[U], uinc[U], lane, err);                  \
-    }
-    MJ_UTF8(MJ_DO_EMIT)
-#undef MJ_DO_EMIT
+    utf8_emits(Utf8Cols{}, U, src, T, rbase, ob, pre, lane, err);
+    if (wave == 0 && lane == 0) utf8_firstlast(Utf8Cols{}, T, ob, run);
 #endif
+    St.lap(3);
 }
 
 DEV void flush_nulls(uint32_t b, uint32_t (&nn)[NPROJ], uint32_t lane) {
@@ -617,30 +789,54 @@ extern "C" __global__ void __launch_bounds__(64 * MJ_NW) murr_jit_decode(mj::Arg
     if (!cur.ok) return;
 
     if (wave == NC) {
-        // ---- loader: tile i+1's DMA and tile i+2's span while the consumers
-        // decode tile i; it issues no other vector-memory instruction, so its
-        // vmcnt(0) waits for exactly those, never for the consumers' stores.
-        span_issue(cur, spans, 0, lane);
+        // ---- loader: NSLOT-1 tiles in flight.  At iteration i (after tile
+        // barrier B_i freed slot (i-1) % NSLOT) it DMAs tile i+NSLOT-1 and
+        // the span of tile i+NSLOT+1.  It issues no other vector-memory
+        // instruction, so its counted vmcnt waits for exactly the DMA it
+        // needs (tile i+1, and the span of tile i+NSLOT it reads next), never
+        // for the consumers' stores.
+        Cur cs = cur;  // next tile whose span to fetch
+        for (uint32_t k = 0; k <= NSLOT; k++) {
+            span_issue(cs, spans + (k & 7) * 16, 0, lane);
+            cur_next(cs);
+        }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        Tile T = tile_info(cur, spans);
-        tile_dma(T, cur, lds, lane);
-        Cur nxt = cur;
-        cur_next(nxt);
-        span_issue(nxt, spans + 16, 0, lane);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        lds_barrier();  // B_0: tile 0 and span 1 landed
-        for (uint32_t it = 0;; it++) {
-            const uint32_t more = nxt.ok;
-            if (more) {
-                const Tile Tn = tile_info(nxt, spans + ((it + 1) & 3) * 16);
-                tile_dma(Tn, nxt, lds + ((it + 1) & 1) * SLOT, lane);
-                cur_next(nxt);
-                span_issue(nxt, spans + ((it + 2) & 3) * 16, 0, lane);
+        Cur cd = cur;  // next tile to DMA
+        uint32_t after0 = 0;
+        for (uint32_t j = 0; j + 1 < NSLOT; j++) {
+            if (cd.ok) {
+                const uint32_t n = tile_dma(tile_info(cd, spans + (j & 7) * 16), cd, lds + j * SLOT, lane);
+                if (j) after0 += n;
             }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            cur_next(cd);
+        }
+        wait_vmcnt(after0);
+        lds_barrier();  // B_0: tile 0 and the spans of tiles 0 .. NSLOT landed
+        Stamps S;
+        S.start();
+        Cur cc = cur;  // the tile the consumers decode in this iteration
+        for (uint32_t it = 0;; it++) {
+            cur_next(cc);
+            const uint32_t more = cc.ok;
+            uint32_t nd = 0, ns = 0;
+            if (cd.ok) {
+                const uint32_t t = it + NSLOT - 1;
+                nd = tile_dma(tile_info(cd, spans + (t & 7) * 16), cd, lds + (t % NSLOT) * SLOT, lane);
+                cur_next(cd);
+            }
+            if (cs.ok) {
+                span_issue(cs, spans + ((it + NSLOT + 1) & 7) * 16, 0, lane);
+                ns = 1;
+                cur_next(cs);
+            }
+            S.lap(0);
+            wait_vmcnt(NSLOT == 2 ? ns : nd + ns);
+            S.lap(2);
             lds_barrier();  // B_i+1: tile i+1 landed, tile i decoded
+            S.lap(3);
             if (!more) break;
         }
+        S.flush(args()->err, 0, 4, lane);
         return;
     }
 
@@ -650,28 +846,32 @@ extern "C" __global__ void __launch_bounds__(64 * MJ_NW) murr_jit_decode(mj::Arg
     uint32_t nn[NPROJ];
     for (uint32_t p = 0; p < NPROJ; p++) nn[p] = 0;
     lds_barrier();  // B_0
+    Stamps S;
+    S.start();
     for (uint32_t it = 0;; it++) {
-        LAS uint8_t* slot = lds + (it & 1) * SLOT;
-        const Tile T = tile_info(cur, spans + (it & 3) * 16);
+        LAS uint8_t* slot = lds + (it % NSLOT) * SLOT;
+        const Tile T = tile_info(cur, spans + (it & 7) * 16);
         const LAS uint32_t* ro = (const LAS uint32_t*)(slot + T.ro_shift);
         if (T.hbm == 2) {  // a tile over 4 GiB of blob bytes (unsupported): report; prefixes undefined
             if (wave == 0 && lane == 0) report(args()->err, err_key(T.b, T.r0, 0, kStMalformed));
             if (NUTF8 && lane == 0) __hip_atomic_fetch_add(pcnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         } else if (T.hbm) {
-            decode_tile(HbmSrc{gp(T.data) + T.abase}, T, ro, wt, run, nn, wave, lane, pcnt, NC * (it + 1));
-            __builtin_amdgcn_s_waitcnt(0x0F70);
+            decode_tile(HbmSrc{gp(T.data) + T.abase}, T, ro, wt, run, nn, wave, lane, S, pcnt, NC * (it + 1));
             // drain the cold path's loads here (a compiler-visible vmcnt(0)),
             // so none is pending into a register the hot path reuses
             __builtin_amdgcn_s_waitcnt(0x0F70);
         } else {
-            decode_tile(StageSrc{slot + RO_BYTES}, T, ro, wt, run, nn, wave, lane, pcnt, NC * (it + 1));
+            decode_tile(StageSrc{slot + RO_BYTES}, T, ro, wt, run, nn, wave, lane, S, pcnt, NC * (it + 1));
         }
         if (T.last) {
             flush_nulls(T.b, nn, lane);
             for (uint32_t u = 0; u < (NUTF8 ? NUTF8 : 1); u++) run[u] = 0;
         }
         cur_next(cur);
+        S.lap(3);
         lds_barrier();  // B_it+1
+        S.lap(0);
         if (!cur.ok) break;
     }
+    S.flush(args()->err, 4, 12, lane);
 }
