@@ -199,7 +199,7 @@ def run_decode(args, dist, rank, world, local_rank):
                    "parallelism": f"{world} key-range shard(s), no collective"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                     "traffic": traffic, "kernel": "decode_kernel",
+                     "traffic": traffic, "kernel": ctx.last_kernel(),
                      "kernel_ms_avg": round(k_avg_ms, 5),
                      "algorithmic_bytes_per_launch": (in_block + out_block) * K},
         "cpu_baseline": None,

@@ -72,6 +72,7 @@ SIGNATURES = {
     "murr_ctx_destroy": (None, [P]),
     "murr_ctx_stream": (P, [P]),
     "murr_ctx_last_kernel_ms": (I32, [P, C.POINTER(C.c_float)]),
+    "murr_ctx_last_kernel": (C.c_char_p, [P]),
     "murr_device_count": (I32, [C.POINTER(I32)]),
     "murr_dev_alloc": (I32, [P, U64, PP]),
     "murr_dev_free": (I32, [P, P]),

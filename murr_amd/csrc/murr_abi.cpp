@@ -71,6 +71,7 @@ struct murr_ctx {
     uint32_t nblocks = 0, nproj = 0;
     uint64_t rb_off = 0;           // readback offset in hs
     int pending_status = MURR_OK;
+    const char* last_kernel = "";  // kernel of the last decode launch
 };
 
 namespace {
@@ -215,6 +216,8 @@ int murr_ctx_last_kernel_ms(murr_ctx_t* c, float* ms) {
     HIPC(hipEventElapsedTime(ms, c->k0, c->k1));
     return MURR_OK;
 }
+
+const char* murr_ctx_last_kernel(murr_ctx_t* c) { return c ? c->last_kernel : ""; }
 
 int murr_dev_alloc(murr_ctx_t* c, uint64_t bytes, void** p) {
     murr_error_t* err = nullptr;
@@ -509,8 +512,10 @@ int murr_decode_enqueue(murr_ctx_t* c, const murr_segment_t* seg, const uint32_t
         ja.sink = c->ws + d_sink;
         ja.norder = nonempty;
         HIPC(jit_decode_launch(jk, ja, (uint32_t)grid, c->stream));
+        c->last_kernel = "murr_jit_decode";
     } else if (tiles) {
         HIPC(launch_decode(a, nw, kc, (uint32_t)grid, c->stream));
+        c->last_kernel = "decode_kernel";
     }
     HIPC(hipEventRecord(c->k1, c->stream));
     c->timed = true;

@@ -68,6 +68,10 @@ class Context:
     def sync(self):
         raise_status(self.L.murr_sync(self.h), what="sync")
 
+    def last_kernel(self) -> str:
+        """Kernel of the last decode: "murr_jit_decode" or "decode_kernel"."""
+        return (self.L.murr_ctx_last_kernel(self.h) or b"").decode()
+
     def last_kernel_ms(self) -> float:
         ms = C.c_float()
         raise_status(self.L.murr_ctx_last_kernel_ms(self.h, C.byref(ms)), what="kernel time")

@@ -21,6 +21,17 @@ def ctx():
     c.close()
 
 
+KERNEL = {"jit": "murr_jit_decode", "generic": "decode_kernel"}
+
+
+@pytest.fixture(autouse=True, params=["jit", "generic"])
+def kernel_mode(request, monkeypatch):
+    """Every decode test runs on both kernels: the run-time specialised one
+    (murr_jit_kernel.hip) and the generic one (murr_decode.hip)."""
+    monkeypatch.setenv("MURR_DECODE_JIT", "1" if request.param == "jit" else "0")
+    return request.param
+
+
 def seg_of(dtypes):
     return SegmentSchema([(f"c{i}", D.parse(d)) for i, d in enumerate(dtypes)])
 
@@ -164,3 +175,28 @@ def test_zero_projection_is_arrow_error(ctx):
     from murr_amd import ArrowError
     with pytest.raises(ArrowError):
         gpu_decode(ctx, seg_of([D.Float32]), [], [(np.zeros(5, np.uint8), np.array([0, 5], np.uint64))])
+
+
+@pytest.mark.parametrize("nblocks", [300, 1100])
+def test_many_blocks_one_launch(ctx, kernel_mode, nblocks):
+    # enough blocks that the JIT kernel's workgroups each own one (300) or
+    # several (1100: more blocks than resident workgroups) blocks: the block
+    # cursor, per-block null counts, utf8 totals and offsets[0] per block
+    rng = np.random.default_rng(13 + nblocks)
+    dtypes = [D.Utf8, D.Int64, D.Bool, D.Utf8, D.Float32, D.UInt8]
+    oseg = O.Segment([int(d) for d in dtypes])
+    proj = [3, 0, 4, 2, 1, 5, 0]
+    blocks, wants = [], []
+    for k in range(nblocks):
+        n = int(rng.choice([0, 1, 63, 64, 65, 200, 511, 512, 513, 700]))
+        cols = random_columns(rng, dtypes, n, null_p=float(rng.choice([0.0, 0.2])), max_str=12)
+        miss = set(rng.choice(n, size=n // 7, replace=False).tolist()) if n > 7 else set()
+        _, data, off = oracle_block(dtypes, cols, n, miss)
+        blocks.append((data, off))
+        wants.append(O.decode_block(oseg, proj, data, off))
+    got = gpu_decode(ctx, seg_of(dtypes), proj, blocks)
+    assert ctx.last_kernel() == KERNEL[kernel_mode]
+    for b in range(nblocks):
+        for p in range(len(proj)):
+            assert_array_equal(got[b][p], wants[b][p], f"block {b} proj {p}")
+            check_padding(got[b][p], len(blocks[b][1]) - 1)

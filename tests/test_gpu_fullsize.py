@@ -13,6 +13,13 @@ from murr_amd.schema import DTypeName as D, SegmentSchema
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True, params=["jit", "generic"])
+def kernel_mode(request, monkeypatch):
+    """Decode through both kernels: run-time specialised and generic."""
+    monkeypatch.setenv("MURR_DECODE_JIT", "1" if request.param == "jit" else "0")
+    return request.param
+
+
 @pytest.fixture(scope="module")
 def ctx():
     c = Context(0)

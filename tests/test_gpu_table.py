@@ -17,6 +17,13 @@ from murr_amd.table import Table
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True, params=["jit", "generic"])
+def kernel_mode(request, monkeypatch):
+    """Decode through both kernels: run-time specialised and generic."""
+    monkeypatch.setenv("MURR_DECODE_JIT", "1" if request.param == "jit" else "0")
+    return request.param
+
+
 def schema_id_score():
     return TableSchema("id", {"id": ColumnSchema(D.Utf8, False), "score": ColumnSchema(D.Float32)})
 
