@@ -368,9 +368,9 @@ int murr_decode_enqueue(murr_ctx_t* c, const murr_segment_t* seg, const uint32_t
     if (!found) {  // very wide rows: the smallest ring; fills past the stage go to HBM
         nw = 4; kc = 1; depth = 2; slots = 4; stage = 16384;
     }
-    // Run-time specialised kernel (murr_jit.cpp): block-local, so it is chosen
-    // when the blocks alone fill the chip or are small enough for latency not
-    // to matter; MURR_DECODE_JIT=0 disables it, =1 forces it.
+    // Run-time specialised kernel (murr_jit.cpp), the default; the generic
+    // kernel only if it cannot be compiled.  MURR_DECODE_JIT=0 selects the
+    // generic kernel, =1 makes a JIT failure an error.
     uint32_t nonempty = 0;
     uint64_t max_rows = 0;
     for (uint32_t b = 0; b < nblocks; b++) {
@@ -382,16 +382,27 @@ int murr_decode_enqueue(murr_ctx_t* c, const murr_segment_t* seg, const uint32_t
     {
         const char* je = std::getenv("MURR_DECODE_JIT");
         const int jmode = je ? std::atoi(je) : -1;
-        JitShape js{5, 2, 0, nutf8, 2};
+        // Tile shape from the mean row size: the largest tile (5 waves x 2
+        // chunks, 5 x 1, 3 x 1) whose two LDS slots, with 25 % slack over the
+        // mean, fit 40 KiB, so that four workgroups share a CU.
+        JitShape js{3, 1, 0, nutf8, 2};
         double slack = 1.25;  // stage bytes over the hinted mean row size
+        static const uint32_t cand[][2] = {{5, 2}, {5, 1}, {3, 1}};
+        for (const auto& cs : cand) {
+            const double t = 64.0 * (cs[0] - 1) * cs[1];
+            if (2.0 * (8.0 * (t + 1) + 32 + t * est_row * slack + 64) <= 40960.0) {
+                js.nw = cs[0];
+                js.r = cs[1];
+                break;
+            }
+        }
         if (const char* e = std::getenv("MURR_JIT_SHAPE"))  // tuning: "NWxR[xSLOTS[xSLACK]]"
             std::sscanf(e, "%ux%ux%ux%lf", &js.nw, &js.r, &js.slots, &slack);
         if (js.nw < 2 || js.nw > 16) js.nw = 5;
         if (js.r < 1 || js.r > 4) js.r = 2;
         if (js.slots < 2 || js.slots > 4) js.slots = 2;
         const uint32_t tr = jit_tile_rows(js);
-        const bool fits = nonempty >= (uint32_t)c->cus || max_rows <= 4ull * tr;
-        if (jmode != 0 && (fits || jmode == 1) && max_rows < 0x7FFFFFFFull) {
+        if (jmode != 0 && max_rows < 0x7FFFFFFFull) {
             double st = tr * est_row * slack + 64;
             if (const char* e = std::getenv("MURR_JIT_STAGE")) st = std::atof(e);  // tuning
             // every slot within the workgroup's LDS budget (64 KiB; tuning: MURR_JIT_LDS)
@@ -432,7 +443,31 @@ int murr_decode_enqueue(murr_ctx_t* c, const murr_segment_t* seg, const uint32_t
 
     const uint64_t nbp = (uint64_t)nblocks * nproj;
     const uint64_t z_err = 0, z_nulls = kErrBytes, z_lens = z_nulls + 8 * nbp, z_lb = z_lens + 8 * nbp;
-    const uint64_t zbytes = round_up(z_lb + (jk ? 0 : 8 * (uint64_t)nutf8 * tiles), 16);
+    // JIT segments: a block is one segment (its workgroup walks it whole) unless
+    // there are fewer blocks than CUs; then blocks are cut into runs of seg_tiles
+    // tiles, about one per resident workgroup, and a length pass (murr_jit_lengths)
+    // gives each segment its utf8 starting offsets.
+    std::vector<JitSeg> jsegs;
+    bool split = false;
+    uint64_t jslots = 1;
+    if (jk) {
+        jslots = std::max<uint64_t>(1, (uint64_t)c->cus * jk->bpc);
+        uint64_t jtiles = 0;
+        for (uint32_t b = 0; b < nblocks; b++) jtiles += (blocks[b].n_rows + jk->tr - 1) / jk->tr;
+        uint64_t seg_tiles = ~0ull;
+        if (nonempty < (uint32_t)c->cus) seg_tiles = std::max<uint64_t>(1, (jtiles + jslots - 1) / jslots);
+        if (const char* e = std::getenv("MURR_JIT_SEGTILES")) seg_tiles = std::max(1, std::atoi(e));  // tuning
+        const uint64_t seg_rows = seg_tiles == ~0ull ? ~0ull : seg_tiles * jk->tr;
+        for (uint32_t b = 0; b < nblocks; b++) {
+            const uint64_t n = blocks[b].n_rows;
+            const uint32_t first = (uint32_t)jsegs.size();
+            for (uint64_t r = 0; r < n; r = (n - r > seg_rows ? r + seg_rows : n))
+                jsegs.push_back(JitSeg{b, first, r, n - r > seg_rows ? r + seg_rows : n});
+            split |= jsegs.size() - first > 1;
+        }
+    }
+    const uint64_t nseg = jsegs.size(), nu = std::max<uint32_t>(nutf8, 1);
+    const uint64_t zbytes = round_up(z_lb + (jk ? 8 * nu * nseg : 8 * (uint64_t)nutf8 * tiles), 16);
     const uint64_t d_blocks = zbytes, d_proj = round_up(d_blocks + sizeof(DecBlock) * nblocks, 16);
     const uint64_t d_outs = round_up(d_proj + sizeof(DecProj) * nproj, 16);
     DecodeArgs a{};
@@ -448,13 +483,12 @@ int murr_decode_enqueue(murr_ctx_t* c, const murr_segment_t* seg, const uint32_t
     // prefix protocol at all.  Otherwise tiles round-robin + window prefix.
     const bool local = nonempty >= grid || std::getenv("MURR_DECODE_LOCAL") != nullptr;
     if (local) grid = std::max<uint64_t>(1, std::min<uint64_t>(grid, nonempty));
-    if (jk) {  // whole blocks per workgroup: equal rounds of blocks for every workgroup
-        const uint64_t slots = std::max<uint64_t>(1, (uint64_t)c->cus * jk->bpc);
-        const uint64_t rounds = std::max<uint64_t>(1, (nonempty + slots - 1) / slots);
-        grid = std::max<uint64_t>(1, (nonempty + rounds - 1) / rounds);
+    if (jk) {  // whole segments per workgroup: equal rounds of segments for every workgroup
+        const uint64_t rounds = std::max<uint64_t>(1, (nseg + jslots - 1) / jslots);
+        grid = std::max<uint64_t>(1, (nseg + rounds - 1) / rounds);
     }
     const uint64_t d_order = round_up(d_outs + sizeof(DecOut) * dout.size(), 16);
-    const uint64_t d_sink = round_up(d_order + (jk ? 4ull * nonempty : 0), 256);
+    const uint64_t d_sink = round_up(d_order + sizeof(JitSeg) * nseg, 256);
     const uint64_t d_end_desc = d_sink + (jk ? 1024 : 0);
     const uint64_t dend = d_end_desc;
     int st = ensure_ws(c, dend, err);
@@ -466,11 +500,7 @@ int murr_decode_enqueue(murr_ctx_t* c, const murr_segment_t* seg, const uint32_t
     std::memcpy(c->hs + (d_blocks - zbytes), db.data(), sizeof(DecBlock) * nblocks);
     std::memcpy(c->hs + (d_proj - zbytes), dp.data(), sizeof(DecProj) * nproj);
     std::memcpy(c->hs + (d_outs - zbytes), dout.data(), sizeof(DecOut) * dout.size());
-    if (jk) {
-        uint32_t* order = (uint32_t*)(c->hs + (d_order - zbytes));
-        for (uint32_t b = 0, k = 0; b < nblocks; b++)
-            if (blocks[b].n_rows) order[k++] = b;
-    }
+    if (jk && nseg) std::memcpy(c->hs + (d_order - zbytes), jsegs.data(), sizeof(JitSeg) * nseg);
 
     HIPC(hipMemsetAsync(c->ws, 0, zbytes, c->stream));
     HIPC(hipMemcpyAsync(c->ws + zbytes, c->hs, hdesc, hipMemcpyHostToDevice, c->stream));
@@ -495,23 +525,26 @@ int murr_decode_enqueue(murr_ctx_t* c, const murr_segment_t* seg, const uint32_t
     for (uint32_t p = 0, u = 0; p < nproj; p++)
         if (dp[p].is_utf8 && u < 2) a.ufix[u++] = p;
     if (verbose && jk)
-        std::fprintf(stderr, "decode launch (jit): grid %llu (%d/CU) blocks %u rows/tile %u lds %u\n",
-                     (unsigned long long)grid, jk->bpc, nonempty, jk->tr, jk->lds);
+        std::fprintf(stderr, "decode launch (jit): grid %llu (%d/CU) blocks %u segments %llu%s rows/tile %u lds %u\n",
+                     (unsigned long long)grid, jk->bpc, nonempty, (unsigned long long)nseg,
+                     split && nutf8 ? " (+length pass)" : "", jk->tr, jk->lds);
     else if (verbose)
         std::fprintf(stderr, "decode launch: grid %llu (%d/CU) tiles %llu shape %ux%u rows/tile %u stage %u slots %u depth %u lds %u local %d\n",
                      (unsigned long long)grid, bpc, (unsigned long long)tiles, nw, kc, rows, a.stage, slots, depth, lds, (int)local);
     HIPC(hipEventRecord(c->k0, c->stream));
-    if (jk && nonempty) {
+    if (jk && nseg) {
         JitArgs ja{};
         ja.blocks = a.blocks;
         ja.outs = a.outs;
-        ja.order = (const uint32_t*)(c->ws + d_order);
+        ja.segs = (const JitSeg*)(c->ws + d_order);
+        ja.seg_tot = (unsigned long long*)(c->ws + z_lb);
         ja.nulls = a.nulls;
         ja.lens = a.lens;
         ja.err = a.err;
         ja.sink = c->ws + d_sink;
-        ja.norder = nonempty;
-        HIPC(jit_decode_launch(jk, ja, (uint32_t)grid, c->stream));
+        ja.norder = (uint32_t)nseg;
+        if (split && nutf8) HIPC(jit_decode_launch(jk, ja, (uint32_t)grid, c->stream, true));
+        HIPC(jit_decode_launch(jk, ja, (uint32_t)grid, c->stream, false));
         c->last_kernel = "murr_jit_decode";
     } else if (tiles) {
         HIPC(launch_decode(a, nw, kc, (uint32_t)grid, c->stream));

@@ -101,14 +101,19 @@ struct JitShape {
     uint32_t slots;                // LDS ring slots (tiles in flight + 1)
 };
 struct JitKernel {
-    hipFunction_t fn;
+    hipFunction_t fn, fn_len;      // decode, and the length pass of split blocks
     uint32_t lds, tr, threads;     // LDS bytes, rows per tile, threads per workgroup
     int bpc;                       // resident workgroups per CU
+};
+struct JitSeg {                    // = mj::Seg: rows [r_begin, r_end) of block b
+    uint32_t b, first;             // first: index of the block's first segment
+    uint64_t r_begin, r_end;
 };
 struct JitArgs {                   // = mj::Args in murr_jit_kernel.hip
     const DecBlock* blocks;
     const DecOut* outs;            // [nblocks * nproj]
-    const uint32_t* order;         // non-empty blocks
+    const JitSeg* segs;            // segments of the non-empty blocks
+    unsigned long long* seg_tot;   // [nseg][max(nutf8, 1)] utf8 bytes per segment
     unsigned long long* nulls;
     unsigned long long* lens;
     unsigned long long* err;
@@ -119,7 +124,7 @@ const JitKernel* jit_decode_kernel(int device, uint32_t bs, const DecProj* dp, u
                                    const JitShape& shape, std::string* why);
 uint32_t jit_tile_rows(const JitShape& s);
 uint32_t jit_lds_bytes(const JitShape& s);
-hipError_t jit_decode_launch(const JitKernel* k, const JitArgs& a, uint32_t grid, hipStream_t s);
+hipError_t jit_decode_launch(const JitKernel* k, const JitArgs& a, uint32_t grid, hipStream_t s, bool lengths);
 
 void decode_lds_plan(DecodeArgs& a, uint32_t nw, uint32_t kc, uint32_t slots, uint32_t depth);
 bool decode_shape_ok(uint32_t nw, uint32_t kc);

@@ -140,6 +140,7 @@ bool compile(Entry& e, const std::string& pre, int device, const JitShape& s) {
     hipSetDevice(device);
     hipError_t he = hipModuleLoadData(&e.mod, code.data());
     if (he == hipSuccess) he = hipModuleGetFunction(&e.fn, e.mod, "murr_jit_decode");
+    if (he == hipSuccess) he = hipModuleGetFunction(&e.k.fn_len, e.mod, "murr_jit_lengths");
     if (he != hipSuccess) {
         e.why = std::string("module load: ") + hipGetErrorString(he);
         hipSetDevice(cur);
@@ -188,11 +189,11 @@ const JitKernel* jit_decode_kernel(int device, uint32_t bs, const DecProj* dp, u
     return &it->second->k;
 }
 
-hipError_t jit_decode_launch(const JitKernel* k, const JitArgs& a, uint32_t grid, hipStream_t s) {
+hipError_t jit_decode_launch(const JitKernel* k, const JitArgs& a, uint32_t grid, hipStream_t s, bool lengths) {
     JitArgs args = a;
     size_t sz = sizeof(args);
     void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &args, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
-    return hipModuleLaunchKernel(k->fn, grid, 1, 1, k->threads, 1, 1, k->lds, s, nullptr, cfg);
+    return hipModuleLaunchKernel(lengths ? k->fn_len : k->fn, grid, 1, 1, k->threads, 1, 1, k->lds, s, nullptr, cfg);
 }
 
 }  // namespace murr

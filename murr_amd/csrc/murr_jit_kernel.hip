@@ -62,10 +62,19 @@ struct Out {  // = murr::DecOut
     int32_t* offsets;
     uint64_t values_cap;
 };
+// A segment: rows [r_begin, r_end) of block b, decoded by one workgroup.  A
+// block is one segment unless the launch has fewer blocks than CUs; then its
+// segments' utf8 byte counts come from a length pass (murr_jit_lengths) and
+// segment k starts at the sum over segments first .. k-1 of its block.
+struct Seg {
+    uint32_t b, first;
+    uint64_t r_begin, r_end;
+};
 struct Args {
     const Blk* blocks;
     const Out* outs;          // [nblocks][MJ_NPROJ]
-    const uint32_t* order;    // non-empty blocks, in launch order
+    const void* segs;         // Seg[norder]: row ranges of non-empty blocks, in launch order
+    unsigned long long* seg_tot;  // [norder][NU] utf8 bytes per segment (length pass)
     unsigned long long* nulls;  // [nblocks][MJ_NPROJ]
     unsigned long long* lens;   // [nblocks][MJ_NPROJ] utf8 data bytes
     unsigned long long* err;    // max of ~key
@@ -87,6 +96,7 @@ constexpr uint32_t LDS_WT = LDS_CNT + 16;              // [NUTF8][NC] u32 wave t
 constexpr uint32_t LDS_TOTAL = LDS_WT + 4 * (NUTF8 ? NUTF8 : 1) * NC;
 static_assert(STAGE % 1024 == 0, "stage is whole 1 KiB pieces");
 
+constexpr uint32_t NU = NUTF8 ? NUTF8 : 1;
 enum : uint32_t { kStUtf8 = 1, kStOverflow = 4, kStMalformed = 5, kStCapacity = 6, kStInternal = 10 };
 
 DEV uint64_t err_key(uint64_t block, uint64_t row, uint32_t col, uint32_t status) {
@@ -196,8 +206,8 @@ DEV void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "m
 struct Cur {
     const uint8_t* data;
     const uint64_t* row_off;
-    uint64_t n_rows, r0;
-    uint32_t k, b, ok;
+    uint64_t n_rows, r0, r_begin, r_end;
+    uint32_t k, b, first, ok;
 };
 DEV const Args* args() {
     const CAS Args* ap = (const CAS Args*)__builtin_amdgcn_kernarg_segment_ptr();
@@ -207,10 +217,14 @@ DEV const Args* args() {
 DEV void cur_load(Cur& c, uint32_t k) {
     const CAS Args* A = (const CAS Args*)args();
     c.k = sgpr(k);
-    c.r0 = 0;
     c.ok = c.k < A->norder;
     if (!c.ok) return;
-    c.b = sgpr(((const CAS uint32_t*)A->order)[c.k]);
+    const CAS Seg* sp = (const CAS Seg*)A->segs + c.k;
+    c.b = sgpr(sp->b);
+    c.first = sgpr(sp->first);
+    c.r_begin = sgpr64(sp->r_begin);
+    c.r_end = sgpr64(sp->r_end);
+    c.r0 = c.r_begin;
     const CAS Blk* bp = (const CAS Blk*)A->blocks + c.b;
     c.data = (const uint8_t*)sgpr64((uint64_t)bp->data);
     c.row_off = (const uint64_t*)sgpr64((uint64_t)bp->row_off);
@@ -219,10 +233,10 @@ DEV void cur_load(Cur& c, uint32_t k) {
 DEV void cur_next(Cur& c) {
     if (!c.ok) return;
     c.r0 += TR;
-    if (c.r0 < c.n_rows) return;
+    if (c.r0 < c.r_end) return;
     cur_load(c, c.k + gridDim.x);
 }
-DEV uint32_t cur_nr(const Cur& c) { return (uint32_t)min((uint64_t)TR, c.n_rows - c.r0); }
+DEV uint32_t cur_nr(const Cur& c) { return (uint32_t)min((uint64_t)TR, c.r_end - c.r0); }
 
 // Span of a tile (row_off[r0], row_off[r0 + nr]) into a 16-B LDS entry:
 // wave 0, lanes 0-3, one LDS-DMA dword each (no register results, so the
@@ -246,6 +260,7 @@ struct Tile {
     uint64_t r0, abase;
     const uint8_t* data;
     uint32_t b, nr, ro_shift, hbm, first, last, span;  // span: staged blob bytes (16-B granules)
+    uint32_t seg_first, seg_last;  // first / last tile of its segment
 };
 
 // A tile's placement, from the cursor and its span (LDS entry `ent`).
@@ -260,6 +275,8 @@ DEV Tile tile_info(const Cur& c, const LAS uint8_t* ent) {
     T.abase = base & ~15ull;
     T.first = c.r0 == 0;
     T.last = c.r0 + T.nr == c.n_rows;
+    T.seg_first = c.r0 == c.r_begin;
+    T.seg_last = c.r0 + T.nr == c.r_end;
     const uint64_t span = ((end + 15) & ~15ull) - T.abase;
     T.hbm = end < base || end - T.abase > 0xFFFFFF00ull ? 2u : span > STAGE ? 1u : 0u;
     T.span = T.hbm ? 0u : (uint32_t)span;
@@ -336,7 +353,7 @@ DEV uint32_t fixed_col(const Src& src, const Rows& W, const Tile& T, uint32_t rb
 // Cells of one utf8 column (ReadRow::read_dynamic, read.rs:45-55): payload
 // address and length per row (0 for null / missing / malformed), chunk
 // inclusive scans, validity words.  Returns its nulls; *tot = wave total.
-template <uint32_t FO, uint32_t BIT, class Src>
+template <uint32_t FO, uint32_t BIT, bool STORE, class Src>
 DEV uint32_t utf8_cells(const Src& src, const Rows& W, const Tile& T, uint32_t rbase, const Out& o,
                         uint32_t* badk, uint32_t lane, uint32_t (&pay)[R], uint32_t (&len)[R],
                         uint32_t (&inc)[R], uint32_t* tot) {
@@ -359,7 +376,7 @@ DEV uint32_t utf8_cells(const Src& src, const Rows& W, const Tile& T, uint32_t r
         wt = __builtin_amdgcn_readlane(inc[k], 63);
         const uint64_t vm = __ballot(!isnull);
         nn += nk - (uint32_t)__popcll(vm);
-        if (nk && lane == 0) gp((uint64_t*)o.validity)[(T.r0 + i - lane) >> 6] = vm;
+        if (STORE && nk && lane == 0) gp((uint64_t*)o.validity)[(T.r0 + i - lane) >> 6] = vm;
     }
     *tot = wt;
     return nn;
@@ -489,17 +506,32 @@ DEV const Out* outs_of(uint32_t b) {
     return (const Out*)sgpr64((uint64_t)o);
 }
 DEV Out ldout(const Out* base, uint32_t p) {
+    // opaque per use: the compiler would otherwise hoist every column's
+    // descriptor into SGPRs up front (spills on wide projections)
+    asm volatile("" : "+s"(base));
     const CAS Out* q = (const CAS Out*)base + p;
     Out r;
     r.values = q->values; r.validity = q->validity; r.offsets = q->offsets; r.values_cap = q->values_cap;
     return r;
 }
 
+// Null counts of a wave: column p's count in lane p % 64 of nn[p / 64]
+// (VGPRs, not an SGPR per column).
+constexpr uint32_t NNV = (NPROJ + 63) / 64;
+template <uint32_t P> DEV void add_nulls(uint32_t (&nn)[NNV], uint32_t lane, uint32_t v) {
+    // readlane / writelane: no per-column lane compare (those masks would be
+    // hoisted out of the tile loop into SGPR pairs)
+    const uint32_t t = __builtin_amdgcn_readlane(nn[P / 64], P % 64) + v;
+    asm("v_writelane_b32 %0, %1, %2" : "+v"(nn[P / 64]) : "s"(t), "i"(P % 64));
+}
+
 // Decode one staged tile.  run[u]: the block's utf8 bytes before this tile
-// (updated to after it); nn[p]: this wave's null counts for the block.
-template <class Src>
+// (updated to after it); nn: this wave's null counts for the segment.
+// LEN (the length pass): utf8 cells only; each wave adds its utf8 bytes to
+// run[] (no prefix, no stores).
+template <bool LEN, class Src>
 DEV void decode_tile(const Src& src, const Tile& T, const LAS uint32_t* ro, LAS uint32_t* wt, uint64_t (&run)[NUTF8 ? NUTF8 : 1],
-                     uint32_t (&nn)[NPROJ], uint32_t wave, uint32_t lane, LAS uint32_t* pcnt, uint32_t ptarget) {
+                     uint32_t (&nn)[NNV], uint32_t wave, uint32_t lane, LAS uint32_t* pcnt, uint32_t ptarget) {
     unsigned long long* err = args()->err;
     const uint32_t rbase = wave * 64 * R;
     const uint32_t abase = (uint32_t)T.abase;
@@ -527,18 +559,25 @@ DEV void decode_tile(const Src& src, const Tile& T, const LAS uint32_t* ro, LAS 
         }
     }
 
+    if constexpr (!LEN) {
 #define MJ_DO_FIXED(P, KIND, FO, BIT) \
-    nn[P] += fixed_col<KIND, FO, BIT>(src, W, T, rbase, ldout(ob, P), &badk, lane);
-    MJ_FIXED(MJ_DO_FIXED)
+    add_nulls<P>(nn, lane, fixed_col<KIND, FO, BIT>(src, W, T, rbase, ldout(ob, P), &badk, lane));
+        MJ_FIXED(MJ_DO_FIXED)
 #undef MJ_DO_FIXED
+    }
 
 #if MJ_NUTF8 > 0
     uint32_t upay[NUTF8][R], ulen[NUTF8][R], uinc[NUTF8][R], utot[NUTF8];
 #define MJ_DO_CELLS(P, U, FO, BIT) \
-    nn[P] += utf8_cells<FO, BIT>(src, W, T, rbase, ldout(ob, P), &badk, lane, upay[U], ulen[U], uinc[U], &utot[U]);
+    add_nulls<P>(nn, lane, utf8_cells<FO, BIT, !LEN>(src, W, T, rbase, ldout(ob, P), &badk, lane, upay[U], ulen[U], uinc[U], &utot[U]));
     MJ_UTF8(MJ_DO_CELLS)
 #undef MJ_DO_CELLS
+    if constexpr (LEN) {
+        for (uint32_t u = 0; u < NUTF8; u++) run[u] += utot[u];
+        return;
+    }
 #endif
+    if constexpr (LEN) return;
 
     if (__ballot(badk != 0)) {  // cold: exact error reports
 #pragma unroll
@@ -587,21 +626,36 @@ DEV void decode_tile(const Src& src, const Tile& T, const LAS uint32_t* ro, LAS 
 #endif
 }
 
-DEV void flush_nulls(uint32_t b, uint32_t (&nn)[NPROJ], uint32_t lane) {
+DEV void flush_nulls(uint32_t b, uint32_t (&nn)[NNV], uint32_t lane) {
     unsigned long long* nulls = args()->nulls + (uint64_t)b * NPROJ;
 #pragma unroll
-    for (uint32_t p = 0; p < NPROJ; p++) {
-        if (nn[p] && lane == 0)
-            __hip_atomic_fetch_add(gp(nulls) + p, (unsigned long long)nn[p], __ATOMIC_RELAXED,
+    for (uint32_t j = 0; j < NNV; j++) {
+        if (j * 64 + lane < NPROJ && nn[j])
+            __hip_atomic_fetch_add(gp(nulls) + j * 64 + lane, (unsigned long long)nn[j], __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
-        nn[p] = 0;
+        nn[j] = 0;
     }
 }
 
 }  // namespace mj
 
-extern "C" __global__ void __launch_bounds__(64 * MJ_NW) murr_jit_decode(mj::Args) {
-    using namespace mj;
+namespace mj {
+
+// utf8 bytes of block rows before segment c (the sum of the length pass's
+// totals of the block's earlier segments), per utf8 column.
+DEV void seg_prefix(const Cur& c, uint64_t (&run)[NU], uint32_t lane) {
+    const unsigned long long* st = args()->seg_tot;
+#pragma unroll
+    for (uint32_t u = 0; u < NUTF8; u++) {
+        uint64_t v = 0;
+        for (uint32_t j = c.first + lane; j < c.k; j += 64) v += __hip_atomic_load(gp(st) + (uint64_t)j * NU + u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (int m = 32; m >= 1; m >>= 1) v += (uint64_t)__shfl_xor((unsigned long long)v, m, 64);
+        run[u] = sgpr64(v);
+    }
+}
+
+template <bool LEN>
+DEV void kernel_body() {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds_[];
     LAS uint8_t* lds = (LAS uint8_t*)lds_;
     const uint32_t lane = lane_id();
@@ -647,27 +701,35 @@ extern "C" __global__ void __launch_bounds__(64 * MJ_NW) murr_jit_decode(mj::Arg
     // ---- consumers ----
     uint64_t run[NUTF8 ? NUTF8 : 1];
     for (uint32_t u = 0; u < (NUTF8 ? NUTF8 : 1); u++) run[u] = 0;
-    uint32_t nn[NPROJ];
-    for (uint32_t p = 0; p < NPROJ; p++) nn[p] = 0;
+    uint32_t nn[NNV];
+    for (uint32_t j = 0; j < NNV; j++) nn[j] = 0;
     lds_barrier();  // B_0
     for (uint32_t it = 0;; it++) {
         LAS uint8_t* slot = lds + (it & 1) * SLOT;
         const Tile T = tile_info(cur, spans + (it & 3) * 16);
         const LAS uint32_t* ro = (const LAS uint32_t*)(slot + T.ro_shift);
+        if (!LEN && NUTF8 && T.seg_first && !T.first) seg_prefix(cur, run, lane);
         if (T.hbm == 2) {  // a tile over 4 GiB of blob bytes (unsupported): report; prefixes undefined
             if (wave == 0 && lane == 0) report(args()->err, err_key(T.b, T.r0, 0, kStMalformed));
-            if (NUTF8 && lane == 0) __hip_atomic_fetch_add(pcnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (!LEN && NUTF8 && lane == 0) __hip_atomic_fetch_add(pcnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         } else if (T.hbm) {
-            decode_tile(HbmSrc{gp(T.data) + T.abase}, T, ro, wt, run, nn, wave, lane, pcnt, NC * (it + 1));
+            decode_tile<LEN>(HbmSrc{gp(T.data) + T.abase}, T, ro, wt, run, nn, wave, lane, pcnt, NC * (it + 1));
             __builtin_amdgcn_s_waitcnt(0x0F70);
             // drain the cold path's loads here (a compiler-visible vmcnt(0)),
             // so none is pending into a register the hot path reuses
             __builtin_amdgcn_s_waitcnt(0x0F70);
         } else {
-            decode_tile(StageSrc{slot + RO_BYTES}, T, ro, wt, run, nn, wave, lane, pcnt, NC * (it + 1));
+            decode_tile<LEN>(StageSrc{slot + RO_BYTES}, T, ro, wt, run, nn, wave, lane, pcnt, NC * (it + 1));
         }
-        if (T.last) {
-            flush_nulls(T.b, nn, lane);
+        if (T.seg_last) {
+            if (LEN) {  // this wave's share of the segment's utf8 bytes
+                for (uint32_t u = 0; u < NUTF8; u++)
+                    if (lane == 0 && run[u])
+                        __hip_atomic_fetch_add(gp(args()->seg_tot) + (uint64_t)cur.k * NU + u, (unsigned long long)run[u],
+                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            } else {
+                flush_nulls(T.b, nn, lane);
+            }
             for (uint32_t u = 0; u < (NUTF8 ? NUTF8 : 1); u++) run[u] = 0;
         }
         cur_next(cur);
@@ -675,3 +737,8 @@ extern "C" __global__ void __launch_bounds__(64 * MJ_NW) murr_jit_decode(mj::Arg
         if (!cur.ok) break;
     }
 }
+
+}  // namespace mj
+
+extern "C" __global__ void __launch_bounds__(64 * MJ_NW) murr_jit_decode(mj::Args) { mj::kernel_body<false>(); }
+extern "C" __global__ void __launch_bounds__(64 * MJ_NW) murr_jit_lengths(mj::Args) { mj::kernel_body<true>(); }

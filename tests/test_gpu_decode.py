@@ -200,3 +200,26 @@ def test_many_blocks_one_launch(ctx, kernel_mode, nblocks):
         for p in range(len(proj)):
             assert_array_equal(got[b][p], wants[b][p], f"block {b} proj {p}")
             check_padding(got[b][p], len(blocks[b][1]) - 1)
+
+
+@pytest.mark.parametrize("seg_tiles", [1, 2, 7])
+def test_split_blocks_utf8_prefix(ctx, kernel_mode, monkeypatch, seg_tiles):
+    # few large blocks: the JIT kernel cuts them into segments whose utf8
+    # starting offsets come from the length pass (murr_jit_lengths)
+    monkeypatch.setenv("MURR_JIT_SEGTILES", str(seg_tiles))
+    rng = np.random.default_rng(40 + seg_tiles)
+    dtypes = [D.Utf8, D.Int16, D.Utf8, D.Bool, D.Float64]
+    oseg = O.Segment([int(d) for d in dtypes])
+    proj = [2, 0, 1, 3, 4, 0]
+    blocks, wants = [], []
+    for n in [30000, 513, 7777]:
+        cols = random_columns(rng, dtypes, n, null_p=0.15, max_str=30)
+        miss = set(rng.choice(n, size=n // 9, replace=False).tolist())
+        _, data, off = oracle_block(dtypes, cols, n, miss)
+        blocks.append((data, off))
+        wants.append(O.decode_block(oseg, proj, data, off))
+    got = gpu_decode(ctx, seg_of(dtypes), proj, blocks)
+    assert ctx.last_kernel() == KERNEL[kernel_mode]
+    for b in range(len(blocks)):
+        for p in range(len(proj)):
+            assert_array_equal(got[b][p], wants[b][p], f"block {b} proj {p}")

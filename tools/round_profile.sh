@@ -24,5 +24,7 @@ if [ -z "${QUICK:-}" ]; then
   run encode_E 300 python3 bench.py --mode encode --steps 10 --warmup 2
   run decode_C 300 python3 bench.py --config C --blocks 10 --steps 10 --warmup 2 --no-cpu
   run decode_D 300 python3 bench.py --config D --rows 100000 --blocks 125 --steps 10 --warmup 2 --no-cpu
+  run decode_D1 300 python3 bench.py --config D --steps 10 --warmup 2 --no-cpu
+  run decode_B_generic 300 env MURR_DECODE_JIT=0 python3 bench.py --steps 10 --warmup 2 --no-cpu
   run host_C 300 python3 bench.py --mode host --config C --rows 1000 --steps 50 --warmup 5
 fi
