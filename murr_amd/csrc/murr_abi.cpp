@@ -383,14 +383,15 @@ int murr_decode_enqueue(murr_ctx_t* c, const murr_segment_t* seg, const uint32_t
         const char* je = std::getenv("MURR_DECODE_JIT");
         const int jmode = je ? std::atoi(je) : -1;
         // Tile shape from the mean row size: the largest tile (5 waves x 2
-        // chunks, 5 x 1, 3 x 1) whose two LDS slots, with 25 % slack over the
-        // mean, fit 40 KiB, so that four workgroups share a CU.
+        // chunks, 5 x 1, 3 x 1) whose two LDS slots, with 15 % slack over the
+        // mean, fit 40 KiB, so that four workgroups share a CU.  (Three slots,
+        // i.e. two tiles in flight, measured no faster: tools/ab_env.sh.)
         JitShape js{3, 1, 0, nutf8, 2};
-        double slack = 1.25;  // stage bytes over the hinted mean row size
+        double slack = 1.15;  // stage bytes over the hinted mean row size
         static const uint32_t cand[][2] = {{5, 2}, {5, 1}, {3, 1}};
         for (const auto& cs : cand) {
             const double t = 64.0 * (cs[0] - 1) * cs[1];
-            if (2.0 * (8.0 * (t + 1) + 32 + t * est_row * slack + 64) <= 40960.0) {
+            if (js.slots * (4.0 * (t + 1) + 32 + t * est_row * slack + 64) <= 40960.0) {
                 js.nw = cs[0];
                 js.r = cs[1];
                 break;

@@ -45,7 +45,8 @@ std::map<std::string, std::unique_ptr<Entry>> g_cache;
 std::string prelude(uint32_t bs, const DecProj* dp, uint32_t nproj, uint32_t nutf8, const JitShape& s) {
     std::ostringstream o;
     o << "#define MJ_NW " << s.nw << "\n#define MJ_R " << s.r << "\n#define MJ_SLOTS " << s.slots << "\n#define MJ_STAGE " << s.stage
-      << (std::getenv("MURR_JIT_STAMPS") ? "\n#define MJ_STAMPS 1" : "") << "\n#define MJ_BS " << bs << "\n#define MJ_NPROJ " << nproj << "\n#define MJ_NUTF8 " << nutf8
+      << (std::getenv("MURR_JIT_STAMPS") ? "\n#define MJ_STAMPS 1" : "")
+      << (std::getenv("MURR_JIT_RO8") ? "\n#define MJ_RO8 1" : "") << "\n#define MJ_BS " << bs << "\n#define MJ_NPROJ " << nproj << "\n#define MJ_NUTF8 " << nutf8
       << "\n#define MJ_FIXED_GROUPS";
     // fixed columns in groups of `group` (loads of a group precede its stores)
     uint32_t group = 4;
@@ -166,7 +167,8 @@ bool compile(Entry& e, const std::string& pre, int device, const JitShape& s) {
 // the span ring and the consumers' utf8 wave totals.
 uint32_t jit_tile_rows(const JitShape& s) { return 64 * (s.nw - 1) * s.r; }
 uint32_t jit_lds_bytes(const JitShape& s) {
-    const uint32_t ro = ((jit_tile_rows(s) + 1) * 8 + 16 + 15) & ~15u;
+    const uint32_t ro8 = std::getenv("MURR_JIT_RO8") ? 2 : 1;  // tuning: unpacked row offsets
+    const uint32_t ro = ((jit_tile_rows(s) + 1) * 4 * ro8 + 16 + 15) & ~15u;
     return s.slots * (ro + s.stage + 64) + 128 + 16 + 4 * std::max<uint32_t>(s.nutf8, 1) * (s.nw - 1);
 }
 

@@ -86,12 +86,23 @@ struct Args {
 constexpr uint32_t NW = MJ_NW, NC = MJ_NW - 1, R = MJ_R, TR = 64 * NC * MJ_R, BS = MJ_BS, NPROJ = MJ_NPROJ,
                    NUTF8 = MJ_NUTF8, STAGE = MJ_STAGE;
 // LDS slot: [row offsets (TR+1)*8 + 16][blob stage STAGE + 64 pad]
-constexpr uint32_t RO_BYTES = ((TR + 1) * 8 + 16 + 15) & ~15u;
+// Row offsets are staged packed: the low dword of each u64 (a gather DMA),
+// 4 B per row; tiles never span 4 GiB of blob bytes.  MJ_RO8 (tuning): stage
+// the u64 slice as is, 1 KiB per DMA instruction.
+#ifndef MJ_RO8
+#define MJ_RO8 0
+#endif
+constexpr uint32_t RO_W = MJ_RO8 ? 2 : 1;  // dwords per staged row offset
+constexpr uint32_t RO_BYTES = ((TR + 1) * 4 * RO_W + 16 + 15) & ~15u;
 constexpr uint32_t SLOT = RO_BYTES + STAGE + 64;
-constexpr uint32_t RO_PIECES = (RO_BYTES + 1023) / 1024;
 constexpr uint32_t ST_PIECES = STAGE / 1024;
-constexpr uint32_t LDS_SPAN = 2 * SLOT;                 // [4][16 B] tile spans
-constexpr uint32_t LDS_CNT = LDS_SPAN + 64;
+#ifndef MJ_SLOTS
+#define MJ_SLOTS 3
+#endif
+constexpr uint32_t NSLOT = MJ_SLOTS;                    // LDS ring slots (tiles in flight + 1)
+static_assert(NSLOT >= 2 && NSLOT <= 4, "2..4 slots");
+constexpr uint32_t LDS_SPAN = NSLOT * SLOT;             // [8][16 B] tile spans
+constexpr uint32_t LDS_CNT = LDS_SPAN + 128;
 constexpr uint32_t LDS_WT = LDS_CNT + 16;              // [NUTF8][NC] u32 wave totals
 constexpr uint32_t LDS_TOTAL = LDS_WT + 4 * (NUTF8 ? NUTF8 : 1) * NC;
 static_assert(STAGE % 1024 == 0, "stage is whole 1 KiB pieces");
@@ -287,15 +298,37 @@ DEV Tile tile_info(const Cur& c, const LAS uint8_t* ent) {
 
 // The loader wave's LDS-DMA of one tile: its row-offset slice, then (unless
 // it outgrew the stage) its blob span, in 1 KiB pieces.
-DEV void tile_dma(const Tile& T, const Cur& c, LAS uint8_t* slot, uint32_t lane) {
-    const GAS uint8_t* s0 = (const GAS uint8_t*)((uintptr_t)(c.row_off + c.r0) & ~(uintptr_t)15);
-    const uint32_t nb_ro = (T.ro_shift + (T.nr + 1) * 8 + 15) & ~15u;
-    for (uint32_t q = 0; q * 1024 < nb_ro; q++)
-        if (q * 1024 + lane * 16 < nb_ro) glds16(s0 + q * 1024 + lane * 16, slot + q * 1024);
-    if (T.hbm) return;
+DEV uint32_t tile_dma(const Tile& T, const Cur& c, LAS uint8_t* slot, uint32_t lane) {
+    // row offsets: lane j of piece q fetches the low dword of row_off[r0 + 64q + j]
+    uint32_t n = 0;
+    if (MJ_RO8) {
+        const GAS uint8_t* s0 = (const GAS uint8_t*)((uintptr_t)(c.row_off + c.r0) & ~(uintptr_t)15);
+        const uint32_t nb_ro = (T.ro_shift + (T.nr + 1) * 8 + 15) & ~15u;
+        for (uint32_t q = 0; q * 1024 < nb_ro; q++, n++)
+            if (q * 1024 + lane * 16 < nb_ro) glds16(s0 + q * 1024 + lane * 16, slot + q * 1024);
+    } else {
+        const GAS uint32_t* ro = (const GAS uint32_t*)(c.row_off + c.r0);
+        for (uint32_t q = 0; q * 64 <= T.nr; q++, n++)  // lane 0 is always active: one instruction each
+            if (q * 64 + lane <= T.nr) glds4(ro + 2 * (q * 64 + lane), slot + q * 256);
+    }
+    if (T.hbm) return n;
     const GAS uint8_t* g = gp(c.data) + T.abase;
-    for (uint32_t q = 0; q * 1024 < T.span; q++)
+    for (uint32_t q = 0; q * 1024 < T.span; q++, n++)
         if (q * 1024 + lane * 16 < T.span) glds16(g + q * 1024 + lane * 16, slot + RO_BYTES + q * 1024);
+    return n;
+}
+
+// s_waitcnt vmcnt(n) for a wave-uniform run-time n (clamped to the 6-bit
+// field: a larger n waits for more than needed, never for less).
+DEV void wait_vmcnt(uint32_t n) {
+    switch (n < 63u ? n : 63u) {
+#define W(N) case N: asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory"); break;
+        W(0) W(1) W(2) W(3) W(4) W(5) W(6) W(7) W(8) W(9) W(10) W(11) W(12) W(13) W(14) W(15)
+        W(16) W(17) W(18) W(19) W(20) W(21) W(22) W(23) W(24) W(25) W(26) W(27) W(28) W(29) W(30) W(31)
+        W(32) W(33) W(34) W(35) W(36) W(37) W(38) W(39) W(40) W(41) W(42) W(43) W(44) W(45) W(46) W(47)
+        W(48) W(49) W(50) W(51) W(52) W(53) W(54) W(55) W(56) W(57) W(58) W(59) W(60) W(61) W(62) W(63)
+#undef W
+    }
 }
 
 // ---- per-row state of a wave's R chunks ----------------------------------------
@@ -541,7 +574,7 @@ DEV void decode_tile(const Src& src, const Tile& T, const LAS uint32_t* ro, LAS 
 #pragma unroll
     for (int k = 0; k < (int)R; k++) {
         const uint32_t i = rbase + k * 64 + lane;
-        const uint32_t a0 = ro[2 * i], a1 = ro[2 * i + 2];
+        const uint32_t a0 = ro[RO_W * i], a1 = ro[RO_W * (i + 1)];
         const uint32_t rl = i < T.nr ? a1 - a0 : 0u;
         W.ra[k] = a0 - abase;
         badk |= (uint32_t)(rl != 0 && rl < BS) << k;
@@ -584,7 +617,7 @@ DEV void decode_tile(const Src& src, const Tile& T, const LAS uint32_t* ro, LAS 
         for (int k = 0; k < (int)R; k++) {
             if (!((badk >> k) & 1)) continue;
             const uint32_t i = rbase + k * 64 + lane;
-            report_row(src, W.ra[k], ro[2 * i + 2] - ro[2 * i], T.b, T.r0 + i, err);
+            report_row(src, W.ra[k], ro[RO_W * (i + 1)] - ro[RO_W * i], T.b, T.r0 + i, err);
         }
     }
 
@@ -671,27 +704,45 @@ DEV void kernel_body() {
     if (!cur.ok) return;
 
     if (wave == NC) {
-        // ---- loader: tile i+1's DMA and tile i+2's span while the consumers
-        // decode tile i; it issues no other vector-memory instruction, so its
-        // vmcnt(0) waits for exactly those, never for the consumers' stores.
-        span_issue(cur, spans, 0, lane);
+        // ---- loader: NSLOT-1 tiles in flight.  At iteration i (after tile
+        // barrier B_i freed slot (i-1) % NSLOT) it DMAs tile i+NSLOT-1 and
+        // the span of tile i+NSLOT+1.  It issues no other vector-memory
+        // instruction, so its counted vmcnt waits for exactly the DMA it
+        // needs (tile i+1, and the span of tile i+NSLOT it reads next), never
+        // for the consumers' stores.
+        Cur cs = cur;  // next tile whose span to fetch
+        for (uint32_t k = 0; k <= NSLOT; k++) {
+            span_issue(cs, spans + (k & 7) * 16, 0, lane);
+            cur_next(cs);
+        }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        Tile T = tile_info(cur, spans);
-        tile_dma(T, cur, lds, lane);
-        Cur nxt = cur;
-        cur_next(nxt);
-        span_issue(nxt, spans + 16, 0, lane);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        lds_barrier();  // B_0: tile 0 and span 1 landed
-        for (uint32_t it = 0;; it++) {
-            const uint32_t more = nxt.ok;
-            if (more) {
-                const Tile Tn = tile_info(nxt, spans + ((it + 1) & 3) * 16);
-                tile_dma(Tn, nxt, lds + ((it + 1) & 1) * SLOT, lane);
-                cur_next(nxt);
-                span_issue(nxt, spans + ((it + 2) & 3) * 16, 0, lane);
+        Cur cd = cur;  // next tile to DMA
+        uint32_t after0 = 0;
+        for (uint32_t j = 0; j + 1 < NSLOT; j++) {
+            if (cd.ok) {
+                const uint32_t n = tile_dma(tile_info(cd, spans + (j & 7) * 16), cd, lds + j * SLOT, lane);
+                if (j) after0 += n;
             }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            cur_next(cd);
+        }
+        wait_vmcnt(after0);
+        lds_barrier();  // B_0: tile 0 and the spans of tiles 0 .. NSLOT landed
+        Cur cc = cur;  // the tile the decode waves work on in this iteration
+        for (uint32_t it = 0;; it++) {
+            cur_next(cc);
+            const uint32_t more = cc.ok;
+            uint32_t nd = 0, ns = 0;
+            if (cd.ok) {
+                const uint32_t t = it + NSLOT - 1;
+                nd = tile_dma(tile_info(cd, spans + (t & 7) * 16), cd, lds + (t % NSLOT) * SLOT, lane);
+                cur_next(cd);
+            }
+            if (cs.ok) {
+                span_issue(cs, spans + ((it + NSLOT + 1) & 7) * 16, 0, lane);
+                ns = 1;
+                cur_next(cs);
+            }
+            wait_vmcnt(NSLOT == 2 ? ns : nd + ns);
             lds_barrier();  // B_i+1: tile i+1 landed, tile i decoded
             if (!more) break;
         }
@@ -705,9 +756,9 @@ DEV void kernel_body() {
     for (uint32_t j = 0; j < NNV; j++) nn[j] = 0;
     lds_barrier();  // B_0
     for (uint32_t it = 0;; it++) {
-        LAS uint8_t* slot = lds + (it & 1) * SLOT;
-        const Tile T = tile_info(cur, spans + (it & 3) * 16);
-        const LAS uint32_t* ro = (const LAS uint32_t*)(slot + T.ro_shift);
+        LAS uint8_t* slot = lds + (it % NSLOT) * SLOT;
+        const Tile T = tile_info(cur, spans + (it & 7) * 16);
+        const LAS uint32_t* ro = (const LAS uint32_t*)(slot + (MJ_RO8 ? T.ro_shift : 0u));
         if (!LEN && NUTF8 && T.seg_first && !T.first) seg_prefix(cur, run, lane);
         if (T.hbm == 2) {  // a tile over 4 GiB of blob bytes (unsupported): report; prefixes undefined
             if (wave == 0 && lane == 0) report(args()->err, err_key(T.b, T.r0, 0, kStMalformed));
