@@ -124,9 +124,9 @@ void* murr_ctx_stream(murr_ctx_t* ctx);
 /* Device time of the last decode / encode kernel(s), HIP events recorded on
  * the context stream around the kernel launches only (no copies). */
 int  murr_ctx_last_kernel_ms(murr_ctx_t* ctx, float* ms);
-/* Name of the kernel the last decode launched: "murr_jit_decode" (the
- * run-time specialised kernel) or "decode_kernel" (the generic one); "" before
- * any decode.  Owned by the context, valid until its next decode. */
+/* Name of the kernel the last decode / encode launched: "murr_jit_decode" /
+ * "murr_jit_encode" (run-time specialised) or "decode_kernel" /
+ * "encode_kernel" (generic); "" before any.  A static string. */
 const char* murr_ctx_last_kernel(murr_ctx_t* ctx);
 int  murr_device_count(int* n);
 

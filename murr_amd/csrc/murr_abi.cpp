@@ -674,10 +674,31 @@ int murr_encode_batch(murr_ctx_t* c, const murr_segment_t* seg, const murr_col_i
     a.nutf8 = nutf8;
     a.bs = seg->bitset_size;
     a.cap = seg->capacity;
+    // Run-time specialised encode kernel unless MURR_ENCODE_JIT=0 (or it cannot
+    // be compiled: then the generic encode_kernel).
+    const JitEncKernel* ek = nullptr;
+    {
+        const char* je = std::getenv("MURR_ENCODE_JIT");
+        if (!(je && std::atoi(je) == 0) && seg->ncols) {
+            std::string why;
+            ek = jit_encode_kernel(c->device, seg->bitset_size, seg->capacity, ec.data(), seg->ncols, &why);
+            if (!ek && (std::getenv("MURR_DECODE_VERBOSE") || (je && std::atoi(je) == 1)))
+                std::fprintf(stderr, "murr: JIT encode unavailable: %s\n", why.c_str());
+            if (!ek && je && std::atoi(je) == 1) return set_err(err, MURR_E_INTERNAL);
+        }
+    }
     HIPC(hipEventRecord(c->k0, c->stream));
     if (tiles) {
-        uint64_t grid = std::min<uint64_t>(tiles, (uint64_t)c->cus * c->enc_grid_per_cu);
-        HIPC(launch_encode(a, (uint32_t)grid, c->stream));
+        // persistent grid, co-resident (the utf8 window prefix waits on tiles t-G+1 .. t-1)
+        const int per_cu = ek ? std::max(1, ek->bpc - 1) : c->enc_grid_per_cu;
+        uint64_t grid = std::min<uint64_t>(tiles, (uint64_t)c->cus * per_cu);
+        if (ek) {
+            HIPC(jit_encode_launch(ek, a, (uint32_t)grid, c->stream));
+            c->last_kernel = "murr_jit_encode";
+        } else {
+            HIPC(launch_encode(a, (uint32_t)grid, c->stream));
+            c->last_kernel = "encode_kernel";
+        }
     }
     HIPC(hipEventRecord(c->k1, c->stream));
     c->timed = true;

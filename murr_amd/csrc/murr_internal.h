@@ -126,6 +126,17 @@ uint32_t jit_tile_rows(const JitShape& s);
 uint32_t jit_lds_bytes(const JitShape& s);
 hipError_t jit_decode_launch(const JitKernel* k, const JitArgs& a, uint32_t grid, hipStream_t s, bool lengths);
 
+// Run-time specialised encode kernel (murr_jit.cpp, murr_jit_encode.hip).
+struct JitEncKernel {
+    hipFunction_t fn;
+    int bpc;  // resident workgroups per CU
+};
+struct EncCol;
+const JitEncKernel* jit_encode_kernel(int device, uint32_t bs, uint32_t cap, const EncCol* cols, uint32_t ncols,
+                                      std::string* why);
+struct EncodeArgs;
+hipError_t jit_encode_launch(const JitEncKernel* k, const EncodeArgs& a, uint32_t grid, hipStream_t s);
+
 void decode_lds_plan(DecodeArgs& a, uint32_t nw, uint32_t kc, uint32_t slots, uint32_t depth);
 bool decode_shape_ok(uint32_t nw, uint32_t kc);
 hipError_t launch_decode(const DecodeArgs& a, uint32_t nw, uint32_t kc, uint32_t grid, hipStream_t s);

@@ -30,6 +30,9 @@ namespace {
 const char* const kJitSrc =
 #include "murr_jit_src.inc"
     ;
+const char* const kJitEncSrc =
+#include "murr_jit_encode_src.inc"
+    ;
 
 struct Entry {
     hipModule_t mod = nullptr;
@@ -189,6 +192,93 @@ const JitKernel* jit_decode_kernel(int device, uint32_t bs, const DecProj* dp, u
         return nullptr;
     }
     return &it->second->k;
+}
+
+// ---- encode ------------------------------------------------------------------
+
+namespace {
+
+struct EncEntry {
+    hipModule_t mod = nullptr;
+    JitEncKernel k{};
+    bool ok = false;
+    std::string why;
+};
+std::map<std::string, std::unique_ptr<EncEntry>> g_enc;
+
+std::string enc_prelude(uint32_t bs, uint32_t cap, const EncCol* cols, uint32_t ncols, uint32_t stage) {
+    std::ostringstream o;
+    uint32_t nutf8 = 0;
+    for (uint32_t c = 0; c < ncols; c++) nutf8 += cols[c].dtype == MURR_UTF8;
+    o << "#define MJE_BS " << bs << "\n#define MJE_CAP " << cap << "\n#define MJE_NCOLS " << ncols
+      << "\n#define MJE_NUTF8 " << nutf8 << "\n#define MJE_STAGE " << stage << "\n#define MJE_COLS(X)";
+    for (uint32_t c = 0, u = 0; c < ncols; c++) {
+        const uint32_t kind = cols[c].dtype == MURR_UTF8 ? 0u : cols[c].dtype == MURR_BOOL ? 9u : cols[c].width;
+        o << " X(" << c << ", " << kind << ", " << cols[c].soff << ", " << (kind == 0 ? u++ : 0u) << ")";
+    }
+    o << "\n";
+    return o.str();
+}
+
+}  // namespace
+
+const JitEncKernel* jit_encode_kernel(int device, uint32_t bs, uint32_t cap, const EncCol* cols, uint32_t ncols,
+                                      std::string* why) {
+    const uint32_t stage = 32768;
+    const std::string pre = enc_prelude(bs, cap, cols, ncols, stage);
+    const std::string key = std::to_string(device) + "\n" + pre;
+    std::lock_guard<std::mutex> lk(g_mu);
+    auto it = g_enc.find(key);
+    if (it == g_enc.end()) {
+        auto e = std::make_unique<EncEntry>();
+        const std::string src = pre + kJitEncSrc;
+        hiprtcProgram prog;
+        const char* opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17"};
+        if (hiprtcCreateProgram(&prog, src.c_str(), "murr_jit_encode.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS) {
+            e->why = "hiprtcCreateProgram failed";
+        } else {
+            const hiprtcResult r = hiprtcCompileProgram(prog, 3, opts);
+            if (r != HIPRTC_SUCCESS) {
+                size_t n = 0;
+                hiprtcGetProgramLogSize(prog, &n);
+                std::string log(n + 1, '\0');
+                if (n) hiprtcGetProgramLog(prog, &log[0]);
+                e->why = std::string("hiprtc: ") + hiprtcGetErrorString(r) + "\n" + log;
+            } else {
+                size_t n = 0;
+                hiprtcGetCodeSize(prog, &n);
+                std::vector<char> code(n);
+                hiprtcGetCode(prog, code.data());
+                int cur = 0;
+                (void)hipGetDevice(&cur);
+                (void)hipSetDevice(device);
+                hipError_t he = hipModuleLoadData(&e->mod, code.data());
+                if (he == hipSuccess) he = hipModuleGetFunction(&e->k.fn, e->mod, "murr_jit_encode");
+                int bpc = 0;
+                if (he == hipSuccess &&
+                    (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, e->k.fn, 256, 0) != hipSuccess || bpc < 1))
+                    bpc = 1;
+                e->k.bpc = bpc;
+                if (he != hipSuccess) e->why = std::string("module load: ") + hipGetErrorString(he);
+                e->ok = he == hipSuccess;
+                (void)hipSetDevice(cur);
+            }
+            hiprtcDestroyProgram(&prog);
+        }
+        it = g_enc.emplace(key, std::move(e)).first;
+    }
+    if (!it->second->ok) {
+        if (why) *why = it->second->why;
+        return nullptr;
+    }
+    return &it->second->k;
+}
+
+hipError_t jit_encode_launch(const JitEncKernel* k, const EncodeArgs& a, uint32_t grid, hipStream_t s) {
+    EncodeArgs args = a;
+    size_t sz = sizeof(args);
+    void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &args, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
+    return hipModuleLaunchKernel(k->fn, grid, 1, 1, 256, 1, 1, 0, s, nullptr, cfg);
 }
 
 hipError_t jit_decode_launch(const JitKernel* k, const JitArgs& a, uint32_t grid, hipStream_t s, bool lengths) {

@@ -1,0 +1,377 @@
+// murr_jit_encode.hip — schema-specialised encode kernel (Arrow buffers -> row
+// blobs), compiled at run time per segment layout like the decode kernel
+// (murr_jit.cpp).  The host prepends a prelude fixing the bitset size, the
+// static capacity and, per column in segment order, its kind and offset.
+//
+// Replaces Table::write's row loop: WriteRow::new (0xFF bitset), then every
+// column's ColumnDecoder::write_to_row (src/io/table/mod.rs:97-109,
+// src/io/row/write.rs:19-52, primitive.rs:85-95, bool_.rs:111-117,
+// utf8.rs:113-119).  Same contract and arguments as encode_kernel
+// (murr_kernels.hip).
+//
+// One thread builds one row of a 256-row tile.  The row's fixed part (bitset
+// + static region) is assembled in registers with compile-time byte
+// placement, shifted to its byte position and merged into an LDS stage of the
+// tile (zeroed first; ds_or on the two edge dwords, plain stores between);
+// utf8 payloads are merged the same way.  The stage then goes out with
+// aligned 16-B stores.  Without utf8 columns every row has the same size and
+// row i starts at i * (bs + cap); with them, row sizes are scanned in the tile
+// and tiles are chained by a one-hop window prefix (persistent grid).
+
+#ifdef __HIPCC_RTC__
+typedef unsigned char uint8_t;
+typedef unsigned short uint16_t;
+typedef unsigned int uint32_t;
+typedef unsigned long long uint64_t;
+typedef int int32_t;
+typedef long long int64_t;
+typedef unsigned long long uintptr_t;
+#else  // offline syntax/ISA check build
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#endif
+
+#define GAS __attribute__((address_space(1)))
+#define LAS __attribute__((address_space(3)))
+#define CAS __attribute__((address_space(4)))
+#define DEV __device__ __forceinline__
+
+typedef uint32_t __attribute__((aligned(1))) u32u;
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+namespace mje {
+
+struct Col {  // = murr::EncCol
+    const uint8_t* values;
+    const uint8_t* validity;
+    const int32_t* offsets;
+    uint64_t offset;
+    uint32_t dtype, index, soff, width;
+};
+struct Args {  // = murr::EncodeArgs
+    const Col* cols;
+    uint8_t* out;
+    uint64_t* row_off;       // n_rows + 1
+    uint64_t* lookback;      // [total_tiles]
+    unsigned long long* err;
+    uint64_t n_rows, out_cap, total_tiles;
+    uint32_t ncols, nutf8, bs, cap;
+};
+
+constexpr uint32_t TILE = 256, BS = MJE_BS, CAP = MJE_CAP, NCOLS = MJE_NCOLS, NUTF8 = MJE_NUTF8,
+                   STAGE = MJE_STAGE;
+constexpr uint32_t FIXED = BS + CAP;
+constexpr uint32_t NR = (FIXED + 3) / 4;  // dwords of the fixed part
+enum : uint32_t { kStCapacity = 6, kStInternal = 10 };
+constexpr uint32_t kSpinLimit = 1u << 22;
+
+DEV uint64_t err_key(uint64_t block, uint64_t row, uint32_t col, uint32_t status) {
+    if (row > 0xFFFFFFFFull) row = 0xFFFFFFFFull;
+    if (block > 0x3FFFFull) block = 0x3FFFFull;
+    return (block << 46) | (row << 14) | ((uint64_t)(col & 0x3FF) << 4) | (status & 0xF);
+}
+DEV void report(unsigned long long* err, uint64_t key) {
+    __hip_atomic_fetch_max((GAS unsigned long long*)err, (unsigned long long)~key, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+}
+template <class T> DEV GAS T* gp(T* p) { return (GAS T*)p; }
+template <class T> DEV const GAS T* gp(const T* p) { return (const GAS T*)p; }
+
+DEV const CAS Args* args() {
+    const CAS Args* ap = (const CAS Args*)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(ap));
+    return ap;
+}
+DEV Col ldcol(uint32_t c) {
+    const CAS Col* p = (const CAS Col*)args()->cols + c;
+    Col r;
+    r.values = p->values; r.validity = p->validity; r.offsets = p->offsets; r.offset = p->offset;
+    return r;
+}
+
+// Arrow validity (null buffer absent = all valid).
+DEV bool valid(const Col& c, uint64_t e) {
+    if (!c.validity) return true;
+    return (gp(c.validity)[e >> 3] >> (e & 7)) & 1;
+}
+
+// The fixed part of one row as dwords, byte placement at compile time.
+struct Row {
+    uint32_t w[NR + 1];
+};
+template <uint32_t OFF> DEV void put8(Row& r, uint32_t v) { r.w[OFF / 4] |= (v & 0xFFu) << (8 * (OFF % 4)); }
+template <uint32_t OFF> DEV void put16(Row& r, uint32_t v) {
+    v &= 0xFFFFu;
+    r.w[OFF / 4] |= v << (8 * (OFF % 4));
+    if constexpr (OFF % 4 == 3) r.w[OFF / 4 + 1] |= v >> 8;
+}
+template <uint32_t OFF> DEV void put32(Row& r, uint32_t v) {
+    r.w[OFF / 4] |= v << (8 * (OFF % 4));
+    if constexpr (OFF % 4 != 0) r.w[OFF / 4 + 1] |= v >> (32 - 8 * (OFF % 4));
+}
+
+// Wave64 inclusive scan (u32) on DPP; block scan across the 4 waves.
+DEV uint32_t wave_scan(uint32_t v) {
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x111, 0xF, 0xF, false);
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x112, 0xF, 0xF, false);
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x114, 0xF, 0xF, false);
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x118, 0xF, 0xF, false);
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x142, 0xA, 0xF, false);
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x143, 0xC, 0xF, false);
+    return v;
+}
+
+// Cross-tile prefix by a one-hop window sum (tiles dealt round-robin to a
+// persistent grid; this workgroup's previous tile is t - G): the aggregates
+// of tiles (t-G, t) are read with agent-scope loads, every tile waited on is
+// resident or done, spins are bounded.
+DEV uint64_t window_prefix(const uint64_t* st, uint64_t lo, uint64_t t, uint64_t base, LAS uint64_t* s_w,
+                           unsigned long long* err, uint64_t ekey) {
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    uint64_t sum = 0;
+    for (uint64_t j = lo + tid; j < t; j += TILE) {
+        uint64_t v = __hip_atomic_load(gp(st) + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        uint32_t spins = 0;
+        while (v == 0) {
+            __builtin_amdgcn_s_sleep(2);
+            v = __hip_atomic_load(gp(st) + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (++spins > kSpinLimit) { report(err, ekey | kStInternal); v = 1; break; }
+        }
+        sum += v - 1;
+    }
+    for (int m = 32; m >= 1; m >>= 1) sum += (uint64_t)__shfl_xor((unsigned long long)sum, m, 64);
+    if (lane == 0) s_w[wave] = sum;
+    __syncthreads();
+    const uint64_t tot = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+    __syncthreads();
+    return base + tot;
+}
+
+// Merge `v` (4 stream bytes starting at stage byte b) into the zeroed stage.
+DEV void or_bytes(LAS uint32_t* stw, uint32_t b, uint32_t v, uint32_t nbytes) {
+    if (nbytes < 4) v &= (1u << (8 * nbytes)) - 1u;
+    const uint32_t d = b >> 2, sh = b & 3u;
+    __hip_atomic_fetch_or(stw + d, v << (8 * sh), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (sh && (v >> (32 - 8 * sh)))
+        __hip_atomic_fetch_or(stw + d + 1, v >> (32 - 8 * sh), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// Copy stage[0, span) to out[g0, g0 + span): aligned 16-B stores in the middle,
+// byte stores for the unaligned head and tail (other tiles own their
+// neighbours).
+DEV void write_out(const LAS uint8_t* buf, GAS uint8_t* out, uint64_t g0, uint64_t span, uint32_t tid) {
+    const uint64_t g1 = g0 + span;
+    const uint64_t a0 = (g0 + 15) & ~15ull, a1 = g1 & ~15ull;
+    if (a0 >= a1) {
+        for (uint64_t k = tid; k < span; k += TILE) out[g0 + k] = buf[k];
+        return;
+    }
+    if (tid < a0 - g0) out[g0 + tid] = buf[tid];
+    if (tid < g1 - a1) out[a1 + tid] = buf[a1 - g0 + tid];
+    const uint32_t lb0 = (uint32_t)(a0 - g0), sh = lb0 & 3u;
+    const LAS uint32_t* w = (const LAS uint32_t*)buf;
+    const uint64_t nch = (a1 - a0) >> 4;
+    GAS u32x4* o = (GAS u32x4*)(out + a0);
+    for (uint64_t c = tid; c < nch; c += TILE) {
+        const uint32_t q = (lb0 >> 2) + 4 * (uint32_t)c;
+        const uint32_t d0 = w[q], d1 = w[q + 1], d2 = w[q + 2], d3 = w[q + 3], d4 = w[q + 4];
+        u32x4 v;
+        v.x = __builtin_amdgcn_alignbyte(d1, d0, sh);
+        v.y = __builtin_amdgcn_alignbyte(d2, d1, sh);
+        v.z = __builtin_amdgcn_alignbyte(d3, d2, sh);
+        v.w = __builtin_amdgcn_alignbyte(d4, d3, sh);
+        o[c] = v;
+    }
+}
+
+// One row's fixed part and payload sizes.  `pos` = payload append position
+// (write.rs:44-52), starting at bs + cap.
+struct RowBuild {
+    Row r;
+    uint32_t vmask[(NCOLS + 31) / 32 ? (NCOLS + 31) / 32 : 1];  // valid bits, segment order
+    uint32_t pos;
+    uint32_t ulen[NUTF8 ? NUTF8 : 1];
+    uint64_t ustart[NUTF8 ? NUTF8 : 1];  // Arrow data offset of the string
+};
+
+template <uint32_t C, uint32_t KIND, uint32_t SOFF, uint32_t U>
+DEV void build_col(RowBuild& B, uint64_t row) {
+    const Col c = ldcol(C);
+    const uint64_t e = c.offset + row;
+    const bool v = valid(c, e);
+    B.vmask[C / 32] |= (uint32_t)v << (C % 32);
+    constexpr uint32_t OFF = BS + SOFF;
+    if constexpr (KIND == 0) {  // utf8: slot = payload offset relative to the static region
+        uint32_t len = 0;
+        uint64_t a = 0;
+        if (v) {
+            const int32_t s0 = gp(c.offsets)[e], s1 = gp(c.offsets)[e + 1];
+            len = (uint32_t)(s1 - s0);
+            a = (uint64_t)(int64_t)s0;
+        }
+        put32<OFF>(B.r, v ? B.pos - BS : 0u);
+        B.ulen[U] = v ? len : 0u;
+        B.ustart[U] = a;
+        if (v) B.pos += 4 + len;
+    } else if constexpr (KIND == 9) {  // bool: b as u8 (bool_.rs:111-117)
+        const uint32_t b = v ? (gp(c.values)[e >> 3] >> (e & 7)) & 1u : 0u;
+        put8<OFF>(B.r, b);
+    } else if constexpr (KIND == 8) {
+        uint32_t lo = 0, hi = 0;
+        if (v) {
+            const GAS uint32_t* p = (const GAS uint32_t*)(gp(c.values) + e * 8);
+            lo = p[0];
+            hi = p[1];
+        }
+        put32<OFF>(B.r, lo);
+        put32<OFF + 4>(B.r, hi);
+    } else if constexpr (KIND == 4) {
+        put32<OFF>(B.r, v ? ((const GAS uint32_t*)gp(c.values))[e] : 0u);
+    } else if constexpr (KIND == 2) {
+        put16<OFF>(B.r, v ? (uint32_t)((const GAS uint16_t*)gp(c.values))[e] : 0u);
+    } else {
+        put8<OFF>(B.r, v ? (uint32_t)gp(c.values)[e] : 0u);
+    }
+}
+
+// The bitset (WriteRow::new fills 0xFF; set_non_null clears a column's bit).
+DEV void put_bitset(RowBuild& B) {
+#pragma unroll
+    for (uint32_t k = 0; k < (BS + 3) / 4; k++) {
+        uint32_t w = ~0u;
+        if (k * 32 < NCOLS) w &= ~B.vmask[k];  // bits of valid columns cleared
+        const uint32_t nb = BS - 4 * k < 4 ? BS - 4 * k : 4;
+        if (nb < 4) w &= (1u << (8 * nb)) - 1u;
+        B.r.w[k] |= w;
+    }
+}
+
+// Utf8 payloads of one row into the stage: u32 len, then the bytes.
+template <uint32_t C, uint32_t U>
+DEV void put_payload(const RowBuild& B, LAS uint32_t* stw, uint32_t rb, uint32_t& p) {
+    const uint32_t n = B.ulen[U];
+    if (!((B.vmask[C / 32] >> (C % 32)) & 1)) return;
+    or_bytes(stw, rb + p, n, 4);
+    p += 4;
+    const Col c = ldcol(C);
+    const GAS uint8_t* s = gp(c.values) + B.ustart[U];
+    uint32_t q = 0;
+    for (; q + 4 <= n; q += 4) or_bytes(stw, rb + p + q, *(const GAS u32u*)(s + q), 4);
+    if (q < n) {
+        uint32_t v = 0;
+        for (uint32_t t = 0; q + t < n; t++) v |= (uint32_t)s[q + t] << (8 * t);
+        or_bytes(stw, rb + p + q, v, n - q);
+    }
+    p += n;
+}
+
+}  // namespace mje
+
+extern "C" __global__ void __launch_bounds__(256) murr_jit_encode(mje::Args) {
+    using namespace mje;
+    __shared__ __attribute__((aligned(16))) uint32_t stage[STAGE / 4 + 8];
+    __shared__ uint64_t s_w[8];
+    LAS uint32_t* stw = (LAS uint32_t*)stage;
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const CAS Args* A = args();
+    const uint64_t n_rows = A->n_rows, total_tiles = A->total_tiles, out_cap = A->out_cap;
+    uint64_t prev_incl = 0;
+
+    for (uint64_t t = blockIdx.x; t < total_tiles; t += gridDim.x) {
+        const uint64_t r0 = t * TILE;
+        const uint32_t nr = (uint32_t)min((uint64_t)TILE, n_rows - r0);
+        const bool active = tid < nr;
+        const uint64_t row = r0 + (active ? tid : 0u);
+
+        RowBuild B;
+#pragma unroll
+        for (uint32_t k = 0; k <= NR; k++) B.r.w[k] = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < sizeof(B.vmask) / 4; k++) B.vmask[k] = 0;
+        B.pos = FIXED;
+#define MJE_DO_COL(C, KIND, SOFF, U) build_col<C, KIND, SOFF, U>(B, row);
+        MJE_COLS(MJE_DO_COL)
+#undef MJE_DO_COL
+        put_bitset(B);
+        const uint32_t size = active ? B.pos : 0u;
+
+        uint64_t start, tstart, span;
+        if (NUTF8 == 0) {
+            start = (r0 + tid) * (uint64_t)FIXED;
+            tstart = r0 * (uint64_t)FIXED;
+            span = (uint64_t)nr * FIXED;
+        } else {
+            // block scan of the row sizes, then the window prefix
+            const uint32_t inc = wave_scan(size);
+            if (lane == 63) s_w[wave] = inc;
+            __syncthreads();
+            uint64_t before = 0, agg = 0;
+#pragma unroll
+            for (uint32_t w = 0; w < 4; w++) {
+                const uint64_t v = s_w[w];
+                before += w < wave ? v : 0u;
+                agg += v;
+            }
+            __syncthreads();
+            if (tid == 0)
+                __hip_atomic_store(gp(A->lookback) + t, agg + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const uint64_t G = gridDim.x;
+            const bool have_prev = t >= G;
+            tstart = window_prefix(A->lookback, have_prev ? t - G + 1 : 0, t, have_prev ? prev_incl : 0, (LAS uint64_t*)(s_w + 4),
+                                   A->err, err_key(0, r0, 0, 0));
+            prev_incl = tstart + agg;
+            start = tstart + before + inc - size;
+            span = agg;
+        }
+        if (active) {
+            gp(A->row_off)[row] = start;
+            if (row + 1 == n_rows) gp(A->row_off)[row + 1] = start + size;
+        }
+        if (tstart + span > out_cap) {
+            if (tid == 0) report(A->err, err_key(0, r0, 0, kStCapacity));
+            continue;  // uniform
+        }
+        if (span <= STAGE) {
+            // zero the stage, merge the rows, write it out
+            for (uint32_t k = tid; k < (uint32_t)((span + 7) >> 2) + 1; k += TILE) stw[k] = 0;
+            __syncthreads();
+            if (active) {
+                const uint32_t rb = (uint32_t)(start - tstart), sh = rb & 3u, d0 = rb >> 2;
+#pragma unroll
+                for (uint32_t k = 0; k <= NR; k++) {
+                    const uint32_t cur = B.r.w[k], prev = k ? B.r.w[k - 1] : 0u;
+                    const uint32_t v = sh ? __builtin_amdgcn_alignbyte(cur, prev, 4 - sh) : cur;
+                    // dwords wholly inside the fixed part are this row's alone
+                    if (k >= 1 && 4 * k + 4 <= FIXED + sh) stw[d0 + k] = v;
+                    else if (v) __hip_atomic_fetch_or(stw + d0 + k, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                }
+                if (NUTF8) {
+                    uint32_t p = FIXED;
+#define MJE_DO_PAY(C, KIND, SOFF, U) if (KIND == 0) put_payload<C, U>(B, stw, rb, p);
+                    MJE_COLS(MJE_DO_PAY)
+#undef MJE_DO_PAY
+                }
+            }
+            __syncthreads();
+            write_out((const LAS uint8_t*)stage, gp(A->out), tstart, span, tid);
+            __syncthreads();
+        } else if (active) {
+            // a tile over the stage: bytes straight to HBM (cold)
+            GAS uint8_t* o = gp(A->out) + start;
+            for (uint32_t b = 0; b < FIXED; b++) o[b] = (uint8_t)(B.r.w[b >> 2] >> (8 * (b & 3)));
+            if (NUTF8) {
+                uint32_t p = FIXED;
+#define MJE_DO_PAYG(C, KIND, SOFF, U)                                                   \
+    if (KIND == 0 && ((B.vmask[C / 32] >> (C % 32)) & 1)) {                             \
+        const uint32_t n = B.ulen[U];                                                   \
+        for (uint32_t b = 0; b < 4; b++) o[p + b] = (uint8_t)(n >> (8 * b));            \
+        const GAS uint8_t* s = gp(ldcol(C).values) + B.ustart[U];                       \
+        for (uint32_t b = 0; b < n; b++) o[p + 4 + b] = s[b];                           \
+        p += 4 + n;                                                                     \
+    }
+                MJE_COLS(MJE_DO_PAYG)
+#undef MJE_DO_PAYG
+            }
+        }
+    }
+}

@@ -11,6 +11,14 @@ from murr_amd.device import Context, encode_batch
 from murr_amd.schema import DTypeName as D, SegmentSchema
 
 pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(autouse=True, params=["jit", "generic"])
+def kernel_mode(request, monkeypatch):
+    """Every encode test runs on both kernels: run-time specialised
+    (murr_jit_encode.hip) and generic (murr_kernels.hip)."""
+    monkeypatch.setenv("MURR_ENCODE_JIT", "1" if request.param == "jit" else "0")
+    return request.param
 CASES = load_cases()
 
 
