@@ -382,20 +382,20 @@ int murr_decode_enqueue(murr_ctx_t* c, const murr_segment_t* seg, const uint32_t
     {
         const char* je = std::getenv("MURR_DECODE_JIT");
         const int jmode = je ? std::atoi(je) : -1;
-        // Tile shape from the mean row size: the largest tile (5 waves x 2
-        // chunks, 5 x 1, 3 x 1) whose two LDS slots, with 15 % slack over the
-        // mean, fit 40 KiB, so that four workgroups share a CU.  (Three slots,
-        // i.e. two tiles in flight, measured no faster: tools/ab_env.sh.)
+        // Tile shape from the mean row size (tools/jit_sweep.sh on configs B,
+        // C, D): 5 waves x 2 chunks (512 rows) when its two LDS slots fit
+        // 40 KiB with 15 % slack (four workgroups per CU); else 5 x 1 (256 rows)
+        // within 64 KiB with 8 % slack (two per CU, wide rows); else 3 x 1.
         JitShape js{3, 1, 0, nutf8, 2};
         double slack = 1.15;  // stage bytes over the hinted mean row size
-        static const uint32_t cand[][2] = {{5, 2}, {5, 1}, {3, 1}};
-        for (const auto& cs : cand) {
-            const double t = 64.0 * (cs[0] - 1) * cs[1];
-            if (js.slots * (4.0 * (t + 1) + 32 + t * est_row * slack + 64) <= 40960.0) {
-                js.nw = cs[0];
-                js.r = cs[1];
-                break;
-            }
+        auto need = [&](uint32_t nw, uint32_t r, double sl) {
+            const double t = 64.0 * (nw - 1) * r;
+            return 2.0 * (4.0 * (t + 1) + 32 + t * est_row * sl + 64) + 256;
+        };
+        if (need(5, 2, 1.15) <= 40960.0) {
+            js.nw = 5; js.r = 2;
+        } else if (need(5, 1, 1.08) <= 65536.0) {
+            js.nw = 5; js.r = 1; slack = 1.08;
         }
         if (const char* e = std::getenv("MURR_JIT_SHAPE"))  // tuning: "NWxR[xSLOTS[xSLACK]]"
             std::sscanf(e, "%ux%ux%ux%lf", &js.nw, &js.r, &js.slots, &slack);
@@ -455,12 +455,19 @@ int murr_decode_enqueue(murr_ctx_t* c, const murr_segment_t* seg, const uint32_t
         jslots = std::max<uint64_t>(1, (uint64_t)c->cus * jk->bpc);
         uint64_t jtiles = 0;
         for (uint32_t b = 0; b < nblocks; b++) jtiles += (blocks[b].n_rows + jk->tr - 1) / jk->tr;
-        uint64_t seg_tiles = ~0ull;
-        if (nonempty < (uint32_t)c->cus) seg_tiles = std::max<uint64_t>(1, (jtiles + jslots - 1) / jslots);
-        if (const char* e = std::getenv("MURR_JIT_SEGTILES")) seg_tiles = std::max(1, std::atoi(e));  // tuning
-        const uint64_t seg_rows = seg_tiles == ~0ull ? ~0ull : seg_tiles * jk->tr;
+        const bool cut = nonempty < (uint32_t)c->cus;
+        const char* fixed_tiles = std::getenv("MURR_JIT_SEGTILES");  // tuning: tiles per segment
         for (uint32_t b = 0; b < nblocks; b++) {
             const uint64_t n = blocks[b].n_rows;
+            const uint64_t tb = (n + jk->tr - 1) / jk->tr;
+            // equal cuts, about jslots segments over the launch (one round)
+            uint64_t per = tb;
+            if (fixed_tiles) per = std::max(1, std::atoi(fixed_tiles));
+            else if (cut && tb) {
+                const uint64_t ns = std::max<uint64_t>(1, tb * jslots / std::max<uint64_t>(jtiles, 1));
+                per = (tb + ns - 1) / ns;
+            }
+            const uint64_t seg_rows = per * jk->tr;
             const uint32_t first = (uint32_t)jsegs.size();
             for (uint64_t r = 0; r < n; r = (n - r > seg_rows ? r + seg_rows : n))
                 jsegs.push_back(JitSeg{b, first, r, n - r > seg_rows ? r + seg_rows : n});
