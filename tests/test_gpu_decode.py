@@ -223,3 +223,20 @@ def test_split_blocks_utf8_prefix(ctx, kernel_mode, monkeypatch, seg_tiles):
     for b in range(len(blocks)):
         for p in range(len(proj)):
             assert_array_equal(got[b][p], wants[b][p], f"block {b} proj {p}")
+
+
+def test_wide_schema_multi_byte_bitset(ctx, kernel_mode):
+    # 70 columns (a 9-byte bitset: the per-byte null path) and a 100-column
+    # projection with duplicates (more than 64 projected columns)
+    rng = np.random.default_rng(77)
+    dtypes = [D(int(d)) for d in rng.choice(ALL, size=70)]
+    n = 700
+    cols = random_columns(rng, dtypes, n, null_p=0.2, max_str=9)
+    oseg, data, off = oracle_block(dtypes, cols, n, missing={5, 64, 699})
+    proj = [int(x) for x in rng.integers(0, 70, size=100)]
+    got = gpu_decode(ctx, seg_of(dtypes), proj, [(data, off)])[0]
+    assert ctx.last_kernel() == KERNEL[kernel_mode]
+    want = O.decode_block(oseg, proj, data, off)
+    for p in range(len(proj)):
+        assert_array_equal(got[p], want[p], f"proj {p} ({dtypes[proj[p]].name})")
+        check_padding(got[p], n)

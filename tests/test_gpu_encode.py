@@ -111,3 +111,15 @@ def test_empty_batch(ctx):
     cols = random_columns(np.random.default_rng(0), dtypes, 0)
     blob, off = gpu_encode(ctx, dtypes, cols, 0)
     assert off.tolist() == [0] and blob.size == 0
+
+
+def test_wide_schema_encode(ctx, kernel_mode):
+    # 70 columns: a 9-byte bitset, every dtype at every field alignment
+    rng = np.random.default_rng(78)
+    dtypes = [D(int(d)) for d in rng.choice(ALL, size=70)]
+    n = 900
+    cols = random_columns(rng, dtypes, n, null_p=0.2, max_str=9)
+    blob, off = gpu_encode(ctx, dtypes, cols, n)
+    wblob, woff = O.encode_batch(O.Segment([int(d) for d in dtypes]), synth.oracle_cols(cols), n)
+    assert np.array_equal(off, woff)
+    assert blob.tobytes() == wblob.tobytes()
