@@ -160,7 +160,8 @@ typedef struct {
  *   utf8:     offsets = n+1 i32 starting at 0, values = string bytes (values_cap)
  *   validity: bitmap (murr_bitmap_bytes(n)), 1 = valid; the caller drops it
  *             when null_count == 0 (arrow-rs NullBufferBuilder materialises
- *             validity only after the first null).
+ *             validity only after the first null), and its bytes are then
+ *             unspecified (the decoder may not write them).
  * null_count / data_len are outputs. */
 typedef struct {
     void*    values;

@@ -386,7 +386,7 @@ int murr_decode_enqueue(murr_ctx_t* c, const murr_segment_t* seg, const uint32_t
         // C, D): 5 waves x 2 chunks (512 rows) when its two LDS slots fit
         // 40 KiB with 15 % slack (four workgroups per CU); else 5 x 1 (256 rows)
         // within 64 KiB with 8 % slack (two per CU, wide rows); else 3 x 1.
-        JitShape js{3, 1, 0, nutf8, 2};
+        JitShape js{3, 1, 0, nutf8, 2, nproj};
         double slack = 1.15;  // stage bytes over the hinted mean row size
         auto need = [&](uint32_t nw, uint32_t r, double sl) {
             const double t = 64.0 * (nw - 1) * r;

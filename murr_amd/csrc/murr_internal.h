@@ -99,6 +99,7 @@ __host__ __device__ inline uint64_t err_key(uint64_t block, uint64_t row, uint32
 struct JitShape {
     uint32_t nw, r, stage, nutf8;  // waves (nw-1 decode, 1 loads), 64-row chunks per decoding wave, stage bytes
     uint32_t slots;                // LDS ring slots (tiles in flight + 1)
+    uint32_t nproj;                // projected columns (LDS of kernel variants)
 };
 struct JitKernel {
     hipFunction_t fn, fn_len;      // decode, and the length pass of split blocks

@@ -172,7 +172,8 @@ uint32_t jit_tile_rows(const JitShape& s) { return 64 * (s.nw - 1) * s.r; }
 uint32_t jit_lds_bytes(const JitShape& s) {
     const uint32_t ro8 = std::getenv("MURR_JIT_RO8") ? 2 : 1;  // tuning: unpacked row offsets
     const uint32_t ro = ((jit_tile_rows(s) + 1) * 4 * ro8 + 16 + 15) & ~15u;
-    return s.slots * (ro + s.stage + 64) + 128 + 16 + 4 * std::max<uint32_t>(s.nutf8, 1) * (s.nw - 1);
+    const uint32_t wt = (4 * std::max<uint32_t>(s.nutf8, 1) * (s.nw - 1) + 15) & ~15u;
+    return s.slots * (ro + s.stage + 64) + 128 + 16 + wt;
 }
 
 const JitKernel* jit_decode_kernel(int device, uint32_t bs, const DecProj* dp, uint32_t nproj, uint32_t nutf8,
