@@ -72,6 +72,16 @@ struct murr_ctx {
     uint64_t rb_off = 0;           // readback offset in hs
     int pending_status = MURR_OK;
     const char* last_kernel = "";  // kernel of the last decode launch
+    // Staging buffers of freed builders, reused by the next ones (a read builds
+    // a ReadBatchBuilder per batch, src/io/row/read.rs:69-83; pinned and device
+    // allocations cost far more than the batch itself).
+    struct Buf {
+        uint8_t* p;
+        uint64_t cap;
+        bool pinned;
+    };
+    std::vector<Buf> pool;
+    std::vector<hipEvent_t> event_pool;
 };
 
 namespace {
@@ -200,6 +210,8 @@ void murr_ctx_destroy(murr_ctx_t* c) {
     if (c->stream) hipStreamSynchronize(c->stream);
     if (c->ws) hipFree(c->ws);
     if (c->hs) hipHostFree(c->hs);
+    for (const auto& b : c->pool) (void)(b.pinned ? hipHostFree(b.p) : hipFree(b.p));
+    for (hipEvent_t e : c->event_pool) (void)hipEventDestroy(e);
     if (c->k0) hipEventDestroy(c->k0);
     if (c->k1) hipEventDestroy(c->k1);
     if (c->stream) hipStreamDestroy(c->stream);
@@ -756,27 +768,56 @@ struct murr_builder {
 
 namespace {
 
-bool grow_pinned(uint8_t** p, uint64_t* cap, uint64_t need, uint64_t keep) {
+// Context buffer pool: the smallest pooled buffer of the kind that holds
+// `need` bytes, else a new allocation of at least `want`.
+constexpr size_t kPoolMax = 32;
+bool pool_take(murr_ctx* c, bool pinned, uint64_t need, uint64_t want, uint8_t** p, uint64_t* cap) {
+    size_t best = c->pool.size();
+    for (size_t i = 0; i < c->pool.size(); i++)
+        if (c->pool[i].pinned == pinned && c->pool[i].cap >= need &&
+            (best == c->pool.size() || c->pool[i].cap < c->pool[best].cap))
+            best = i;
+    if (best < c->pool.size()) {
+        *p = c->pool[best].p;
+        *cap = c->pool[best].cap;
+        c->pool.erase(c->pool.begin() + best);
+        return true;
+    }
+    *p = nullptr;
+    if ((pinned ? hipHostMalloc(p, want, hipHostMallocDefault) : hipMalloc(p, want)) != hipSuccess) return false;
+    *cap = want;
+    return true;
+}
+void pool_give(murr_ctx* c, bool pinned, uint8_t* p, uint64_t cap) {
+    if (!p) return;
+    if (c && c->pool.size() < kPoolMax) {
+        c->pool.push_back(murr_ctx::Buf{p, cap, pinned});
+        return;
+    }
+    (void)(pinned ? hipHostFree(p) : hipFree(p));
+}
+
+bool grow_pinned(murr_ctx* c, uint8_t** p, uint64_t* cap, uint64_t need, uint64_t keep) {
     if (need <= *cap) return true;
-    uint64_t nc = std::max<uint64_t>(need, std::max<uint64_t>(*cap * 2, 1 << 16));
+    const uint64_t nc = std::max<uint64_t>(need, std::max<uint64_t>(*cap * 2, 1 << 16));
     uint8_t* q = nullptr;
-    if (hipHostMalloc(&q, nc, hipHostMallocDefault) != hipSuccess) return false;
+    uint64_t qc = 0;
+    if (!pool_take(c, true, need, nc, &q, &qc)) return false;
     if (*p) {
         if (keep) std::memcpy(q, *p, keep);
-        hipHostFree(*p);
+        pool_give(c, true, *p, *cap);
     }
     *p = q;
-    *cap = nc;
+    *cap = qc;
     return true;
 }
 
-bool grow_dev(uint8_t** p, uint64_t* cap, uint64_t need) {
+bool grow_dev(murr_ctx* c, uint8_t** p, uint64_t* cap, uint64_t need) {
     if (need <= *cap) return true;
-    if (*p) hipFree(*p);
+    pool_give(c, false, *p, *cap);
     *p = nullptr;
-    uint64_t nc = round_up(std::max<uint64_t>(need, 1 << 16), 1 << 16);
-    if (hipMalloc(p, nc) != hipSuccess) { *cap = 0; return false; }
-    *cap = nc;
+    const uint64_t nc = round_up(std::max<uint64_t>(need, 1 << 16), 1 << 16);
+    if (!pool_take(c, false, need, nc, p, cap)) { *cap = 0; return false; }
     return true;
 }
 
@@ -784,7 +825,7 @@ bool push_off(murr_builder* b) {
     if (b->n + 2 > b->hoff_cap) {
         uint8_t* p = (uint8_t*)b->hoff;
         uint64_t capb = b->hoff_cap * 8;
-        if (!grow_pinned(&p, &capb, (b->n + 2) * 8, (b->n + 1) * 8)) return false;
+        if (!grow_pinned(b->ctx, &p, &capb, (b->n + 2) * 8, (b->n + 1) * 8)) return false;
         b->hoff = (uint64_t*)p;
         b->hoff_cap = capb / 8;
     }
@@ -812,15 +853,22 @@ int murr_builder_new(murr_ctx_t* c, const murr_segment_t* seg, const uint32_t* p
     uint64_t cap = std::max<uint64_t>(capacity, 16);
     uint64_t capb = 0;
     uint8_t* p = nullptr;
-    if (!grow_pinned(&p, &capb, (cap + 2) * 8, 0)) { delete b; return MURR_E_HIP; }
+    if (!grow_pinned(c, &p, &capb, (cap + 2) * 8, 0)) { delete b; return MURR_E_HIP; }
     b->hoff = (uint64_t*)p;
     b->hoff_cap = capb / 8;
     b->hoff[0] = 0;
-    if (!grow_pinned(&b->hdata, &b->hdata_cap, cap * ((uint64_t)seg->bitset_size + seg->capacity + 16), 0)) {
+    if (!grow_pinned(c, &b->hdata, &b->hdata_cap, cap * ((uint64_t)seg->bitset_size + seg->capacity + 16), 0)) {
         murr_builder_free(b);
         return MURR_E_HIP;
     }
-    hipEventCreate(&b->e0); hipEventCreate(&b->e1); hipEventCreate(&b->e2); hipEventCreate(&b->e3);
+    for (hipEvent_t* e : {&b->e0, &b->e1, &b->e2, &b->e3}) {
+        if (!c->event_pool.empty()) {
+            *e = c->event_pool.back();
+            c->event_pool.pop_back();
+        } else {
+            (void)hipEventCreate(e);
+        }
+    }
     *out = b;
     return MURR_OK;
 }
@@ -830,7 +878,7 @@ int murr_builder_new(murr_ctx_t* c, const murr_segment_t* seg, const uint32_t* p
 int murr_builder_add_row(murr_builder_t* b, const uint8_t* bytes, uint64_t len) {
     if (!b || (len && !bytes)) return MURR_E_ARGUMENT;
     if (len == 0) return MURR_E_MALFORMED_ROW;  // a present row is never empty (write.rs:21)
-    if (!grow_pinned(&b->hdata, &b->hdata_cap, b->hdata_len + len, b->hdata_len)) return MURR_E_HIP;
+    if (!grow_pinned(b->ctx, &b->hdata, &b->hdata_cap, b->hdata_len + len, b->hdata_len)) return MURR_E_HIP;
     std::memcpy(b->hdata + b->hdata_len, bytes, len);
     b->hdata_len += len;
     b->present++;
@@ -881,9 +929,9 @@ int murr_builder_build(murr_builder_t* b, murr_host_array_t* outs, murr_error_t*
         if (col.dtype == MURR_UTF8) off = round_up(off + (n + 1) * 4, 64);
     }
     const uint64_t total_out = std::max<uint64_t>(off, 64);
-    if (!grow_dev(&b->ddata, &b->ddata_cap, dbytes + obytes + 64) ||
-        !grow_dev(&b->dout, &b->dout_cap, total_out) ||
-        !grow_pinned(&b->hout, &b->hout_cap, total_out, 0))
+    if (!grow_dev(c, &b->ddata, &b->ddata_cap, dbytes + obytes + 64) ||
+        !grow_dev(c, &b->dout, &b->dout_cap, total_out) ||
+        !grow_pinned(c, &b->hout, &b->hout_cap, total_out, 0))
         return set_err(err, MURR_E_HIP);
     uint8_t* ddata = b->ddata;
     uint64_t* doff = (uint64_t*)(b->ddata + round_up(dbytes, 64));
@@ -901,23 +949,41 @@ int murr_builder_build(murr_builder_t* b, murr_host_array_t* outs, murr_error_t*
         a.offsets = col.dtype == MURR_UTF8 ? (int32_t*)(b->dout + b->out_off[3 * p + 2]) : nullptr;
         a.values_cap = utf8_cap;
     }
-    int st = murr_decode_blocks(c, &b->seg, b->proj.data(), (uint32_t)np, &blk, 1, b->arr.data(), err);
-    if (st) return st;
-    HIPC(hipEventRecord(b->e2, c->stream));
-    for (uint64_t p = 0; p < np; p++) {
-        const murr_column_t& col = b->cols[b->proj[p]];
-        const murr_array_t& a = b->arr[p];
-        uint64_t vlen = a.data_len;
-        if (vlen) HIPC(hipMemcpyAsync(b->hout + b->out_off[3 * p], a.values, vlen, hipMemcpyDeviceToHost, c->stream));
-        if (a.null_count)
-            HIPC(hipMemcpyAsync(b->hout + b->out_off[3 * p + 1], a.validity, (n + 7) / 8,
-                                hipMemcpyDeviceToHost, c->stream));
-        if (col.dtype == MURR_UTF8)
-            HIPC(hipMemcpyAsync(b->hout + b->out_off[3 * p + 2], a.offsets, (n + 1) * 4,
-                                hipMemcpyDeviceToHost, c->stream));
+    // A small batch (the point-lookup case) copies its whole output region
+    // back in one D2H right behind the decode, with no round trip to learn
+    // the sizes; a large one waits for the sizes and copies exactly the bytes.
+    constexpr uint64_t kOneCopy = 1 << 20;
+    int st = murr_decode_enqueue(c, &b->seg, b->proj.data(), (uint32_t)np, &blk, 1, b->arr.data());
+    if (st) {
+        if (err && st != MURR_E_HIP) set_err(err, st);
+        else if (err) set_err(err, st, (int)hipGetLastError());
+        return st;
     }
-    HIPC(hipEventRecord(b->e3, c->stream));
-    HIPC(hipStreamSynchronize(c->stream));
+    if (total_out <= kOneCopy) {
+        HIPC(hipEventRecord(b->e2, c->stream));
+        HIPC(hipMemcpyAsync(b->hout, b->dout, total_out, hipMemcpyDeviceToHost, c->stream));
+        HIPC(hipEventRecord(b->e3, c->stream));
+        st = murr_decode_wait(c, err);
+        if (st) return st;
+    } else {
+        st = murr_decode_wait(c, err);
+        if (st) return st;
+        HIPC(hipEventRecord(b->e2, c->stream));
+        for (uint64_t p = 0; p < np; p++) {
+            const murr_column_t& col = b->cols[b->proj[p]];
+            const murr_array_t& a = b->arr[p];
+            uint64_t vlen = a.data_len;
+            if (vlen) HIPC(hipMemcpyAsync(b->hout + b->out_off[3 * p], a.values, vlen, hipMemcpyDeviceToHost, c->stream));
+            if (a.null_count)
+                HIPC(hipMemcpyAsync(b->hout + b->out_off[3 * p + 1], a.validity, (n + 7) / 8,
+                                    hipMemcpyDeviceToHost, c->stream));
+            if (col.dtype == MURR_UTF8)
+                HIPC(hipMemcpyAsync(b->hout + b->out_off[3 * p + 2], a.offsets, (n + 1) * 4,
+                                    hipMemcpyDeviceToHost, c->stream));
+        }
+        HIPC(hipEventRecord(b->e3, c->stream));
+        HIPC(hipStreamSynchronize(c->stream));
+    }
     for (uint64_t p = 0; p < np; p++) {
         const murr_column_t& col = b->cols[b->proj[p]];
         const murr_array_t& a = b->arr[p];
@@ -950,16 +1016,19 @@ int murr_builder_last_timing(murr_builder_t* b, double* total_ms, float* h2d_ms,
 
 void murr_builder_free(murr_builder_t* b) {
     if (!b) return;
-    if (b->ctx) hipSetDevice(b->ctx->device);
-    if (b->hdata) hipHostFree(b->hdata);
-    if (b->hoff) hipHostFree(b->hoff);
-    if (b->hout) hipHostFree(b->hout);
-    if (b->ddata) hipFree(b->ddata);
-    if (b->dout) hipFree(b->dout);
-    if (b->e0) hipEventDestroy(b->e0);
-    if (b->e1) hipEventDestroy(b->e1);
-    if (b->e2) hipEventDestroy(b->e2);
-    if (b->e3) hipEventDestroy(b->e3);
+    murr_ctx* c = b->ctx;
+    if (c) (void)hipSetDevice(c->device);
+    // buffers and events go back to the context's pool for the next builder
+    pool_give(c, true, b->hdata, b->hdata_cap);
+    pool_give(c, true, (uint8_t*)b->hoff, b->hoff_cap * 8);
+    pool_give(c, true, b->hout, b->hout_cap);
+    pool_give(c, false, b->ddata, b->ddata_cap);
+    pool_give(c, false, b->dout, b->dout_cap);
+    for (hipEvent_t e : {b->e0, b->e1, b->e2, b->e3}) {
+        if (!e) continue;
+        if (c) c->event_pool.push_back(e);
+        else (void)hipEventDestroy(e);
+    }
     delete b;
 }
 
