@@ -249,7 +249,7 @@ def run_encode(args):
     """configs[4] write shape: Arrow (10 x f32) -> row blobs, device-resident."""
     ctx = Context(0)
     n = args.rows
-    cols = synth.config_e(n)
+    cols = make_columns(args.enc_config, n, 0)
     seg = SegmentSchema([(f"col_{i}", c["dtype"]) for i, c in enumerate(cols)])
     dcols = synth.upload_columns(ctx, cols)
     for _ in range(args.warmup):
@@ -261,10 +261,11 @@ def run_encode(args):
         kms.append(ctx.last_kernel_ms())
         del blob, off
     el = time.perf_counter() - t0
-    bytes_in = sum(c["values"].nbytes for c in cols)
+    bytes_in = sum(c["values"].nbytes + (c["offsets"].nbytes if c["offsets"] is not None else 0)
+                   + (c["validity"].nbytes if c["validity"] is not None else 0) for c in cols)
     bytes_out = blen + 8 * (n + 1)
     k = float(np.mean(kms))
-    print(json.dumps({"mode": "encode", "rows": n, "bytes_in": bytes_in, "bytes_out": bytes_out,
+    print(json.dumps({"mode": "encode", "config": args.enc_config, "kernel": ctx.last_kernel(), "rows": n, "bytes_in": bytes_in, "bytes_out": bytes_out,
                       "kernel_ms_avg": round(k, 4), "ms_per_step": round(el / args.steps * 1e3, 3),
                       "GB_s_algorithmic": round((bytes_in + bytes_out) / (k * 1e-3) / 1e9, 1),
                       "frac_of_8TBs": round((bytes_in + bytes_out) / (k * 1e-3) / 8e12, 4),
@@ -283,6 +284,7 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--pmc-csv", default=None)
+    ap.add_argument("--enc-config", default="E", choices=["B", "C", "E"], help="encode mode: column set")
     ap.add_argument("--proj", default=None, help="comma-separated projected columns (default all)")
     args = ap.parse_args()
     if args.rows is None:

@@ -129,7 +129,7 @@ hipError_t jit_decode_launch(const JitKernel* k, const JitArgs& a, uint32_t grid
 
 // Run-time specialised encode kernel (murr_jit.cpp, murr_jit_encode.hip).
 struct JitEncKernel {
-    hipFunction_t fn;
+    hipFunction_t fn, fn_sizes, fn_scan;  // encode; tile sizes and their scan (utf8 layouts)
     int bpc;  // resident workgroups per CU
 };
 struct EncCol;

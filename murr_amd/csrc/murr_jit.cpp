@@ -255,6 +255,8 @@ const JitEncKernel* jit_encode_kernel(int device, uint32_t bs, uint32_t cap, con
                 (void)hipSetDevice(device);
                 hipError_t he = hipModuleLoadData(&e->mod, code.data());
                 if (he == hipSuccess) he = hipModuleGetFunction(&e->k.fn, e->mod, "murr_jit_encode");
+                if (he == hipSuccess) he = hipModuleGetFunction(&e->k.fn_sizes, e->mod, "murr_jit_encode_sizes");
+                if (he == hipSuccess) he = hipModuleGetFunction(&e->k.fn_scan, e->mod, "murr_jit_encode_scan");
                 int bpc = 0;
                 if (he == hipSuccess &&
                     (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, e->k.fn, 256, 0) != hipSuccess || bpc < 1))
@@ -279,6 +281,26 @@ hipError_t jit_encode_launch(const JitEncKernel* k, const EncodeArgs& a, uint32_
     EncodeArgs args = a;
     size_t sz = sizeof(args);
     void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &args, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
+    if (a.nutf8) {
+        // tile starts: tile sums (a workgroup per tile), then their exclusive
+        // scan over 4096-tile groups (sums, one-workgroup scan of the sums, prefixes)
+        const uint32_t tiles = (uint32_t)std::min<uint64_t>(a.total_tiles, 0x7FFFFFFFull);
+        const uint32_t groups = (uint32_t)((a.total_tiles + 4095) / 4096);
+        hipError_t e = hipModuleLaunchKernel(k->fn_sizes, tiles, 1, 1, 256, 1, 1, 0, s, nullptr, cfg);
+        struct {
+            EncodeArgs a;
+            uint32_t pass;
+        } sa{a, 0};
+        size_t ssz = sizeof(sa);
+        void* scfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &sa, HIP_LAUNCH_PARAM_BUFFER_SIZE, &ssz, HIP_LAUNCH_PARAM_END};
+        if (e == hipSuccess) e = hipModuleLaunchKernel(k->fn_scan, groups, 1, 1, 1024, 1, 1, 0, s, nullptr, scfg);
+        sa.pass = 2;
+        if (e == hipSuccess) e = hipModuleLaunchKernel(k->fn_scan, 1, 1, 1, 1024, 1, 1, 0, s, nullptr, scfg);
+        sa.pass = 1;
+        if (e == hipSuccess) e = hipModuleLaunchKernel(k->fn_scan, groups, 1, 1, 1024, 1, 1, 0, s, nullptr, scfg);
+        if (e != hipSuccess) return e;
+        grid = tiles;  // no co-resident grid needed: a workgroup per tile
+    }
     return hipModuleLaunchKernel(k->fn, grid, 1, 1, 256, 1, 1, 0, s, nullptr, cfg);
 }
 

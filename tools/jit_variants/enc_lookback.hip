@@ -15,10 +15,9 @@
 // tile (zeroed first; ds_or on the two edge dwords, plain stores between);
 // utf8 payloads are merged the same way.  The stage then goes out with
 // aligned 16-B stores.  Without utf8 columns every row has the same size and
-// row i starts at i * (bs + cap); with them, murr_jit_encode_sizes sums each
-// tile's row sizes (validity and utf8 offsets only), murr_jit_encode_scan
-// turns the sums into tile starts, and the encode scans its rows inside the
-// tile.
+// row i starts at i * (bs + cap); with them, a workgroup per tile takes tiles
+// in ticket order, scans its row sizes, and chains tiles by a decoupled
+// look-back over the tile status words.
 
 #ifdef __HIPCC_RTC__
 typedef unsigned char uint8_t;
@@ -256,13 +255,23 @@ DEV void put_payload(const RowBuild& B, LAS uint32_t* stw, uint32_t rb, uint32_t
 extern "C" __global__ void __launch_bounds__(256) murr_jit_encode(mje::Args) {
     using namespace mje;
     __shared__ __attribute__((aligned(16))) uint32_t stage[STAGE / 4 + 8];
-    __shared__ uint64_t s_w[8];
+    __shared__ uint64_t s_w[8];  // [0..3] wave sums, [5] tile prefix, [6] ticket
     LAS uint32_t* stw = (LAS uint32_t*)stage;
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const CAS Args* A = args();
     const uint64_t n_rows = A->n_rows, total_tiles = A->total_tiles, out_cap = A->out_cap;
 
-    for (uint64_t t = blockIdx.x; t < total_tiles; t += gridDim.x) {
+    for (uint64_t t0 = blockIdx.x; t0 < total_tiles; t0 += gridDim.x) {
+        // utf8 layouts: tiles in ticket order (a workgroup per tile), so that
+        // every tile the look-back waits on has started
+        uint64_t t = t0;
+        if (NUTF8) {
+            if (tid == 0) s_w[6] = __hip_atomic_fetch_add(gp(A->lookback) + total_tiles, 1ull, __ATOMIC_RELAXED,
+                                                          __HIP_MEMORY_SCOPE_AGENT);
+            __syncthreads();
+            t = s_w[6];
+            __syncthreads();
+        }
         const uint64_t r0 = t * TILE;
         const uint32_t nr = (uint32_t)min((uint64_t)TILE, n_rows - r0);
         const bool active = tid < nr;
@@ -297,10 +306,47 @@ extern "C" __global__ void __launch_bounds__(256) murr_jit_encode(mje::Args) {
                 before += w < wave ? v : 0u;
                 agg += v;
             }
+            // Decoupled look-back: publish the aggregate (flag 1), find the
+            // nearest predecessor with an inclusive prefix (flag 2), summing
+            // the aggregates in between (64 predecessors per pass, wave 0),
+            // then publish this tile's inclusive prefix.  Status word: flag in
+            // bits 62-63, bytes below.
+            GAS unsigned long long* st = (GAS unsigned long long*)A->lookback;
+            constexpr unsigned long long kAgg = 1ull << 62, kInc = 2ull << 62, kVal = (1ull << 62) - 1;
+            if (tid == 0)
+                __hip_atomic_store(st + t, (t == 0 ? kInc : kAgg) | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (wave == 0) {
+                uint64_t pre = 0;
+                uint32_t spins = 0;
+                for (uint64_t j = t; j > 0;) {  // predecessors j-1, j-2, ...
+                    const uint64_t q = j > (uint64_t)lane ? j - 1 - lane : ~0ull;
+                    const unsigned long long v =
+                        q != ~0ull ? __hip_atomic_load(st + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kInc;
+                    const uint64_t inc_m = __ballot((v >> 62) == 2), any_m = __ballot((v >> 62) != 0);
+                    const uint32_t d = inc_m ? (uint32_t)__builtin_ctzll(inc_m) : 64u;  // first inclusive
+                    const uint64_t need = d >= 63 ? ~0ull : (2ull << d) - 1;
+                    if (d < 64 ? (any_m & need) == need : any_m == ~0ull) {
+                        uint64_t x = (uint32_t)lane <= d ? (uint64_t)(v & kVal) : 0ull;
+                        for (int m = 32; m >= 1; m >>= 1) x += (uint64_t)__shfl_xor((unsigned long long)x, m, 64);
+                        pre += x;
+                        if (d < 64) break;
+                        j = j > 64 ? j - 64 : 0;
+                        continue;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                    if (++spins > kSpinLimit) {
+                        if (lane == 0) report(A->err, err_key(0, r0, 0, kStInternal));
+                        break;
+                    }
+                }
+                if (lane == 0) {
+                    if (t) __hip_atomic_store(st + t, kInc | (pre + agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    s_w[5] = pre;
+                }
+            }
             __syncthreads();
-            // the tile's start: murr_jit_encode_sizes + murr_jit_encode_scan
-            // left the exclusive prefix of the tile totals in lookback[t]
-            tstart = ((const GAS uint64_t*)A->lookback)[t];
+            tstart = s_w[5];
+            __syncthreads();
             start = tstart + before + inc - size;
             span = agg;
         }
@@ -354,104 +400,5 @@ extern "C" __global__ void __launch_bounds__(256) murr_jit_encode(mje::Args) {
 #undef MJE_DO_PAYG
             }
         }
-    }
-}
-
-// Row sizes of each tile: bs + cap + sum over non-null utf8 of (4 + len),
-// summed into lookback[t] (the Arrow validity and offsets only).
-extern "C" __global__ void __launch_bounds__(256) murr_jit_encode_sizes(mje::Args) {
-    using namespace mje;
-    __shared__ uint64_t s_w[4];
-    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const CAS Args* A = args();
-    const uint64_t n_rows = A->n_rows, total_tiles = A->total_tiles;
-    for (uint64_t t = blockIdx.x; t < total_tiles; t += gridDim.x) {
-        const uint64_t row = t * TILE + tid;
-        uint64_t size = 0;
-        if (row < n_rows) {
-            size = FIXED;
-#define MJE_DO_SIZE(C, KIND, SOFF, U)                                                        \
-            if (KIND == 0) {                                                                 \
-                const Col c = ldcol(C);                                                      \
-                const uint64_t e = c.offset + row;                                           \
-                if (valid(c, e)) size += 4 + (uint32_t)(gp(c.offsets)[e + 1] - gp(c.offsets)[e]); \
-            }
-            MJE_COLS(MJE_DO_SIZE)
-#undef MJE_DO_SIZE
-        }
-        for (int m = 32; m >= 1; m >>= 1) size += (uint64_t)__shfl_xor((unsigned long long)size, m, 64);
-        if (lane == 0) s_w[wave] = size;
-        __syncthreads();
-        if (tid == 0) gp(A->lookback)[t] = s_w[0] + s_w[1] + s_w[2] + s_w[3];
-        __syncthreads();
-    }
-}
-
-// Exclusive prefix of the tile totals in place, in two launches of this
-// kernel over contiguous ranges of SCAN_PER tiles per workgroup: pass 0 sums
-// each range into lookback[T + 1 + g]; pass 1 (after a one-workgroup scan of
-// those sums) rewrites each range as its exclusive prefix.
-constexpr uint32_t SCAN_PER = 4096;
-DEV uint64_t block_excl(uint64_t x, LAS uint64_t* s_t, uint64_t* total) {
-    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    uint64_t inc = x;
-    for (uint32_t d = 1; d < 64; d <<= 1) {
-        const uint64_t y = (uint64_t)__shfl_up((unsigned long long)inc, d, 64);
-        if (lane >= d) inc += y;
-    }
-    if (lane == 63) s_t[wave] = inc;
-    __syncthreads();
-    uint64_t before = 0, all = 0;
-    for (uint32_t w = 0; w < 16; w++) {
-        const uint64_t v = s_t[w];
-        before += w < wave ? v : 0u;
-        all += v;
-    }
-    __syncthreads();
-    *total = all;
-    return before + inc - x;
-}
-extern "C" __global__ void __launch_bounds__(1024) murr_jit_encode_scan(mje::Args, uint32_t pass) {
-    using namespace mje;
-    __shared__ uint64_t s_t[16];
-    const uint32_t tid = threadIdx.x;
-    const CAS Args* A = args();
-    GAS uint64_t* v = gp(A->lookback);
-    const uint64_t T = A->total_tiles;
-    GAS uint64_t* sums = v + T + 1;
-    const uint64_t ngroups = (T + SCAN_PER - 1) / SCAN_PER;
-    if (pass == 2) {  // one workgroup: exclusive scan of the group sums (ngroups <= 1024 * 64)
-        uint64_t carry = 0;
-        for (uint64_t g0 = 0; g0 < ngroups; g0 += 1024) {
-            const uint64_t g = g0 + tid;
-            const uint64_t x = g < ngroups ? sums[g] : 0;
-            uint64_t tot;
-            const uint64_t ex = block_excl(x, (LAS uint64_t*)s_t, &tot);
-            if (g < ngroups) sums[g] = carry + ex;
-            carry += tot;
-        }
-        return;
-    }
-    const uint64_t g = blockIdx.x, lo = g * SCAN_PER, hi = min(T, lo + SCAN_PER);
-    constexpr uint32_t PER = SCAN_PER / 1024;  // 4 per thread, contiguous
-    uint64_t x[PER], s = 0;
-#pragma unroll
-    for (uint32_t q = 0; q < PER; q++) {
-        const uint64_t j = lo + tid * PER + q;
-        x[q] = j < hi ? v[j] : 0;
-        s += x[q];
-    }
-    uint64_t tot;
-    const uint64_t ex = block_excl(s, (LAS uint64_t*)s_t, &tot);
-    if (pass == 0) {
-        if (tid == 0) sums[g] = tot;
-        return;
-    }
-    uint64_t run = sums[g] + ex;
-#pragma unroll
-    for (uint32_t q = 0; q < PER; q++) {
-        const uint64_t j = lo + tid * PER + q;
-        if (j < hi) v[j] = run;
-        run += x[q];
     }
 }
