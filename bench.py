@@ -32,7 +32,7 @@ sys.path.insert(0, ROOT)
 import murr_amd  # noqa: E402
 from murr_amd import _abi, synth  # noqa: E402
 from murr_amd.device import Context, DecodeOutputs, DeviceBlock, device_count, encode_batch  # noqa: E402
-from murr_amd.schema import SegmentSchema  # noqa: E402
+from murr_amd.schema import DTypeName as D, SegmentSchema  # noqa: E402
 from murr_amd.shard import Group, shard_rows  # noqa: E402
 
 murr_amd.lib()
@@ -272,6 +272,70 @@ def run_encode(args):
                       "GiB_s_blob_out": round(bytes_out / (k * 1e-3) / GIB, 2)}))
 
 
+def run_resident(args):
+    """Device-resident Table::read (SURVEY.md §8(f) rank 1): config C table of
+    args.rows rows in HBM, `--keys` random keys per read (about 5 % misses, as
+    config C), lookup + gather (murr_index_gather) + decode (murr_decode_blocks)
+    with no host round trip in between.  Reports the wall time per read
+    (host-synchronous, launches included) and the Arrow GiB/s."""
+    from murr_amd.resident import DeviceIndex, _upload_utf8
+    import pyarrow as pa
+    ctx = Context(0)
+    n, nq = args.rows, args.keys
+    cols = make_columns("C", n, 0)
+    seg = SegmentSchema([(f"c{i}", c["dtype"]) for i, c in enumerate(cols)])
+    dblob, doff, blen = encode_batch(ctx, seg, synth.upload_columns(ctx, cols), n)
+    offs = doff.download((n + 1) * 8).view(np.uint64)
+    max_row = int(np.diff(offs).max())
+    ix = DeviceIndex(ctx, pa.array([f"key{i}" for i in range(n)], pa.string()))
+    rng = np.random.default_rng(44)
+    qsets = []
+    for _ in range(4):
+        ids = rng.integers(0, int(n * 1.05), size=nq)
+        qsets.append(_upload_utf8(ctx, pa.array([f"key{i}" for i in ids], pa.string())))
+    cap = nq * max_row
+    data, roff, needed = ctx.alloc(cap + 16), ctx.alloc((nq + 1) * 8), ctx.alloc(8)
+    blk = DeviceBlock(data, roff, nq, cap)
+    proj = list(range(len(cols)))
+    outs = DecodeOutputs(ctx, seg, proj, [blk])
+    cb = (_abi.Block * 1)()
+    cb[0].data, cb[0].row_off, cb[0].n_rows, cb[0].data_bytes = data.ptr, roff.ptr, nq, cap
+    pj = (C.c_uint32 * len(proj))(*proj)
+    err = _abi.Error()
+    L = ctx.L
+
+    def read(q):
+        st = L.murr_index_gather(ctx.h, ix.h, q[0].ptr, q[1].ptr, nq, dblob.ptr, doff.ptr, data.ptr, cap,
+                                 roff.ptr, None, needed.ptr)
+        assert st == 0, st
+        st = L.murr_decode_blocks(ctx.h, C.byref(seg.c), pj, len(proj), cb, 1, outs.arrays, C.byref(err))
+        assert st == 0, (st, err.status)
+
+    for i in range(args.warmup):
+        read(qsets[i % 4])
+    ts = []
+    for i in range(args.steps):
+        t0 = time.perf_counter()
+        read(qsets[i % 4])
+        ts.append(time.perf_counter() - t0)
+    nb = int(needed.download(8).view(np.uint64)[0])
+    assert nb <= cap
+    out_bytes = 0
+    for p in range(len(proj)):
+        a = outs.array(0, p)
+        dt = cols[p]["dtype"]
+        bm = (nq + 7) // 8
+        out_bytes += (a.data_len + 4 * (nq + 1)) if dt == D.Utf8 else a.data_len
+        out_bytes += bm if a.null_count else 0
+    med = float(np.median(ts))
+    print(json.dumps({"mode": "resident", "config": "C", "table_rows": n, "keys_per_read": nq,
+                      "gathered_bytes": nb, "arrow_bytes_out": out_bytes,
+                      "us_per_read_median": round(med * 1e6, 1),
+                      "us_per_read_p95": round(float(np.percentile(ts, 95)) * 1e6, 1),
+                      "GiB_s_arrow_out": round(out_bytes / med / GIB, 3),
+                      "kernels": "index_probe, gather_scan, gather_copy, " + ctx.last_kernel()}))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -280,7 +344,8 @@ def main():
     ap.add_argument("--config", default="B", choices=["B", "C", "D", "E"])
     ap.add_argument("--rows", type=int, default=None, help="rows per block")
     ap.add_argument("--blocks", type=int, default=None, help="blocks per launch")
-    ap.add_argument("--mode", default="decode", choices=["decode", "host", "encode"])
+    ap.add_argument("--mode", default="decode", choices=["decode", "host", "encode", "resident"])
+    ap.add_argument("--keys", type=int, default=1000, help="resident mode: keys per read")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--pmc-csv", default=None)
@@ -291,12 +356,16 @@ def main():
         args.rows = {"B": 100_000, "C": 1_000_000, "D": 1_250_000, "E": 20_000_000}[args.config]
         if args.mode == "encode":
             args.rows = 20_000_000
+        if args.mode == "resident":
+            args.rows = 1_000_000
     if args.blocks is None:
         args.blocks = {"B": 1000, "C": 1, "D": 1, "E": 1}[args.config]
     if args.mode == "host":
         return run_host(args)
     if args.mode == "encode":
         return run_encode(args)
+    if args.mode == "resident":
+        return run_resident(args)
     dist, rank, world, local_rank = dist_init(args)
     if world != args.gpus and rank == 0:
         print(f"note: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)

@@ -270,6 +270,47 @@ int murr_encode_host(murr_ctx_t* ctx, const murr_segment_t* seg,
                      uint8_t** out_blob, uint64_t* blob_len,
                      uint64_t** out_row_off, murr_error_t* err);
 
+/* ---- device-resident key index ------------------ */
+
+/* The key lookups of Store::read for a table whose row blobs live in HBM:
+ * replaces RocksDBStore::read's ParGet/MultiGet and its serial present/missing
+ * feed (src/io/store/rocksdb/mod.rs:241-267; MemoryStore::read,
+ * src/io/store/memory.rs:28-45), so lookup -> gather -> decode runs on the
+ * device with no host round trip.  Keys are the table's utf8 key column
+ * (src/io/table/mod.rs:70-96); row i of the index is row i of the blobs
+ * murr_encode_batch wrote for the same batch. */
+typedef struct murr_index murr_index_t;
+
+#define MURR_ROW_MISSING 0xFFFFFFFFu
+
+/* Build over n keys (device Arrow utf8: key_offsets[n+1], key_data; offset =
+ * Arrow array offset in elements).  The index copies the keys.  Equal keys
+ * follow put semantics: the later row wins (memory.rs:47-56).  n < 2^32 - 1.
+ * Synchronous. */
+int murr_index_build(murr_ctx_t* ctx, const uint8_t* key_data, const int32_t* key_offsets,
+                     uint64_t key_offset, uint64_t n, murr_index_t** out, murr_error_t* err);
+void murr_index_free(murr_index_t* idx);
+/* Rows indexed (n at build) and hash-table slots. */
+int murr_index_info(const murr_index_t* idx, uint64_t* n, uint64_t* slots);
+
+/* Enqueue on the ctx stream: rows[i] = row of query key i, or MURR_ROW_MISSING.
+ * Query keys are device Arrow utf8 (q_offsets[nq+1] from element 0). */
+int murr_index_lookup(murr_ctx_t* ctx, const murr_index_t* idx, const uint8_t* q_data,
+                      const int32_t* q_offsets, uint64_t nq, uint32_t* rows);
+
+/* Enqueue: lookup, then gather the hit rows of (blob, row_off) back to back
+ * into a decode block in caller order: out_row_off[nq+1] (from 0), out_data
+ * (16-B aligned, out_cap bytes); a miss is an empty row, i.e. add_empty
+ * (rocksdb/mod.rs:262-263).  rows (optional, device u32[nq]) receives the
+ * lookup.  needed (optional, device u64) receives the block bytes; offsets
+ * are clamped to out_cap, so when *needed > out_cap the block is cut short
+ * (rows past the cap read as missing) -- size out_cap as nq * the longest row
+ * to rule that out.  Feed the result to murr_decode_enqueue as one block. */
+int murr_index_gather(murr_ctx_t* ctx, const murr_index_t* idx, const uint8_t* q_data,
+                      const int32_t* q_offsets, uint64_t nq, const uint8_t* blob,
+                      const uint64_t* row_off, uint8_t* out_data, uint64_t out_cap,
+                      uint64_t* out_row_off, uint32_t* rows, uint64_t* needed);
+
 /* Human-readable name of a status code. */
 const char* murr_status_str(int status);
 

@@ -101,6 +101,11 @@ SIGNATURES = {
     "murr_encode_host": (I32, [P, C.POINTER(Segment), C.POINTER(HostColIn), U64,
                                C.POINTER(C.POINTER(C.c_uint8)), C.POINTER(U64),
                                C.POINTER(C.POINTER(C.c_uint64)), C.POINTER(Error)]),
+    "murr_index_build": (I32, [P, P, P, U64, U64, PP, C.POINTER(Error)]),
+    "murr_index_free": (None, [P]),
+    "murr_index_info": (I32, [P, C.POINTER(U64), C.POINTER(U64)]),
+    "murr_index_lookup": (I32, [P, P, P, P, U64, P]),
+    "murr_index_gather": (I32, [P, P, P, P, U64, P, P, P, U64, P, P, P]),
     "murr_status_str": (C.c_char_p, [I32]),
 }
 

@@ -13,6 +13,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <new>
+#include <memory>
 #include <vector>
 
 #include "../../include/murr_codec.h"
@@ -82,6 +83,18 @@ struct murr_ctx {
     };
     std::vector<Buf> pool;
     std::vector<hipEvent_t> event_pool;
+    uint64_t* aux = nullptr;  // device scratch of the gather scan (group sums)
+    uint64_t aux_cap = 0;     // entries
+};
+
+// Device key index (murr_index.hip): the keys' own copy and the slot table.
+struct murr_index {
+    int device = 0;
+    uint8_t* key_data = nullptr;
+    int32_t* key_off = nullptr;
+    uint64_t* slots = nullptr;
+    unsigned long long* err = nullptr;
+    uint64_t n = 0, mask = 0;
 };
 
 namespace {
@@ -131,6 +144,127 @@ int unpack_err(unsigned long long word, murr_error_t* err) {
 }  // namespace
 
 extern "C" {
+
+// ---- device key index ------------------------------------------------------
+
+void murr_index_free(murr_index_t* x) {
+    if (!x) return;
+    (void)hipSetDevice(x->device);
+    for (void* p : {(void*)x->key_data, (void*)x->key_off, (void*)x->slots, (void*)x->err})
+        if (p) (void)hipFree(p);
+    delete x;
+}
+
+int murr_index_build(murr_ctx_t* c, const uint8_t* key_data, const int32_t* key_offsets, uint64_t key_offset,
+                     uint64_t n, murr_index_t** out, murr_error_t* err) {
+    if (!c || !out || c->pending || (n && (!key_data || !key_offsets)) || n >= kMissing)
+        return set_err(err, MURR_E_ARGUMENT);
+    *out = nullptr;
+    HIPC(hipSetDevice(c->device));
+    std::unique_ptr<murr_index, void (*)(murr_index*)> x(new murr_index, murr_index_free);
+    x->device = c->device;
+    x->n = n;
+    uint64_t slots = 64;
+    while (slots < 2 * n) slots <<= 1;
+    x->mask = slots - 1;
+    // the key bytes up to the last key's end (offsets keep their values)
+    int32_t last = 0;
+    if (n) {
+        HIPC(hipMemcpyAsync(&last, key_offsets + key_offset + n, 4, hipMemcpyDeviceToHost, c->stream));
+        HIPC(hipStreamSynchronize(c->stream));
+        if (last < 0) return set_err(err, MURR_E_ARGUMENT);
+    }
+    HIPC(hipMalloc(&x->key_data, std::max<uint64_t>((uint64_t)last, 16)));
+    HIPC(hipMalloc(&x->key_off, 4 * (n + 1)));
+    HIPC(hipMalloc(&x->slots, 8 * slots));
+    HIPC(hipMalloc(&x->err, 8));
+    if (last) HIPC(hipMemcpyAsync(x->key_data, key_data, (uint64_t)last, hipMemcpyDeviceToDevice, c->stream));
+    if (n) HIPC(hipMemcpyAsync(x->key_off, key_offsets + key_offset, 4 * (n + 1), hipMemcpyDeviceToDevice, c->stream));
+    HIPC(hipMemsetAsync(x->slots, 0xFF, 8 * slots, c->stream));
+    HIPC(hipMemsetAsync(x->err, 0, 8, c->stream));
+    IndexArgs a{};
+    a.key_data = x->key_data;
+    a.key_off = x->key_off;
+    a.slots = x->slots;
+    a.mask = x->mask;
+    a.n = n;
+    a.err = x->err;
+    HIPC(launch_index_insert(a, c->stream));
+    unsigned long long word = 0;
+    HIPC(hipMemcpyAsync(&word, x->err, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPC(hipStreamSynchronize(c->stream));
+    if (word) return set_err(err, MURR_E_INTERNAL);
+    *out = x.release();
+    return MURR_OK;
+}
+
+int murr_index_info(const murr_index_t* x, uint64_t* n, uint64_t* slots) {
+    if (!x) return MURR_E_ARGUMENT;
+    if (n) *n = x->n;
+    if (slots) *slots = x->mask + 1;
+    return MURR_OK;
+}
+
+namespace {
+IndexArgs index_args(const murr_index_t* x, const uint8_t* q_data, const int32_t* q_offsets, uint64_t nq) {
+    IndexArgs a{};
+    a.key_data = x->key_data;
+    a.key_off = x->key_off;
+    a.slots = x->slots;
+    a.mask = x->mask;
+    a.n = x->n;
+    a.q_data = q_data;
+    a.q_off = q_offsets;
+    a.nq = nq;
+    return a;
+}
+}  // namespace
+
+int murr_index_lookup(murr_ctx_t* c, const murr_index_t* x, const uint8_t* q_data, const int32_t* q_offsets,
+                      uint64_t nq, uint32_t* rows) {
+    murr_error_t* err = nullptr;
+    if (!c || !x || x->device != c->device || c->pending || (nq && (!q_data || !q_offsets || !rows)))
+        return MURR_E_ARGUMENT;
+    HIPC(hipSetDevice(c->device));
+    IndexArgs a = index_args(x, q_data, q_offsets, nq);
+    a.rows = rows;
+    HIPC(launch_index_probe(a, c->stream));
+    return MURR_OK;
+}
+
+int murr_index_gather(murr_ctx_t* c, const murr_index_t* x, const uint8_t* q_data, const int32_t* q_offsets,
+                      uint64_t nq, const uint8_t* blob, const uint64_t* row_off, uint8_t* out_data,
+                      uint64_t out_cap, uint64_t* out_row_off, uint32_t* rows, uint64_t* needed) {
+    murr_error_t* err = nullptr;
+    if (!c || !x || x->device != c->device || c->pending || !out_row_off ||
+        (nq && (!q_data || !q_offsets || !row_off || (x->n && !blob) || !out_data)))
+        return MURR_E_ARGUMENT;
+    if (nq >= kMissing || ((uintptr_t)out_data & 15)) return MURR_E_ARGUMENT;
+    HIPC(hipSetDevice(c->device));
+    // scratch: the scan's group sums, then the rows when the caller wants none
+    const uint64_t groups = gather_scan_groups(nq);
+    const uint64_t need = groups + 1 + (rows ? 0 : (nq + 1) / 2);
+    if (need > c->aux_cap) {
+        if (c->aux) HIPC(hipFree(c->aux));
+        c->aux = nullptr;
+        c->aux_cap = 0;
+        const uint64_t cap = std::max<uint64_t>(need, 1 << 16);
+        HIPC(hipMalloc(&c->aux, 8 * cap));
+        c->aux_cap = cap;
+    }
+    IndexArgs a = index_args(x, q_data, q_offsets, nq);
+    a.rows = rows ? rows : (uint32_t*)(c->aux + groups + 1);
+    a.blob = blob;
+    a.row_off = row_off;
+    a.sizes = out_row_off;
+    a.out = out_data;
+    a.out_cap = out_cap;
+    a.needed = needed;
+    a.scratch = c->aux;
+    HIPC(launch_index_probe(a, c->stream));
+    HIPC(launch_gather(a, c->stream));
+    return MURR_OK;
+}
 
 const char* murr_status_str(int s) {
     switch (s) {
@@ -209,6 +343,7 @@ void murr_ctx_destroy(murr_ctx_t* c) {
     hipSetDevice(c->device);
     if (c->stream) hipStreamSynchronize(c->stream);
     if (c->ws) hipFree(c->ws);
+    if (c->aux) hipFree(c->aux);
     if (c->hs) hipHostFree(c->hs);
     for (const auto& b : c->pool) (void)(b.pinned ? hipHostFree(b.p) : hipFree(b.p));
     for (hipEvent_t e : c->event_pool) (void)hipEventDestroy(e);

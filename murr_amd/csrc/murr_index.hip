@@ -1,0 +1,250 @@
+// murr_index.hip — device-resident key index and row gather (SURVEY.md §8(f)
+// rank 1): the point lookups of Store::read for a table held in HBM.
+//
+// Replaces, for a resident table, RocksDBStore::read's key lookups and its
+// serial present/missing feed (src/io/store/rocksdb/mod.rs:241-267;
+// MemoryStore::read, src/io/store/memory.rs:28-45): every query key is looked
+// up in an open-addressing hash table, and the hit rows are gathered back to
+// back into a block in caller order (a miss = an empty row, which the decode
+// turns into ReadBatchBuilder::add_empty, src/io/row/read.rs:93-98).  Writes
+// follow put semantics: of equal keys the later row wins (memory.rs:47-56,
+// RocksDB's newest sequence number).
+//
+// Table: capacity = 2^k >= 2n slots of u64 {hash tag (32) | row (32)}, empty
+// = ~0.  Insert is lock-free: CAS into the first empty slot of the linear
+// probe sequence, or atomicMax onto the slot of an equal key (same tag, so
+// the max picks the larger row = the later write).  Two inserts of one key
+// see the same probe sequence and meet at the same slot, so keys stay unique.
+// All integer work; the lookup is latency-bound (one or two dependent HBM
+// reads per probe), the gather HBM-bound byte copy.
+#include "murr_device.h"
+
+namespace murr {
+
+namespace {
+
+using namespace dev;
+
+constexpr uint64_t kEmpty = ~0ull;
+
+// FNV-1a over the key bytes, finished with the murmur3 avalanche (fmix64) so
+// the low bits (slot) and high bits (tag) are both well mixed.
+__device__ __forceinline__ uint64_t key_hash(const GAS uint8_t* k, uint32_t n) {
+    uint64_t h = 0xcbf29ce484222325ull;
+    for (uint32_t i = 0; i < n; i++) h = (h ^ k[i]) * 0x100000001b3ull;
+    h ^= h >> 33;
+    h *= 0xff51afd7ed558ccdull;
+    h ^= h >> 33;
+    h *= 0xc4ceb9fe1a85ec53ull;
+    h ^= h >> 33;
+    return h;
+}
+
+__device__ __forceinline__ bool key_eq(const GAS uint8_t* a, const GAS uint8_t* b, uint32_t n) {
+    for (uint32_t i = 0; i < n; i++)
+        if (a[i] != b[i]) return false;
+    return true;
+}
+
+__global__ void __launch_bounds__(256) index_insert(IndexArgs A) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= A.n) return;
+    const GAS int32_t* ko = gp(A.key_off);
+    const int32_t k0 = ko[i], k1 = ko[i + 1];
+    const uint32_t len = (uint32_t)(k1 - k0);
+    const GAS uint8_t* key = gp(A.key_data) + k0;
+    const uint64_t h = key_hash(key, len);
+    const uint64_t mine = (h & 0xFFFFFFFF00000000ull) | i;
+    GAS unsigned long long* slots = (GAS unsigned long long*)gp(A.slots);
+    uint64_t s = h & A.mask;
+    for (uint64_t probe = 0; probe <= A.mask; probe++, s = (s + 1) & A.mask) {
+        unsigned long long e = __hip_atomic_load(slots + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (e == kEmpty) {
+            unsigned long long want = kEmpty;
+            if (__hip_atomic_compare_exchange_strong(slots + s, &want, (unsigned long long)mine, __ATOMIC_RELAXED,
+                                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+                return;
+            e = want;  // another key took it first
+        }
+        if ((e >> 32) == (mine >> 32)) {
+            const uint32_t r = (uint32_t)e;
+            const int32_t o0 = ko[r];
+            if ((uint32_t)(ko[r + 1] - o0) == len && key_eq(gp(A.key_data) + o0, key, len)) {
+                __hip_atomic_fetch_max(slots + s, (unsigned long long)mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                return;
+            }
+        }
+    }
+    report(A.err, err_key(0, i, 0, kStInternal));  // table full: cannot happen at load <= 1/2
+}
+
+// One query per thread: rows[i] = the key's row or kMissing; sizes[i] = its
+// blob length (0 for a miss) when a gather follows.
+__global__ void __launch_bounds__(256) index_probe(IndexArgs A) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= A.nq) return;
+    const GAS int32_t* qo = gp(A.q_off);
+    const int32_t q0 = qo[i];
+    const uint32_t len = (uint32_t)(qo[i + 1] - q0);
+    const GAS uint8_t* q = gp(A.q_data) + q0;
+    const uint64_t h = key_hash(q, len);
+    const GAS uint64_t* slots = gp(A.slots);
+    const GAS int32_t* ko = gp(A.key_off);
+    uint32_t row = kMissing;
+    uint64_t s = h & A.mask;
+    for (uint64_t probe = 0; probe <= A.mask; probe++, s = (s + 1) & A.mask) {
+        const uint64_t e = slots[s];
+        if (e == kEmpty) break;
+        if ((e >> 32) == (h >> 32)) {
+            const uint32_t r = (uint32_t)e;
+            const int32_t o0 = ko[r];
+            if ((uint32_t)(ko[r + 1] - o0) == len && key_eq(gp(A.key_data) + o0, q, len)) {
+                row = r;
+                break;
+            }
+        }
+    }
+    if (A.rows) gp(A.rows)[i] = row;
+    if (A.sizes) {
+        uint64_t sz = 0;
+        if (row != kMissing) sz = gp(A.row_off)[row + 1] - gp(A.row_off)[row];
+        gp(A.sizes)[i] = sz;
+    }
+}
+
+// Exclusive scan of sizes[0..nq) in place into block row offsets, in groups
+// of kScanGroup entries per 1024-thread workgroup:
+//   pass 0: group sums -> sums[g];
+//   pass 2: one workgroup scans sums[] (exclusive) and writes the total;
+//   pass 1: each group rewrites its entries as offsets (sums[g] + local prefix).
+// A single group runs pass 1 alone with a zero group prefix.  Offsets are
+// clamped to out_cap so the block never points past its buffer; the true
+// total goes to *needed.
+constexpr uint32_t kScanThreads = 1024, kScanPer = 4, kScanGroup = kScanThreads * kScanPer;
+
+__device__ uint64_t block_excl1024(uint64_t x, uint64_t* s_t, uint64_t* total) {
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint64_t inc = wave_incl_scan64(x, lane);
+    if (lane == 63) s_t[wave] = inc;
+    __syncthreads();
+    uint64_t before = 0, all = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < kScanThreads / 64; w++) {
+        const uint64_t v = s_t[w];
+        before += w < wave ? v : 0u;
+        all += v;
+    }
+    __syncthreads();
+    *total = all;
+    return before + inc - x;
+}
+
+__global__ void __launch_bounds__(kScanThreads) gather_scan(IndexArgs A, uint32_t pass) {
+    __shared__ uint64_t s_t[kScanThreads / 64];
+    const uint32_t tid = threadIdx.x;
+    GAS uint64_t* v = gp(A.sizes);
+    GAS uint64_t* sums = gp(A.scratch);
+    const uint64_t nq = A.nq, ngroups = (nq + kScanGroup - 1) / kScanGroup;
+    if (pass == 2) {
+        uint64_t carry = 0;
+        for (uint64_t g0 = 0; g0 < ngroups; g0 += kScanThreads) {
+            const uint64_t g = g0 + tid;
+            const uint64_t x = g < ngroups ? sums[g] : 0;
+            uint64_t tot;
+            const uint64_t ex = block_excl1024(x, s_t, &tot);
+            if (g < ngroups) sums[g] = carry + ex;
+            carry += tot;
+        }
+        if (tid == 0) {
+            v[nq] = min(carry, A.out_cap);
+            if (A.needed) gp(A.needed)[0] = carry;
+        }
+        return;
+    }
+    const uint64_t g = blockIdx.x, lo = g * kScanGroup, hi = min(nq, lo + kScanGroup);
+    uint64_t x[kScanPer], s = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < kScanPer; q++) {
+        const uint64_t j = lo + tid * kScanPer + q;
+        x[q] = j < hi ? v[j] : 0;
+        s += x[q];
+    }
+    uint64_t tot;
+    const uint64_t ex = block_excl1024(s, s_t, &tot);
+    if (pass == 0) {
+        if (tid == 0) sums[g] = tot;
+        return;
+    }
+    const bool single = ngroups == 1;
+    uint64_t run = (single ? 0 : sums[g]) + ex;
+#pragma unroll
+    for (uint32_t q = 0; q < kScanPer; q++) {
+        const uint64_t j = lo + tid * kScanPer + q;
+        if (j < hi) v[j] = min(run, A.out_cap);
+        run += x[q];
+    }
+    if (single && tid == kScanThreads - 1) {
+        v[nq] = min(run, A.out_cap);
+        if (A.needed) gp(A.needed)[0] = run;
+    }
+}
+
+// A wave per query row: copy its blob bytes to the block (rows clamped by the
+// scan copy only what fits).  Bytes move as dwords where source and
+// destination share their alignment mod 4 (then 256 B per wave step), bytes
+// otherwise.
+__global__ void __launch_bounds__(256) gather_copy(IndexArgs A) {
+    const uint64_t i = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint32_t lane = threadIdx.x & 63;
+    if (i >= A.nq) return;
+    const uint32_t row = gp(A.rows)[i];
+    if (row == kMissing) return;
+    const uint64_t d0 = gp(A.sizes)[i], d1 = gp(A.sizes)[i + 1];
+    const uint64_t s0 = gp(A.row_off)[row];
+    const GAS uint8_t* src = gp(A.blob) + s0;
+    GAS uint8_t* dst = gp(A.out) + d0;
+    const uint64_t n = d1 - d0;  // the clamped length
+    if (((s0 ^ d0) & 3) == 0 && n >= 8) {
+        const uint32_t head = (uint32_t)((4 - (d0 & 3)) & 3);
+        if (lane < head) dst[lane] = src[lane];
+        const uint64_t nw = (n - head) >> 2;
+        const GAS uint32_t* sw = (const GAS uint32_t*)(src + head);
+        GAS uint32_t* dw = (GAS uint32_t*)(dst + head);
+        for (uint64_t k = lane; k < nw; k += 64) dw[k] = sw[k];
+        const uint64_t t0 = head + 4 * nw;
+        if (t0 + lane < n) dst[t0 + lane] = src[t0 + lane];
+    } else {
+        for (uint64_t k = lane; k < n; k += 64) dst[k] = src[k];
+    }
+}
+
+}  // namespace
+
+hipError_t launch_index_insert(const IndexArgs& a, hipStream_t s) {
+    if (!a.n) return hipSuccess;
+    hipLaunchKernelGGL(index_insert, dim3((uint32_t)((a.n + 255) / 256)), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_index_probe(const IndexArgs& a, hipStream_t s) {
+    if (!a.nq) return hipSuccess;
+    hipLaunchKernelGGL(index_probe, dim3((uint32_t)((a.nq + 255) / 256)), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+uint64_t gather_scan_groups(uint64_t nq) { return (nq + kScanGroup - 1) / kScanGroup; }
+
+hipError_t launch_gather(const IndexArgs& a, hipStream_t s) {
+    const uint64_t groups = gather_scan_groups(a.nq);
+    if (groups <= 1) {
+        hipLaunchKernelGGL(gather_scan, dim3(1), dim3(kScanThreads), 0, s, a, 1u);
+    } else {
+        hipLaunchKernelGGL(gather_scan, dim3((uint32_t)groups), dim3(kScanThreads), 0, s, a, 0u);
+        hipLaunchKernelGGL(gather_scan, dim3(1), dim3(kScanThreads), 0, s, a, 2u);
+        hipLaunchKernelGGL(gather_scan, dim3((uint32_t)groups), dim3(kScanThreads), 0, s, a, 1u);
+    }
+    if (a.nq) hipLaunchKernelGGL(gather_copy, dim3((uint32_t)((a.nq + 3) / 4)), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+}  // namespace murr

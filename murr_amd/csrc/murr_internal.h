@@ -145,4 +145,30 @@ int decode_blocks_per_cu(uint32_t nw, uint32_t kc, uint32_t lds);
 hipError_t launch_encode(const EncodeArgs& a, uint32_t grid, hipStream_t s);
 int encode_blocks_per_cu();
 
+// Device key index + row gather (murr_index.hip).
+constexpr uint32_t kMissing = 0xFFFFFFFFu;
+struct IndexArgs {
+    const uint8_t* key_data;    // the index's own copy of the keys (Arrow utf8)
+    const int32_t* key_off;     // n + 1
+    uint64_t* slots;            // mask + 1 entries {tag:32 | row:32}, ~0 = empty
+    uint64_t mask;
+    uint64_t n;
+    unsigned long long* err;
+    const uint8_t* q_data;      // query keys (Arrow utf8)
+    const int32_t* q_off;       // nq + 1
+    uint64_t nq;
+    uint32_t* rows;             // out: nq rows (kMissing = not found)
+    const uint8_t* blob;        // gather: the table's row blobs
+    const uint64_t* row_off;    //   and their offsets (n + 1)
+    uint64_t* sizes;            //   out: the block's row offsets (nq + 1)
+    uint8_t* out;               //   out: the block's bytes
+    uint64_t out_cap;
+    uint64_t* needed;           //   out (optional): unclamped block bytes
+    uint64_t* scratch;          //   scan group sums
+};
+hipError_t launch_index_insert(const IndexArgs& a, hipStream_t s);
+hipError_t launch_index_probe(const IndexArgs& a, hipStream_t s);
+uint64_t gather_scan_groups(uint64_t nq);
+hipError_t launch_gather(const IndexArgs& a, hipStream_t s);
+
 }  // namespace murr

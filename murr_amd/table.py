@@ -58,9 +58,11 @@ class Table:
         return self.table
 
     # -- write ------------------------------------------------------------------
-    def encode(self, batch: pa.RecordBatch):
-        """Table::write up to the store call: returns (keys StringArray, blob
-        uint8 ndarray, row_off uint64 ndarray)."""
+    def validate(self, batch: pa.RecordBatch):
+        """Table::write's checks (table/mod.rs:54-96): canonical projection,
+        Utf8 non-null key, make_decoder's dtype downcast per column
+        (src/io/codec/mod.rs:78-85).  Returns (key array, arrays in segment
+        order)."""
         canonical = self.table.to_arrow()
         names = batch.schema.names
         indices = []
@@ -76,16 +78,25 @@ class Table:
             raise SegmentError(f"key column '{self.table.key}' must be Utf8")
         if key_array.null_count > 0:
             raise SegmentError("null in key column")
-        n = ordered.num_rows
+        arrays = []
+        for col in self.segment.columns:
+            arr = ordered.column(canonical.get_field_index(col.name))
+            want = col.dtype.arrow_dtype()
+            if arr.type != want:
+                raise SegmentError(f"expected {want}, got {arr.type}")
+            arrays.append(arr)
+        return key_array, arrays
+
+    def encode(self, batch: pa.RecordBatch):
+        """Table::write up to the store call: returns (keys StringArray, blob
+        uint8 ndarray, row_off uint64 ndarray)."""
+        key_array, arrays = self.validate(batch)
+        n = batch.num_rows
         seg = self.segment
         hcols = (_abi.HostColIn * max(len(seg), 1))()
         keep = []
         for i, col in enumerate(seg.columns):
-            arr = ordered.column(canonical.get_field_index(col.name))
-            want = col.dtype.arrow_dtype()
-            if arr.type != want:
-                # make_decoder's downcast (src/io/codec/mod.rs:78-85)
-                raise SegmentError(f"expected {want}, got {arr.type}")
+            arr = arrays[i]
             bufs = arr.buffers()
             keep.append(bufs)
             hc = hcols[i]

@@ -1,0 +1,170 @@
+"""Device key index + gather (murr_index.hip through the C ABI) and
+ResidentTable.read, against the store semantics the reference tests pin:
+caller order with misses as all-null rows (src/io/store/rocksdb/mod.rs:368-399,
+src/io/store/memory.rs:71-165), request column order and duplicates
+(src/io/table/mod.rs:248-462), later writes of a key winning (memory.rs:47-56).
+
+The expected side is (i) a dict restatement of MemoryStore (key -> last row)
+over the written Arrow arrays and (ii) the builder path (Table over
+MemoryStore, itself parity-tested against the oracle), compared buffer by
+buffer."""
+import numpy as np
+import pyarrow as pa
+import pytest
+
+from murr_amd import ColumnSchema, DTypeName as D, TableSchema
+from murr_amd.resident import ROW_MISSING, DeviceIndex, ResidentTable
+from murr_amd.row import default_context
+from murr_amd.store import MemoryStore
+from murr_amd.table import Table
+from murr_amd import synth
+
+pytestmark = pytest.mark.gpu
+
+C_DTYPES = [D.Bool, D.Int8, D.Int16, D.Int32, D.Int64, D.UInt8, D.UInt16, D.UInt32, D.UInt64,
+            D.Float32, D.Float64, D.Utf8, D.Utf8, D.Float32, D.Float64, D.Int64]
+
+
+@pytest.fixture(autouse=True, params=["jit", "generic"])
+def kernel_mode(request, monkeypatch):
+    monkeypatch.setenv("MURR_DECODE_JIT", "1" if request.param == "jit" else "0")
+    return request.param
+
+
+def schema_c():
+    cols = {"key": ColumnSchema(D.Utf8, False)}
+    for i, d in enumerate(C_DTYPES):
+        cols[f"c{i}"] = ColumnSchema(d)
+    return TableSchema("key", cols)
+
+
+def batch_c(n, start=0, seed=42, keys=None):
+    cols = synth.config_c(n, start=start, seed_nulls=seed)
+    arrays = [pa.array(keys if keys is not None else [f"key{start + i}" for i in range(n)], pa.string())]
+    arrays += [synth.to_arrow(c) for c in cols]
+    return pa.RecordBatch.from_arrays(arrays, names=["key"] + [f"c{i}" for i in range(len(C_DTYPES))])
+
+
+def expected(batches, keys, columns):
+    """MemoryStore restatement: key -> last written row; misses all-null."""
+    whole = pa.Table.from_batches(batches).combine_chunks()
+    last = {}
+    for i, k in enumerate(whole.column("key").to_pylist()):
+        last[k] = i
+    idx = [last.get(k) for k in keys]
+    take = pa.array(idx, pa.int64())
+    return pa.RecordBatch.from_arrays([whole.column(c).combine_chunks().take(take) for c in columns],
+                                      names=columns)
+
+
+def assert_same(got, want):
+    assert got.schema.names == want.schema.names
+    for a, b in zip(got.columns, want.columns):
+        assert a.equals(b), (a, b)
+
+
+def test_index_lookup_rows_and_misses():
+    ctx = default_context()
+    keys = pa.array([f"k{i}" for i in range(5000)], pa.string())
+    ix = DeviceIndex(ctx, keys)
+    n, slots = ix.info()
+    assert n == 5000 and slots >= 10000 and slots & (slots - 1) == 0
+    q = ["k0", "k4999", "nope", "k17", "", "k17", "k5000"]
+    assert ix.lookup(q).tolist() == [0, 4999, ROW_MISSING, 17, ROW_MISSING, 17, ROW_MISSING]
+    assert ix.lookup([]).tolist() == []
+
+
+def test_index_later_duplicate_wins():
+    ctx = default_context()
+    ks = ["a", "b", "a", "c", "b", "a"]
+    ix = DeviceIndex(ctx, pa.array(ks, pa.string()))
+    assert ix.lookup(["a", "b", "c", "d"]).tolist() == [5, 4, 3, ROW_MISSING]
+
+
+def test_index_edge_keys():
+    ctx = default_context()
+    rng = np.random.default_rng(5)
+    ks = ["", "x", "x" * 300, "xy", "yx", "éè", "pre" * 50 + "1", "pre" * 50 + "2"]
+    ks += ["".join(chr(97 + c) for c in rng.integers(0, 3, size=int(rng.integers(1, 6)))) for _ in range(200)]
+    uniq = list(dict.fromkeys(ks))
+    last = {k: i for i, k in enumerate(ks)}
+    ix = DeviceIndex(ctx, pa.array(ks, pa.string()))
+    assert ix.lookup(uniq + ["zzz"]).tolist() == [last[k] for k in uniq] + [ROW_MISSING]
+
+
+def test_index_all_rows_permutation_1m():
+    # size-independent property at scale: every key finds its own row
+    ctx = default_context()
+    n = 1_000_000
+    keys = pa.array([str(i) for i in range(n)], pa.string())
+    ix = DeviceIndex(ctx, keys)
+    rng = np.random.default_rng(9)
+    perm = rng.permutation(n)
+    rows = ix.lookup([str(i) for i in perm])
+    assert np.array_equal(rows, perm.astype(np.uint32))
+
+
+def test_resident_read_matches_store_semantics():
+    t = ResidentTable(schema_c())
+    b0 = batch_c(20000, seed=42)
+    t.write(b0)
+    rng = np.random.default_rng(44)
+    ids = rng.integers(0, 21000, size=3000)  # ~5% misses
+    keys = [f"key{i}" for i in ids]
+    cols = [f"c{i}" for i in range(16)]
+    got = t.read(keys, cols)
+    assert_same(got, expected([b0], keys, cols))
+    # request order, duplicates, subset
+    cols2 = ["c11", "c0", "c11", "c15", "c12"]
+    assert_same(t.read(keys[:777], cols2), expected([b0], keys[:777], cols2))
+
+
+def test_resident_read_bit_exact_vs_builder_path():
+    ts = schema_c()
+    b0 = batch_c(5000, seed=7)
+    rt = ResidentTable(ts)
+    rt.write(b0)
+    mt = Table.create(MemoryStore(), "t", ts)
+    mt.write(b0)
+    rng = np.random.default_rng(8)
+    keys = [f"key{i}" for i in rng.integers(0, 5300, size=1000)]
+    cols = [f"c{i}" for i in range(16)]
+    got, want = rt.read(keys, cols), mt.read(keys, cols)
+    for a, b in zip(got.columns, want.columns):
+        ba, bb = a.buffers(), b.buffers()
+        assert a.null_count == b.null_count
+        for x, y in zip(ba[1:], bb[1:]):
+            assert x.to_pybytes() == y.to_pybytes()
+        if a.null_count:
+            nb = (len(a) + 7) // 8
+            assert ba[0].to_pybytes()[:nb] == bb[0].to_pybytes()[:nb]
+
+
+def test_resident_overwrite_and_append():
+    t = ResidentTable(schema_c())
+    b0 = batch_c(3000, seed=1)
+    b1 = batch_c(1500, start=2000, seed=2)  # keys 2000..3499: 1000 overwrite, 500 new
+    t.write(b0)
+    t.write(b1)
+    keys = [f"key{i}" for i in (0, 1999, 2000, 2999, 3000, 3499, 3500)]
+    cols = [f"c{i}" for i in range(16)]
+    assert_same(t.read(keys, cols), expected([b0, b1], keys, cols))
+
+
+def test_resident_all_miss_and_empty_query():
+    t = ResidentTable(schema_c())
+    t.write(batch_c(100))
+    got = t.read(["x", "y", "z"], ["c3", "c11"])
+    assert got.num_rows == 3 and all(c.null_count == 3 for c in got.columns)
+    got = t.read([], ["c3", "c11"])
+    assert got.num_rows == 0
+
+
+def test_resident_table_schema_errors():
+    from murr_amd.errors import SegmentError
+    t = ResidentTable(schema_c())
+    t.write(batch_c(10))
+    with pytest.raises(SegmentError):
+        t.read(["key1"], ["key"])
+    with pytest.raises(SegmentError):
+        t.read(["key1"], ["nope"])
