@@ -93,6 +93,7 @@ struct murr_index {
     uint8_t* key_data = nullptr;
     int32_t* key_off = nullptr;
     uint64_t* slots = nullptr;
+    uint64_t* loc = nullptr;
     unsigned long long* err = nullptr;
     uint64_t n = 0, mask = 0;
 };
@@ -150,7 +151,7 @@ extern "C" {
 void murr_index_free(murr_index_t* x) {
     if (!x) return;
     (void)hipSetDevice(x->device);
-    for (void* p : {(void*)x->key_data, (void*)x->key_off, (void*)x->slots, (void*)x->err})
+    for (void* p : {(void*)x->key_data, (void*)x->key_off, (void*)x->slots, (void*)x->loc, (void*)x->err})
         if (p) (void)hipFree(p);
     delete x;
 }
@@ -177,6 +178,7 @@ int murr_index_build(murr_ctx_t* c, const uint8_t* key_data, const int32_t* key_
     HIPC(hipMalloc(&x->key_data, std::max<uint64_t>((uint64_t)last, 16)));
     HIPC(hipMalloc(&x->key_off, 4 * (n + 1)));
     HIPC(hipMalloc(&x->slots, 8 * slots));
+    HIPC(hipMalloc(&x->loc, 8 * slots));
     HIPC(hipMalloc(&x->err, 8));
     if (last) HIPC(hipMemcpyAsync(x->key_data, key_data, (uint64_t)last, hipMemcpyDeviceToDevice, c->stream));
     if (n) HIPC(hipMemcpyAsync(x->key_off, key_offsets + key_offset, 4 * (n + 1), hipMemcpyDeviceToDevice, c->stream));
@@ -186,6 +188,7 @@ int murr_index_build(murr_ctx_t* c, const uint8_t* key_data, const int32_t* key_
     a.key_data = x->key_data;
     a.key_off = x->key_off;
     a.slots = x->slots;
+    a.loc = x->loc;
     a.mask = x->mask;
     a.n = n;
     a.err = x->err;
@@ -211,6 +214,7 @@ IndexArgs index_args(const murr_index_t* x, const uint8_t* q_data, const int32_t
     a.key_data = x->key_data;
     a.key_off = x->key_off;
     a.slots = x->slots;
+    a.loc = x->loc;
     a.mask = x->mask;
     a.n = x->n;
     a.q_data = q_data;

@@ -11,12 +11,15 @@
 // RocksDB's newest sequence number).
 //
 // Table: capacity = 2^k >= 2n slots of u64 {hash tag (32) | row (32)}, empty
-// = ~0.  Insert is lock-free: CAS into the first empty slot of the linear
+// = ~0, and beside each slot the key's {start (32) | length (32)} in the
+// index's key copy, so a probe reads slot and key location together and then
+// the key bytes.  Insert is lock-free: CAS into the first empty slot of the linear
 // probe sequence, or atomicMax onto the slot of an equal key (same tag, so
 // the max picks the larger row = the later write).  Two inserts of one key
 // see the same probe sequence and meet at the same slot, so keys stay unique.
-// All integer work; the lookup is latency-bound (one or two dependent HBM
-// reads per probe), the gather HBM-bound byte copy.
+// All integer work; the lookup is latency-bound (query key, slot + location,
+// stored key: three dependent memory round trips per probe), the gather an
+// HBM-bound byte copy.
 #include "murr_device.h"
 
 namespace murr {
@@ -27,11 +30,57 @@ using namespace dev;
 
 constexpr uint64_t kEmpty = ~0ull;
 
-// FNV-1a over the key bytes, finished with the murmur3 avalanche (fmix64) so
-// the low bits (slot) and high bits (tag) are both well mixed.
-__device__ __forceinline__ uint64_t key_hash(const GAS uint8_t* k, uint32_t n) {
-    uint64_t h = 0xcbf29ce484222325ull;
-    for (uint32_t i = 0; i < n; i++) h = (h ^ k[i]) * 0x100000001b3ull;
+// Keys are read as the aligned dwords that cover them (an aligned dword never
+// crosses a page, so the bytes around a key are safe to load whatever buffer
+// it sits in) and realigned with v_alignbyte into key words: word j = key
+// bytes [4j, 4j + 4), the last one zero-padded.  Eight words (32 bytes) per
+// chunk with their loads issued together, so a short key costs one memory
+// round trip instead of one per byte.
+constexpr uint32_t kChunkWords = 8;
+
+struct KeyChunk {
+    uint32_t w[kChunkWords];
+};
+
+// Words [8c, 8c + 8) of the key at p (n bytes); words past the end are 0.
+__device__ __forceinline__ KeyChunk key_chunk(const GAS uint8_t* p, uint32_t n, uint32_t c) {
+    const uintptr_t a = (uintptr_t)p;
+    const uint32_t sa = (uint32_t)(a & 3);
+    const GAS uint32_t* al = (const GAS uint32_t*)(a - sa);
+    const uint32_t nal = (sa + n + 3) >> 2;  // aligned dwords covering the key
+    uint32_t raw[kChunkWords + 1];
+#pragma unroll
+    for (uint32_t k = 0; k <= kChunkWords; k++) {
+        const uint32_t idx = kChunkWords * c + k;
+        raw[k] = idx < nal ? al[idx] : 0u;
+    }
+    KeyChunk out;
+#pragma unroll
+    for (uint32_t k = 0; k < kChunkWords; k++) {
+        uint32_t v = __builtin_amdgcn_alignbyte(raw[k + 1], raw[k], sa);
+        const int32_t left = (int32_t)n - 4 * (int32_t)(kChunkWords * c + k);  // key bytes in this word
+        if (left <= 0) v = 0;
+        else if (left < 4) v &= (1u << (8 * left)) - 1u;
+        out.w[k] = v;
+    }
+    return out;
+}
+
+__device__ __forceinline__ uint64_t mix_words(uint64_t h, const KeyChunk& k) {
+#pragma unroll
+    for (uint32_t j = 0; j < kChunkWords; j++) h = (h ^ k.w[j]) * 0x100000001b3ull;
+    return h;
+}
+
+// Hash of the key bytes (whatever their alignment): FNV-style over the
+// zero-padded key words and the length, finished with the murmur3 avalanche
+// (fmix64) so the low bits (slot) and high bits (tag) are both well mixed.
+// *first gets the first chunk (all a short key's comparison needs).
+__device__ __forceinline__ uint64_t key_hash(const GAS uint8_t* k, uint32_t n, KeyChunk* first) {
+    uint64_t h = 0xcbf29ce484222325ull ^ n;
+    *first = key_chunk(k, n, 0);
+    h = mix_words(h, *first);
+    for (uint32_t c = 1; kChunkWords * 4 * c < n; c++) h = mix_words(h, key_chunk(k, n, c));
     h ^= h >> 33;
     h *= 0xff51afd7ed558ccdull;
     h ^= h >> 33;
@@ -40,9 +89,18 @@ __device__ __forceinline__ uint64_t key_hash(const GAS uint8_t* k, uint32_t n) {
     return h;
 }
 
-__device__ __forceinline__ bool key_eq(const GAS uint8_t* a, const GAS uint8_t* b, uint32_t n) {
-    for (uint32_t i = 0; i < n; i++)
-        if (a[i] != b[i]) return false;
+__device__ __forceinline__ bool chunk_eq(const KeyChunk& a, const KeyChunk& b) {
+    uint32_t d = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < kChunkWords; j++) d |= a.w[j] ^ b.w[j];
+    return d == 0;
+}
+
+// Keys a and q of the same length n; qc = q's first chunk.
+__device__ __forceinline__ bool key_eq(const GAS uint8_t* a, const KeyChunk& qc, const GAS uint8_t* q, uint32_t n) {
+    if (!chunk_eq(key_chunk(a, n, 0), qc)) return false;
+    for (uint32_t c = 1; kChunkWords * 4 * c < n; c++)
+        if (!chunk_eq(key_chunk(a, n, c), key_chunk(q, n, c))) return false;
     return true;
 }
 
@@ -53,7 +111,8 @@ __global__ void __launch_bounds__(256) index_insert(IndexArgs A) {
     const int32_t k0 = ko[i], k1 = ko[i + 1];
     const uint32_t len = (uint32_t)(k1 - k0);
     const GAS uint8_t* key = gp(A.key_data) + k0;
-    const uint64_t h = key_hash(key, len);
+    KeyChunk kc;
+    const uint64_t h = key_hash(key, len, &kc);
     const uint64_t mine = (h & 0xFFFFFFFF00000000ull) | i;
     GAS unsigned long long* slots = (GAS unsigned long long*)gp(A.slots);
     uint64_t s = h & A.mask;
@@ -62,14 +121,19 @@ __global__ void __launch_bounds__(256) index_insert(IndexArgs A) {
         if (e == kEmpty) {
             unsigned long long want = kEmpty;
             if (__hip_atomic_compare_exchange_strong(slots + s, &want, (unsigned long long)mine, __ATOMIC_RELAXED,
-                                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+                                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                // where a probe finds the key bytes; equal keys share them, so
+                // the row a later atomicMax installs needs no update here
+                gp(A.loc)[s] = ((uint64_t)(uint32_t)k0 << 32) | len;
                 return;
+            }
             e = want;  // another key took it first
         }
         if ((e >> 32) == (mine >> 32)) {
+            // (loc[s] may not be written yet: compare through the row's offsets)
             const uint32_t r = (uint32_t)e;
             const int32_t o0 = ko[r];
-            if ((uint32_t)(ko[r + 1] - o0) == len && key_eq(gp(A.key_data) + o0, key, len)) {
+            if ((uint32_t)(ko[r + 1] - o0) == len && key_eq(gp(A.key_data) + o0, kc, key, len)) {
                 __hip_atomic_fetch_max(slots + s, (unsigned long long)mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 return;
             }
@@ -87,21 +151,19 @@ __global__ void __launch_bounds__(256) index_probe(IndexArgs A) {
     const int32_t q0 = qo[i];
     const uint32_t len = (uint32_t)(qo[i + 1] - q0);
     const GAS uint8_t* q = gp(A.q_data) + q0;
-    const uint64_t h = key_hash(q, len);
+    KeyChunk qc;
+    const uint64_t h = key_hash(q, len, &qc);
     const GAS uint64_t* slots = gp(A.slots);
-    const GAS int32_t* ko = gp(A.key_off);
+    const GAS uint64_t* loc = gp(A.loc);
     uint32_t row = kMissing;
     uint64_t s = h & A.mask;
     for (uint64_t probe = 0; probe <= A.mask; probe++, s = (s + 1) & A.mask) {
-        const uint64_t e = slots[s];
+        const uint64_t e = slots[s], l = loc[s];  // independent loads
         if (e == kEmpty) break;
-        if ((e >> 32) == (h >> 32)) {
-            const uint32_t r = (uint32_t)e;
-            const int32_t o0 = ko[r];
-            if ((uint32_t)(ko[r + 1] - o0) == len && key_eq(gp(A.key_data) + o0, q, len)) {
-                row = r;
-                break;
-            }
+        if ((e >> 32) == (h >> 32) && (uint32_t)l == len &&
+            key_eq(gp(A.key_data) + (uint32_t)(l >> 32), qc, q, len)) {
+            row = (uint32_t)e;
+            break;
         }
     }
     if (A.rows) gp(A.rows)[i] = row;

@@ -151,6 +151,7 @@ struct IndexArgs {
     const uint8_t* key_data;    // the index's own copy of the keys (Arrow utf8)
     const int32_t* key_off;     // n + 1
     uint64_t* slots;            // mask + 1 entries {tag:32 | row:32}, ~0 = empty
+    uint64_t* loc;              // mask + 1 entries {key start:32 | key length:32}
     uint64_t mask;
     uint64_t n;
     unsigned long long* err;
