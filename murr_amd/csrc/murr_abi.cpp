@@ -265,8 +265,7 @@ int murr_index_gather(murr_ctx_t* c, const murr_index_t* x, const uint8_t* q_dat
     a.out_cap = out_cap;
     a.needed = needed;
     a.scratch = c->aux;
-    HIPC(launch_index_probe(a, c->stream));
-    HIPC(launch_gather(a, c->stream));
+    HIPC(launch_gather(a, c->stream));  // probe included
     return MURR_OK;
 }
 
@@ -653,16 +652,22 @@ int murr_decode_enqueue(murr_ctx_t* c, const murr_segment_t* seg, const uint32_t
     int st = ensure_ws(c, dend, err);
     if (st) return st;
     // host scratch: [descriptors (dend - zbytes)] [readback z_lb bytes]
-    const uint64_t hdesc = d_end_desc - zbytes, rb = round_up(dend - zbytes, 64);
+    // A small zeroed region travels with the descriptors in one H2D (one
+    // stream op fewer per launch: it matters for small reads); a large one
+    // (generic kernel, many tiles) is a device memset.
+    const uint64_t hz = zbytes <= 65536 ? zbytes : 0;
+    const uint64_t hdesc = d_end_desc - zbytes, rb = round_up(hz + dend - zbytes, 64);
     st = ensure_hs(c, rb + z_lb, err);
     if (st) return st;
-    std::memcpy(c->hs + (d_blocks - zbytes), db.data(), sizeof(DecBlock) * nblocks);
-    std::memcpy(c->hs + (d_proj - zbytes), dp.data(), sizeof(DecProj) * nproj);
-    std::memcpy(c->hs + (d_outs - zbytes), dout.data(), sizeof(DecOut) * dout.size());
-    if (jk && nseg) std::memcpy(c->hs + (d_order - zbytes), jsegs.data(), sizeof(JitSeg) * nseg);
+    uint8_t* hd = c->hs + hz;
+    if (hz) std::memset(c->hs, 0, hz);
+    std::memcpy(hd + (d_blocks - zbytes), db.data(), sizeof(DecBlock) * nblocks);
+    std::memcpy(hd + (d_proj - zbytes), dp.data(), sizeof(DecProj) * nproj);
+    std::memcpy(hd + (d_outs - zbytes), dout.data(), sizeof(DecOut) * dout.size());
+    if (jk && nseg) std::memcpy(hd + (d_order - zbytes), jsegs.data(), sizeof(JitSeg) * nseg);
 
-    HIPC(hipMemsetAsync(c->ws, 0, zbytes, c->stream));
-    HIPC(hipMemcpyAsync(c->ws + zbytes, c->hs, hdesc, hipMemcpyHostToDevice, c->stream));
+    if (!hz) HIPC(hipMemsetAsync(c->ws, 0, zbytes, c->stream));
+    HIPC(hipMemcpyAsync(c->ws + zbytes - hz, c->hs, hz + hdesc, hipMemcpyHostToDevice, c->stream));
     // Empty blocks: utf8 offsets = [0] (StringBuilder starts with offset 0).
     for (uint32_t b = 0; b < nblocks; b++)
         if (blocks[b].n_rows == 0)

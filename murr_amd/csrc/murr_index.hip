@@ -142,11 +142,8 @@ __global__ void __launch_bounds__(256) index_insert(IndexArgs A) {
     report(A.err, err_key(0, i, 0, kStInternal));  // table full: cannot happen at load <= 1/2
 }
 
-// One query per thread: rows[i] = the key's row or kMissing; sizes[i] = its
-// blob length (0 for a miss) when a gather follows.
-__global__ void __launch_bounds__(256) index_probe(IndexArgs A) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= A.nq) return;
+// Row of query i, or kMissing.
+__device__ __forceinline__ uint32_t probe_one(const IndexArgs& A, uint64_t i) {
     const GAS int32_t* qo = gp(A.q_off);
     const int32_t q0 = qo[i];
     const uint32_t len = (uint32_t)(qo[i + 1] - q0);
@@ -166,12 +163,21 @@ __global__ void __launch_bounds__(256) index_probe(IndexArgs A) {
             break;
         }
     }
+    return row;
+}
+
+__device__ __forceinline__ uint64_t row_size(const IndexArgs& A, uint32_t row) {
+    return row == kMissing ? 0 : gp(A.row_off)[row + 1] - gp(A.row_off)[row];
+}
+
+// One query per thread: rows[i] = the key's row or kMissing; sizes[i] = its
+// blob length (0 for a miss) when a gather follows.
+__global__ void __launch_bounds__(256) index_probe(IndexArgs A) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= A.nq) return;
+    const uint32_t row = probe_one(A, i);
     if (A.rows) gp(A.rows)[i] = row;
-    if (A.sizes) {
-        uint64_t sz = 0;
-        if (row != kMissing) sz = gp(A.row_off)[row + 1] - gp(A.row_off)[row];
-        gp(A.sizes)[i] = sz;
-    }
+    if (A.sizes) gp(A.sizes)[i] = row_size(A, row);
 }
 
 // Exclusive scan of sizes[0..nq) in place into block row offsets, in groups
@@ -251,6 +257,26 @@ __global__ void __launch_bounds__(kScanThreads) gather_scan(IndexArgs A, uint32_
     }
 }
 
+// nq <= kScanThreads: probe, sizes and their scan in one workgroup (one
+// launch instead of two for a small read).
+__global__ void __launch_bounds__(kScanThreads) gather_probe_scan(IndexArgs A) {
+    __shared__ uint64_t s_t[kScanThreads / 64];
+    const uint32_t tid = threadIdx.x;
+    uint32_t row = kMissing;
+    if (tid < A.nq) row = probe_one(A, tid);
+    const uint64_t sz = tid < A.nq ? row_size(A, row) : 0;
+    uint64_t tot;
+    const uint64_t ex = block_excl1024(sz, s_t, &tot);
+    if (tid < A.nq) {
+        gp(A.rows)[tid] = row;
+        gp(A.sizes)[tid] = min(ex, A.out_cap);
+    }
+    if (tid == 0) {
+        gp(A.sizes)[A.nq] = min(tot, A.out_cap);
+        if (A.needed) gp(A.needed)[0] = tot;
+    }
+}
+
 // A wave per query row: copy its blob bytes to the block (rows clamped by the
 // scan copy only what fits).  Bytes move as dwords where source and
 // destination share their alignment mod 4 (then 256 B per wave step), bytes
@@ -298,12 +324,18 @@ uint64_t gather_scan_groups(uint64_t nq) { return (nq + kScanGroup - 1) / kScanG
 
 hipError_t launch_gather(const IndexArgs& a, hipStream_t s) {
     const uint64_t groups = gather_scan_groups(a.nq);
-    if (groups <= 1) {
-        hipLaunchKernelGGL(gather_scan, dim3(1), dim3(kScanThreads), 0, s, a, 1u);
+    if (a.nq <= kScanThreads) {
+        hipLaunchKernelGGL(gather_probe_scan, dim3(1), dim3(kScanThreads), 0, s, a);
     } else {
-        hipLaunchKernelGGL(gather_scan, dim3((uint32_t)groups), dim3(kScanThreads), 0, s, a, 0u);
-        hipLaunchKernelGGL(gather_scan, dim3(1), dim3(kScanThreads), 0, s, a, 2u);
-        hipLaunchKernelGGL(gather_scan, dim3((uint32_t)groups), dim3(kScanThreads), 0, s, a, 1u);
+        const hipError_t e = launch_index_probe(a, s);
+        if (e != hipSuccess) return e;
+        if (groups <= 1) {
+            hipLaunchKernelGGL(gather_scan, dim3(1), dim3(kScanThreads), 0, s, a, 1u);
+        } else {
+            hipLaunchKernelGGL(gather_scan, dim3((uint32_t)groups), dim3(kScanThreads), 0, s, a, 0u);
+            hipLaunchKernelGGL(gather_scan, dim3(1), dim3(kScanThreads), 0, s, a, 2u);
+            hipLaunchKernelGGL(gather_scan, dim3((uint32_t)groups), dim3(kScanThreads), 0, s, a, 1u);
+        }
     }
     if (a.nq) hipLaunchKernelGGL(gather_copy, dim3((uint32_t)((a.nq + 3) / 4)), dim3(256), 0, s, a);
     return hipGetLastError();

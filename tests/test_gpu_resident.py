@@ -168,3 +168,52 @@ def test_resident_table_schema_errors():
         t.read(["key1"], ["key"])
     with pytest.raises(SegmentError):
         t.read(["key1"], ["nope"])
+
+
+def test_resident_read_many_keys_three_pass_scan():
+    # > 4096 queries: probe, three scan passes over 4096-query groups, copy
+    t = ResidentTable(schema_c())
+    b0 = batch_c(30000, seed=3)
+    t.write(b0)
+    rng = np.random.default_rng(11)
+    keys = [f"key{i}" for i in rng.integers(0, 31500, size=20000)]
+    cols = ["c12", "c4", "c0", "c11"]
+    assert_same(t.read(keys, cols), expected([b0], keys, cols))
+
+
+def test_gather_capacity_clamp():
+    # out_cap too small: offsets clamp to the cap, `needed` reports the size
+    import ctypes as C
+    from murr_amd.resident import _upload_utf8
+    t = ResidentTable(schema_c())
+    t.write(batch_c(2000, seed=4))
+    ctx = t.ctx
+    keys = [f"key{i}" for i in range(1500)]
+    qd, qo = _upload_utf8(ctx, pa.array(keys, pa.string()))
+    cap = 5000
+    data, offs, needed = ctx.alloc(cap + 16), ctx.alloc((len(keys) + 1) * 8), ctx.alloc(8)
+    rows = ctx.alloc(len(keys) * 4)
+    st = ctx.L.murr_index_gather(ctx.h, t.index.h, qd.ptr, qo.ptr, len(keys), t.blob.ptr, t.row_off.ptr,
+                                 data.ptr, cap, offs.ptr, rows.ptr, needed.ptr)
+    assert st == 0
+    off = offs.download((len(keys) + 1) * 8).view(np.uint64)
+    full = t.row_off.download((t.n + 1) * 8).view(np.uint64)
+    sizes = np.diff(full)[:1500].astype(np.uint64)
+    want = np.concatenate([[0], np.cumsum(sizes)]).astype(np.uint64)
+    assert int(needed.download(8).view(np.uint64)[0]) == int(want[-1])
+    assert np.array_equal(off, np.minimum(want, cap))
+    assert rows.download(len(keys) * 4).view(np.uint32).tolist() == list(range(1500))
+    blob = t.blob.download(int(full[-1]))
+    got = data.download(cap)
+    k = int(np.searchsorted(want, cap, side="right")) - 1  # rows wholly inside the cap
+    assert got[:int(want[k])].tobytes() == blob[:int(want[k])].tobytes()
+
+
+def test_index_long_duplicate_keys():
+    # multi-chunk keys (> 32 B) through the insert's equal-key path
+    ctx = default_context()
+    base = "k" * 95
+    ks = [base + "a", base + "b", base + "a", "z" * 64, base + "b", "z" * 64, "z" * 65]
+    ix = DeviceIndex(ctx, pa.array(ks, pa.string()))
+    assert ix.lookup([base + "a", base + "b", "z" * 64, "z" * 65, base + "c", "z" * 63]).tolist() == \
+        [2, 4, 5, 6, ROW_MISSING, ROW_MISSING]
