@@ -27,4 +27,7 @@ if [ -z "${QUICK:-}" ]; then
   run decode_D1 300 python3 bench.py --config D --steps 10 --warmup 2 --no-cpu
   run decode_B_generic 300 env MURR_DECODE_JIT=0 python3 bench.py --steps 10 --warmup 2 --no-cpu
   run host_C 300 python3 bench.py --mode host --config C --rows 1000 --steps 50 --warmup 5
+  run encode_B 300 python3 bench.py --mode encode --enc-config B --steps 10 --warmup 2
+  run encode_C 300 python3 bench.py --mode encode --enc-config C --steps 10 --warmup 2
+  run resident_1000 300 python3 bench.py --mode resident --keys 1000 --steps 30 --warmup 5
 fi
