@@ -318,6 +318,38 @@ def run_resident(args):
         t0 = time.perf_counter()
         read(qsets[i % 4])
         ts.append(time.perf_counter() - t0)
+    ipc_res = {}
+    if args.ipc:
+        # + Arrow IPC record-batch message packed in HBM (murr_ipc_batch_device)
+        # and one D2H into pinned memory: the HTTP fetch handler's StreamWriter
+        # body (src/api/http/handlers.rs:93-101) ready for the socket.
+        mlen = C.c_uint64()
+        st = L.murr_ipc_batch_device(ctx.h, C.byref(seg.c), pj, len(proj), outs.arrays, nq, 64, None, 0,
+                                     C.byref(mlen), C.byref(err))
+        assert st == 0, st
+        mcap = int(mlen.value) + 4096 * len(proj)  # body sizes vary a little with the key set
+        dmsg = ctx.alloc(mcap)
+        hmsg = C.c_void_p()
+        assert L.murr_host_alloc(ctx.h, mcap, C.byref(hmsg)) == 0
+
+        def read_ipc(q):
+            read(q)
+            st = L.murr_ipc_batch_device(ctx.h, C.byref(seg.c), pj, len(proj), outs.arrays, nq, 64, dmsg.ptr,
+                                         mcap, C.byref(mlen), C.byref(err))
+            assert st == 0, (st, err.required)
+            assert L.murr_memcpy_d2h(ctx.h, hmsg, dmsg.ptr, mlen.value) == 0
+
+        for i in range(args.warmup):
+            read_ipc(qsets[i % 4])
+        ti = []
+        for i in range(args.steps):
+            t0 = time.perf_counter()
+            read_ipc(qsets[i % 4])
+            ti.append(time.perf_counter() - t0)
+        L.murr_host_free(ctx.h, hmsg)
+        ipc_res = {"ipc_message_bytes": int(mlen.value),
+                   "us_per_read_ipc_median": round(float(np.median(ti)) * 1e6, 1),
+                   "ipc_path": "gather + decode + ipc_pack + one D2H (pinned)"}
     nb = int(needed.download(8).view(np.uint64)[0])
     assert nb <= cap
     out_bytes = 0
@@ -333,7 +365,7 @@ def run_resident(args):
                       "us_per_read_median": round(med * 1e6, 1),
                       "us_per_read_p95": round(float(np.percentile(ts, 95)) * 1e6, 1),
                       "GiB_s_arrow_out": round(out_bytes / med / GIB, 3),
-                      "kernels": "index_probe, gather_scan, gather_copy, " + ctx.last_kernel()}))
+                      "kernels": "index_probe, gather_scan, gather_copy, " + ctx.last_kernel(), **ipc_res}))
 
 
 def main():
@@ -346,6 +378,7 @@ def main():
     ap.add_argument("--blocks", type=int, default=None, help="blocks per launch")
     ap.add_argument("--mode", default="decode", choices=["decode", "host", "encode", "resident"])
     ap.add_argument("--keys", type=int, default=1000, help="resident mode: keys per read")
+    ap.add_argument("--ipc", action="store_true", help="resident mode: also time the Arrow IPC message path")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--pmc-csv", default=None)

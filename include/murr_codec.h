@@ -311,6 +311,42 @@ int murr_index_gather(murr_ctx_t* ctx, const murr_index_t* idx, const uint8_t* q
                       const uint64_t* row_off, uint8_t* out_data, uint64_t out_cap,
                       uint64_t* out_row_off, uint32_t* rows, uint64_t* needed);
 
+/* ---- Arrow IPC framing --------------------------- */
+
+/* The read path's last step: the HTTP fetch handler serialises the batch with
+ * arrow-rs StreamWriter (schema message, record-batch message, end-of-stream;
+ * src/api/http/handlers.rs:93-101) and Flight DoGet with FlightDataEncoderBuilder
+ * (src/api/flight/mod.rs:85-87).  These write the same encapsulated messages
+ * (0xFFFFFFFF, int32 metadata size, flatbuffer Message V5 padded to
+ * `alignment`, body buffers each at a multiple of `alignment`, zero padding;
+ * arrow-rs IpcWriteOptions::default() uses alignment 64, Arrow C++ 8).
+ * Fields are nullable with no metadata (src/io/row/read.rs:105).  A column
+ * without nulls gets a zero-length validity buffer.  Every call with out ==
+ * NULL only reports *out_len; cap < *out_len returns MURR_E_CAPACITY.
+ * `alignment` is a power of two in [8, 4096]. */
+
+/* Schema message for the projected columns; names[p] is column p's name. */
+int murr_ipc_schema(const murr_segment_t* seg, const uint32_t* proj, uint32_t nproj,
+                    const char* const* names, uint32_t alignment, uint8_t* out,
+                    uint64_t cap, uint64_t* out_len);
+
+/* Record-batch message from the host arrays of murr_builder_build (host memory). */
+int murr_ipc_batch_host(const murr_segment_t* seg, const uint32_t* proj, uint32_t nproj,
+                        const murr_host_array_t* arrays, uint64_t n_rows, uint32_t alignment,
+                        uint8_t* out, uint64_t cap, uint64_t* out_len);
+
+/* Record-batch message from one block's decode outputs (device arrays whose
+ * null_count / data_len murr_decode_blocks filled), packed into dev_out by one
+ * kernel on the ctx stream so a single D2H copy yields the wire bytes.
+ * Synchronous. */
+int murr_ipc_batch_device(murr_ctx_t* ctx, const murr_segment_t* seg, const uint32_t* proj,
+                          uint32_t nproj, const murr_array_t* arrays, uint64_t n_rows,
+                          uint32_t alignment, uint8_t* dev_out, uint64_t cap,
+                          uint64_t* out_len, murr_error_t* err);
+
+/* End-of-stream marker (0xFFFFFFFF, 0) into out[8]; returns 8. */
+uint64_t murr_ipc_eos(uint8_t* out);
+
 /* Human-readable name of a status code. */
 const char* murr_status_str(int status);
 

@@ -106,6 +106,13 @@ SIGNATURES = {
     "murr_index_info": (I32, [P, C.POINTER(U64), C.POINTER(U64)]),
     "murr_index_lookup": (I32, [P, P, P, P, U64, P]),
     "murr_index_gather": (I32, [P, P, P, P, U64, P, P, P, U64, P, P, P]),
+    "murr_ipc_schema": (I32, [C.POINTER(Segment), C.POINTER(U32), U32, C.POINTER(C.c_char_p), U32, P, U64,
+                              C.POINTER(U64)]),
+    "murr_ipc_batch_host": (I32, [C.POINTER(Segment), C.POINTER(U32), U32, C.POINTER(HostArray), U64, U32, P,
+                                  U64, C.POINTER(U64)]),
+    "murr_ipc_batch_device": (I32, [P, C.POINTER(Segment), C.POINTER(U32), U32, C.POINTER(Array), U64, U32, P,
+                                    U64, C.POINTER(U64), C.POINTER(Error)]),
+    "murr_ipc_eos": (U64, [P]),
     "murr_status_str": (C.c_char_p, [I32]),
 }
 

@@ -1249,3 +1249,69 @@ int murr_encode_host(murr_ctx_t* c, const murr_segment_t* seg, const murr_host_c
 }
 
 }  // extern "C"
+
+// ---- Arrow IPC framing on the device (murr_ipc.cpp plans, murr_ipc.hip packs) ----
+extern "C" {
+
+int murr_ipc_batch_device(murr_ctx_t* c, const murr_segment_t* seg, const uint32_t* proj, uint32_t nproj,
+                          const murr_array_t* arrays, uint64_t n_rows, uint32_t alignment, uint8_t* dev_out,
+                          uint64_t cap, uint64_t* out_len, murr_error_t* err) {
+    set_err(err, MURR_OK);
+    if (!c || !out_len || !valid_segment(seg) || (nproj && (!proj || !arrays)) || !ipc_align_ok(alignment))
+        return set_err(err, MURR_E_ARGUMENT);
+    if (!nproj) return set_err(err, MURR_E_ARROW);  // RecordBatch without columns (read.rs:106-108)
+    std::vector<uint64_t> nulls(nproj), lens(nproj);
+    for (uint32_t p = 0; p < nproj; p++) {
+        if (proj[p] >= seg->ncols) return set_err(err, MURR_E_BAD_COLUMN);
+        nulls[p] = arrays[p].null_count;
+        lens[p] = arrays[p].data_len;
+    }
+    IpcPlan plan;
+    ipc_batch_plan(seg, proj, nproj, n_rows, nulls.data(), lens.data(), alignment, &plan);
+    const uint64_t meta = plan.meta.size(), total = meta + plan.body_len;
+    *out_len = total;
+    if (!dev_out) return MURR_OK;
+    if (cap < total) {
+        set_err(err, MURR_E_CAPACITY);
+        if (err) err->required = total;
+        return MURR_E_CAPACITY;
+    }
+    // Job table + metadata bytes, staged through pinned memory in one H2D.
+    std::vector<IpcJob> jobs;
+    jobs.reserve(plan.buf_off.size() + 1);
+    jobs.push_back(IpcJob{nullptr, dev_out, meta, meta});  // src patched below
+    uint64_t max_padded = meta;
+    for (size_t i = 0; i < plan.buf_off.size(); i++) {
+        const uint64_t len = plan.buf_len[i];
+        const uint64_t padded = round_up(len, alignment);
+        if (!padded) continue;
+        const murr_array_t& a = arrays[plan.buf_field[i]];
+        const void* src = plan.buf_kind[i] == kIpcValidity  ? (const void*)a.validity
+                          : plan.buf_kind[i] == kIpcOffsets ? (const void*)a.offsets
+                                                            : a.values;
+        if (!src) return set_err(err, MURR_E_ARGUMENT);
+        jobs.push_back(IpcJob{(const uint8_t*)src, dev_out + meta + plan.buf_off[i], len, padded});
+        max_padded = std::max(max_padded, padded);
+    }
+    const uint64_t jb = round_up(jobs.size() * sizeof(IpcJob), 16), stage = jb + meta;
+    uint8_t *hp = nullptr, *dp = nullptr;
+    uint64_t hcap = 0, dcap = 0;
+    if (!pool_take(c, true, stage, std::max<uint64_t>(stage, 1 << 16), &hp, &hcap)) return set_err(err, MURR_E_HIP);
+    if (!pool_take(c, false, stage, std::max<uint64_t>(stage, 1 << 16), &dp, &dcap)) {
+        pool_give(c, true, hp, hcap);
+        return set_err(err, MURR_E_HIP);
+    }
+    jobs[0].src = dp + jb;
+    std::memcpy(hp, jobs.data(), jobs.size() * sizeof(IpcJob));
+    std::memcpy(hp + jb, plan.meta.data(), meta);
+    hipError_t e = hipMemcpyAsync(dp, hp, stage, hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess) e = launch_ipc_pack((const IpcJob*)dp, (uint32_t)jobs.size(), max_padded, c->stream);
+    hipError_t e2 = hipStreamSynchronize(c->stream);
+    pool_give(c, true, hp, hcap);
+    pool_give(c, false, dp, dcap);
+    if (e != hipSuccess || e2 != hipSuccess) return hip_fail(err, e != hipSuccess ? e : e2);
+    c->last_kernel = "ipc_pack";
+    return MURR_OK;
+}
+
+}  // extern "C"

@@ -5,6 +5,9 @@
 #include <stdint.h>
 
 #include <string>
+#include <vector>
+
+#include "../../include/murr_codec.h"
 
 namespace murr {
 
@@ -171,5 +174,25 @@ hipError_t launch_index_insert(const IndexArgs& a, hipStream_t s);
 hipError_t launch_index_probe(const IndexArgs& a, hipStream_t s);
 uint64_t gather_scan_groups(uint64_t nq);
 hipError_t launch_gather(const IndexArgs& a, hipStream_t s);
+
+// Arrow IPC framing (murr_ipc.cpp, murr_ipc.hip).
+enum : uint32_t { kIpcValidity = 0, kIpcOffsets = 1, kIpcValues = 2 };
+struct IpcPlan {
+    std::vector<uint8_t> meta;          // 0xFFFFFFFF, size, flatbuffer, padding
+    std::vector<uint64_t> buf_off, buf_len;  // body buffers in IPC order (offsets from the body start)
+    std::vector<uint32_t> buf_field, buf_kind;
+    uint64_t body_len = 0;
+};
+bool ipc_align_ok(uint32_t a);
+int ipc_schema(const murr_segment_t* seg, const uint32_t* proj, uint32_t nproj, const char* const* names,
+               uint32_t align, std::vector<uint8_t>* out);
+int ipc_batch_plan(const murr_segment_t* seg, const uint32_t* proj, uint32_t nproj, uint64_t n,
+                   const uint64_t* null_counts, const uint64_t* data_lens, uint32_t align, IpcPlan* plan);
+struct IpcJob {                 // copy src[0..len) to dst[0..len), zero dst[len..padded)
+    const uint8_t* src;
+    uint8_t* dst;
+    uint64_t len, padded;
+};
+hipError_t launch_ipc_pack(const IpcJob* jobs, uint32_t njobs, uint64_t max_padded, hipStream_t s);
 
 }  // namespace murr

@@ -185,6 +185,58 @@ class ResidentTable:
         return pa.RecordBatch.from_arrays(arrays, schema=pa.schema(fields))
 
 
+    def read_ipc(self, keys, columns, alignment: int = 64) -> bytes:
+        """read() as the Arrow IPC stream of the HTTP fetch handler's StreamWriter
+        (src/api/http/handlers.rs:88-101), built on the device: lookup + gather +
+        decode, then one kernel packs the record-batch message in HBM
+        (murr_ipc_batch_device) and one D2H copy brings it back."""
+        from . import ipc
+        req = []
+        for name in columns:
+            idx = self.t.columns.get(name)
+            if idx is None:
+                raise SegmentError(f"column '{name}' not found")
+            req.append(self.segment.columns[idx])
+        if not req:
+            from .errors import ArrowError
+            raise ArrowError("Arrow error: must either specify a row count or at least one column")
+        nq = len(keys)
+        schema = ipc.schema_message(self.segment, req, alignment)
+        if self.index is None:
+            return ipc.stream(schema, _all_null_message(self.segment, req, nq, alignment))
+        blk, needed, _keep = self.gather(keys)
+        blk.data_bytes = max(nq * self.max_row, 16)
+        proj = [c.index for c in req]
+        outs = DecodeOutputs(self.ctx, self.segment, proj, [blk])
+        decode_blocks(self.ctx, self.segment, proj, [blk], outs)
+        dev, n = ipc.batch_message_device(self.ctx, self.segment, proj, outs, 0, nq, alignment)
+        return ipc.stream(schema, ipc.download_message(self.ctx, dev, n))
+
+
+def _all_null_message(segment, req, n: int, alignment: int) -> bytes:
+    """Every key missing (add_empty for each, rocksdb/mod.rs:262-263)."""
+    from . import ipc
+    nb = (n + 7) // 8
+    keep = []
+    arr = (_abi.HostArray * len(req))()
+
+    def zeros(k):
+        b = C.create_string_buffer(max(k, 1))
+        keep.append(b)
+        return C.addressof(b)
+    for p, c in enumerate(req):
+        h = arr[p]
+        h.length, h.null_count, h.dtype = n, n, int(c.dtype)
+        h.validity = zeros(nb) if n else None
+        if c.dtype == DTypeName.Utf8:
+            h.offsets, h.values, h.values_len = zeros(4 * (n + 1)), zeros(0), 0
+        elif c.dtype == DTypeName.Bool:
+            h.values, h.values_len = zeros(nb), nb
+        else:
+            h.values, h.values_len = zeros(n * c.dtype.size()), n * c.dtype.size()
+    return ipc.batch_message_host(segment, req, arr, n, alignment)
+
+
 def _to_arrow(h: dict, dt: DTypeName) -> pa.Array:
     n = h["length"]
     nb = (n + 7) // 8  # bitmaps come back padded (murr_bitmap_bytes); Arrow's are ceil(n/8)

@@ -76,12 +76,16 @@ class ReadBatchBuilder:
                 lens[i] = len(r)
         raise_status(self.L.murr_builder_add_rows(self.h, ptrs, lens, n), what="add_rows")
 
-    def build(self) -> pa.RecordBatch:
+    def _build_host(self):
         if self._nproj == 0:
             raise ArrowError("Arrow error: must either specify a row count or at least one column")
         outs = (_abi.HostArray * self._nproj)()
         err = _abi.Error()
         raise_status(self.L.murr_builder_build(self.h, outs, C.byref(err)), err, "ReadBatchBuilder::build")
+        return outs
+
+    def build(self) -> pa.RecordBatch:
+        outs = self._build_host()
         arrays, fields = [], []
         for p, col in enumerate(self.columns):
             seg_col = col if isinstance(col, SegmentColumnSchema) else self.segment.columns[int(col)]
@@ -93,6 +97,25 @@ class ReadBatchBuilder:
         tot, h2d, k, d2h = C.c_double(), C.c_float(), C.c_float(), C.c_float()
         self.L.murr_builder_last_timing(self.h, C.byref(tot), C.byref(h2d), C.byref(k), C.byref(d2h))
         return {"total_ms": tot.value, "h2d_ms": h2d.value, "kernel_ms": k.value, "d2h_ms": d2h.value}
+
+
+class IpcReadBatchBuilder(ReadBatchBuilder):
+    """ReadBatchBuilder whose build() returns the Arrow IPC stream the HTTP
+    fetch handler writes with StreamWriter (src/api/http/handlers.rs:93-101):
+    schema message, one record-batch message, end-of-stream.  The builder's
+    host arrays are framed in place (murr_ipc_batch_host), no pyarrow copy."""
+
+    def __init__(self, segment, columns, capacity, ctx=None, alignment: int = 64):
+        super().__init__(segment, columns, capacity, ctx)
+        self.alignment = alignment
+
+    def build(self) -> bytes:
+        from . import ipc
+        outs = self._build_host()
+        n = outs[0].length
+        cols = [c if isinstance(c, SegmentColumnSchema) else self.segment.columns[int(c)] for c in self.columns]
+        return ipc.stream(ipc.schema_message(self.segment, cols, self.alignment),
+                          ipc.batch_message_host(self.segment, cols, outs, n, self.alignment))
 
 
 def _copy(ptr, n) -> pa.Buffer:

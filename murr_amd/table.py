@@ -16,7 +16,7 @@ import pyarrow as pa
 
 from . import _abi
 from .errors import ArrowError, SegmentError, TableError, raise_status
-from .row import ReadBatchBuilder, default_context
+from .row import IpcReadBatchBuilder, ReadBatchBuilder, default_context
 from .schema import DTypeName, SegmentSchema, TableSchema
 from .store import KeyValue, Store
 
@@ -148,6 +148,20 @@ class Table:
                 raise SegmentError(f"column '{name}' not found")
             req.append(self.segment.columns[idx])
         builder = ReadBatchBuilder(self.segment, req, len(keys), self.ctx)
+        key_bytes = [k.encode() if isinstance(k, str) else bytes(k) for k in keys]
+        with self.lock:
+            return self.store.read(self.name, key_bytes, builder)
+
+    def read_ipc(self, keys, columns, alignment: int = 64) -> bytes:
+        """Table::read + the HTTP handler's StreamWriter (handlers.rs:88-101):
+        the read as an Arrow IPC stream (arrow-rs default alignment 64)."""
+        req = []
+        for name in columns:
+            idx = self.columns.get(name)
+            if idx is None:
+                raise SegmentError(f"column '{name}' not found")
+            req.append(self.segment.columns[idx])
+        builder = IpcReadBatchBuilder(self.segment, req, len(keys), self.ctx, alignment)
         key_bytes = [k.encode() if isinstance(k, str) else bytes(k) for k in keys]
         with self.lock:
             return self.store.read(self.name, key_bytes, builder)
