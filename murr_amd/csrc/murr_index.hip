@@ -277,32 +277,54 @@ __global__ void __launch_bounds__(kScanThreads) gather_probe_scan(IndexArgs A) {
     }
 }
 
-// A wave per query row: copy its blob bytes to the block (rows clamped by the
-// scan copy only what fits).  Bytes move as dwords where source and
-// destination share their alignment mod 4 (then 256 B per wave step), bytes
-// otherwise.
+// Eight lanes per query row, eight rows per wave: copy the row's blob bytes
+// to the block (rows clamped by the scan copy only what fits).  A lane owns
+// 16-B destination blocks b = lane%8, +8, ... aligned to the block buffer; it
+// loads the five aligned source dwords that cover the block (only the words
+// that overlap the row, so nothing outside the blob is read) and realigns them
+// with v_alignbyte.  Interior blocks are one 16-B store, the row's first and
+// last blocks byte stores.  One row per wave (the first version) spent most of
+// its time creating waves: ~100-B rows gave a wave one load and one store.
+constexpr uint32_t kCopyLanes = 8;
 __global__ void __launch_bounds__(256) gather_copy(IndexArgs A) {
-    const uint64_t i = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t i = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / kCopyLanes;
+    const uint32_t j = threadIdx.x % kCopyLanes;
     if (i >= A.nq) return;
     const uint32_t row = gp(A.rows)[i];
     if (row == kMissing) return;
     const uint64_t d0 = gp(A.sizes)[i], d1 = gp(A.sizes)[i + 1];
+    if (d1 <= d0) return;
     const uint64_t s0 = gp(A.row_off)[row];
-    const GAS uint8_t* src = gp(A.blob) + s0;
-    GAS uint8_t* dst = gp(A.out) + d0;
-    const uint64_t n = d1 - d0;  // the clamped length
-    if (((s0 ^ d0) & 3) == 0 && n >= 8) {
-        const uint32_t head = (uint32_t)((4 - (d0 & 3)) & 3);
-        if (lane < head) dst[lane] = src[lane];
-        const uint64_t nw = (n - head) >> 2;
-        const GAS uint32_t* sw = (const GAS uint32_t*)(src + head);
-        GAS uint32_t* dw = (GAS uint32_t*)(dst + head);
-        for (uint64_t k = lane; k < nw; k += 64) dw[k] = sw[k];
-        const uint64_t t0 = head + 4 * nw;
-        if (t0 + lane < n) dst[t0 + lane] = src[t0 + lane];
-    } else {
-        for (uint64_t k = lane; k < n; k += 64) dst[k] = src[k];
+    const GAS uint8_t* blob = gp(A.blob);
+    GAS uint8_t* out = gp(A.out);
+    const uint64_t first = d0 & ~(uint64_t)15;
+    for (uint64_t D = first + 16 * (uint64_t)j; D < d1; D += 16 * kCopyLanes) {
+        const uint64_t lo = D > d0 ? D : d0, hi = D + 16 < d1 ? D + 16 : d1;
+        // source bytes of [lo, hi): [s0 + lo - d0, s0 + hi - d0); of D: S (may precede the row)
+        const uint64_t slo = s0 + (lo - d0), shi = s0 + (hi - d0);
+        const uint64_t S = slo - (lo - D);  // = s0 - d0 + D, computed without underflow past lo
+        const uint32_t sh = (uint32_t)(S & 3);
+        const uint64_t wb = S & ~(uint64_t)3;
+        uint32_t w[5];
+#pragma unroll
+        for (int t = 0; t < 5; t++) {
+            const uint64_t a = wb + 4 * t;
+            w[t] = (a < shi && a + 4 > slo) ? *(const GAS uint32_t*)(blob + a) : 0u;
+        }
+        uint32_t q[4];
+#pragma unroll
+        for (int t = 0; t < 4; t++) q[t] = __builtin_amdgcn_alignbyte(w[t + 1], w[t], sh);
+        if (lo == D && hi == D + 16) {
+            typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+            u32x4 v = {q[0], q[1], q[2], q[3]};
+            *(GAS u32x4*)(out + D) = v;
+        } else {
+#pragma unroll
+            for (int k = 0; k < 16; k++) {
+                const uint64_t b = D + k;
+                if (b >= lo && b < hi) out[b] = (uint8_t)(q[k >> 2] >> (8 * (k & 3)));
+            }
+        }
     }
 }
 
@@ -337,7 +359,9 @@ hipError_t launch_gather(const IndexArgs& a, hipStream_t s) {
             hipLaunchKernelGGL(gather_scan, dim3((uint32_t)groups), dim3(kScanThreads), 0, s, a, 1u);
         }
     }
-    if (a.nq) hipLaunchKernelGGL(gather_copy, dim3((uint32_t)((a.nq + 3) / 4)), dim3(256), 0, s, a);
+    if (a.nq)
+        hipLaunchKernelGGL(gather_copy, dim3((uint32_t)((a.nq + 256 / kCopyLanes - 1) / (256 / kCopyLanes))),
+                           dim3(256), 0, s, a);
     return hipGetLastError();
 }
 
