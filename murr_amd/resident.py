@@ -155,8 +155,7 @@ class ResidentTable:
         raise_status(st, what="murr_index_gather")
         return DeviceBlock(data, offs, nq, 0), needed, (qd, qo)
 
-    def read(self, keys, columns) -> pa.RecordBatch:
-        """Table::read (table/mod.rs:114-129) with the store lookup on the device."""
+    def _resolve(self, columns):
         req = []
         for name in columns:
             idx = self.t.columns.get(name)
@@ -166,24 +165,28 @@ class ResidentTable:
         if not req:
             from .errors import ArrowError
             raise ArrowError("Arrow error: must either specify a row count or at least one column")
+        return req
+
+    def read_host(self, keys, columns):
+        """Lookup + gather + decode on the device, then D2H: (requested
+        SegmentColumnSchema list, host buffer dicts as download_array returns
+        them).  A miss is an all-null row (add_empty)."""
+        req = self._resolve(columns)
         nq = len(keys)
         if self.index is None:
-            # nothing written: every key misses (add_empty)
-            arrays = [pa.nulls(nq, c.dtype.arrow_dtype()) for c in req]
-        else:
-            blk, needed, _keep = self.gather(keys)
-            blk.data_bytes = max(nq * self.max_row, 16)
-            proj = [c.index for c in req]
-            outs = DecodeOutputs(self.ctx, self.segment, proj, [blk])
-            decode_blocks(self.ctx, self.segment, proj, [blk], outs)
-            assert int(needed.download(8).view(np.uint64)[0]) <= max(nq * self.max_row, 16)
-            arrays = []
-            for p, c in enumerate(req):
-                h = download_array(self.ctx, outs.array(0, p), int(c.dtype), nq)
-                arrays.append(_to_arrow(h, c.dtype))
-        fields = [pa.field(c.name, c.dtype.arrow_dtype(), True) for c in req]
-        return pa.RecordBatch.from_arrays(arrays, schema=pa.schema(fields))
+            return req, [_null_dict(c.dtype, nq) for c in req]
+        blk, needed, _keep = self.gather(keys)
+        blk.data_bytes = max(nq * self.max_row, 16)
+        proj = [c.index for c in req]
+        outs = DecodeOutputs(self.ctx, self.segment, proj, [blk])
+        decode_blocks(self.ctx, self.segment, proj, [blk], outs)
+        assert int(needed.download(8).view(np.uint64)[0]) <= max(nq * self.max_row, 16)
+        return req, [download_array(self.ctx, outs.array(0, p), int(c.dtype), nq) for p, c in enumerate(req)]
 
+    def read(self, keys, columns) -> pa.RecordBatch:
+        """Table::read (table/mod.rs:114-129) with the store lookup on the device."""
+        req, hs = self.read_host(keys, columns)
+        return host_batch(req, hs)
 
     def read_ipc(self, keys, columns, alignment: int = 64) -> bytes:
         """read() as the Arrow IPC stream of the HTTP fetch handler's StreamWriter
@@ -235,6 +238,25 @@ def _all_null_message(segment, req, n: int, alignment: int) -> bytes:
         else:
             h.values, h.values_len = zeros(n * c.dtype.size()), n * c.dtype.size()
     return ipc.batch_message_host(segment, req, arr, n, alignment)
+
+
+def _null_dict(dt: DTypeName, n: int) -> dict:
+    nb = (n + 7) // 8
+    h = {"dtype": int(dt), "length": n, "null_count": n, "validity": bytes(nb), "offsets": None}
+    if dt == DTypeName.Utf8:
+        h["offsets"], h["values"] = np.zeros(n + 1, np.int32), b""
+    elif dt == DTypeName.Bool:
+        h["values"] = bytes(nb)
+    else:
+        h["values"] = bytes(n * dt.size())
+    return h
+
+
+def host_batch(req, hs) -> pa.RecordBatch:
+    """Host buffer dicts -> RecordBatch (nullable fields, no metadata, read.rs:105)."""
+    arrays = [_to_arrow(h, c.dtype) for c, h in zip(req, hs)]
+    fields = [pa.field(c.name, c.dtype.arrow_dtype(), True) for c in req]
+    return pa.RecordBatch.from_arrays(arrays, schema=pa.schema(fields))
 
 
 def _to_arrow(h: dict, dt: DTypeName) -> pa.Array:

@@ -58,3 +58,128 @@ class Group:
         if self.dist is not None:
             self.dist.destroy_process_group()
             self.dist = None
+
+
+# ---- random-key batch read across key-range shards (SURVEY.md §8(e) mode 2) ----
+#
+# Every rank receives the same keys (the caller's batch) and reads them against
+# its own shard on its own GPU: lookup + gather + decode (ResidentTable), so a
+# key it does not own is a miss -- an all-null row, zero bytes in every buffer
+# (arrow-rs null slots are zero, validity bit 0, utf8 length 0).  A key lives in
+# exactly one shard, so for every row at most one rank contributes non-zero
+# bytes, and the caller-order result (src/io/store/rocksdb/mod.rs:368-399:
+# output row i is key i) is the byte-wise SUM of the ranks' buffers.  That is
+# the one exchange step of the read: fixed-width values, bool bitmaps and
+# validity bitmaps are summed as u8 (disjoint bytes / bits, so no carries),
+# utf8 lengths are summed, every rank places its strings at the merged
+# offsets, and the string bytes are summed.  Three all-reduces per read, each
+# over all projected columns at once (few, large collectives); on GPUs the
+# buffers can stay in HBM and go over RCCL, on CPU (tests) gloo carries them.
+
+
+def _bitmap(h, n):
+    nb = (n + 7) // 8
+    if h["validity"] is None:  # no nulls on this rank: every row valid here
+        import numpy as np
+        v = np.full(nb, 0xFF, np.uint8)
+        if n % 8:
+            v[-1] = (1 << (n % 8)) - 1
+        return v
+    import numpy as np
+    return np.frombuffer(bytes(h["validity"][:nb]), np.uint8)
+
+
+def merge_reads(group, dtypes, n: int, hs):
+    """Merge this rank's host buffer dicts (one per requested column, caller
+    order, misses all-null) with every other rank's: returns the dicts of the
+    whole read.  `group` is a Group (world 1 returns the input unchanged)."""
+    if group.dist is None:
+        return hs
+    import numpy as np
+    import torch
+    from .schema import DTypeName as D
+    nb = (n + 7) // 8
+    # 1. validity + fixed values + bool bitmaps + utf8 lengths: one u8 buffer
+    parts, lens_parts = [], []
+    for dt, h in zip(dtypes, hs):
+        parts.append(_bitmap(h, n))
+        if dt == D.Utf8:
+            lens_parts.append(np.diff(np.asarray(h["offsets"], np.int64)))
+        else:
+            parts.append(np.frombuffer(bytes(h["values"]), np.uint8)[: (nb if dt == D.Bool else n * dt.size())])
+    flat = torch.from_numpy(np.concatenate(parts) if parts else np.zeros(0, np.uint8))
+    group.dist.all_reduce(flat)
+    lens = None
+    if lens_parts:
+        lens = torch.from_numpy(np.concatenate(lens_parts))
+        group.dist.all_reduce(lens)
+        lens = lens.numpy().reshape(len(lens_parts), n)
+    flat = flat.numpy()
+    # 2. utf8: merged offsets, this rank's strings placed there, summed
+    goffs, data_parts, at, u = [], [], 0, 0
+    for dt, h in zip(dtypes, hs):
+        if dt != D.Utf8:
+            continue
+        go = np.zeros(n + 1, np.int64)
+        np.cumsum(lens[u], out=go[1:])
+        if go[-1] > np.iinfo(np.int32).max:
+            from .errors import SegmentError
+            raise SegmentError("byte array offset overflow")
+        lo = np.asarray(h["offsets"], np.int64)
+        mine = np.diff(lo)
+        buf = np.zeros(int(go[-1]), np.uint8)
+        rows = np.flatnonzero(mine)
+        if rows.size:
+            ln = mine[rows]
+            src = np.repeat(lo[rows] - np.cumsum(ln) + ln, ln) + np.arange(int(ln.sum()))
+            dst = np.repeat(go[rows] - np.cumsum(ln) + ln, ln) + np.arange(int(ln.sum()))
+            buf[dst] = np.frombuffer(bytes(h["values"]), np.uint8)[src]
+        goffs.append(go)
+        data_parts.append(buf)
+        u += 1
+    if data_parts:
+        data = torch.from_numpy(np.concatenate(data_parts))
+        group.dist.all_reduce(data)
+        data = data.numpy()
+    # 3. unpack
+    out, pos, dpos, u = [], 0, 0, 0
+    for dt, h in zip(dtypes, hs):
+        valid = flat[pos:pos + nb]
+        pos += nb
+        nulls = n - int(np.unpackbits(valid, bitorder="little")[:n].sum()) if n else 0
+        r = {"dtype": int(dt), "length": n, "null_count": nulls,
+             "validity": valid.tobytes() if nulls else None, "offsets": None}
+        if dt == D.Utf8:
+            go = goffs[u]
+            r["offsets"] = go.astype(np.int32)
+            r["values"] = data[dpos:dpos + int(go[-1])].tobytes()
+            dpos += int(go[-1])
+            u += 1
+        else:
+            w = nb if dt == D.Bool else n * dt.size()
+            r["values"] = flat[pos:pos + w].tobytes()
+            pos += w
+        out.append(r)
+    return out
+
+
+class ShardedResidentTable:
+    """One key-range shard of a table per rank (one process per GPU), each a
+    ResidentTable in that GPU's HBM.  `read` is Table::read over the whole
+    table: every rank passes the same keys and gets the same caller-order
+    batch."""
+
+    def __init__(self, table, group: "Group", ctx=None, name: str = "shard"):
+        from .resident import ResidentTable
+        self.group = group
+        self.local = ResidentTable(table, ctx, name)
+
+    def write_shard(self, batch):
+        """Write this rank's key range (Table::write on its own shard)."""
+        self.local.write(batch)
+
+    def read(self, keys, columns):
+        from .resident import host_batch
+        req, hs = self.local.read_host(keys, columns)
+        merged = merge_reads(self.group, [c.dtype for c in req], len(keys), hs)
+        return host_batch(req, merged)

@@ -97,3 +97,81 @@ def test_two_rank_shards_concatenate_to_whole():
     assert offs_all == ref[1]["offsets"].tolist()
     assert vals_all == ref[1]["values"]
     assert whole_bytes == ref_blob  # sum over ranks of shard blob bytes == whole-range blob
+
+
+# ---- random-key batch read across shards (SURVEY.md §8(e) mode 2) -----------------
+# Each rank "reads" the caller's keys against its own shard (here the oracle
+# decodes a block where the keys it does not own are missing rows, exactly what
+# ResidentTable.read_host returns on a GPU), then merge_reads exchanges and
+# restores the whole read in caller order.  It must equal the oracle's decode
+# of the read against the whole table.
+READ_ROWS, READ_KEYS = 3001, 1500
+
+
+def _read_case():
+    from randgen import ALL, random_columns
+    rng = np.random.default_rng(77)
+    dtypes = ALL + [O_UTF8_EXTRA]
+    cols = random_columns(rng, dtypes, READ_ROWS, null_p=0.15)
+    seg = O.Segment([int(d) for d in dtypes])
+    blob, off = O.encode_batch(seg, synth.oracle_cols(cols), READ_ROWS)
+    q = rng.integers(0, int(READ_ROWS * 1.05), size=READ_KEYS)  # ~5 % misses, duplicates
+    proj = [0, 12, 3, 1, 10, 11, 9, 5, 0]
+    return dtypes, seg, blob, off, q, proj
+
+
+O_UTF8_EXTRA = 0  # a second utf8 column
+
+
+def _block_for(blob, off, q, owned):
+    parts, ro = [], [0]
+    for k in q:
+        k = int(k)
+        b = blob[int(off[k]):int(off[k + 1])].tobytes() if (k < READ_ROWS and owned(k)) else b""
+        parts.append(b)
+        ro.append(ro[-1] + len(b))
+    return np.frombuffer(b"".join(parts), np.uint8).copy(), np.array(ro, np.uint64)
+
+
+def _read_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    from murr_amd.schema import DTypeName as D
+    from murr_amd.shard import merge_reads
+    g = Group("gloo")
+    dtypes, seg, blob, off, keys, proj = _read_case()
+    start, n = shard_rows(rank, world, READ_ROWS)
+    data, ro = _block_for(blob, off, keys, lambda k: start <= k < start + n)
+    local = O.decode_block(seg, proj, data, ro)
+    merged = merge_reads(g, [D(dtypes[p]) for p in proj], len(keys), local)
+    q.put((rank, [(m["null_count"], m["validity"], m["values"],
+                   None if m["offsets"] is None else m["offsets"].tolist()) for m in merged]))
+    g.close()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_random_key_read_restores_caller_order(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_read_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=180) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    dtypes, seg, blob, off, keys, proj = _read_case()
+    data, ro = _block_for(blob, off, keys, lambda k: True)
+    want = O.decode_block(seg, proj, data, ro)
+    nb = (len(keys) + 7) // 8
+    for rank, cols in got:  # every rank holds the whole read
+        for p, (nulls, validity, values, offsets) in enumerate(cols):
+            w = want[p]
+            assert nulls == w["null_count"], (rank, p)
+            assert (validity is None) == (w["validity"] is None), (rank, p)
+            if validity is not None:
+                assert validity[:nb] == w["validity"], (rank, p)
+            assert values == w["values"], (rank, p)
+            if w["offsets"] is not None:
+                assert offsets == w["offsets"].tolist(), (rank, p)
