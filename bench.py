@@ -133,6 +133,45 @@ def cpu_baseline(seg, proj, host_blob, host_off, rows, target_s):
                       f"oracle/libmurr_oracle.so (serial ReadBatchBuilder restatement), {dt:.1f} s"}
 
 
+def cpu_baseline_threads(seg, proj, host_blob, host_off, rows, target_s, threads):
+    """Upper bound the reference does not implement: the
+    same oracle on `threads` host threads, each decoding a contiguous row range
+    of the block (ctypes drops the GIL inside the C call)."""
+    import threading
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    oseg = O.Segment([int(c.dtype) for c in seg.columns])
+    parts = []
+    for t in range(threads):
+        r0, r1 = rows * t // threads, rows * (t + 1) // threads
+        b0, b1 = int(host_off[r0]), int(host_off[r1])
+        parts.append((host_blob[b0:b1].copy(), (host_off[r0:r1 + 1] - host_off[r0]).astype(np.uint64), r1 - r0))
+    part_bytes = []
+    for blob, off, n in parts:
+        res = O.decode_block(oseg, proj, blob, off)
+        part_bytes.append(arrow_out_bytes(seg, proj, n, [r["null_count"] for r in res],
+                                          [len(r["values"]) if r["dtype"] == 0 else 0 for r in res]))
+    done = [0] * threads
+    deadline = time.perf_counter() + target_s
+
+    def work(i):
+        blob, off, _ = parts[i]
+        while time.perf_counter() < deadline:
+            O.decode_block(oseg, proj, blob, off)
+            done[i] += 1
+    ths = [threading.Thread(target=work, args=(i,)) for i in range(threads)]
+    t = time.perf_counter()
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    dt = time.perf_counter() - t
+    total = sum(d * b for d, b in zip(done, part_bytes))
+    return {"value": round(total / dt / GIB, 4), "unit": "GiB/s", "cores": threads, "kind": "port",
+            "sample": f"{sum(done)} row-range parts ({threads} per block of {rows} rows) on {threads} "
+                      f"threads, oracle/libmurr_oracle.so, {dt:.1f} s"}
+
+
 def run_decode(args, dist, rank, world, local_rank):
     ctx = Context(local_rank % max(device_count(), 1))  # one GPU per rank (modulo: rehearsal on fewer GPUs)
     rows, K = args.rows, args.blocks
@@ -206,6 +245,10 @@ def run_decode(args, dist, rank, world, local_rank):
     }
     if rank == 0 and world == 1 and not args.no_cpu:
         line["cpu_baseline"] = cpu_baseline(seg, proj, host_blob, host_off, rows, args.cpu_seconds)
+        threads = min(16, os.cpu_count() or 1)  # the GPU box's CPU share is 16
+        if threads > 1:
+            line["cpu_baseline_all_cores"] = cpu_baseline_threads(seg, proj, host_blob, host_off, rows,
+                                                                  min(5.0, args.cpu_seconds), threads)
     if rank == 0:
         print(json.dumps(line), flush=True)
     ctx.close()
