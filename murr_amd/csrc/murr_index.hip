@@ -20,6 +20,8 @@
 // All integer work; the lookup is latency-bound (query key, slot + location,
 // stored key: three dependent memory round trips per probe), the gather an
 // HBM-bound byte copy.
+#include <cstdlib>
+
 #include "murr_device.h"
 
 namespace murr {
@@ -285,7 +287,7 @@ __global__ void __launch_bounds__(kScanThreads) gather_probe_scan(IndexArgs A) {
 // with v_alignbyte.  Interior blocks are one 16-B store, the row's first and
 // last blocks byte stores.  One row per wave (the first version) spent most of
 // its time creating waves: ~100-B rows gave a wave one load and one store.
-constexpr uint32_t kCopyLanes = 8;
+template <uint32_t kCopyLanes>
 __global__ void __launch_bounds__(256) gather_copy(IndexArgs A) {
     const uint64_t i = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / kCopyLanes;
     const uint32_t j = threadIdx.x % kCopyLanes;
@@ -359,9 +361,19 @@ hipError_t launch_gather(const IndexArgs& a, hipStream_t s) {
             hipLaunchKernelGGL(gather_scan, dim3((uint32_t)groups), dim3(kScanThreads), 0, s, a, 1u);
         }
     }
-    if (a.nq)
-        hipLaunchKernelGGL(gather_copy, dim3((uint32_t)((a.nq + 256 / kCopyLanes - 1) / (256 / kCopyLanes))),
-                           dim3(256), 0, s, a);
+    if (a.nq) {
+        // lanes per row (tuning: MURR_GATHER_LANES = 4, 8 or 16; 8 measured best on config C rows)
+        static const int lanes = [] {
+            const char* e = std::getenv("MURR_GATHER_LANES");
+            const int v = e ? std::atoi(e) : 8;
+            return (v == 4 || v == 16) ? v : 8;
+        }();
+        const uint32_t rows_per_wg = 256 / (uint32_t)lanes;
+        const dim3 grid((uint32_t)((a.nq + rows_per_wg - 1) / rows_per_wg));
+        if (lanes == 4) hipLaunchKernelGGL(gather_copy<4>, grid, dim3(256), 0, s, a);
+        else if (lanes == 16) hipLaunchKernelGGL(gather_copy<16>, grid, dim3(256), 0, s, a);
+        else hipLaunchKernelGGL(gather_copy<8>, grid, dim3(256), 0, s, a);
+    }
     return hipGetLastError();
 }
 
