@@ -47,52 +47,7 @@ __global__ void __launch_bounds__(kPackThreads) ipc_pack(const IpcJob* __restric
     }
 }
 
-// Small messages: the job table and the metadata travel in the kernel
-// arguments (no H2D, no staging to keep alive), so the pack is one stream op.
-// Job 0 (src == nullptr) is the metadata, copied from the arguments.
-__global__ void __launch_bounds__(kPackThreads) ipc_pack_inline(const IpcInline a) {
-    if (blockIdx.y == 0) {
-        if (blockIdx.x) return;
-        const IpcJob j = a.jobs[0];
-        for (uint32_t k = threadIdx.x; k < j.padded; k += kPackThreads) j.dst[k] = k < j.len ? a.meta[k] : 0;
-        return;
-    }
-    const IpcJob j = a.jobs[blockIdx.y];
-    const uint64_t units = (j.padded + 15) / 16;
-    const uintptr_t mis = (reinterpret_cast<uintptr_t>(j.src) | reinterpret_cast<uintptr_t>(j.dst));
-    const bool a16 = (mis & 15) == 0, a8 = (mis & 7) == 0;
-    for (uint64_t u = (uint64_t)blockIdx.x * kPackThreads + threadIdx.x; u < units;
-         u += (uint64_t)gridDim.x * kPackThreads) {
-        const uint64_t b = u * 16;
-        if (b + 16 <= j.len) {
-            if (a16) {
-                *reinterpret_cast<uint4*>(j.dst + b) = *reinterpret_cast<const uint4*>(j.src + b);
-                continue;
-            }
-            if (a8) {
-                const uint2* s = reinterpret_cast<const uint2*>(j.src + b);
-                uint2* d = reinterpret_cast<uint2*>(j.dst + b);
-                uint2 x = s[0], y = s[1];
-                d[0] = x;
-                d[1] = y;
-                continue;
-            }
-        }
-        const uint64_t end = b + 16 < j.padded ? b + 16 : j.padded;
-        for (uint64_t k = b; k < end; k++) j.dst[k] = k < j.len ? j.src[k] : (uint8_t)0;
-    }
-}
-
 }  // namespace
-
-hipError_t launch_ipc_pack_inline(const IpcInline& a, uint64_t max_padded, hipStream_t s) {
-    uint64_t units = (max_padded + 15) / 16;
-    uint64_t gx = (units + kPackThreads * 4 - 1) / (kPackThreads * 4);
-    if (gx < 1) gx = 1;
-    if (gx > 2048) gx = 2048;
-    hipLaunchKernelGGL(ipc_pack_inline, dim3((uint32_t)gx, a.njobs), dim3(kPackThreads), 0, s, a);
-    return hipGetLastError();
-}
 
 hipError_t launch_ipc_pack(const IpcJob* jobs, uint32_t njobs, uint64_t max_padded, hipStream_t s) {
     if (!njobs) return hipSuccess;
