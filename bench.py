@@ -112,6 +112,20 @@ def pmc_traffic(paths):
     return round((2.0 * sum(fetch) / len(fetch) + sum(write) / len(write)) * 1024.0)
 
 
+def cpu_model() -> str:
+    """The host CPU's model name (lscpu model next to every
+    CPU number), from /proc/cpuinfo."""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.lower().startswith("model name"):
+                    return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or "unknown"
+
+
 def cpu_baseline(seg, proj, host_blob, host_off, rows, target_s):
     """The oracle (C restatement of ReadBatchBuilder, 1 thread) on this host."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -128,7 +142,7 @@ def cpu_baseline(seg, proj, host_blob, host_off, rows, target_s):
         O.decode_block(oseg, proj, host_blob, host_off)
     dt = time.perf_counter() - t
     return {"value": round(out_bytes * reps / dt / GIB, 4), "unit": "GiB/s", "cores": 1,
-            "kind": "port",
+            "kind": "port", "cpu_model": cpu_model(), "host_cpus": os.cpu_count(),
             "sample": f"{reps} blocks x {rows} rows of the same workload decoded by "
                       f"oracle/libmurr_oracle.so (serial ReadBatchBuilder restatement), {dt:.1f} s"}
 
@@ -168,12 +182,19 @@ def cpu_baseline_threads(seg, proj, host_blob, host_off, rows, target_s, threads
     dt = time.perf_counter() - t
     total = sum(d * b for d, b in zip(done, part_bytes))
     return {"value": round(total / dt / GIB, 4), "unit": "GiB/s", "cores": threads, "kind": "port",
+            "cpu_model": cpu_model(), "host_cpus": os.cpu_count(),
             "sample": f"{sum(done)} row-range parts ({threads} per block of {rows} rows) on {threads} "
                       f"threads, oracle/libmurr_oracle.so, {dt:.1f} s"}
 
 
 def run_decode(args, dist, rank, world, local_rank):
-    ctx = Context(local_rank % max(device_count(), 1))  # one GPU per rank (modulo: rehearsal on fewer GPUs)
+    ndev = device_count()
+    if local_rank >= ndev:
+        # one GPU per rank: more ranks than GPUs would share a GPU and report a
+        # wrong aggregate, so refuse instead of wrapping around
+        raise SystemExit(f"rank {rank} (local {local_rank}) has no GPU of its own: {ndev} visible, "
+                         f"WORLD_SIZE {world}")
+    ctx = Context(local_rank)
     rows, K = args.rows, args.blocks
     start, _ = shard_rows(rank, world, rows * world)  # weak scaling: `rows` per rank
     cols = make_columns(args.config, rows, start=start)

@@ -71,6 +71,13 @@ struct murr_ctx {
     std::vector<uint32_t> dtypes;  // per projected column
     uint32_t nblocks = 0, nproj = 0;
     uint64_t rb_off = 0;           // readback offset in hs
+    // a stream-mode JIT launch, re-run in local mode if its look-back timed out
+    bool retry_local = false;
+    std::vector<murr_column_t> r_cols;
+    murr_segment_t r_seg{};
+    std::vector<uint32_t> r_proj;
+    std::vector<murr_block_t> r_blocks;
+    double r_est = 0;
     int pending_status = MURR_OK;
     const char* last_kernel = "";  // kernel of the last decode launch
     // Staging buffers of freed builders, reused by the next ones (a read builds
@@ -435,6 +442,231 @@ int murr_sync(murr_ctx_t* c) {
 
 // ---- decode ------------------------------------------------------------------
 
+namespace {
+
+// After an enqueue: what murr_decode_wait needs to fill the counts.
+int pending_set(murr_ctx* c, murr_array_t* outs, const murr_block_t* blocks, uint32_t nblocks, uint32_t nproj,
+                const std::vector<DecProj>& dp, uint64_t rb) {
+    c->pending = true;
+    c->outs = outs;
+    c->nblocks = nblocks;
+    c->nproj = nproj;
+    c->rb_off = rb;
+    c->n_rows.resize(nblocks);
+    for (uint32_t b = 0; b < nblocks; b++) c->n_rows[b] = blocks[b].n_rows;
+    c->dtypes.resize(nproj);
+    for (uint32_t p = 0; p < nproj; p++) c->dtypes[p] = dp[p].dtype;
+    return MURR_OK;
+}
+
+// The layout-specialised decode (murr_jit_kernel.hip).  Tile shape from the
+// mean row size; local mode (a workgroup owns whole blocks) when the blocks
+// fill the co-resident grid, else stream mode (tiles round-robin, utf8
+// prefixes by decoupled look-back).  A projection naming a column twice runs
+// one launch per occurrence round (the later rounds only fill the duplicate
+// outputs, so they report no errors).
+int decode_enqueue_jit(murr_ctx* c, const murr_segment_t* seg, const JitLayout* jl, const uint32_t* proj,
+                       uint32_t nproj, const murr_block_t* blocks, uint32_t nblocks, murr_array_t* outs,
+                       const std::vector<DecProj>& dp, double est_row, bool force_local = false) {
+    murr_error_t* err = nullptr;
+    const bool verbose = std::getenv("MURR_DECODE_VERBOSE") != nullptr;
+    uint32_t nu_layout = 0;
+    for (uint32_t i = 0; i < seg->ncols; i++) nu_layout += seg->cols[i].dtype == MURR_UTF8;
+    const uint32_t nu = std::max<uint32_t>(nu_layout, 1);
+    // Shape: 5 waves x 2 chunks (512 rows) when its two LDS slots fit 40 KiB
+    // with 15 % slack over the mean row (four workgroups per CU); else 5 x 1
+    // (256 rows) within 64 KiB with 8 % slack (two per CU, wide rows); else 3 x 1.
+    auto lds_for = [&](uint32_t s, double slack) {
+        const JitShapeK& k = jl->shapes[s];
+        const uint32_t st = (uint32_t)round_up((uint64_t)(k.tr * est_row * slack) + 64, 1024);
+        return jit_lds_bytes(k.nw, k.r, st, nu_layout);
+    };
+    uint32_t si = 2;
+    double slack = 1.08;
+    uint32_t budget = 65536;
+    if (lds_for(0, 1.15) <= 40960) { si = 0; slack = 1.15; budget = 40960; }
+    else if (lds_for(1, 1.08) <= 65536) si = 1;
+    if (const char* e = std::getenv("MURR_JIT_SHAPE")) {  // tuning: "NWxR"
+        uint32_t w = 0, r = 0;
+        if (std::sscanf(e, "%ux%u", &w, &r) == 2)
+            for (uint32_t s = 0; s < kJitShapes; s++)
+                if (jl->shapes[s].nw == w && jl->shapes[s].r == r) si = s;
+    }
+    if (const char* e = std::getenv("MURR_JIT_LDS")) budget = (uint32_t)std::atoi(e);  // tuning
+    const JitShapeK& K = jl->shapes[si];
+    const uint32_t smax = std::max<uint32_t>(1024, ((budget - std::min(budget, jit_lds_bytes(K.nw, K.r, 0, nu_layout))) / 2) & ~1023u);
+    uint32_t stage = (uint32_t)std::min<uint64_t>(round_up((uint64_t)(K.tr * est_row * slack) + 64, 1024), smax);
+    if (const char* e = std::getenv("MURR_JIT_STAGE")) stage = (uint32_t)round_up((uint64_t)std::atof(e), 1024);
+    const uint32_t lds = jit_lds_bytes(K.nw, K.r, stage, nu_layout);
+
+    // Workgroups per CU: the occupancy answer, never above the LDS bound.
+    // Stream mode needs the whole grid resident at once (workgroups wait on
+    // each other's tiles), and the API over-counts when SGPRs bind, so its
+    // grid also respects a worst-case register bound: 106 SGPRs allow 6 waves
+    // per SIMD (MI355X_MICROARCH.md, residency), the VGPR count allows
+    // 512 / alloc, and a 5-wave workgroup may put 2 waves on one SIMD.
+    auto occupancy = [&](hipFunction_t fn) {
+        int n = 0;
+        if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, 64 * K.nw, lds) != hipSuccess || n < 1) n = 1;
+        return std::min<int>(n, std::max<int>(1, (int)(163840 / std::max<uint32_t>(lds, 1))));
+    };
+    const int bpc = occupancy(K.fn);
+    int bpc_safe = occupancy(K.fn_split);
+    {
+        int vgprs = 0;
+        if (hipFuncGetAttribute(&vgprs, HIP_FUNC_ATTRIBUTE_NUM_REGS, K.fn_split) != hipSuccess || vgprs < 1) vgprs = 128;
+        const int alloc = (vgprs + 7) / 8 * 8;
+        const int per_simd = std::min(std::min(8, 512 / alloc), 6);
+        const int waves_per_simd_per_wg = (int)(K.nw + 3) / 4;
+        bpc_safe = std::max(1, std::min(bpc_safe, per_simd / waves_per_simd_per_wg));
+    }
+    const uint64_t G = (uint64_t)c->cus * bpc;
+
+    std::vector<DecBlock> db(nblocks);
+    std::vector<uint32_t> order;
+    uint64_t tiles = 0;
+    for (uint32_t b = 0; b < nblocks; b++) {
+        db[b] = DecBlock{blocks[b].data, blocks[b].row_off, blocks[b].n_rows, tiles};
+        tiles += (blocks[b].n_rows + K.tr - 1) / K.tr;
+        if (blocks[b].n_rows) order.push_back(b);
+    }
+    const uint64_t nonempty = order.size();
+    // local mode when whole blocks keep >= 75 % of the grid busy
+    bool local = false;
+    (void)bpc_safe;
+    if (nonempty) {
+        const uint64_t rounds = (nonempty + G - 1) / G;
+        local = nonempty * 4 >= rounds * G * 3;
+    }
+    if (const char* e = std::getenv("MURR_JIT_MODE")) local = std::string(e) == "local";  // tuning
+    if (force_local) local = true;
+    // Split mode: segments of seg_tiles tiles dealt round-robin over a
+    // co-resident grid; a grid round of segments (the distance between a
+    // segment's two passes) is kept near 96 MiB so the second pass still
+    // finds it in the Infinity Cache.
+    const uint64_t G_split = (uint64_t)c->cus * bpc_safe;
+    // segment tiles: the launch's tiles over whole grid rounds of <= 96 MiB
+    const double tile_in = K.tr * (est_row + 8.0);
+    const uint64_t grid_rounds = std::max<uint64_t>(1, (uint64_t)std::ceil(tiles * tile_in / 100663296.0));
+    uint64_t seg_tiles = std::max<uint64_t>(1, (tiles + grid_rounds * G_split - 1) / (grid_rounds * G_split));
+    if (const char* e = std::getenv("MURR_JIT_SEGTILES")) seg_tiles = std::max(1, std::atoi(e));  // tuning
+    std::vector<JitSeg> jsegs;
+    if (!local) {
+        for (uint32_t b = 0; b < nblocks; b++) {
+            const uint64_t n = blocks[b].n_rows, seg_rows = seg_tiles * K.tr;
+            const uint32_t first = (uint32_t)jsegs.size();
+            for (uint64_t r = 0; r < n; r += seg_rows) jsegs.push_back(JitSeg{b, first, r, std::min(n, r + seg_rows)});
+        }
+    }
+    const uint64_t nseg = jsegs.size();
+    const uint64_t grid = std::max<uint64_t>(1, local ? std::min<uint64_t>(G, nonempty) : std::min<uint64_t>(G_split, nseg));
+    bool emit = false;
+    for (uint32_t p = 0; p < nproj; p++) emit |= dp[p].is_utf8;
+
+    // projection rounds: round r decodes the r-th occurrence of every column
+    std::vector<std::vector<uint32_t>> occ(seg->ncols);
+    for (uint32_t p = 0; p < nproj; p++) occ[proj[p]].push_back(p);
+    uint32_t rounds = 1;
+    for (const auto& v : occ) rounds = std::max<uint32_t>(rounds, (uint32_t)v.size());
+    const uint32_t ncols = seg->ncols, npad = (ncols + 1) & ~1u;
+
+    std::vector<DecOut> dout((uint64_t)nblocks * nproj);
+    for (uint64_t i = 0; i < dout.size(); i++)
+        dout[i] = DecOut{(uint8_t*)outs[i].values, outs[i].validity, outs[i].offsets, outs[i].values_cap};
+
+    const uint64_t nbp = (uint64_t)nblocks * nproj;
+    const uint64_t flag_bytes = local || !emit ? 0 : round_up(8 * nu * nseg, 16);  // granules per projection round
+    const uint64_t z_err = 0, z_nulls = kErrBytes, z_lens = z_nulls + 8 * nbp, z_flags = round_up(z_lens + 8 * nbp, 16);
+    const uint64_t zbytes = round_up(z_flags + flag_bytes * rounds, 16);
+    const uint64_t d_blocks = zbytes;
+    const uint64_t d_outs = round_up(d_blocks + sizeof(DecBlock) * nblocks, 16);
+    const uint64_t d_order = round_up(d_outs + sizeof(DecOut) * dout.size(), 16);
+    const uint64_t d_segs = round_up(d_order + 4 * order.size(), 16);
+    const uint64_t d_slots = round_up(d_segs + sizeof(JitSeg) * nseg, 16);
+    const uint64_t d_projc = round_up(d_slots + 2 * (uint64_t)npad * rounds, 16);
+    const uint64_t d_sink = round_up(d_projc + 2 * (uint64_t)nproj, 256);
+    const uint64_t dend = d_sink + 1024;
+    int st = ensure_ws(c, dend, err);
+    if (st) return st;
+    const uint64_t z_lb = z_flags;  // readback: error word, stamps, nulls, lens
+    const uint64_t hz = zbytes <= 65536 ? zbytes : 0;
+    const uint64_t hdesc = d_sink - zbytes, rb = round_up(hz + hdesc, 64);
+    st = ensure_hs(c, rb + z_lb, err);
+    if (st) return st;
+    uint8_t* hd = c->hs + hz;
+    if (hz) std::memset(c->hs, 0, hz);
+    std::memcpy(hd + (d_blocks - zbytes), db.data(), sizeof(DecBlock) * nblocks);
+    std::memcpy(hd + (d_outs - zbytes), dout.data(), sizeof(DecOut) * dout.size());
+    if (!order.empty()) std::memcpy(hd + (d_order - zbytes), order.data(), 4 * order.size());
+    if (nseg) std::memcpy(hd + (d_segs - zbytes), jsegs.data(), sizeof(JitSeg) * nseg);
+    std::vector<uint16_t> slots((uint64_t)npad * rounds, 0xFFFF);
+    for (uint32_t col = 0; col < ncols; col++)
+        for (uint32_t r = 0; r < occ[col].size(); r++) slots[(uint64_t)r * npad + col] = (uint16_t)occ[col][r];
+    std::memcpy(hd + (d_slots - zbytes), slots.data(), 2 * slots.size());
+    for (uint32_t p = 0; p < nproj; p++) ((uint16_t*)(hd + (d_projc - zbytes)))[p] = (uint16_t)proj[p];
+
+    if (!hz) HIPC(hipMemsetAsync(c->ws, 0, zbytes, c->stream));
+    HIPC(hipMemcpyAsync(c->ws + zbytes - hz, c->hs, hz + hdesc, hipMemcpyHostToDevice, c->stream));
+    // Empty blocks: utf8 offsets = [0] (StringBuilder starts with offset 0).
+    for (uint32_t b = 0; b < nblocks; b++)
+        if (blocks[b].n_rows == 0)
+            for (uint32_t p = 0; p < nproj; p++)
+                if (dp[p].is_utf8 && outs[(uint64_t)b * nproj + p].offsets)
+                    HIPC(hipMemsetAsync(outs[(uint64_t)b * nproj + p].offsets, 0, 4, c->stream));
+
+    std::vector<uint8_t> karg(round_up(sizeof(JitArgsHead) + 2 * (uint64_t)npad, 8), 0);
+    JitArgsHead h{};
+    h.blocks = (const DecBlock*)(c->ws + d_blocks);
+    h.outs = (const DecOut*)(c->ws + d_outs);
+    h.order = (const uint32_t*)(c->ws + d_order);
+    h.segs = (const JitSeg*)(c->ws + d_segs);
+    h.projcols = (const uint16_t*)(c->ws + d_projc);
+    h.nulls = (unsigned long long*)(c->ws + z_nulls);
+    h.lens = (unsigned long long*)(c->ws + z_lens);
+    h.err = (unsigned long long*)(c->ws + z_err);
+    h.sink = c->ws + d_sink;
+    h.nseg = nseg;
+    h.emit = emit;
+    h.nblocks = nblocks;
+    h.nproj = nproj;
+    h.norder = (uint32_t)order.size();
+    h.mode = local ? 0 : 1;
+    h.stage = stage;
+    if (verbose)
+        std::fprintf(stderr, "decode launch (jit %ux%u): %s grid %llu (%d/CU, %d split) blocks %llu tiles %llu segments %llu (%llu tiles) rows/tile %u stage %u lds %u rounds %u\n",
+                     K.nw, K.r, local ? "local" : "split", (unsigned long long)grid, bpc, bpc_safe, (unsigned long long)nonempty,
+                     (unsigned long long)tiles, (unsigned long long)nseg, (unsigned long long)seg_tiles, K.tr, stage, lds, rounds);
+    HIPC(hipEventRecord(c->k0, c->stream));
+    if (tiles) {
+        for (uint32_t r = 0; r < rounds; r++) {
+            h.slot_tab = (const uint16_t*)(c->ws + d_slots + 2 * (uint64_t)npad * r);
+            h.abort_word = local || !emit ? nullptr : (unsigned int*)(c->ws + 8);  // read back beside the error word
+            h.flags = (unsigned long long*)(c->ws + z_flags + flag_bytes * r);
+            h.report = r == 0;
+            std::memcpy(karg.data(), &h, sizeof h);
+            std::memcpy(karg.data() + sizeof h, slots.data() + (uint64_t)npad * r, 2 * (uint64_t)npad);
+            HIPC(jit_decode_launch(K, !local, karg.data(), karg.size(), (uint32_t)grid, lds, c->stream));
+        }
+        c->last_kernel = "murr_jit_decode";
+    }
+    HIPC(hipEventRecord(c->k1, c->stream));
+    c->timed = true;
+    HIPC(hipMemcpyAsync(c->hs + rb, c->ws, z_lb, hipMemcpyDeviceToHost, c->stream));
+    c->retry_local = !local && emit && tiles;
+    if (c->retry_local) {
+        c->r_cols.assign(seg->cols, seg->cols + seg->ncols);
+        c->r_seg = *seg;
+        c->r_seg.cols = c->r_cols.data();
+        c->r_proj.assign(proj, proj + nproj);
+        c->r_blocks.assign(blocks, blocks + nblocks);
+        c->r_est = est_row;
+    }
+    return pending_set(c, outs, blocks, nblocks, nproj, dp, rb);
+}
+
+}  // namespace
+
+
 int murr_decode_enqueue(murr_ctx_t* c, const murr_segment_t* seg, const uint32_t* proj,
                         uint32_t nproj, const murr_block_t* blocks, uint32_t nblocks,
                         murr_array_t* outs) {
@@ -454,6 +686,20 @@ int murr_decode_enqueue(murr_ctx_t* c, const murr_segment_t* seg, const uint32_t
         const murr_column_t& col = seg->cols[proj[p]];
         dp[p] = DecProj{col.dtype, col.index, col.offset, col.size, col.dtype == MURR_UTF8, 0};
         if (col.dtype == MURR_UTF8) dp[p].uslot = nutf8++;
+    }
+    for (uint32_t b = 0; b < nblocks; b++) {
+        const murr_block_t& bl = blocks[b];
+        if (bl.n_rows && (!bl.data || !bl.row_off || ((uintptr_t)bl.data & 15)))
+            return MURR_E_ARGUMENT;
+        for (uint32_t p = 0; p < nproj; p++) {
+            const murr_array_t& o = outs[(uint64_t)b * nproj + p];
+            if (bl.n_rows && (!o.validity || !o.values || (dp[p].is_utf8 && !o.offsets)))
+                return MURR_E_ARGUMENT;
+            if (dp[p].is_utf8 && !o.offsets) return MURR_E_ARGUMENT;
+            if (((uintptr_t)o.validity & 7) || (dp[p].dtype == MURR_BOOL && ((uintptr_t)o.values & 7)) ||
+                (!dp[p].is_utf8 && ((uintptr_t)o.values & (dp[p].width - 1))))
+                return MURR_E_ARGUMENT;
+        }
     }
     // Tile shape: NW waves x KC 64-row chunks per wave.  The largest tile whose
     // two LDS buffers (row-offset slice + blob stage, +25 % for row-size
@@ -518,114 +764,48 @@ int murr_decode_enqueue(murr_ctx_t* c, const murr_segment_t* seg, const uint32_t
     if (!found) {  // very wide rows: the smallest ring; fills past the stage go to HBM
         nw = 4; kc = 1; depth = 2; slots = 4; stage = 16384;
     }
-    // Run-time specialised kernel (murr_jit.cpp), the default; the generic
-    // kernel only if it cannot be compiled.  MURR_DECODE_JIT=0 selects the
-    // generic kernel, =1 makes a JIT failure an error.
-    uint32_t nonempty = 0;
-    uint64_t max_rows = 0;
-    for (uint32_t b = 0; b < nblocks; b++) {
-        nonempty += blocks[b].n_rows != 0;
-        max_rows = std::max<uint64_t>(max_rows, blocks[b].n_rows);
-    }
-    const bool verbose = std::getenv("MURR_DECODE_VERBOSE") != nullptr;
-    const JitKernel* jk = nullptr;
+    // Layout-specialised kernel (murr_jit.cpp), the default.  MURR_DECODE_JIT=0
+    // selects the generic kernel; =1 makes a JIT failure an error; otherwise a
+    // layout hiprtc cannot compile falls back to the generic kernel with one
+    // message per process.
     {
         const char* je = std::getenv("MURR_DECODE_JIT");
         const int jmode = je ? std::atoi(je) : -1;
-        // Tile shape from the mean row size (tools/jit_sweep.sh on configs B,
-        // C, D): 5 waves x 2 chunks (512 rows) when its two LDS slots fit
-        // 40 KiB with 15 % slack (four workgroups per CU); else 5 x 1 (256 rows)
-        // within 64 KiB with 8 % slack (two per CU, wide rows); else 3 x 1.
-        JitShape js{3, 1, 0, nutf8, 2, nproj};
-        double slack = 1.15;  // stage bytes over the hinted mean row size
-        auto need = [&](uint32_t nw, uint32_t r, double sl) {
-            const double t = 64.0 * (nw - 1) * r;
-            return 2.0 * (4.0 * (t + 1) + 32 + t * est_row * sl + 64) + 256;
-        };
-        if (need(5, 2, 1.15) <= 40960.0) {
-            js.nw = 5; js.r = 2;
-        } else if (need(5, 1, 1.08) <= 65536.0) {
-            js.nw = 5; js.r = 1; slack = 1.08;
-        }
-        if (const char* e = std::getenv("MURR_JIT_SHAPE"))  // tuning: "NWxR[xSLOTS[xSLACK]]"
-            std::sscanf(e, "%ux%ux%ux%lf", &js.nw, &js.r, &js.slots, &slack);
-        if (js.nw < 2 || js.nw > 16) js.nw = 5;
-        if (js.r < 1 || js.r > 4) js.r = 2;
-        if (js.slots < 2 || js.slots > 4) js.slots = 2;
-        const uint32_t tr = jit_tile_rows(js);
+        uint64_t max_rows = 0;
+        for (uint32_t b = 0; b < nblocks; b++) max_rows = std::max<uint64_t>(max_rows, blocks[b].n_rows);
         if (jmode != 0 && max_rows < 0x7FFFFFFFull) {
-            double st = tr * est_row * slack + 64;
-            if (const char* e = std::getenv("MURR_JIT_STAGE")) st = std::atof(e);  // tuning
-            // every slot within the workgroup's LDS budget (64 KiB; tuning: MURR_JIT_LDS)
-            uint32_t budget = 65536;
-            if (const char* e = std::getenv("MURR_JIT_LDS")) budget = (uint32_t)std::atoi(e);
-            js.stage = 0;
-            const uint32_t smax = ((budget - jit_lds_bytes(js)) / js.slots) & ~1023u;
-            js.stage = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(round_up((uint64_t)st, 1024), 1024), smax);
             std::string why;
-            jk = jit_decode_kernel(c->device, seg->bitset_size, dp.data(), nproj, nutf8, js, &why);
-            if (!jk && (verbose || jmode == 1)) std::fprintf(stderr, "murr: JIT decode unavailable: %s\n", why.c_str());
-            if (!jk && jmode == 1) return MURR_E_INTERNAL;
+            const JitLayout* jl = jit_layout(c->device, seg, &why);
+            if (jl) return decode_enqueue_jit(c, seg, jl, proj, nproj, blocks, nblocks, outs, dp, est_row);
+            if (jmode == 1) {
+                std::fprintf(stderr, "murr: JIT decode unavailable: %s\n", why.c_str());
+                return MURR_E_INTERNAL;
+            }
+            static bool said = false;
+            if (!said) {
+                said = true;
+                std::fprintf(stderr, "murr: JIT decode unavailable, using the generic kernel: %s\n", why.c_str());
+            }
         }
     }
     const uint32_t rows = 64 * kc * (nw - 1);
     const uint64_t R = rows;
     std::vector<DecBlock> db(nblocks);
     uint64_t tiles = 0;
+    uint32_t nonempty = 0;
     for (uint32_t b = 0; b < nblocks; b++) {
-        const murr_block_t& bl = blocks[b];
-        if (bl.n_rows && (!bl.data || !bl.row_off || ((uintptr_t)bl.data & 15)))
-            return MURR_E_ARGUMENT;
-        db[b] = DecBlock{bl.data, bl.row_off, bl.n_rows, tiles};
-        tiles += (bl.n_rows + R - 1) / R;
-        for (uint32_t p = 0; p < nproj; p++) {
-            const murr_array_t& o = outs[(uint64_t)b * nproj + p];
-            if (bl.n_rows && (!o.validity || !o.values || (dp[p].is_utf8 && !o.offsets)))
-                return MURR_E_ARGUMENT;
-            if (dp[p].is_utf8 && !o.offsets) return MURR_E_ARGUMENT;
-            if (((uintptr_t)o.validity & 7) || (dp[p].dtype == MURR_BOOL && ((uintptr_t)o.values & 7)) ||
-                (!dp[p].is_utf8 && ((uintptr_t)o.values & (dp[p].width - 1))))
-                return MURR_E_ARGUMENT;
-        }
+        db[b] = DecBlock{blocks[b].data, blocks[b].row_off, blocks[b].n_rows, tiles};
+        tiles += (blocks[b].n_rows + R - 1) / R;
+        nonempty += blocks[b].n_rows != 0;
     }
+    const bool verbose = std::getenv("MURR_DECODE_VERBOSE") != nullptr;
     std::vector<DecOut> dout((uint64_t)nblocks * nproj);
     for (uint64_t i = 0; i < dout.size(); i++)
         dout[i] = DecOut{(uint8_t*)outs[i].values, outs[i].validity, outs[i].offsets, outs[i].values_cap};
 
     const uint64_t nbp = (uint64_t)nblocks * nproj;
     const uint64_t z_err = 0, z_nulls = kErrBytes, z_lens = z_nulls + 8 * nbp, z_lb = z_lens + 8 * nbp;
-    // JIT segments: a block is one segment (its workgroup walks it whole) unless
-    // there are fewer blocks than CUs; then blocks are cut into runs of seg_tiles
-    // tiles, about one per resident workgroup, and a length pass (murr_jit_lengths)
-    // gives each segment its utf8 starting offsets.
-    std::vector<JitSeg> jsegs;
-    bool split = false;
-    uint64_t jslots = 1;
-    if (jk) {
-        jslots = std::max<uint64_t>(1, (uint64_t)c->cus * jk->bpc);
-        uint64_t jtiles = 0;
-        for (uint32_t b = 0; b < nblocks; b++) jtiles += (blocks[b].n_rows + jk->tr - 1) / jk->tr;
-        const bool cut = nonempty < (uint32_t)c->cus;
-        const char* fixed_tiles = std::getenv("MURR_JIT_SEGTILES");  // tuning: tiles per segment
-        for (uint32_t b = 0; b < nblocks; b++) {
-            const uint64_t n = blocks[b].n_rows;
-            const uint64_t tb = (n + jk->tr - 1) / jk->tr;
-            // equal cuts, about jslots segments over the launch (one round)
-            uint64_t per = tb;
-            if (fixed_tiles) per = std::max(1, std::atoi(fixed_tiles));
-            else if (cut && tb) {
-                const uint64_t ns = std::max<uint64_t>(1, tb * jslots / std::max<uint64_t>(jtiles, 1));
-                per = (tb + ns - 1) / ns;
-            }
-            const uint64_t seg_rows = per * jk->tr;
-            const uint32_t first = (uint32_t)jsegs.size();
-            for (uint64_t r = 0; r < n; r = (n - r > seg_rows ? r + seg_rows : n))
-                jsegs.push_back(JitSeg{b, first, r, n - r > seg_rows ? r + seg_rows : n});
-            split |= jsegs.size() - first > 1;
-        }
-    }
-    const uint64_t nseg = jsegs.size(), nu = std::max<uint32_t>(nutf8, 1);
-    const uint64_t zbytes = round_up(z_lb + (jk ? 8 * nu * nseg : 8 * (uint64_t)nutf8 * tiles), 16);
+    const uint64_t zbytes = round_up(z_lb + 8 * (uint64_t)nutf8 * tiles, 16);
     const uint64_t d_blocks = zbytes, d_proj = round_up(d_blocks + sizeof(DecBlock) * nblocks, 16);
     const uint64_t d_outs = round_up(d_proj + sizeof(DecProj) * nproj, 16);
     DecodeArgs a{};
@@ -641,13 +821,7 @@ int murr_decode_enqueue(murr_ctx_t* c, const murr_segment_t* seg, const uint32_t
     // prefix protocol at all.  Otherwise tiles round-robin + window prefix.
     const bool local = nonempty >= grid || std::getenv("MURR_DECODE_LOCAL") != nullptr;
     if (local) grid = std::max<uint64_t>(1, std::min<uint64_t>(grid, nonempty));
-    if (jk) {  // whole segments per workgroup: equal rounds of segments for every workgroup
-        const uint64_t rounds = std::max<uint64_t>(1, (nseg + jslots - 1) / jslots);
-        grid = std::max<uint64_t>(1, (nseg + rounds - 1) / rounds);
-    }
-    const uint64_t d_order = round_up(d_outs + sizeof(DecOut) * dout.size(), 16);
-    const uint64_t d_sink = round_up(d_order + sizeof(JitSeg) * nseg, 256);
-    const uint64_t d_end_desc = d_sink + (jk ? 1024 : 0);
+    const uint64_t d_end_desc = round_up(d_outs + sizeof(DecOut) * dout.size(), 16);
     const uint64_t dend = d_end_desc;
     int st = ensure_ws(c, dend, err);
     if (st) return st;
@@ -664,7 +838,6 @@ int murr_decode_enqueue(murr_ctx_t* c, const murr_segment_t* seg, const uint32_t
     std::memcpy(hd + (d_blocks - zbytes), db.data(), sizeof(DecBlock) * nblocks);
     std::memcpy(hd + (d_proj - zbytes), dp.data(), sizeof(DecProj) * nproj);
     std::memcpy(hd + (d_outs - zbytes), dout.data(), sizeof(DecOut) * dout.size());
-    if (jk && nseg) std::memcpy(hd + (d_order - zbytes), jsegs.data(), sizeof(JitSeg) * nseg);
 
     if (!hz) HIPC(hipMemsetAsync(c->ws, 0, zbytes, c->stream));
     HIPC(hipMemcpyAsync(c->ws + zbytes - hz, c->hs, hz + hdesc, hipMemcpyHostToDevice, c->stream));
@@ -688,29 +861,11 @@ int murr_decode_enqueue(murr_ctx_t* c, const murr_segment_t* seg, const uint32_t
     a.local = local ? 1 : 0;
     for (uint32_t p = 0, u = 0; p < nproj; p++)
         if (dp[p].is_utf8 && u < 2) a.ufix[u++] = p;
-    if (verbose && jk)
-        std::fprintf(stderr, "decode launch (jit): grid %llu (%d/CU) blocks %u segments %llu%s rows/tile %u lds %u\n",
-                     (unsigned long long)grid, jk->bpc, nonempty, (unsigned long long)nseg,
-                     split && nutf8 ? " (+length pass)" : "", jk->tr, jk->lds);
-    else if (verbose)
+    if (verbose)
         std::fprintf(stderr, "decode launch: grid %llu (%d/CU) tiles %llu shape %ux%u rows/tile %u stage %u slots %u depth %u lds %u local %d\n",
                      (unsigned long long)grid, bpc, (unsigned long long)tiles, nw, kc, rows, a.stage, slots, depth, lds, (int)local);
     HIPC(hipEventRecord(c->k0, c->stream));
-    if (jk && nseg) {
-        JitArgs ja{};
-        ja.blocks = a.blocks;
-        ja.outs = a.outs;
-        ja.segs = (const JitSeg*)(c->ws + d_order);
-        ja.seg_tot = (unsigned long long*)(c->ws + z_lb);
-        ja.nulls = a.nulls;
-        ja.lens = a.lens;
-        ja.err = a.err;
-        ja.sink = c->ws + d_sink;
-        ja.norder = (uint32_t)nseg;
-        if (split && nutf8) HIPC(jit_decode_launch(jk, ja, (uint32_t)grid, c->stream, true));
-        HIPC(jit_decode_launch(jk, ja, (uint32_t)grid, c->stream, false));
-        c->last_kernel = "murr_jit_decode";
-    } else if (tiles) {
+    if (tiles) {
         HIPC(launch_decode(a, nw, kc, (uint32_t)grid, c->stream));
         c->last_kernel = "decode_kernel";
     }
@@ -718,16 +873,7 @@ int murr_decode_enqueue(murr_ctx_t* c, const murr_segment_t* seg, const uint32_t
     c->timed = true;
     HIPC(hipMemcpyAsync(c->hs + rb, c->ws, z_lb, hipMemcpyDeviceToHost, c->stream));
 
-    c->pending = true;
-    c->outs = outs;
-    c->nblocks = nblocks;
-    c->nproj = nproj;
-    c->rb_off = rb;
-    c->n_rows.resize(nblocks);
-    for (uint32_t b = 0; b < nblocks; b++) c->n_rows[b] = blocks[b].n_rows;
-    c->dtypes.resize(nproj);
-    for (uint32_t p = 0; p < nproj; p++) c->dtypes[p] = dp[p].dtype;
-    return MURR_OK;
+    return pending_set(c, outs, blocks, nblocks, nproj, dp, rb);
 }
 
 int murr_decode_wait(murr_ctx_t* c, murr_error_t* err) {
@@ -737,6 +883,33 @@ int murr_decode_wait(murr_ctx_t* c, murr_error_t* err) {
     const uint8_t* rb = c->hs + c->rb_off;
     unsigned long long word;
     std::memcpy(&word, rb, 8);
+    uint32_t aborted = 0;
+    std::memcpy(&aborted, rb + 8, 4);
+    if (c->retry_local && aborted) {
+        // a stream-mode wait timed out (the grid was not co-resident, e.g. a
+        // shared GPU): the same decode in local mode, which never waits
+        c->retry_local = false;
+        static bool said = false;
+        if (!said) {
+            said = true;
+            std::fprintf(stderr, "murr: stream-mode decode timed out; re-running in local mode\n");
+        }
+        std::string why;
+        const JitLayout* jl = jit_layout(c->device, &c->r_seg, &why);
+        std::vector<DecProj> dp(c->r_proj.size());
+        for (size_t p = 0; p < dp.size(); p++) {
+            const murr_column_t& col = c->r_seg.cols[c->r_proj[p]];
+            dp[p] = DecProj{col.dtype, col.index, col.offset, col.size, col.dtype == MURR_UTF8, 0};
+        }
+        const std::vector<uint32_t> proj = c->r_proj;
+        const std::vector<murr_block_t> blocks = c->r_blocks;
+        const int st = jl ? decode_enqueue_jit(c, &c->r_seg, jl, proj.data(), (uint32_t)proj.size(), blocks.data(),
+                                               (uint32_t)blocks.size(), c->outs, dp, c->r_est, true)
+                          : MURR_E_INTERNAL;
+        if (st) return set_err(err, st);
+        return murr_decode_wait(c, err);
+    }
+    c->retry_local = false;
     const uint64_t nbp = (uint64_t)c->nblocks * c->nproj;
     const unsigned long long* nulls = (const unsigned long long*)(rb + kErrBytes);
     if (std::getenv("MURR_DECODE_VERBOSE")) {  // phase stamps of a MURR_ABLATE & 8 build

@@ -20,8 +20,6 @@
 // All integer work; the lookup is latency-bound (query key, slot + location,
 // stored key: three dependent memory round trips per probe), the gather an
 // HBM-bound byte copy.
-#include <cstdlib>
-
 #include "murr_device.h"
 
 namespace murr {
@@ -362,17 +360,10 @@ hipError_t launch_gather(const IndexArgs& a, hipStream_t s) {
         }
     }
     if (a.nq) {
-        // lanes per row (tuning: MURR_GATHER_LANES = 4, 8 or 16; 8 measured best on config C rows)
-        static const int lanes = [] {
-            const char* e = std::getenv("MURR_GATHER_LANES");
-            const int v = e ? std::atoi(e) : 8;
-            return (v == 4 || v == 16) ? v : 8;
-        }();
-        const uint32_t rows_per_wg = 256 / (uint32_t)lanes;
+        // eight lanes per row (measured best of 4 / 8 / 16 on config C rows)
+        constexpr uint32_t rows_per_wg = 256 / 8;
         const dim3 grid((uint32_t)((a.nq + rows_per_wg - 1) / rows_per_wg));
-        if (lanes == 4) hipLaunchKernelGGL(gather_copy<4>, grid, dim3(256), 0, s, a);
-        else if (lanes == 16) hipLaunchKernelGGL(gather_copy<16>, grid, dim3(256), 0, s, a);
-        else hipLaunchKernelGGL(gather_copy<8>, grid, dim3(256), 0, s, a);
+        hipLaunchKernelGGL(gather_copy<8>, grid, dim3(256), 0, s, a);
     }
     return hipGetLastError();
 }

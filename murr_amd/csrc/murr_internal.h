@@ -98,37 +98,46 @@ __host__ __device__ inline uint64_t err_key(uint64_t block, uint64_t row, uint32
     return (block << 46) | (row << 14) | ((uint64_t)(col & 0x3FF) << 4) | (status & 0xF);
 }
 
-// Run-time specialised decode kernel (murr_jit.cpp, murr_jit_kernel.hip).
-struct JitShape {
-    uint32_t nw, r, stage, nutf8;  // waves (nw-1 decode, 1 loads), 64-row chunks per decoding wave, stage bytes
-    uint32_t slots;                // LDS ring slots (tiles in flight + 1)
-    uint32_t nproj;                // projected columns (LDS of kernel variants)
+// Layout-specialised decode kernel (murr_jit.cpp, murr_jit_kernel.hip): one
+// module per segment layout holds every tile shape; the projection is a
+// kernel argument.
+constexpr uint32_t kJitShapes = 3;
+constexpr uint32_t kJitShapeTab[kJitShapes][2] = {{5, 2}, {5, 1}, {3, 1}};  // waves x 64-row chunks per wave
+struct JitShapeK {
+    hipFunction_t fn = nullptr, fn_split = nullptr;  // local / split mode kernels
+    uint32_t nw = 0, r = 0, tr = 0;  // waves (nw-1 decode, 1 loads), chunks per decode wave, rows per tile
 };
-struct JitKernel {
-    hipFunction_t fn, fn_len;      // decode, and the length pass of split blocks
-    uint32_t lds, tr, threads;     // LDS bytes, rows per tile, threads per workgroup
-    int bpc;                       // resident workgroups per CU
+struct JitLayout {
+    JitShapeK shapes[kJitShapes];
+    uint32_t ncols = 0;
 };
-struct JitSeg {                    // = mj::Seg: rows [r_begin, r_end) of block b
+struct JitSeg {                    // = mj::Seg: rows [r_begin, r_end) of block b (split mode)
     uint32_t b, first;             // first: index of the block's first segment
     uint64_t r_begin, r_end;
 };
-struct JitArgs {                   // = mj::Args in murr_jit_kernel.hip
+struct JitArgsHead {               // = mj::Args without its trailing slot[] (murr_jit_kernel.hip)
     const DecBlock* blocks;
-    const DecOut* outs;            // [nblocks * nproj]
-    const JitSeg* segs;            // segments of the non-empty blocks
-    unsigned long long* seg_tot;   // [nseg][max(nutf8, 1)] utf8 bytes per segment
+    const DecOut* outs;            // [nblocks][nproj]
+    const uint32_t* order;         // local mode: non-empty blocks
+    const JitSeg* segs;            // split mode: segments
+    const uint16_t* slot_tab;      // [ncols] output position per column (0xFFFF = not decoded)
+    const uint16_t* projcols;      // [nproj] column per output position
     unsigned long long* nulls;
     unsigned long long* lens;
     unsigned long long* err;
-    uint8_t* sink;                 // >= 1 KiB scratch for inactive lanes' stores
-    uint32_t norder, pad;
+    unsigned long long* flags;     // split mode: [nseg][max(nutf8, 1)] look-back granules
+    uint8_t* sink;
+    uint64_t nseg;
+    uint32_t nblocks, nproj, norder, mode;  // mode: 0 local, 1 split
+    uint32_t stage, report;
+    uint32_t emit, pad1;           // split mode: a second pass writes utf8 cells
+    unsigned int* abort_word;      // split mode: a timed-out wait aborts the launch (zeroed)
 };
-const JitKernel* jit_decode_kernel(int device, uint32_t bs, const DecProj* dp, uint32_t nproj, uint32_t nutf8,
-                                   const JitShape& shape, std::string* why);
-uint32_t jit_tile_rows(const JitShape& s);
-uint32_t jit_lds_bytes(const JitShape& s);
-hipError_t jit_decode_launch(const JitKernel* k, const JitArgs& a, uint32_t grid, hipStream_t s, bool lengths);
+static_assert(sizeof(JitArgsHead) == 136, "mj::Args layout");
+const JitLayout* jit_layout(int device, const murr_segment_t* seg, std::string* why);
+uint32_t jit_lds_bytes(uint32_t nw, uint32_t r, uint32_t stage, uint32_t nutf8);
+hipError_t jit_decode_launch(const JitShapeK& k, bool split, const void* args, size_t bytes, uint32_t grid,
+                             uint32_t lds, hipStream_t s);
 
 // Run-time specialised encode kernel (murr_jit.cpp, murr_jit_encode.hip).
 struct JitEncKernel {

@@ -11,6 +11,10 @@
 #include <hip/hip_runtime.h>
 #include <hip/hiprtc.h>
 
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <map>
@@ -34,56 +38,126 @@ const char* const kJitEncSrc =
 #include "murr_jit_encode_src.inc"
     ;
 
+// ---- code-object cache ----------------------------------------------------------
+//
+// Compiled layouts are kept per (device, prelude) in memory (bounded, least
+// recently used evicted) and on disk, so a process that opens a table whose
+// layout an earlier process compiled loads the code object instead of running
+// hiprtc.  Disk directory: $MURR_JIT_CACHE, else $HOME/.cache/murr ("0" or an
+// unwritable directory disables it).
+
+uint64_t fnv64(const std::string& s, uint64_t h = 0xcbf29ce484222325ull) {
+    for (unsigned char ch : s) h = (h ^ ch) * 0x100000001b3ull;
+    return h;
+}
+
+std::string cache_dir() {
+    const char* e = std::getenv("MURR_JIT_CACHE");
+    if (e) return std::string(e) == "0" ? std::string() : std::string(e);
+    const char* home = std::getenv("HOME");
+    if (!home || !*home) return std::string();
+    return std::string(home) + "/.cache/murr";
+}
+
+bool read_file(const std::string& path, std::vector<char>* out) {
+    FILE* fp = std::fopen(path.c_str(), "rb");
+    if (!fp) return false;
+    char buf[65536];
+    size_t n;
+    out->clear();
+    while ((n = std::fread(buf, 1, sizeof buf, fp)) > 0) out->insert(out->end(), buf, buf + n);
+    std::fclose(fp);
+    return !out->empty();
+}
+
+void write_file_atomic(const std::string& dir, const std::string& name, const std::vector<char>& data) {
+    if (dir.empty()) return;
+    ::mkdir((dir.substr(0, dir.rfind('/'))).c_str(), 0755);
+    ::mkdir(dir.c_str(), 0755);
+    const std::string tmp = dir + "/." + name + "." + std::to_string((long)::getpid());
+    FILE* fp = std::fopen(tmp.c_str(), "wb");
+    if (!fp) return;
+    const bool ok = std::fwrite(data.data(), 1, data.size(), fp) == data.size();
+    std::fclose(fp);
+    if (!ok || std::rename(tmp.c_str(), (dir + "/" + name).c_str()) != 0) std::remove(tmp.c_str());
+}
+
+// hiprtc compile of `src` for gfx950 (or the disk cache's copy of it).
+bool compile_code(const std::string& src, const char* name, std::vector<char>* code, std::string* why) {
+    const char* opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17"};
+    const std::string dir = cache_dir();
+    std::string file;
+    if (!dir.empty()) {
+        char hex[32];
+        std::snprintf(hex, sizeof hex, "%016llx", (unsigned long long)fnv64(src, fnv64(std::string(opts[0]) + opts[1] + opts[2])));
+        file = std::string(name) + "-" + hex + ".co";
+        if (read_file(dir + "/" + file, code)) return true;
+    }
+    hiprtcProgram prog;
+    if (hiprtcCreateProgram(&prog, src.c_str(), name, 0, nullptr, nullptr) != HIPRTC_SUCCESS) {
+        *why = "hiprtcCreateProgram failed";
+        return false;
+    }
+    const hiprtcResult r = hiprtcCompileProgram(prog, 3, opts);
+    if (r != HIPRTC_SUCCESS) {
+        size_t n = 0;
+        hiprtcGetProgramLogSize(prog, &n);
+        std::string log(n + 1, '\0');
+        if (n) hiprtcGetProgramLog(prog, &log[0]);
+        *why = std::string("hiprtc: ") + hiprtcGetErrorString(r) + "\n" + log;
+        hiprtcDestroyProgram(&prog);
+        return false;
+    }
+    size_t n = 0;
+    hiprtcGetCodeSize(prog, &n);
+    code->assign(n, 0);
+    hiprtcGetCode(prog, code->data());
+    hiprtcDestroyProgram(&prog);
+    if (!file.empty()) write_file_atomic(dir, file, *code);
+    return true;
+}
+
+// ---- decode: one module per segment layout ------------------------------------------
+
 struct Entry {
     hipModule_t mod = nullptr;
-    hipFunction_t fn = nullptr;
-    JitKernel k;
+    JitLayout k;
     bool ok = false;
     std::string why;
+    uint64_t used = 0;
 };
 
 std::mutex g_mu;
 std::map<std::string, std::unique_ptr<Entry>> g_cache;
+uint64_t g_clock = 0;
+constexpr size_t kMaxLayouts = 64;
 
-std::string prelude(uint32_t bs, const DecProj* dp, uint32_t nproj, uint32_t nutf8, const JitShape& s) {
+// Evict the least recently used layouts beyond kMaxLayouts (caller holds g_mu).
+void evict() {
+    while (g_cache.size() > kMaxLayouts) {
+        auto victim = g_cache.begin();
+        for (auto it = g_cache.begin(); it != g_cache.end(); ++it)
+            if (it->second->used < victim->second->used) victim = it;
+        if (victim->second->mod) (void)hipModuleUnload(victim->second->mod);
+        g_cache.erase(victim);
+    }
+}
+
+// Prelude: the segment layout (src/io/schema.rs:23-54), nothing of the
+// projection.  MJ_COLS(X) lists every column as X(index, width, row offset of
+// its field, utf8 ordinal); width 0 = utf8 slot, 9 = bool byte.
+std::string prelude(const murr_segment_t* seg) {
     std::ostringstream o;
-    o << "#define MJ_NW " << s.nw << "\n#define MJ_R " << s.r << "\n#define MJ_SLOTS " << s.slots << "\n#define MJ_STAGE " << s.stage
-      << (std::getenv("MURR_JIT_STAMPS") ? "\n#define MJ_STAMPS 1" : "")
-      << (std::getenv("MURR_JIT_RO8") ? "\n#define MJ_RO8 1" : "") << "\n#define MJ_BS " << bs << "\n#define MJ_NPROJ " << nproj << "\n#define MJ_NUTF8 " << nutf8
-      << "\n#define MJ_FIXED_GROUPS";
-    // fixed columns in groups of `group` (loads of a group precede its stores)
-    uint32_t group = 4;
-    if (const char* e = std::getenv("MURR_JIT_GROUP")) group = std::max(1, std::atoi(e));  // tuning
-    for (uint32_t p = 0, inq = 0, ng = 0; p < nproj; p++) {
-        if (dp[p].is_utf8) continue;
-        if (inq == 0) o << (ng++ ? ">, G<" : " G<");
-        else o << ", ";
-        o << "FC<" << p << ", " << (dp[p].dtype == MURR_BOOL ? 0u : dp[p].width) << ", " << bs + dp[p].offset << ", "
-          << dp[p].bit << ">";
-        if (++inq == group) inq = 0;
+    uint32_t nu = 0;
+    for (uint32_t c = 0; c < seg->ncols; c++) nu += seg->cols[c].dtype == MURR_UTF8;
+    o << "#define MJ_BS " << seg->bitset_size << "\n#define MJ_FIX " << seg->bitset_size + seg->capacity
+      << "\n#define MJ_NCOLS " << seg->ncols << "\n#define MJ_NUTF8 " << nu << "\n#define MJ_COLS(X)";
+    for (uint32_t c = 0, u = 0; c < seg->ncols; c++) {
+        const murr_column_t& col = seg->cols[c];
+        const uint32_t w = col.dtype == MURR_UTF8 ? 0u : col.dtype == MURR_BOOL ? 9u : col.size;
+        o << " X(" << col.index << ", " << w << ", " << seg->bitset_size + col.offset << ", "
+          << (w == 0 ? u++ : 0u) << ")";
     }
-    {
-        bool any = false;
-        for (uint32_t p = 0; p < nproj; p++) any |= !dp[p].is_utf8;
-        if (any) o << ">";
-    }
-    o << "\n#define MJ_UTF8_COLS";
-    for (uint32_t p = 0, u = 0; p < nproj; p++)
-        if (dp[p].is_utf8) o << (u ? ", " : " ") << "UC<" << p << ", " << u++ << ", " << bs + dp[p].offset << ", " << dp[p].bit << ">";
-    o << "\n#define MJ_FIXED(X)";
-    for (uint32_t p = 0; p < nproj; p++)
-        if (!dp[p].is_utf8)
-            o << " X(" << p << ", " << (dp[p].dtype == MURR_BOOL ? 0u : dp[p].width) << ", " << bs + dp[p].offset
-              << ", " << dp[p].bit << ")";
-    o << "\n#define MJ_UTF8(X)";
-    for (uint32_t p = 0, u = 0; p < nproj; p++)
-        if (dp[p].is_utf8) o << " X(" << p << ", " << u++ << ", " << bs + dp[p].offset << ", " << dp[p].bit << ")";
-    o << "\n#define MJ_COL_FO";
-    for (uint32_t p = 0; p < nproj; p++) o << (p ? ", " : " ") << bs + dp[p].offset;
-    o << "\n#define MJ_COL_BIT";
-    for (uint32_t p = 0; p < nproj; p++) o << (p ? ", " : " ") << dp[p].bit;
-    o << "\n#define MJ_COL_WID";
-    for (uint32_t p = 0; p < nproj; p++) o << (p ? ", " : " ") << (dp[p].is_utf8 ? 0u : dp[p].width);
     o << "\n";
     // tuning: MURR_JIT_DEFS="NAME=VALUE,..." extra #defines (ablation builds)
     if (const char* e = std::getenv("MURR_JIT_DEFS")) {
@@ -104,95 +178,78 @@ std::string prelude(uint32_t bs, const DecProj* dp, uint32_t nproj, uint32_t nut
 // The kernel source: embedded, or (tuning) the file MURR_JIT_SRC names.
 std::string kernel_source() {
     if (const char* f = std::getenv("MURR_JIT_SRC")) {
-        if (FILE* fp = std::fopen(f, "rb")) {
-            std::string t;
-            char buf[65536];
-            size_t n;
-            while ((n = std::fread(buf, 1, sizeof buf, fp)) > 0) t.append(buf, n);
-            std::fclose(fp);
-            return t;
-        }
+        std::vector<char> t;
+        if (read_file(f, &t)) return std::string(t.begin(), t.end());
     }
     return kJitSrc;
 }
 
-bool compile(Entry& e, const std::string& pre, int device, const JitShape& s) {
-    const std::string src = pre + kernel_source();
-    hiprtcProgram prog;
-    if (hiprtcCreateProgram(&prog, src.c_str(), "murr_jit_decode.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS) {
-        e.why = "hiprtcCreateProgram failed";
-        return false;
-    }
-    const char* opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17"};
-    const hiprtcResult r = hiprtcCompileProgram(prog, 3, opts);
-    if (r != HIPRTC_SUCCESS) {
-        size_t n = 0;
-        hiprtcGetProgramLogSize(prog, &n);
-        std::string log(n + 1, '\0');
-        if (n) hiprtcGetProgramLog(prog, &log[0]);
-        e.why = std::string("hiprtc: ") + hiprtcGetErrorString(r) + "\n" + log;
-        hiprtcDestroyProgram(&prog);
-        return false;
-    }
-    size_t n = 0;
-    hiprtcGetCodeSize(prog, &n);
-    std::vector<char> code(n);
-    hiprtcGetCode(prog, code.data());
-    hiprtcDestroyProgram(&prog);
+bool compile(Entry& e, const std::string& pre, int device) {
+    std::vector<char> code;
+    if (!compile_code(pre + kernel_source(), "murr_jit_decode", &code, &e.why)) return false;
     int cur = 0;
-    hipGetDevice(&cur);
-    hipSetDevice(device);
+    (void)hipGetDevice(&cur);
+    (void)hipSetDevice(device);
     hipError_t he = hipModuleLoadData(&e.mod, code.data());
-    if (he == hipSuccess) he = hipModuleGetFunction(&e.fn, e.mod, "murr_jit_decode");
-    if (he == hipSuccess) he = hipModuleGetFunction(&e.k.fn_len, e.mod, "murr_jit_lengths");
+    for (uint32_t s = 0; s < kJitShapes && he == hipSuccess; s++) {
+        JitShapeK& k = e.k.shapes[s];
+        k.nw = kJitShapeTab[s][0];
+        k.r = kJitShapeTab[s][1];
+        k.tr = 64 * (k.nw - 1) * k.r;
+        const std::string name = "murr_jit_decode_" + std::to_string(k.nw) + "x" + std::to_string(k.r);
+        he = hipModuleGetFunction(&k.fn, e.mod, name.c_str());
+        if (he == hipSuccess)
+            he = hipModuleGetFunction(&k.fn_split, e.mod,
+                                      ("murr_jit_decode_split_" + std::to_string(k.nw) + "x" + std::to_string(k.r)).c_str());
+    }
+    (void)hipSetDevice(cur);
     if (he != hipSuccess) {
         e.why = std::string("module load: ") + hipGetErrorString(he);
-        hipSetDevice(cur);
         return false;
     }
-    const uint32_t tr = jit_tile_rows(s);
-    e.k.lds = jit_lds_bytes(s);
-    e.k.tr = tr;
-    e.k.threads = 64 * s.nw;
-    int bpc = 0;
-    if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, e.fn, e.k.threads, e.k.lds) != hipSuccess || bpc < 1)
-        bpc = 1;
-    e.k.bpc = bpc;
-    e.k.fn = e.fn;
-    hipSetDevice(cur);
     return true;
 }
 
 }  // namespace
 
-// Rows per tile and LDS bytes of a shape (murr_jit_kernel.hip TR, LDS_TOTAL):
-// NW-1 consumer waves x R chunks of 64 rows; two slots [row offsets | stage],
-// the span ring and the consumers' utf8 wave totals.
-uint32_t jit_tile_rows(const JitShape& s) { return 64 * (s.nw - 1) * s.r; }
-uint32_t jit_lds_bytes(const JitShape& s) {
-    const uint32_t ro8 = std::getenv("MURR_JIT_RO8") ? 2 : 1;  // tuning: unpacked row offsets
-    const uint32_t ro = ((jit_tile_rows(s) + 1) * 4 * ro8 + 16 + 15) & ~15u;
-    const uint32_t wt = (4 * std::max<uint32_t>(s.nutf8, 1) * (s.nw - 1) + 15) & ~15u;
-    return s.slots * (ro + s.stage + 64) + 128 + 16 + wt;
+// LDS bytes of a shape (murr_jit_kernel.hip Shape): two ring slots [row
+// offsets | stage], the span and tile rings, counters, tile prefixes, the
+// decode waves' utf8 totals and the loader's 1 KiB prefetch scratch.
+uint32_t jit_lds_bytes(uint32_t nw, uint32_t r, uint32_t stage, uint32_t nutf8) {
+    const uint32_t tr = 64 * (nw - 1) * r;
+    const uint32_t ro = ((tr + 1) * 4 + 16 + 15) & ~15u;
+    const uint32_t nu = std::max<uint32_t>(nutf8, 1);
+    return 2 * (ro + stage + 64) + 128 + 256 + 16 + 8 * nu + ((4 * nu * (nw - 1) + 15) & ~15u) + 1024;
 }
 
-const JitKernel* jit_decode_kernel(int device, uint32_t bs, const DecProj* dp, uint32_t nproj, uint32_t nutf8,
-                                   const JitShape& shape, std::string* why) {
-    const std::string pre = prelude(bs, dp, nproj, nutf8, shape);
+const JitLayout* jit_layout(int device, const murr_segment_t* seg, std::string* why) {
+    const std::string pre = prelude(seg);
     const char* srcf = std::getenv("MURR_JIT_SRC");
     const std::string key = std::to_string(device) + "\n" + (srcf ? srcf : "") + "\n" + pre;
     std::lock_guard<std::mutex> lk(g_mu);
     auto it = g_cache.find(key);
     if (it == g_cache.end()) {
         auto e = std::make_unique<Entry>();
-        e->ok = compile(*e, pre, device, shape);
+        e->ok = compile(*e, pre, device);
+        e->k.ncols = seg->ncols;
         it = g_cache.emplace(key, std::move(e)).first;
+        evict();
+        it = g_cache.find(key);
     }
+    it->second->used = ++g_clock;
     if (!it->second->ok) {
         if (why) *why = it->second->why;
         return nullptr;
     }
     return &it->second->k;
+}
+
+hipError_t jit_decode_launch(const JitShapeK& k, bool split, const void* args, size_t bytes, uint32_t grid,
+                             uint32_t lds, hipStream_t s) {
+    size_t sz = bytes;
+    void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, const_cast<void*>(args), HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz,
+                   HIP_LAUNCH_PARAM_END};
+    return hipModuleLaunchKernel(split ? k.fn_split : k.fn, grid, 1, 1, 64 * k.nw, 1, 1, lds, s, nullptr, cfg);
 }
 
 // ---- encode ------------------------------------------------------------------
@@ -232,41 +289,23 @@ const JitEncKernel* jit_encode_kernel(int device, uint32_t bs, uint32_t cap, con
     auto it = g_enc.find(key);
     if (it == g_enc.end()) {
         auto e = std::make_unique<EncEntry>();
-        const std::string src = pre + kJitEncSrc;
-        hiprtcProgram prog;
-        const char* opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17"};
-        if (hiprtcCreateProgram(&prog, src.c_str(), "murr_jit_encode.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS) {
-            e->why = "hiprtcCreateProgram failed";
-        } else {
-            const hiprtcResult r = hiprtcCompileProgram(prog, 3, opts);
-            if (r != HIPRTC_SUCCESS) {
-                size_t n = 0;
-                hiprtcGetProgramLogSize(prog, &n);
-                std::string log(n + 1, '\0');
-                if (n) hiprtcGetProgramLog(prog, &log[0]);
-                e->why = std::string("hiprtc: ") + hiprtcGetErrorString(r) + "\n" + log;
-            } else {
-                size_t n = 0;
-                hiprtcGetCodeSize(prog, &n);
-                std::vector<char> code(n);
-                hiprtcGetCode(prog, code.data());
-                int cur = 0;
-                (void)hipGetDevice(&cur);
-                (void)hipSetDevice(device);
-                hipError_t he = hipModuleLoadData(&e->mod, code.data());
-                if (he == hipSuccess) he = hipModuleGetFunction(&e->k.fn, e->mod, "murr_jit_encode");
-                if (he == hipSuccess) he = hipModuleGetFunction(&e->k.fn_sizes, e->mod, "murr_jit_encode_sizes");
-                if (he == hipSuccess) he = hipModuleGetFunction(&e->k.fn_scan, e->mod, "murr_jit_encode_scan");
-                int bpc = 0;
-                if (he == hipSuccess &&
-                    (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, e->k.fn, 256, 0) != hipSuccess || bpc < 1))
-                    bpc = 1;
-                e->k.bpc = bpc;
-                if (he != hipSuccess) e->why = std::string("module load: ") + hipGetErrorString(he);
-                e->ok = he == hipSuccess;
-                (void)hipSetDevice(cur);
-            }
-            hiprtcDestroyProgram(&prog);
+        std::vector<char> code;
+        if (compile_code(pre + kJitEncSrc, "murr_jit_encode", &code, &e->why)) {
+            int cur = 0;
+            (void)hipGetDevice(&cur);
+            (void)hipSetDevice(device);
+            hipError_t he = hipModuleLoadData(&e->mod, code.data());
+            if (he == hipSuccess) he = hipModuleGetFunction(&e->k.fn, e->mod, "murr_jit_encode");
+            if (he == hipSuccess) he = hipModuleGetFunction(&e->k.fn_sizes, e->mod, "murr_jit_encode_sizes");
+            if (he == hipSuccess) he = hipModuleGetFunction(&e->k.fn_scan, e->mod, "murr_jit_encode_scan");
+            int bpc = 0;
+            if (he == hipSuccess &&
+                (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, e->k.fn, 256, 0) != hipSuccess || bpc < 1))
+                bpc = 1;
+            e->k.bpc = bpc;
+            if (he != hipSuccess) e->why = std::string("module load: ") + hipGetErrorString(he);
+            e->ok = he == hipSuccess;
+            (void)hipSetDevice(cur);
         }
         it = g_enc.emplace(key, std::move(e)).first;
     }
@@ -302,13 +341,6 @@ hipError_t jit_encode_launch(const JitEncKernel* k, const EncodeArgs& a, uint32_
         grid = tiles;  // no co-resident grid needed: a workgroup per tile
     }
     return hipModuleLaunchKernel(k->fn, grid, 1, 1, 256, 1, 1, 0, s, nullptr, cfg);
-}
-
-hipError_t jit_decode_launch(const JitKernel* k, const JitArgs& a, uint32_t grid, hipStream_t s, bool lengths) {
-    JitArgs args = a;
-    size_t sz = sizeof(args);
-    void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &args, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
-    return hipModuleLaunchKernel(lengths ? k->fn_len : k->fn, grid, 1, 1, k->threads, 1, 1, k->lds, s, nullptr, cfg);
 }
 
 }  // namespace murr

@@ -1,9 +1,11 @@
-// murr_jit_kernel.hip — schema-specialised decode kernel, compiled at run time
-// (hiprtc, gfx950) once per (segment layout, projection, tile shape) and
-// cached by the context (murr_jit.cpp).  The host prepends a prelude of
-// #defines (MJ_*) that fixes the bitset size, every projected column's kind,
-// field offset and null bit, and the tile shape, so the per-row code is
-// straight-line: no descriptor loads, no dtype dispatch, no column loops.
+// murr_jit_kernel.hip — layout-specialised decode kernel, compiled at run time
+// (hiprtc, gfx950) once per segment layout and cached by murr_jit.cpp (in
+// memory and on disk).  The host prepends a prelude of #defines (MJ_*) that
+// fixes the bitset size, the fixed row size and every column's kind, field
+// offset and utf8 ordinal.  The projection is a run-time argument: a column
+// is decoded when args.slot[c] names its output position, so every
+// projection of a table runs the same code object (no compile on the read
+// path).
 //
 // Same contract as the generic decode kernel (murr_decode.hip) and the
 // reference path it replaces: ReadBatchBuilder::add_row / add_empty / build
@@ -11,16 +13,29 @@
 // src/io/codec/primitive.rs:38-61, bool_.rs:85-104, utf8.rs:85-105);
 // bit-exact Arrow buffers (arrow-rs 58 builder layout).
 //
-// Shape (block-local): a persistent workgroup of MJ_NW waves owns whole
-// blocks (order[w], order[w+G], ...) and walks each block in tiles of
-// TR = 64*MJ_NW*MJ_R rows.  Tile i+1's row-offset slice and blob span stream
-// into the other half of a two-slot LDS ring (global_load_lds_dwordx4, 1 KiB
-// per wave-instruction) while tile i is decoded; tile i+2's span (two u64 row
-// offsets) is fetched a tile ahead, so the only dependent HBM round trip per
-// tile is hidden behind a whole tile of work.  One lane decodes one row per
-// 64-row chunk; wave w owns rows [w*64*R, (w+1)*64*R) of the tile.  The utf8
-// offset prefix is the workgroup's running sum over its block (no cross-
-// workgroup protocol): a DPP wave scan per chunk, wave totals through LDS.
+// Shape: a workgroup of NW waves; NC = NW - 1 decode waves, the last wave only
+// loads.  Tiles of TR = 64 * NC * R rows stream through an LDS ring of two
+// slots (row-offset slice + blob span by global_load_lds, 1 KiB per
+// wave-instruction); one lane decodes one row of a 64-row chunk.  Per row the
+// bitset and the static region are read once as aligned dwords and realigned
+// to the row (v_alignbyte), so every field is a compile-time register pick.
+// Validity and bool words are ballots stashed in lane c of a VGPR and stored
+// by one instruction per chunk for all columns.
+//
+// Two work modes (args.mode):
+//  * local: a workgroup owns whole blocks (the launch has at least as many
+//    blocks as workgroups); the utf8 offset prefix is a running sum in SGPRs.
+//  * split: few blocks.  Blocks are cut into segments of a few tiles, dealt
+//    round-robin over a co-resident grid (segment s -> workgroup s mod G).  A
+//    workgroup streams a segment twice: the first pass decodes the fixed-width
+//    columns and validity and sums the utf8 lengths; a decoupled look-back
+//    over the segments before it (one 8-byte {status, value} granule per
+//    segment and utf8 column) gives the segment's utf8 starting offsets; the
+//    second pass re-reads the segment -- about G segments ago, so it is still
+//    in the 256 MiB Infinity Cache -- and writes offsets and strings.  HBM sees
+//    the blobs once.  Every wait is bounded in time; one that expires aborts
+//    the launch and the host re-runs it in local mode, so a grid that was not
+//    co-resident costs time, never a hang.
 //
 // Malformed rows (the reference panics) are flagged in the fast path and
 // reported exactly, in row-major / projection order, by a cold path.  Errors
@@ -54,7 +69,13 @@ struct Blk {  // = murr::DecBlock
     const uint8_t* data;
     const uint64_t* row_off;
     uint64_t n_rows;
-    uint64_t tile_base;
+    uint64_t tile_base;  // first global tile of this block (stream mode)
+};
+// A segment: rows [r_begin, r_end) of block b (split mode); `first` is the
+// index of the block's first segment.
+struct Seg {  // = murr::JitSeg
+    uint32_t b, first;
+    uint64_t r_begin, r_end;
 };
 struct Out {  // = murr::DecOut
     uint8_t* values;
@@ -62,53 +83,51 @@ struct Out {  // = murr::DecOut
     int32_t* offsets;
     uint64_t values_cap;
 };
-// A segment: rows [r_begin, r_end) of block b, decoded by one workgroup.  A
-// block is one segment unless the launch has fewer blocks than CUs; then its
-// segments' utf8 byte counts come from a length pass (murr_jit_lengths) and
-// segment k starts at the sum over segments first .. k-1 of its block.
-struct Seg {
-    uint32_t b, first;
-    uint64_t r_begin, r_end;
-};
+constexpr uint32_t NCOLS = MJ_NCOLS, BS = MJ_BS, FIX = MJ_FIX, NUTF8 = MJ_NUTF8;
+constexpr uint32_t NU = NUTF8 ? NUTF8 : 1;
+constexpr uint32_t NCW = (NCOLS + 63) / 64;  // 64-column lane groups
 struct Args {
     const Blk* blocks;
-    const Out* outs;          // [nblocks][MJ_NPROJ]
-    const void* segs;         // Seg[norder]: row ranges of non-empty blocks, in launch order
-    unsigned long long* seg_tot;  // [norder][NU] utf8 bytes per segment (length pass)
-    unsigned long long* nulls;  // [nblocks][MJ_NPROJ]
-    unsigned long long* lens;   // [nblocks][MJ_NPROJ] utf8 data bytes
-    unsigned long long* err;    // max of ~key
+    const Out* outs;              // [nblocks][nproj]
+    const uint32_t* order;        // local mode: non-empty blocks in launch order
+    const void* segs;             // split mode: Seg[nseg]
+    const uint16_t* slot_tab;     // = slot[], in memory (per-lane reads)
+    const uint16_t* projcols;     // [nproj]: segment column of projection position p
+    unsigned long long* nulls;    // [nblocks][nproj]
+    unsigned long long* lens;     // [nblocks][nproj] utf8 data bytes
+    unsigned long long* err;      // max of ~key
+    unsigned long long* flags;    // split mode: [nseg][NU] look-back granules
     uint8_t* sink;
-    uint32_t norder, pad;
+    uint64_t nseg;                // split mode: segments
+    uint32_t nblocks, nproj, norder, mode;
+    uint32_t stage;               // stage bytes per ring slot (multiple of 1 KiB)
+    uint32_t report;              // report malformed rows (the first projection round)
+    uint32_t emit, pad1;          // split mode: some utf8 column is projected (second pass)
+    unsigned int* abort_word;     // split mode: set when a wait timed out (every wait then gives up)
+    uint16_t slot[(NCOLS + 1) & ~1u];  // output position of column c, 0xFFFF = not decoded
 };
+constexpr uint16_t kNone = 0xFFFF;
 
-// MJ_NW waves: NC = MJ_NW - 1 consumers decode, the last wave only loads.
-constexpr uint32_t NW = MJ_NW, NC = MJ_NW - 1, R = MJ_R, TR = 64 * NC * MJ_R, BS = MJ_BS, NPROJ = MJ_NPROJ,
-                   NUTF8 = MJ_NUTF8, STAGE = MJ_STAGE;
-// LDS slot: [row offsets (TR+1)*8 + 16][blob stage STAGE + 64 pad]
-// Row offsets are staged packed: the low dword of each u64 (a gather DMA),
-// 4 B per row; tiles never span 4 GiB of blob bytes.  MJ_RO8 (tuning): stage
-// the u64 slice as is, 1 KiB per DMA instruction.
-#ifndef MJ_RO8
-#define MJ_RO8 0
-#endif
-constexpr uint32_t RO_W = MJ_RO8 ? 2 : 1;  // dwords per staged row offset
-constexpr uint32_t RO_BYTES = ((TR + 1) * 4 * RO_W + 16 + 15) & ~15u;
-constexpr uint32_t SLOT = RO_BYTES + STAGE + 64;
-constexpr uint32_t ST_PIECES = STAGE / 1024;
-#ifndef MJ_SLOTS
-#define MJ_SLOTS 3
-#endif
-constexpr uint32_t NSLOT = MJ_SLOTS;                    // LDS ring slots (tiles in flight + 1)
-static_assert(NSLOT >= 2 && NSLOT <= 4, "2..4 slots");
-constexpr uint32_t LDS_SPAN = NSLOT * SLOT;             // [8][16 B] tile spans
-constexpr uint32_t LDS_CNT = LDS_SPAN + 128;
-constexpr uint32_t LDS_WT = LDS_CNT + 16;              // [NUTF8][NC] u32 wave totals
-constexpr uint32_t LDS_TOTAL = LDS_WT + 4 * (NUTF8 ? NUTF8 : 1) * NC;
-static_assert(STAGE % 1024 == 0, "stage is whole 1 KiB pieces");
-
-constexpr uint32_t NU = NUTF8 ? NUTF8 : 1;
 enum : uint32_t { kStUtf8 = 1, kStOverflow = 4, kStMalformed = 5, kStCapacity = 6, kStInternal = 10 };
+// Phase stamps of tuning builds (MURR_JIT_DEFS=MJ_STAMPS): shader cycles
+// summed over waves into err[2 + k] (murr_abi.cpp prints them with
+// MURR_DECODE_VERBOSE).  k: 0 decode-wave tile barrier, 1 wave-total wait,
+// 2 segment-prefix wait, 3 look-back, 4 first-pass tiles, 5 second-pass
+// tiles, 6 local tiles, 7 loader waits, 8 loader total, 9 decode-wave total.
+#ifdef MJ_STAMPS
+#define MJ_TIC const uint64_t mj_t0_ = __builtin_amdgcn_s_memtime();
+#define MJ_TOC(k)                                                                                             \
+    if (lane_id() == 0)                                                                                       \
+        __hip_atomic_fetch_add((GAS unsigned long long*)args()->err + 2 + (k),                              \
+                               (unsigned long long)(__builtin_amdgcn_s_memtime() - mj_t0_), __ATOMIC_RELAXED, \
+                               __HIP_MEMORY_SCOPE_AGENT);
+#else
+#define MJ_TIC
+#define MJ_TOC(k)
+#endif
+
+// Waits are bounded in wall time (s_memrealtime, 100 MHz): 50 ms.
+constexpr uint64_t kWaitTicks = 5000000;
 
 DEV uint64_t err_key(uint64_t block, uint64_t row, uint32_t col, uint32_t status) {
     if (row > 0xFFFFFFFFull) row = 0xFFFFFFFFull;
@@ -123,10 +142,44 @@ template <class T> DEV GAS T* gp(T* p) { return (GAS T*)p; }
 template <class T> DEV const GAS T* gp(const T* p) { return (const GAS T*)p; }
 DEV uint32_t sgpr(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 DEV uint64_t sgpr64(uint64_t v) { return ((uint64_t)sgpr((uint32_t)(v >> 32)) << 32) | sgpr((uint32_t)v); }
-DEV uint32_t lane_id() {
-    uint32_t t = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
-    return t;
+// by value (HIP's min/max of mixed temporaries bind references, which ends
+// up as a stack slot)
+DEV uint64_t umin64(uint64_t a, uint64_t b) { return a < b ? a : b; }
+DEV uint32_t umin32(uint32_t a, uint32_t b) { return a < b ? a : b; }
+DEV uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
+DEV const CAS Args* args() {
+    const CAS Args* ap = (const CAS Args*)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(ap));
+    return ap;
 }
+// Output position of column c (compile-time c): one scalar dword load of the
+// kernel arguments (a 16-bit load would be a vector load and a vmcnt wait).
+DEV uint32_t slot_of(uint32_t c) {
+    const CAS uint32_t* w = (const CAS uint32_t*)args()->slot;
+    return (w[c >> 1] >> (16 * (c & 1))) & 0xFFFFu;
+}
+
+// A bounded wait.  `expired()` once the deadline passed or another wave of
+// the launch gave up (the abort word; stream mode only), after reporting.
+struct Wait {
+    uint64_t t0 = 0;
+    uint32_t n = 0;
+    DEV bool expired(uint64_t block, uint64_t row) {
+        __builtin_amdgcn_s_sleep(1);
+        if ((++n & 63) != 1) return false;
+        const uint64_t now = __builtin_amdgcn_s_memrealtime();
+        if (n == 1) t0 = now;
+        unsigned int* ab = args()->abort_word;
+        const bool late = now - t0 > kWaitTicks;
+        const bool gave_up = ab && __hip_atomic_load((const GAS unsigned int*)ab, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (!late && !gave_up) return false;
+        if (late) {
+            report(args()->err, err_key(block, row, 0, kStInternal));
+            if (ab) __hip_atomic_store((GAS unsigned int*)ab, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        return true;
+    }
+};
 
 // Wave64 inclusive scan on DPP (row_shr 1/2/4/8, row_bcast 15/31).
 DEV uint32_t wave_scan(uint32_t v) {
@@ -162,6 +215,18 @@ struct Utf8Dfa {
     DEV bool ok() const { return !bad && need == 0; }
 };
 
+// ---- layout tables (cold paths, run-time column index) ----------------------
+constexpr uint32_t kColFo[NCOLS] = {
+#define MJ_X(C, W, FO, U) FO,
+    MJ_COLS(MJ_X)
+#undef MJ_X
+};
+constexpr uint32_t kColW[NCOLS] = {  // 0 = utf8, 9 = bool
+#define MJ_X(C, W, FO, U) W,
+    MJ_COLS(MJ_X)
+#undef MJ_X
+};
+
 // ---- byte sources ------------------------------------------------------------
 // Tile bytes staged in LDS (hot path).  Aligned dword reads + v_alignbyte (an
 // unaligned ds_read_b32 is correct on gfx950 but far slower).  Reads are
@@ -171,38 +236,29 @@ struct StageSrc {
     static constexpr bool kHbm = false;
     const LAS uint8_t* s;
     DEV uint32_t u8(uint32_t a) const { return s[a]; }
+    DEV uint32_t w(uint32_t a4) const { return ((const LAS uint32_t*)s)[a4]; }  // aligned dword a4
     DEV uint32_t u32(uint32_t a) const {
-        const LAS uint32_t* w = (const LAS uint32_t*)(s + (a & ~3u));
-        return __builtin_amdgcn_alignbyte(w[1], w[0], a & 3u);
+        const LAS uint32_t* p = (const LAS uint32_t*)(s + (a & ~3u));
+        return __builtin_amdgcn_alignbyte(p[1], p[0], a & 3u);
     }
-    DEV uint32_t u16(uint32_t a) const { return u32(a) & 0xFFFFu; }
-    DEV uint64_t u64(uint32_t a) const {
-        const LAS uint32_t* w = (const LAS uint32_t*)(s + (a & ~3u));
-        const uint32_t sh = a & 3u, w0 = w[0], w1 = w[1], w2 = w[2];
-        return (uint64_t)__builtin_amdgcn_alignbyte(w1, w0, sh) |
-               ((uint64_t)__builtin_amdgcn_alignbyte(w2, w1, sh) << 32);
-    }
-    // three aligned dwords covering [a & ~3, (a & ~3) + 12)
     DEV void win3(uint32_t a, uint32_t& w0, uint32_t& w1, uint32_t& w2) const {
-        const LAS uint32_t* w = (const LAS uint32_t*)(s + (a & ~3u));
-        w0 = w[0]; w1 = w[1]; w2 = w[2];
+        const LAS uint32_t* p = (const LAS uint32_t*)(s + (a & ~3u));
+        w0 = p[0]; w1 = p[1]; w2 = p[2];
     }
 };
-// A tile whose span outgrew the stage is decoded from HBM: exact-width
-// unaligned loads, never a byte past the field; unwanted reads are pointed at
-// the tile's first byte by the caller (at()).
+// A tile whose span outgrew the stage is decoded from HBM: aligned dword loads
+// that never leave the row's own dwords (callers point unwanted reads at the
+// tile's first byte).
 struct HbmSrc {
     static constexpr bool kHbm = true;
     const GAS uint8_t* g;
     DEV uint32_t u8(uint32_t a) const { return g[a]; }
-    DEV uint32_t u16(uint32_t a) const { return *(const GAS u16u*)(g + a); }
+    DEV uint32_t w(uint32_t a4) const { return ((const GAS uint32_t*)g)[a4]; }
     DEV uint32_t u32(uint32_t a) const { return *(const GAS u32u*)(g + a); }
-    DEV uint64_t u64(uint32_t a) const { return *(const GAS u64u*)(g + a); }
 };
-template <class Src> DEV uint32_t at(bool ok, uint32_t a) { return Src::kHbm && !ok ? 0u : a; }
 
 // ---- LDS-DMA (inline asm: kept out of the compiler's waitcnt bookkeeping;
-// every wave drains its own with vmcnt(0) before the tile barrier) ----------
+// the loader wave waits for exactly its own DMA with counted vmcnt) ----------
 DEV void glds16(const GAS void* src, LAS void* dst) {
     uint32_t keep;
     asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
@@ -210,48 +266,6 @@ DEV void glds16(const GAS void* src, LAS void* dst) {
                  : "v"(src), "s"(__builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)dst))
                  : "memory");
 }
-DEV void tile_barrier() { asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
-DEV void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
-
-// ---- the workgroup's tile cursor (wave-uniform, every wave keeps a copy) -----
-struct Cur {
-    const uint8_t* data;
-    const uint64_t* row_off;
-    uint64_t n_rows, r0, r_begin, r_end;
-    uint32_t k, b, first, ok;
-};
-DEV const Args* args() {
-    const CAS Args* ap = (const CAS Args*)__builtin_amdgcn_kernarg_segment_ptr();
-    asm volatile("" : "+s"(ap));
-    return (const Args*)ap;
-}
-DEV void cur_load(Cur& c, uint32_t k) {
-    const CAS Args* A = (const CAS Args*)args();
-    c.k = sgpr(k);
-    c.ok = c.k < A->norder;
-    if (!c.ok) return;
-    const CAS Seg* sp = (const CAS Seg*)A->segs + c.k;
-    c.b = sgpr(sp->b);
-    c.first = sgpr(sp->first);
-    c.r_begin = sgpr64(sp->r_begin);
-    c.r_end = sgpr64(sp->r_end);
-    c.r0 = c.r_begin;
-    const CAS Blk* bp = (const CAS Blk*)A->blocks + c.b;
-    c.data = (const uint8_t*)sgpr64((uint64_t)bp->data);
-    c.row_off = (const uint64_t*)sgpr64((uint64_t)bp->row_off);
-    c.n_rows = sgpr64(bp->n_rows);
-}
-DEV void cur_next(Cur& c) {
-    if (!c.ok) return;
-    c.r0 += TR;
-    if (c.r0 < c.r_end) return;
-    cur_load(c, c.k + gridDim.x);
-}
-DEV uint32_t cur_nr(const Cur& c) { return (uint32_t)min((uint64_t)TR, c.r_end - c.r0); }
-
-// Span of a tile (row_off[r0], row_off[r0 + nr]) into a 16-B LDS entry:
-// wave 0, lanes 0-3, one LDS-DMA dword each (no register results, so the
-// compiler never waits on it; the loop-top vmcnt(0) + barrier publish it).
 DEV void glds4(const GAS void* src, LAS void* dst) {
     uint32_t keep;
     asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
@@ -259,64 +273,7 @@ DEV void glds4(const GAS void* src, LAS void* dst) {
                  : "v"(src), "s"(__builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)dst))
                  : "memory");
 }
-DEV void span_issue(const Cur& c, LAS uint8_t* ent, uint32_t wave, uint32_t lane) {
-    if (wave == 0 && c.ok && lane < 4) {
-        const uint64_t r = c.r0 + (lane < 2 ? 0u : cur_nr(c));
-        glds4((const GAS uint8_t*)(c.row_off + r) + (lane & 1) * 4, ent);
-    }
-}
-
-// The staged tile: where its bytes are and how they map to LDS.
-struct Tile {
-    uint64_t r0, abase;
-    const uint8_t* data;
-    uint32_t b, nr, ro_shift, hbm, first, last, span;  // span: staged blob bytes (16-B granules)
-    uint32_t seg_first, seg_last;  // first / last tile of its segment
-};
-
-// A tile's placement, from the cursor and its span (LDS entry `ent`).
-DEV Tile tile_info(const Cur& c, const LAS uint8_t* ent) {
-    Tile T;
-    const uint64_t base = sgpr64(((const LAS uint64_t*)ent)[0]);
-    const uint64_t end = sgpr64(((const LAS uint64_t*)ent)[1]);
-    T.r0 = c.r0;
-    T.nr = cur_nr(c);
-    T.b = c.b;
-    T.data = c.data;
-    T.abase = base & ~15ull;
-    T.first = c.r0 == 0;
-    T.last = c.r0 + T.nr == c.n_rows;
-    T.seg_first = c.r0 == c.r_begin;
-    T.seg_last = c.r0 + T.nr == c.r_end;
-    const uint64_t span = ((end + 15) & ~15ull) - T.abase;
-    T.hbm = end < base || end - T.abase > 0xFFFFFF00ull ? 2u : span > STAGE ? 1u : 0u;
-    T.span = T.hbm ? 0u : (uint32_t)span;
-    const uintptr_t rp = (uintptr_t)(c.row_off + c.r0);
-    T.ro_shift = (uint32_t)(rp & 15);
-    return T;
-}
-
-// The loader wave's LDS-DMA of one tile: its row-offset slice, then (unless
-// it outgrew the stage) its blob span, in 1 KiB pieces.
-DEV uint32_t tile_dma(const Tile& T, const Cur& c, LAS uint8_t* slot, uint32_t lane) {
-    // row offsets: lane j of piece q fetches the low dword of row_off[r0 + 64q + j]
-    uint32_t n = 0;
-    if (MJ_RO8) {
-        const GAS uint8_t* s0 = (const GAS uint8_t*)((uintptr_t)(c.row_off + c.r0) & ~(uintptr_t)15);
-        const uint32_t nb_ro = (T.ro_shift + (T.nr + 1) * 8 + 15) & ~15u;
-        for (uint32_t q = 0; q * 1024 < nb_ro; q++, n++)
-            if (q * 1024 + lane * 16 < nb_ro) glds16(s0 + q * 1024 + lane * 16, slot + q * 1024);
-    } else {
-        const GAS uint32_t* ro = (const GAS uint32_t*)(c.row_off + c.r0);
-        for (uint32_t q = 0; q * 64 <= T.nr; q++, n++)  // lane 0 is always active: one instruction each
-            if (q * 64 + lane <= T.nr) glds4(ro + 2 * (q * 64 + lane), slot + q * 256);
-    }
-    if (T.hbm) return n;
-    const GAS uint8_t* g = gp(c.data) + T.abase;
-    for (uint32_t q = 0; q * 1024 < T.span; q++, n++)
-        if (q * 1024 + lane * 16 < T.span) glds16(g + q * 1024 + lane * 16, slot + RO_BYTES + q * 1024);
-    return n;
-}
+DEV void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 // s_waitcnt vmcnt(n) for a wave-uniform run-time n (clamped to the 6-bit
 // field: a larger n waits for more than needed, never for less).
@@ -331,93 +288,344 @@ DEV void wait_vmcnt(uint32_t n) {
     }
 }
 
-// ---- per-row state of a wave's R chunks ----------------------------------------
-struct Rows {
-    uint32_t ra[R], rl[R], bits[R];
+// ---- shape ---------------------------------------------------------------------
+template <uint32_t NW_, uint32_t R_>
+struct Shape {
+    static constexpr uint32_t NW = NW_, NC = NW_ - 1, R = R_, TR = 64 * (NW_ - 1) * R_;
+    // LDS slot: [row offsets, low dwords: (TR+1)*4 + 16][stage + 64 pad]
+    static constexpr uint32_t RO_BYTES = ((TR + 1) * 4 + 16 + 15) & ~15u;
+    static constexpr uint32_t NSLOT = 2;
+    // after the slots: span ring [8][16 B] | tile ring [8][32 B] | counters |
+    // tile prefixes [NU] u64 | wave totals [NU][NC] u32 | prefetch scratch 1 KiB
+    static constexpr uint32_t SPAN_B = 128, INFO_B = 256, CNT_B = 16, PF_B = 1024;
+    DEV static uint32_t slot_bytes(uint32_t stage) { return RO_BYTES + stage + 64; }
 };
 
-template <class Src> DEV bool null_bit(const Rows& W, int k, uint32_t bit, const Src& src) {
-    if (BS <= 4) return W.rl[k] == 0 || ((W.bits[k] >> bit) & 1);
-    const uint32_t b = src.u8(at<Src>(W.rl[k] != 0, W.ra[k] + (bit >> 3)));
-    return W.rl[k] == 0 || ((b >> (bit & 7)) & 1);
-}
+// One tile as the loader dealt it (tile ring entry, 32 B).
+struct TileInfo {
+    uint32_t b, nr;
+    uint64_t r0;
+    uint64_t t;       // split mode: segment index (look-back granules)
+    uint32_t flags;   // bit 0: first tile of its block, 1: last, 2: valid, 3: first of its segment
+                      // (this pass), 4: last of its segment (this pass), 5-6: pass (0 local, 1, 2)
+    uint32_t first;   // split mode: the block's first segment
+};
 
-// One fixed-width (KIND = 1/2/4/8 bytes) or bool (KIND = 0) column over the
-// wave's chunks.  Returns its nulls.
-template <int KIND, uint32_t FO, uint32_t BIT, class Src>
-DEV uint32_t fixed_col(const Src& src, const Rows& W, const Tile& T, uint32_t rbase, const Out& o,
-                       uint32_t* badk, uint32_t lane) {
-    constexpr uint32_t WID = KIND == 0 ? 1 : KIND;
-    uint32_t nn = 0;
-#pragma unroll
-    for (int k = 0; k < (int)R; k++) {
-        const uint32_t i = rbase + k * 64 + lane;
-        const uint32_t nk = i - lane < T.nr ? min(64u, T.nr - (i - lane)) : 0u;
-        const bool isnull = null_bit(W, k, BIT, src);
-        const bool have = !isnull && FO + WID <= W.rl[k];
-        *badk |= (uint32_t)(!isnull && !have) << k;
-        const uint32_t a = at<Src>(have, W.ra[k] + FO);
-        const uint64_t vm = __ballot(!isnull);
-        nn += nk - (uint32_t)__popcll(vm);
-        const uint64_t word = (T.r0 + i - lane) >> 6;
-        if (nk && lane == 0) gp((uint64_t*)o.validity)[word] = vm;
-        const bool act = lane < nk;
-        if constexpr (KIND == 0) {
-            const uint32_t v = src.u8(a);
-            const uint64_t m = __ballot(have && v != 0);
-            if (nk && lane == 0) gp((uint64_t*)o.values)[word] = m;
-        } else if constexpr (KIND == 8) {
-            const uint64_t v = src.u64(a);
-            if (act) gp((uint64_t*)o.values)[T.r0 + i] = have ? v : 0;
-        } else if constexpr (KIND == 4) {
-            const uint32_t v = src.u32(a);
-            if (act) gp((uint32_t*)o.values)[T.r0 + i] = have ? v : 0;
-        } else if constexpr (KIND == 2) {
-            const uint32_t v = src.u16(a);
-            if (act) gp((uint16_t*)o.values)[T.r0 + i] = have ? (uint16_t)v : 0;
+// ---- the loader's tile cursor (wave-uniform) -------------------------------------
+struct Cur {
+    const uint8_t* data;
+    const uint64_t* row_off;
+    uint64_t n_rows, r0, r_begin, r_end;
+    uint32_t k, b, first, phase, ok;
+};
+// Cursors are built whole by value (every field assigned on every path: a
+// conditionally stored field would keep the struct on the stack, and stack
+// traffic would disturb the loader's counted vmcnt waits).
+DEV Cur cur_make(uint32_t ok, uint32_t k, uint32_t b, uint32_t first, uint32_t phase, uint64_t r_begin, uint64_t r_end,
+                 uint64_t r0) {
+    Cur c;
+    const CAS Blk* bp = (const CAS Blk*)args()->blocks + (ok ? b : 0u);
+    c.ok = ok;
+    c.k = k;
+    c.b = b;
+    c.first = first;
+    c.phase = phase;
+    c.r0 = r0;
+    c.data = ok ? (const uint8_t*)sgpr64((uint64_t)bp->data) : nullptr;
+    c.row_off = ok ? (const uint64_t*)sgpr64((uint64_t)bp->row_off) : nullptr;
+    c.n_rows = ok ? sgpr64(bp->n_rows) : 0;
+    c.r_begin = r_begin;
+    c.r_end = ok && r_end == ~0ull ? c.n_rows : r_end;
+    return c;
+}
+// local mode: the k-th entry of the launch's block order (whole blocks)
+DEV Cur cur_local(uint32_t k) {
+    k = sgpr(k);
+    const uint32_t ok = k < args()->norder;
+    const uint32_t b = ok ? sgpr(((const CAS uint32_t*)args()->order)[k]) : 0u;
+    return cur_make(ok, k, b, 0, 0, 0, ~0ull, 0);
+}
+// split mode: segment k, first pass
+DEV Cur cur_seg(uint32_t k) {
+    k = sgpr(k);
+    const uint32_t ok = k < args()->nseg;
+    const CAS Seg* sp = (const CAS Seg*)args()->segs + (ok ? k : 0u);
+    const uint64_t rb = ok ? sgpr64(sp->r_begin) : 0, re = ok ? sgpr64(sp->r_end) : 0;
+    return cur_make(ok, k, ok ? sgpr(sp->b) : 0u, ok ? sgpr(sp->first) : 0u, 1, rb, re, rb);
+}
+template <uint32_t MODE> DEV Cur cur_first() { return MODE == 0 ? cur_local(blockIdx.x) : cur_seg(blockIdx.x); }
+// The next tile: local mode walks the block, then the next block of the
+// order; split mode walks the segment, then walks it again (second pass,
+// when there are utf8 cells to write), then takes segment k + G.
+template <uint32_t TR> DEV Cur cur_next(const Cur& c) {
+    if (!c.ok) return c;
+    if (c.r0 + TR < c.r_end) {
+        Cur n = c;
+        n.r0 = c.r0 + TR;
+        return n;
+    }
+    if (c.phase == 0) return cur_local(c.k + gridDim.x);
+    if (c.phase == 1 && args()->emit) {
+        Cur n = c;
+        n.phase = 2;
+        n.r0 = c.r_begin;
+        return n;
+    }
+    return cur_seg(c.k + gridDim.x);
+}
+template <uint32_t TR> DEV uint32_t cur_nr(const Cur& c) { return (uint32_t)umin64((uint64_t)TR, c.r_end - c.r0); }
+
+// The loader publishes tile i's identity (ring entry i & 7, lane 0) and
+// fetches its span (row_off[r0], row_off[r0 + nr]) by LDS-DMA (lanes 0-3).
+template <uint32_t TR>
+DEV uint32_t tile_announce(const Cur& c, LAS uint8_t* span_ent, LAS uint8_t* info_ent, uint32_t lane) {
+    if (lane == 0) {
+        LAS TileInfo* ti = (LAS TileInfo*)info_ent;
+        if (c.ok) {
+            const uint32_t nr = cur_nr<TR>(c);
+            ti->b = c.b;
+            ti->nr = nr;
+            ti->r0 = c.r0;
+            ti->t = c.k;
+            ti->first = c.first;
+            ti->flags = (c.r0 == 0 ? 1u : 0u) | (c.r0 + nr == c.n_rows ? 2u : 0u) | 4u |
+                        (c.r0 == c.r_begin ? 8u : 0u) | (c.r0 + nr == c.r_end ? 16u : 0u) | (c.phase << 5);
         } else {
-            const uint32_t v = src.u8(a);
-            if (act) gp(o.values)[T.r0 + i] = have ? (uint8_t)v : 0;
+            ti->flags = 0;
         }
     }
-    return nn;
-}
-
-// Cells of one utf8 column (ReadRow::read_dynamic, read.rs:45-55): payload
-// address and length per row (0 for null / missing / malformed), chunk
-// inclusive scans, validity words.  Returns its nulls; *tot = wave total.
-template <uint32_t FO, uint32_t BIT, bool STORE, class Src>
-DEV uint32_t utf8_cells(const Src& src, const Rows& W, const Tile& T, uint32_t rbase, const Out& o,
-                        uint32_t* badk, uint32_t lane, uint32_t (&pay)[R], uint32_t (&len)[R],
-                        uint32_t (&inc)[R], uint32_t* tot) {
-    uint32_t nn = 0, wt = 0;
-#pragma unroll
-    for (int k = 0; k < (int)R; k++) {
-        const uint32_t i = rbase + k * 64 + lane;
-        const uint32_t nk = i - lane < T.nr ? min(64u, T.nr - (i - lane)) : 0u;
-        const bool isnull = null_bit(W, k, BIT, src);
-        const bool s_ok = !isnull && FO + 4 <= W.rl[k];
-        const uint32_t slot = src.u32(at<Src>(s_ok, W.ra[k] + FO));
-        const uint32_t vlen = W.rl[k] - BS;  // >= 4 when s_ok
-        const bool p_ok = s_ok && slot <= vlen - 4;
-        const uint32_t l = src.u32(at<Src>(p_ok, W.ra[k] + BS + slot));
-        const bool good = p_ok && l <= vlen - 4 - slot;
-        *badk |= (uint32_t)(!isnull && !good) << k;
-        pay[k] = W.ra[k] + BS + slot + 4;
-        len[k] = good ? l : 0u;
-        inc[k] = wave_scan(len[k]) + wt;
-        wt = __builtin_amdgcn_readlane(inc[k], 63);
-        const uint64_t vm = __ballot(!isnull);
-        nn += nk - (uint32_t)__popcll(vm);
-        if (STORE && nk && lane == 0) gp((uint64_t*)o.validity)[(T.r0 + i - lane) >> 6] = vm;
+    if (!c.ok) return 0;
+    if (lane < 4) {
+        const uint64_t r = c.r0 + (lane < 2 ? 0u : cur_nr<TR>(c));
+        glds4((const GAS uint8_t*)(c.row_off + r) + (lane & 1) * 4, span_ent);
     }
-    *tot = wt;
-    return nn;
+    return 1;
 }
 
-// Copy one string from the stage to vb[d .. d+n): overlapping unaligned dword
-// stores of its own bytes (head and tail), short/byte stores below 4 bytes.
-// Returns the OR of its bytes (UTF-8 pre-check).
+// The staged tile: where its bytes are and how they map to LDS.
+struct Tile {
+    uint64_t r0, abase, t;
+    const uint8_t* data;
+    const uint64_t* row_off;
+    uint32_t b, nr, hbm, span, first, last, seg_first, seg_last, first_seg;
+};
+DEV Tile tile_read(const LAS uint8_t* span_ent, const LAS uint8_t* info_ent, uint32_t stage) {
+    const LAS TileInfo* ti = (const LAS TileInfo*)info_ent;
+    Tile T;
+    T.b = sgpr(ti->b);
+    T.nr = sgpr(ti->nr);
+    T.r0 = sgpr64(ti->r0);
+    T.t = sgpr64(ti->t);
+    const uint32_t f = sgpr(ti->flags);
+    T.first = f & 1u;
+    T.last = (f >> 1) & 1u;
+    T.seg_first = (f >> 3) & 1u;
+    T.seg_last = (f >> 4) & 1u;
+    T.first_seg = sgpr(ti->first);
+    const uint64_t base = sgpr64(((const LAS uint64_t*)span_ent)[0]);
+    const uint64_t end = sgpr64(((const LAS uint64_t*)span_ent)[1]);
+    T.abase = base & ~15ull;
+    const uint64_t span = ((end + 15) & ~15ull) - T.abase;
+    T.hbm = end < base || end - T.abase > 0xFFFFFF00ull ? 2u : span > stage ? 1u : 0u;
+    T.span = T.hbm ? 0u : (uint32_t)span;
+    const CAS Blk* bp = (const CAS Blk*)args()->blocks + T.b;
+    T.data = (const uint8_t*)sgpr64((uint64_t)bp->data);
+    T.row_off = (const uint64_t*)sgpr64((uint64_t)bp->row_off);
+    return T;
+}
+DEV uint32_t tile_valid(const LAS uint8_t* info_ent) { return sgpr(((const LAS TileInfo*)info_ent)->flags) & 4u; }
+DEV uint32_t tile_phase(const LAS uint8_t* info_ent) { return (sgpr(((const LAS TileInfo*)info_ent)->flags) >> 5) & 3u; }
+
+// The loader wave's LDS-DMA of one tile: its row-offset slice (low dwords,
+// a gather: lane j of piece q fetches row_off[r0 + 64q + j]), then (unless it
+// outgrew the stage) its blob span in 1 KiB pieces.
+template <uint32_t TR, uint32_t RO_BYTES>
+DEV uint32_t tile_dma(const Tile& T, LAS uint8_t* slot, uint32_t lane) {
+    uint32_t n = 0;
+    const GAS uint32_t* ro = (const GAS uint32_t*)(T.row_off + T.r0);
+    for (uint32_t q = 0; q * 64 <= T.nr; q++, n++)  // lane 0 is always active: one instruction each
+        if (q * 64 + lane <= T.nr) glds4(ro + 2 * (q * 64 + lane), slot + q * 256);
+    if (T.hbm) return n;
+    const GAS uint8_t* g = gp(T.data) + T.abase;
+    for (uint32_t q = 0; q * 1024 < T.span; q++, n++)
+        if (q * 1024 + lane * 16 < T.span) glds16(g + q * 1024 + lane * 16, slot + RO_BYTES + q * 1024);
+    return n;
+}
+
+// L2 prefetch of a later tile's blob span: the same LDS-DMA pieces, all
+// landing in one 1 KiB scratch slot of LDS (the data is dropped; the lines
+// stay in L2), so a second tile is in flight without a second ring slot.
+// Returns the instructions issued.
+DEV uint32_t tile_prefetch(const Tile& T, LAS uint8_t* scratch, uint32_t lane) {
+    if (T.hbm) return 0;
+    uint32_t n = 0;
+    const GAS uint8_t* g = gp(T.data) + T.abase;
+    for (uint32_t q = 0; q * 1024 < T.span; q++, n++)
+        if (q * 1024 + lane * 16 < T.span) glds16(g + q * 1024 + lane * 16, scratch);
+    return n;
+}
+
+// ---- row windows -----------------------------------------------------------------
+// NRA dwords of the row's fixed part (bitset + static region) realigned to
+// the row start: r[j] = row bytes [4j, 4j + 4).  Wide layouts (more than
+// MJ_WINMAX dwords) read each field on its own instead.
+constexpr uint32_t NRA = (FIX + 3) / 4;
+#ifndef MJ_PREFETCH
+#define MJ_PREFETCH 0
+#endif
+#ifndef MJ_WINMAX
+#define MJ_WINMAX 32
+#endif
+constexpr bool WIN = NRA <= MJ_WINMAX;
+constexpr uint32_t NRW = WIN ? NRA : (BS + 3) / 4;  // dwords kept per row
+constexpr uint32_t NBW = (BS + 3) / 4;              // bitset dwords
+
+template <class Src> DEV void read_window(const Src& src, uint32_t ra, bool ok, uint32_t (&r)[NRW]) {
+    // aligned dwords [ra & ~3, (ra & ~3) + 4 (NRW + 1)) cover the row's first
+    // 4 NRW bytes (with ok, every one of them holds a byte of the row)
+    const uint32_t a4 = (Src::kHbm && !ok ? 0u : ra) >> 2, sh = ra & 3u;
+    uint32_t w[NRW + 1];
+#pragma unroll
+    for (uint32_t j = 0; j <= NRW; j++) {
+        if constexpr (Src::kHbm) {
+            // the last dword only when the row reaches into it
+            w[j] = (j < NRW || sh) && ok ? src.w(a4 + j) : 0u;
+        } else {
+            w[j] = src.w(a4 + j);
+        }
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < NRW; j++) r[j] = __builtin_amdgcn_alignbyte(w[j + 1], w[j], sh);
+}
+// Field at compile-time row byte FO (realigned window).
+template <uint32_t FO> DEV uint32_t get32(const uint32_t (&r)[NRW]) {
+    if constexpr (FO % 4 == 0) return r[FO / 4];
+    else return __builtin_amdgcn_alignbyte(r[FO / 4 + 1], r[FO / 4], FO % 4);
+}
+template <uint32_t FO> DEV uint32_t get16(const uint32_t (&r)[NRW]) {
+    if constexpr (FO % 4 <= 2) return __builtin_amdgcn_ubfe(r[FO / 4], 8 * (FO % 4), 16);
+    else return __builtin_amdgcn_alignbyte(r[FO / 4 + 1], r[FO / 4], 3) & 0xFFFFu;
+}
+template <uint32_t FO> DEV uint32_t get8(const uint32_t (&r)[NRW]) { return __builtin_amdgcn_ubfe(r[FO / 4], 8 * (FO % 4), 8); }
+
+// Field of width W at row byte FO: from the window, or (wide layouts) read on
+// its own from the source.
+template <uint32_t W, uint32_t FO, class Src>
+DEV void field(const Src& src, const uint32_t (&r)[NRW], uint32_t ra, bool ok, uint32_t& lo, uint32_t& hi) {
+    if constexpr (WIN) {
+        if constexpr (W == 8) { lo = get32<FO>(r); hi = get32<FO + 4>(r); }
+        else if constexpr (W == 4) lo = get32<FO>(r);
+        else if constexpr (W == 2) lo = get16<FO>(r);
+        else lo = get8<FO>(r);
+    } else {
+        const uint32_t a = Src::kHbm && !ok ? 0u : ra + FO;
+        if constexpr (Src::kHbm) {
+            const GAS uint8_t* p = src.g + a;
+            if constexpr (W == 8) { lo = *(const GAS u32u*)p; hi = *(const GAS u32u*)(p + 4); }
+            else if constexpr (W == 4) lo = *(const GAS u32u*)p;
+            else if constexpr (W == 2) lo = *(const GAS u16u*)p;
+            else lo = *p;
+        } else {
+            if constexpr (W == 8) { lo = src.u32(a); hi = src.u32(a + 4); }
+            else if constexpr (W == 4) lo = src.u32(a);
+            else if constexpr (W == 2) lo = src.u32(a) & 0xFFFFu;
+            else lo = src.u8(a);
+        }
+    }
+}
+
+// Ballot of `b` stashed in lane C % 64 of the pair (lo, hi) of lane group
+// C / 64 (v_writelane with a compile-time lane).  The ballot's SGPRs come
+// straight from a v_cmp: the nop covers the VALU-writes-SGPR ->
+// v_writelane-reads-it hazard, which the compiler cannot see inside asm
+// (without it the lane is written with a stale mask).
+template <uint32_t C> DEV void stash(uint32_t (&lo)[NCW], uint32_t (&hi)[NCW], bool b) {
+    const uint64_t m = __ballot(b);
+    asm volatile("s_nop 4\n\tv_writelane_b32 %0, %2, %4\n\tv_writelane_b32 %1, %3, %4"
+                 : "+v"(lo[C / 64]), "+v"(hi[C / 64])
+                 : "s"((uint32_t)m), "s"((uint32_t)(m >> 32)), "i"(C % 64));
+}
+
+// ---- per-wave state of a tile --------------------------------------------------
+template <uint32_t R> struct Rows {
+    uint32_t ra[R], rl[R];          // stage offset and length of the row (0 = missing / past the tile)
+    uint32_t vb[R][NBW];            // valid bits (~bitset; 0 for a missing row)
+    uint32_t r[R][NRW];             // realigned window
+};
+
+// Per-lane per-column state (lane c % 64 of group c / 64).
+struct Lanes {
+    uint64_t vptr[NCW], bptr[NCW];  // validity / bool values pointer of column c for the current block
+    uint32_t proj[NCW];             // column c decoded (0/1)
+    uint32_t isbool[NCW];
+    uint32_t nacc[NCW];             // nulls of column c since the last flush
+    uint32_t blk;                   // block the pointers belong to (~0 = none)
+};
+
+DEV const Out* outs_of(uint32_t b) {
+    const Out* o = args()->outs + (uint64_t)sgpr(b) * sgpr(args()->nproj);
+    return (const Out*)sgpr64((uint64_t)o);
+}
+DEV Out ldout(const Out* base, uint32_t p) {
+    // opaque per use: the compiler would otherwise hoist every column's
+    // descriptor into SGPRs up front (spills on wide projections)
+    asm volatile("" : "+s"(base));
+    const CAS Out* q = (const CAS Out*)base + p;
+    Out r;
+    r.values = q->values; r.validity = q->validity; r.offsets = q->offsets; r.values_cap = q->values_cap;
+    return r;
+}
+
+// Per-lane output pointers of block b (lane c: column c's validity and bool
+// values), reloaded when the block changes; null counts of the previous
+// block flushed first.
+DEV void lanes_flush(Lanes& L, uint32_t lane) {
+    if (L.blk == ~0u) return;
+    unsigned long long* nulls = args()->nulls + (uint64_t)L.blk * args()->nproj;
+#pragma unroll
+    for (uint32_t j = 0; j < NCW; j++) {
+        const uint32_t c = j * 64 + lane;
+        if (c < NCOLS && L.proj[j] && L.nacc[j])
+            __hip_atomic_fetch_add(gp(nulls) + gp(args()->slot_tab)[c], (unsigned long long)L.nacc[j], __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        L.nacc[j] = 0;
+    }
+}
+DEV void lanes_block(Lanes& L, uint32_t b, uint32_t lane) {
+    if (L.blk == b) return;
+    lanes_flush(L, lane);
+    L.blk = b;
+    const Out* ob = outs_of(b);
+#pragma unroll
+    for (uint32_t j = 0; j < NCW; j++) {
+        const uint32_t c = j * 64 + lane;
+        const uint32_t s = c < NCOLS ? (uint32_t)gp(args()->slot_tab)[c] : (uint32_t)kNone;
+        L.proj[j] = s != kNone;
+        L.isbool[j] = c < NCOLS && kColW[c < NCOLS ? c : 0] == 9;
+        const GAS Out* o = (const GAS Out*)ob + (s != kNone ? s : 0u);
+        L.vptr[j] = s != kNone ? (uint64_t)o->validity : 0;
+        L.bptr[j] = s != kNone ? (uint64_t)o->values : 0;
+    }
+}
+
+// Validity (and bool values) words of one chunk for every decoded column: one
+// store per lane group, lane c writes column c's word.
+DEV void store_words(Lanes& L, const uint32_t (&vlo)[NCW], const uint32_t (&vhi)[NCW], const uint32_t (&blo)[NCW],
+                     const uint32_t (&bhi)[NCW], uint64_t word, uint32_t nk, uint32_t lane) {
+#pragma unroll
+    for (uint32_t j = 0; j < NCW; j++) {
+        if (L.proj[j]) {
+            const uint64_t v = ((uint64_t)vhi[j] << 32) | vlo[j];
+            gp((uint64_t*)L.vptr[j])[word] = v;
+            if (L.isbool[j]) gp((uint64_t*)L.bptr[j])[word] = ((uint64_t)bhi[j] << 32) | blo[j];
+            L.nacc[j] += nk - (uint32_t)__popcll(v);
+        }
+    }
+}
+
+// Copy one string from the stage to vb[0 .. n): overlapping unaligned stores
+// of its own bytes (head and tail).  Returns the OR of its bytes (UTF-8
+// pre-check).
 DEV uint32_t pick(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t x) {  // dword at byte x in [0, 8)
     return x < 4 ? __builtin_amdgcn_alignbyte(w1, w0, x) : __builtin_amdgcn_alignbyte(w2, w1, x - 4);
 }
@@ -447,6 +655,21 @@ DEV uint32_t copy_str(const Src& src, GAS uint8_t* vb, uint32_t pay, uint32_t n)
             }
             return 0u;
         }
+        // 8-byte steps from realigned dword pairs, the last one overlapping
+        uint32_t hib = 0;
+        const uint32_t sh = pay & 3u;
+        const LAS uint32_t* p = (const LAS uint32_t*)(src.s + (pay & ~3u));
+#pragma unroll 1
+        for (uint32_t q = 0;; q += 8) {
+            const uint32_t at = q + 8 <= n ? q : n - 8;
+            const uint32_t b = sh + at, d = b >> 2, s2 = b & 3u;
+            const uint32_t x0 = p[d], x1 = p[d + 1], x2 = p[d + 2];
+            const uint32_t lo = __builtin_amdgcn_alignbyte(x1, x0, s2), hi = __builtin_amdgcn_alignbyte(x2, x1, s2);
+            *(GAS u64u*)(vb + at) = ((uint64_t)hi << 32) | lo;
+            hib |= lo | hi;
+            if (q + 8 >= n) break;
+        }
+        return hib;
     }
     uint32_t hib = 0, q = 0;
     if (n >= 4) {
@@ -477,48 +700,16 @@ template <class Src> DEV bool utf8_valid_slow(const Src& src, uint32_t a, uint32
     return dfa.ok();
 }
 
-// Offsets and string bytes of one utf8 column (projection index P) for the
-// wave's chunks, from the wave's prefix `base`.
-template <uint32_t P, class Src>
-DEV void utf8_emit(const Src& src, const Tile& T, uint32_t rbase, const Out& o, uint64_t base,
-                   const uint32_t (&pay)[R], const uint32_t (&len)[R], const uint32_t (&inc)[R], uint32_t lane,
-                   unsigned long long* err) {
-    GAS int32_t* ob = gp(o.offsets) + T.r0 + 1;
-#pragma unroll
-    for (int k = 0; k < (int)R; k++) {
-        const uint32_t i = rbase + k * 64 + lane;
-        const bool act = i < T.nr;
-        const uint32_t n = len[k];
-        const uint64_t e = base + inc[k];
-        const uint64_t cend = base + __builtin_amdgcn_readlane(inc[k], 63);
-        uint32_t hib = 0;
-        if (cend <= 0x7FFFFFFFull && cend <= o.values_cap) {  // wave-uniform fast path
-            if (act) ob[i] = (int32_t)e;
-            if (n) hib = copy_str(src, gp(o.values) + (e - n), pay[k], n);
-        } else {
-            if (act) {
-                if (e > 0x7FFFFFFFull) report(err, err_key(T.b, T.r0 + i, P, kStOverflow));
-                else ob[i] = (int32_t)e;
-                if (n && e > o.values_cap) report(err, err_key(T.b, T.r0 + i, P, kStCapacity));
-            }
-            for (uint32_t q = 0; q < n; q++) hib |= src.u8(pay[k] + q);
-        }
-        if ((hib & 0x80808080u) && !utf8_valid_slow(src, pay[k], n))
-            report(err, err_key(T.b, T.r0 + i, P, kStUtf8));
-    }
-}
-
 // Exact error of a flagged row: the first projected column (projection order)
 // whose cell the reference would reject (read.rs:39-55 bounds).
-constexpr uint32_t kColFo[NPROJ] = {MJ_COL_FO};
-constexpr uint32_t kColBit[NPROJ] = {MJ_COL_BIT};
-constexpr uint32_t kColWid[NPROJ] = {MJ_COL_WID};  // 0 = utf8
 template <class Src>
 DEV void report_row(const Src& src, uint32_t ra, uint32_t rl, uint64_t b, uint64_t row, unsigned long long* err) {
     if (rl < BS) { report(err, err_key(b, row, 0, kStMalformed)); return; }
-    for (uint32_t p = 0; p < NPROJ; p++) {
-        const uint32_t bit = kColBit[p], fo = kColFo[p], wid = kColWid[p];
-        if ((src.u8(ra + (bit >> 3)) >> (bit & 7)) & 1) continue;
+    const uint32_t np = args()->nproj;
+    for (uint32_t p = 0; p < np; p++) {
+        const uint32_t c = gp(args()->projcols)[p];
+        const uint32_t fo = kColFo[c], wid = kColW[c] == 9 ? 1u : kColW[c];
+        if ((src.u8(ra + (c >> 3)) >> (c & 7)) & 1) continue;
         bool bad;
         if (wid == 0) {
             bad = fo + 4 > rl;
@@ -534,262 +725,471 @@ DEV void report_row(const Src& src, uint32_t ra, uint32_t rl, uint64_t b, uint64
     }
 }
 
-DEV const Out* outs_of(uint32_t b) {
-    const Out* o = args()->outs + (uint64_t)sgpr(b) * NPROJ;
-    return (const Out*)sgpr64((uint64_t)o);
+// ---- decoupled look-back (stream mode) -----------------------------------------
+// Granule = status (2 bits: 0 none, 1 aggregate, 2 inclusive prefix) | value.
+constexpr uint64_t kAgg = 1ull << 62, kPre = 2ull << 62, kValMask = (1ull << 62) - 1;
+DEV void publish(unsigned long long* g, uint64_t v) {
+    __hip_atomic_store((GAS unsigned long long*)g, (unsigned long long)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-DEV Out ldout(const Out* base, uint32_t p) {
-    // opaque per use: the compiler would otherwise hoist every column's
-    // descriptor into SGPRs up front (spills on wide projections)
-    asm volatile("" : "+s"(base));
-    const CAS Out* q = (const CAS Out*)base + p;
-    Out r;
-    r.values = q->values; r.validity = q->validity; r.offsets = q->offsets; r.values_cap = q->values_cap;
-    return r;
+DEV uint64_t peek(const unsigned long long* g) {
+    return __hip_atomic_load((const GAS unsigned long long*)g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// Exclusive prefix of segment t (first segment of its block t0) for utf8
+// column u: 512 predecessors per round (8 per lane, lane l holds t-1-8l-q),
+// newest first, summed back to the nearest inclusive prefix (or the block's
+// first segment).  The segments of one round of the grid all publish their
+// aggregates at about the same time, so one round usually ends at the
+// previous round's prefixes.
+constexpr uint32_t kLbPer = 8;
+DEV uint64_t look_back(uint64_t t, uint64_t t0, uint32_t u, uint32_t lane, uint64_t b) {
+    const unsigned long long* fl = args()->flags;
+    uint64_t sum = 0;
+    uint64_t j = t;  // segments [t0, j) remain
+    Wait w;
+    while (j > t0) {
+        uint64_t g[kLbPer];
+        bool in[kLbPer];
+#pragma unroll
+        for (uint32_t q = 0; q < kLbPer; q++) {
+            const uint64_t back = 1 + kLbPer * lane + q;  // segment j - back
+            in[q] = j >= t0 + back;
+            g[q] = in[q] ? peek(fl + (j - back) * NU + u) : kPre;  // past the block: prefix 0
+        }
+        // predecessors with nothing published yet: re-read (bounded)
+        for (;;) {
+            bool pend = false;
+#pragma unroll
+            for (uint32_t q = 0; q < kLbPer; q++) pend |= in[q] && (g[q] >> 62) == 0;
+            if (!__ballot(pend)) break;
+            if (w.expired(b, 0)) return sum;
+#pragma unroll
+            for (uint32_t q = 0; q < kLbPer; q++)
+                if (in[q] && (g[q] >> 62) == 0) g[q] = peek(fl + (j - 1 - kLbPer * lane - q) * NU + u);
+        }
+        // the nearest prefix: lowest lane holding one, lowest q in it
+        uint32_t qp = kLbPer;
+#pragma unroll
+        for (uint32_t q = kLbPer; q-- > 0;)
+            if ((g[q] >> 62) == 2) qp = q;
+        const uint64_t pm = __ballot(qp < kLbPer);
+        const uint32_t stop = pm ? (uint32_t)__builtin_ctzll(pm) : 64u;
+        const uint32_t qstop = __builtin_amdgcn_readlane(qp, stop < 64 ? stop : 0);
+        uint64_t v = 0;
+#pragma unroll
+        for (uint32_t q = 0; q < kLbPer; q++) {
+            const bool take = in[q] && (lane < stop || (lane == stop && q <= qstop));
+            v += take ? (g[q] & kValMask) : 0;
+        }
+        for (int m = 32; m >= 1; m >>= 1) v += (uint64_t)__shfl_xor((unsigned long long)v, m, 64);
+        sum += sgpr64(v);
+        if (pm) break;
+        j = j > 64 * kLbPer ? j - 64 * kLbPer : 0;
+    }
+    return sum;
 }
 
-// Null counts of a wave: column p's count in lane p % 64 of nn[p / 64]
-// (VGPRs, not an SGPR per column).
-constexpr uint32_t NNV = (NPROJ + 63) / 64;
-template <uint32_t P> DEV void add_nulls(uint32_t (&nn)[NNV], uint32_t lane, uint32_t v) {
-    // readlane / writelane: no per-column lane compare (those masks would be
-    // hoisted out of the tile loop into SGPR pairs)
-    const uint32_t t = __builtin_amdgcn_readlane(nn[P / 64], P % 64) + v;
-    asm("v_writelane_b32 %0, %1, %2" : "+v"(nn[P / 64]) : "s"(t), "i"(P % 64));
-}
-
-// Decode one staged tile.  run[u]: the block's utf8 bytes before this tile
-// (updated to after it); nn: this wave's null counts for the segment.
-// LEN (the length pass): utf8 cells only; each wave adds its utf8 bytes to
-// run[] (no prefix, no stores).
-template <bool LEN, class Src>
-DEV void decode_tile(const Src& src, const Tile& T, const LAS uint32_t* ro, LAS uint32_t* wt, uint64_t (&run)[NUTF8 ? NUTF8 : 1],
-                     uint32_t (&nn)[NNV], uint32_t wave, uint32_t lane, LAS uint32_t* pcnt, uint32_t ptarget) {
+// ---- one tile of one decode wave ---------------------------------------------------
+// PH 0: everything (local mode); 1: first pass of a split segment (fixed
+// columns, validity, utf8 lengths); 2: second pass (utf8 offsets and bytes).
+template <class SH, uint32_t PH, class Src>
+DEV void decode_tile(const Src& src, const Tile& T, const LAS uint32_t* ro, LAS uint8_t* ctl, uint64_t (&run)[NU],
+                     Lanes& L, uint32_t wave, uint32_t lane, uint32_t it) {
+    constexpr uint32_t R = SH::R, NC = SH::NC;
     unsigned long long* err = args()->err;
     const uint32_t rbase = wave * 64 * R;
     const uint32_t abase = (uint32_t)T.abase;
     const Out* ob = outs_of(T.b);
-    Rows W;
-    uint32_t badk = 0;
+    LAS uint32_t* pcnt = (LAS uint32_t*)ctl;         // wave totals published (monotone)
+    LAS uint32_t* pready = (LAS uint32_t*)ctl + 1;   // segments whose prefix is in tpre (split mode)
+    LAS uint64_t* tpre = (LAS uint64_t*)(ctl + SH::CNT_B);
+    LAS uint32_t* wt = (LAS uint32_t*)(ctl + SH::CNT_B + 8 * NU);
+    lanes_block(L, T.b, lane);
+
+    Rows<R> W;
+    uint32_t badk = 0, partial = 0;
 #pragma unroll
-    for (int k = 0; k < (int)R; k++) {
+    for (uint32_t k = 0; k < R; k++) {
         const uint32_t i = rbase + k * 64 + lane;
-        const uint32_t a0 = ro[RO_W * i], a1 = ro[RO_W * (i + 1)];
+        const uint32_t a0 = ro[i], a1 = ro[i + 1];
         const uint32_t rl = i < T.nr ? a1 - a0 : 0u;
         W.ra[k] = a0 - abase;
-        badk |= (uint32_t)(rl != 0 && rl < BS) << k;
-        W.rl[k] = rl >= BS ? rl : 0u;
-        if (BS <= 4) {
-            if constexpr (Src::kHbm) {
+        W.rl[k] = rl;
+        const bool full = rl >= FIX;
+        partial |= (uint32_t)(rl != 0 && !full) << k;
+        read_window(src, W.ra[k], full, W.r[k]);
+        if (!full) {
+            // a short row: only the bytes it has (the cold path reports it)
+#pragma unroll
+            for (uint32_t j = 0; j < NRW; j++) {
+                const uint32_t have = rl > 4 * j ? umin32(rl - 4 * j, 4u) : 0u;
                 uint32_t v = 0;
-                for (uint32_t q = 0; q < BS; q++) v |= src.u8(at<Src>(W.rl[k] != 0, W.ra[k] + q)) << (8 * q);
-                W.bits[k] = v;
-            } else {
-                W.bits[k] = src.u32(W.ra[k]);
+                if (!Src::kHbm || have) {
+                    for (uint32_t q = 0; q < have; q++) v |= src.u8(W.ra[k] + 4 * j + q) << (8 * q);
+                }
+                W.r[k][j] = v;
             }
-        } else {
-            W.bits[k] = 0;
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < NBW; j++) {
+            uint32_t bits = W.r[k][j];
+            if (BS - 4 * j < 4) bits |= ~0u << (8 * (BS - 4 * j));  // padding bytes read as null
+            W.vb[k][j] = rl >= BS ? ~bits : 0u;
+        }
+        badk |= (uint32_t)(rl != 0 && rl < BS) << k;
+    }
+    const bool safe = __ballot(partial != 0) != 0;  // some row shorter than the fixed part
+
+    uint32_t vlo[R][NCW], vhi[R][NCW], blo[R][NCW], bhi[R][NCW];
+#pragma unroll
+    for (uint32_t k = 0; k < R; k++)
+#pragma unroll
+        for (uint32_t j = 0; j < NCW; j++) vlo[k][j] = vhi[k][j] = blo[k][j] = bhi[k][j] = 0;
+
+    // ---- utf8 cells: payload position and length, chunk scans (read.rs:45-55)
+    uint32_t upay[NU][R], ulen[NU][R], uinc[NU][R], utot[NU];
+#pragma unroll
+    for (uint32_t u = 0; u < NU; u++) utot[u] = 0;
+#define MJ_U(C, W_, FO, U)                                                                              \
+    if constexpr (W_ == 0) {                                                                            \
+        if (slot_of(C) != kNone) {                                                                      \
+            uint32_t wtot = 0;                                                                          \
+            _Pragma("unroll") for (uint32_t k = 0; k < R; k++) {                                        \
+                const uint32_t rl = W.rl[k];                                                            \
+                const bool valid = (W.vb[k][C / 32] >> (C % 32)) & 1u;                                  \
+                const bool s_ok = valid && FO + 4 <= rl;                                                \
+                uint32_t sl, dummy = 0;                                                                 \
+                field<4, FO>(src, W.r[k], W.ra[k], s_ok, sl, dummy);                                    \
+                const uint32_t vlen = rl - BS; /* >= 4 when s_ok */                                     \
+                const bool p_ok = s_ok && sl <= vlen - 4;                                               \
+                const uint32_t pa = W.ra[k] + BS + sl;                                                  \
+                const uint32_t l = src.u32(Src::kHbm && !p_ok ? 0u : pa);                               \
+                const bool good = p_ok && l <= vlen - 4 - sl;                                           \
+                badk |= (uint32_t)(valid && !good) << k;                                                \
+                upay[U][k] = pa + 4;                                                                    \
+                ulen[U][k] = good ? l : 0u;                                                             \
+                uinc[U][k] = wave_scan(ulen[U][k]) + wtot;                                              \
+                wtot = __builtin_amdgcn_readlane(uinc[U][k], 63);                                       \
+                if constexpr (PH != 2) stash<C>(vlo[k], vhi[k], valid);                                 \
+            }                                                                                           \
+            utot[U] = wtot;                                                                             \
+        }                                                                                               \
+    }
+    MJ_COLS(MJ_U)
+#undef MJ_U
+
+    // wave totals -> LDS; the tile total and every wave's prefix follow
+    if (NUTF8) {
+        if (lane == 0) {
+            for (uint32_t u = 0; u < NU; u++) wt[u * NC + wave] = utot[u];
+            __hip_atomic_fetch_add(pcnt, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
     }
 
-    if constexpr (!LEN) {
-#define MJ_DO_FIXED(P, KIND, FO, BIT) \
-    add_nulls<P>(nn, lane, fixed_col<KIND, FO, BIT>(src, W, T, rbase, ldout(ob, P), &badk, lane));
-        MJ_FIXED(MJ_DO_FIXED)
-#undef MJ_DO_FIXED
+    // ---- fixed-width and bool columns (primitive.rs:43-56, bool_.rs:86-99)
+#define MJ_F(C, W_, FO, U)                                                                              \
+    if constexpr (W_ != 0 && PH != 2) {                                                                 \
+        if (slot_of(C) != kNone) {                                                                      \
+            constexpr uint32_t WW = W_ == 9 ? 1u : W_;                                                  \
+            const Out o = ldout(ob, slot_of(C));                                                        \
+            _Pragma("unroll") for (uint32_t k = 0; k < R; k++) {                                        \
+                const uint32_t i = rbase + k * 64 + lane;                                               \
+                bool valid = (W.vb[k][C / 32] >> (C % 32)) & 1u;                                        \
+                if (safe) {                                                                             \
+                    const bool have = FO + WW <= W.rl[k];                                               \
+                    badk |= (uint32_t)(valid && !have) << k;                                            \
+                    valid = valid && have;                                                              \
+                }                                                                                       \
+                uint32_t lo = 0, hi = 0;                                                                \
+                field<WW, FO>(src, W.r[k], W.ra[k], valid || !Src::kHbm, lo, hi);                       \
+                const uint32_t m = valid ? ~0u : 0u;                                                    \
+                lo &= m;                                                                                \
+                hi &= m;                                                                                \
+                stash<C>(vlo[k], vhi[k], (W.vb[k][C / 32] >> (C % 32)) & 1u);                           \
+                if constexpr (W_ == 9) {                                                                \
+                    stash<C>(blo[k], bhi[k], lo != 0);                                                  \
+                } else if (i < T.nr) {                                                                  \
+                    const uint64_t row = T.r0 + i;                                                      \
+                    if constexpr (W_ == 8) gp((uint64_t*)o.values)[row] = ((uint64_t)hi << 32) | lo;    \
+                    else if constexpr (W_ == 4) gp((uint32_t*)o.values)[row] = lo;                      \
+                    else if constexpr (W_ == 2) gp((uint16_t*)o.values)[row] = (uint16_t)lo;            \
+                    else gp((uint8_t*)o.values)[row] = (uint8_t)lo;                                     \
+                }                                                                                       \
+            }                                                                                           \
+        }                                                                                               \
     }
+    MJ_COLS(MJ_F)
+#undef MJ_F
 
-#if MJ_NUTF8 > 0
-    uint32_t upay[NUTF8][R], ulen[NUTF8][R], uinc[NUTF8][R], utot[NUTF8];
-#define MJ_DO_CELLS(P, U, FO, BIT) \
-    add_nulls<P>(nn, lane, utf8_cells<FO, BIT, !LEN>(src, W, T, rbase, ldout(ob, P), &badk, lane, upay[U], ulen[U], uinc[U], &utot[U]));
-    MJ_UTF8(MJ_DO_CELLS)
-#undef MJ_DO_CELLS
-    if constexpr (LEN) {
-        for (uint32_t u = 0; u < NUTF8; u++) run[u] += utot[u];
-        return;
-    }
-#endif
-    if constexpr (LEN) return;
-
-    if (__ballot(badk != 0)) {  // cold: exact error reports
+    if constexpr (PH != 2) {
 #pragma unroll
-        for (int k = 0; k < (int)R; k++) {
+        for (uint32_t k = 0; k < R; k++) {
+            const uint32_t c0 = rbase + k * 64;
+            const uint32_t nk = c0 < T.nr ? umin32(64u, T.nr - c0) : 0u;
+            if (nk) store_words(L, vlo[k], vhi[k], blo[k], bhi[k], (T.r0 + c0) >> 6, nk, lane);
+        }
+    }
+
+    if (PH != 2 && args()->report && __ballot(badk != 0)) {  // cold: exact error reports
+#pragma unroll
+        for (uint32_t k = 0; k < R; k++) {
             if (!((badk >> k) & 1)) continue;
             const uint32_t i = rbase + k * 64 + lane;
-            report_row(src, W.ra[k], ro[RO_W * (i + 1)] - ro[RO_W * i], T.b, T.r0 + i, err);
+            report_row(src, W.ra[k], W.rl[k], T.b, T.r0 + i, err);
         }
     }
+    if (!NUTF8) return;
 
-#if MJ_NUTF8 > 0
-    // wave totals -> LDS; every wave derives its prefix and the tile total
-    if (lane == 0) {
-        for (uint32_t u = 0; u < NUTF8; u++) wt[u * NC + wave] = utot[u];
-        __hip_atomic_fetch_add(pcnt, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
+    // ---- the tile's utf8 prefix
     {
-        uint32_t spins = 0;
-        while (__hip_atomic_load(pcnt, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < ptarget) {
-            __builtin_amdgcn_s_sleep(1);
-            if (++spins > (1u << 24)) { report(err, err_key(T.b, T.r0, 0, kStInternal)); break; }
-        }
+        MJ_TIC
+        Wait w;
+        while (__hip_atomic_load(pcnt, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < NC * (it + 1))
+            if (w.expired(T.b, T.r0)) break;
+        MJ_TOC(1)
     }
-    uint64_t pre[NUTF8];
+    uint64_t tot[NU], before[NU];
 #pragma unroll
-    for (uint32_t u = 0; u < NUTF8; u++) {
-        uint64_t before = 0, all = 0;
+    for (uint32_t u = 0; u < NU; u++) {
+        uint64_t bf = 0, all = 0;
 #pragma unroll
         for (uint32_t w = 0; w < NC; w++) {
             const uint32_t v = wt[u * NC + w];
-            before += w < wave ? v : 0u;
+            bf += w < wave ? v : 0u;
             all += v;
         }
-        pre[u] = run[u] + sgpr64(before);
-        run[u] += sgpr64(all);
+        tot[u] = sgpr64(all);
+        before[u] = sgpr64(bf);
     }
-#define MJ_DO_EMIT(P, U, FO, BIT)                                                                      \
-    {                                                                                                  \
-        const Out o = ldout(ob, P);                                                                    \
-        if (T.first && wave == 0 && lane == 0) gp(o.offsets)[0] = 0;                                   \
-        if (T.last && wave == 0 && lane == 0) gp(args()->lens)[(uint64_t)T.b * NPROJ + P] = run[U];    \
-        utf8_emit<P>(src, T, rbase, o, pre[U], upay[U], ulen[U], uinc[U], lane, err);                  \
-    }
-    MJ_UTF8(MJ_DO_EMIT)
-#undef MJ_DO_EMIT
-#endif
-}
-
-DEV void flush_nulls(uint32_t b, uint32_t (&nn)[NNV], uint32_t lane) {
-    unsigned long long* nulls = args()->nulls + (uint64_t)b * NPROJ;
+    uint64_t tile_pre[NU];
+    if constexpr (PH == 0) {
 #pragma unroll
-    for (uint32_t j = 0; j < NNV; j++) {
-        if (j * 64 + lane < NPROJ && nn[j])
-            __hip_atomic_fetch_add(gp(nulls) + j * 64 + lane, (unsigned long long)nn[j], __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-        nn[j] = 0;
-    }
-}
-
-}  // namespace mj
-
-namespace mj {
-
-// utf8 bytes of block rows before segment c (the sum of the length pass's
-// totals of the block's earlier segments), per utf8 column.
-DEV void seg_prefix(const Cur& c, uint64_t (&run)[NU], uint32_t lane) {
-    const unsigned long long* st = args()->seg_tot;
+        for (uint32_t u = 0; u < NU; u++) {
+            tile_pre[u] = run[u];
+            run[u] += tot[u];
+        }
+    } else if constexpr (PH == 1) {
+        // the segment's utf8 bytes; after its last tile, wave 0 publishes the
+        // aggregate, looks back, publishes the inclusive prefix and leaves the
+        // exclusive one in LDS for the second pass
 #pragma unroll
-    for (uint32_t u = 0; u < NUTF8; u++) {
-        uint64_t v = 0;
-        for (uint32_t j = c.first + lane; j < c.k; j += 64) v += __hip_atomic_load(gp(st) + (uint64_t)j * NU + u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        for (int m = 32; m >= 1; m >>= 1) v += (uint64_t)__shfl_xor((unsigned long long)v, m, 64);
-        run[u] = sgpr64(v);
+        for (uint32_t u = 0; u < NU; u++) run[u] = (T.seg_first ? 0 : run[u]) + tot[u];
+        if (T.seg_last && wave == 0 && args()->emit) {
+            unsigned long long* fl = args()->flags + T.t * NU;
+            const bool head = T.t == T.first_seg;
+#pragma unroll
+            for (uint32_t u = 0; u < NU; u++)
+                if (lane == 0) publish(fl + u, (head ? kPre : kAgg) | run[u]);
+#pragma unroll
+            for (uint32_t u = 0; u < NU; u++) {
+                MJ_TIC
+                const uint64_t ex = head ? 0 : look_back(T.t, T.first_seg, u, lane, T.b);
+                MJ_TOC(3)
+                if (!head && lane == 0) publish(fl + u, kPre | ((ex + run[u]) & kValMask));
+                if (lane == 0) tpre[u] = ex;
+            }
+            if (lane == 0) __hip_atomic_store(pready, (uint32_t)T.t + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        return;
+    } else {
+        if (T.seg_first) {
+            MJ_TIC
+            Wait w;
+            while (__hip_atomic_load(pready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != (uint32_t)T.t + 1)
+                if (w.expired(T.b, T.r0)) break;
+            MJ_TOC(2)
+#pragma unroll
+            for (uint32_t u = 0; u < NU; u++) run[u] = sgpr64(tpre[u]);
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < NU; u++) {
+            tile_pre[u] = run[u];
+            run[u] += tot[u];
+        }
     }
+
+    // ---- offsets and string bytes (utf8.rs:86-96 append_value)
+#define MJ_E(C, W_, FO, U)                                                                              \
+    if constexpr (W_ == 0 && PH != 1) {                                                                 \
+        if (slot_of(C) != kNone) {                                                                      \
+            const uint32_t P = slot_of(C);                                                              \
+            const Out o = ldout(ob, P);                                                                 \
+            const uint64_t base = tile_pre[U] + before[U];                                              \
+            if (T.first && wave == 0 && lane == 0) gp(o.offsets)[0] = 0;                                \
+            if (T.last && wave == 0 && lane == 0)                                                       \
+                gp(args()->lens)[(uint64_t)T.b * args()->nproj + P] = tile_pre[U] + tot[U];            \
+            GAS int32_t* obf = gp(o.offsets) + T.r0 + 1;                                                \
+            _Pragma("unroll") for (uint32_t k = 0; k < R; k++) {                                        \
+                const uint32_t i = rbase + k * 64 + lane;                                               \
+                const bool act = i < T.nr;                                                              \
+                const uint32_t n = ulen[U][k];                                                          \
+                const uint64_t e = base + uinc[U][k];                                                   \
+                const uint64_t cend = base + __builtin_amdgcn_readlane(uinc[U][k], 63);                 \
+                uint32_t hib = 0;                                                                       \
+                if (cend <= 0x7FFFFFFFull && cend <= o.values_cap) { /* wave-uniform fast path */       \
+                    if (act) obf[i] = (int32_t)e;                                                       \
+                    if (n) hib = copy_str(src, gp(o.values) + (e - n), upay[U][k], n);                  \
+                } else {                                                                                \
+                    if (act) {                                                                          \
+                        if (e > 0x7FFFFFFFull) report(err, err_key(T.b, T.r0 + i, P, kStOverflow));     \
+                        else obf[i] = (int32_t)e;                                                       \
+                        if (n && e > o.values_cap) report(err, err_key(T.b, T.r0 + i, P, kStCapacity)); \
+                    }                                                                                   \
+                    for (uint32_t q = 0; q < n; q++) hib |= src.u8(upay[U][k] + q);                     \
+                }                                                                                       \
+                if ((hib & 0x80808080u) && !utf8_valid_slow(src, upay[U][k], n))                        \
+                    report(err, err_key(T.b, T.r0 + i, P, kStUtf8));                                    \
+            }                                                                                           \
+        }                                                                                               \
+    }
+    MJ_COLS(MJ_E)
+#undef MJ_E
 }
 
-template <bool LEN>
+// ---- kernel body ---------------------------------------------------------------------
+// MODE 0: local, 1: split (separate kernels: the split path's look-back
+// registers would otherwise cost the local kernel occupancy).
+template <uint32_t NW, uint32_t R, uint32_t MODE>
 DEV void kernel_body() {
+    using SH = Shape<NW, R>;
+    constexpr uint32_t NC = SH::NC, TR = SH::TR, NSLOT = SH::NSLOT;
     extern __shared__ __attribute__((aligned(16))) uint8_t lds_[];
     LAS uint8_t* lds = (LAS uint8_t*)lds_;
     const uint32_t lane = lane_id();
     const uint32_t wave = sgpr(threadIdx.x >> 6);
-    LAS uint32_t* wt = (LAS uint32_t*)(lds + LDS_WT);
-    LAS uint32_t* pcnt = (LAS uint32_t*)(lds + LDS_CNT);
-    if (threadIdx.x == 0) *pcnt = 0;
-
-    LAS uint8_t* spans = lds + LDS_SPAN;
-
-    Cur cur;
-    cur_load(cur, blockIdx.x);
-    if (!cur.ok) return;
+    const uint32_t stage = sgpr(args()->stage);
+    const uint32_t SLOT = SH::slot_bytes(stage);
+    LAS uint8_t* spans = lds + NSLOT * SLOT;
+    LAS uint8_t* infos = spans + SH::SPAN_B;
+    LAS uint8_t* ctl = infos + SH::INFO_B;
+    LAS uint8_t* pf = ctl + SH::CNT_B + 8 * NU + ((4 * NU * NC + 15) & ~15u);
+    if (threadIdx.x < 2) ((LAS uint32_t*)ctl)[threadIdx.x] = 0;
 
     if (wave == NC) {
-        // ---- loader: NSLOT-1 tiles in flight.  At iteration i (after tile
-        // barrier B_i freed slot (i-1) % NSLOT) it DMAs tile i+NSLOT-1 and
-        // the span of tile i+NSLOT+1.  It issues no other vector-memory
-        // instruction, so its counted vmcnt waits for exactly the DMA it
-        // needs (tile i+1, and the span of tile i+NSLOT it reads next), never
-        // for the consumers' stores.
-        Cur cs = cur;  // next tile whose span to fetch
-        for (uint32_t k = 0; k <= NSLOT; k++) {
-            span_issue(cs, spans + (k & 7) * 16, 0, lane);
-            cur_next(cs);
+        // ---- loader: one tile in flight.  At iteration i (after barrier B_i
+        // freed slot (i+1) % 2) it DMAs tile i+1 and announces tile i+4 (its
+        // identity and span).  It issues no other vector-memory instruction,
+        // so its counted vmcnt waits for exactly the DMA it needs.
+        Cur cs = cur_first<MODE>();  // next tile to announce
+#pragma unroll
+        for (uint32_t k = 0; k <= NSLOT + 1; k++) {
+            tile_announce<TR>(cs, spans + (k & 7) * 16, infos + (k & 7) * 32, lane);
+            cs = cur_next<TR>(cs);
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        Cur cd = cur;  // next tile to DMA
-        uint32_t after0 = 0;
-        for (uint32_t j = 0; j + 1 < NSLOT; j++) {
-            if (cd.ok) {
-                const uint32_t n = tile_dma(tile_info(cd, spans + (j & 7) * 16), cd, lds + j * SLOT, lane);
-                if (j) after0 += n;
-            }
-            cur_next(cd);
-        }
-        wait_vmcnt(after0);
-        lds_barrier();  // B_0: tile 0 and the spans of tiles 0 .. NSLOT landed
-        Cur cc = cur;  // the tile the decode waves work on in this iteration
+#ifdef MJ_STAMPS
+        const uint64_t lt0 = __builtin_amdgcn_s_memtime();
+        uint64_t lwait = 0;
+#endif
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        if (tile_valid(infos)) tile_dma<TR, SH::RO_BYTES>(tile_read(spans, infos, stage), lds, lane);
+        wait_vmcnt(0);
+        lds_barrier();  // B_0: tile 0 and the spans of tiles 0 .. 3 landed
         for (uint32_t it = 0;; it++) {
-            cur_next(cc);
-            const uint32_t more = cc.ok;
-            uint32_t nd = 0, ns = 0;
-            if (cd.ok) {
-                const uint32_t t = it + NSLOT - 1;
-                nd = tile_dma(tile_info(cd, spans + (t & 7) * 16), cd, lds + (t % NSLOT) * SLOT, lane);
-                cur_next(cd);
-            }
-            if (cs.ok) {
-                span_issue(cs, spans + ((it + NSLOT + 1) & 7) * 16, 0, lane);
-                ns = 1;
-                cur_next(cs);
-            }
-            wait_vmcnt(NSLOT == 2 ? ns : nd + ns);
-            lds_barrier();  // B_i+1: tile i+1 landed, tile i decoded
-            if (!more) break;
+            if (!tile_valid(infos + (it & 7) * 32)) break;  // the decode waves leave too
+            const uint32_t t1 = it + 1, k = it + NSLOT + 2;
+            if (tile_valid(infos + (t1 & 7) * 32))
+                tile_dma<TR, SH::RO_BYTES>(tile_read(spans + (t1 & 7) * 16, infos + (t1 & 7) * 32, stage),
+                                           lds + (t1 % NSLOT) * SLOT, lane);
+            // tile it+2 into L2 (tuning: MJ_PREFETCH=1; measured slower on configs C/D)
+            uint32_t np = 0;
+#if MJ_PREFETCH
+            const uint32_t t2 = it + 2;
+            if (tile_valid(infos + (t2 & 7) * 32))
+                np = tile_prefetch(tile_read(spans + (t2 & 7) * 16, infos + (t2 & 7) * 32, stage), pf, lane);
+#endif
+            const uint32_t ns = tile_announce<TR>(cs, spans + (k & 7) * 16, infos + (k & 7) * 32, lane) + np;
+            cs = cur_next<TR>(cs);
+#ifdef MJ_STAMPS
+            const uint64_t w0 = __builtin_amdgcn_s_memtime();
+#endif
+            wait_vmcnt(ns);
+            lds_barrier();  // B_it+1: tile it+1 landed, tile it decoded
+#ifdef MJ_STAMPS
+            lwait += __builtin_amdgcn_s_memtime() - w0;
+#endif
         }
+#ifdef MJ_STAMPS
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0) {
+            __hip_atomic_fetch_add((GAS unsigned long long*)args()->err + 2 + 7, (unsigned long long)lwait, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_add((GAS unsigned long long*)args()->err + 2 + 8, (unsigned long long)(__builtin_amdgcn_s_memtime() - lt0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+#endif
         return;
     }
 
-    // ---- consumers ----
-    uint64_t run[NUTF8 ? NUTF8 : 1];
-    for (uint32_t u = 0; u < (NUTF8 ? NUTF8 : 1); u++) run[u] = 0;
-    uint32_t nn[NNV];
-    for (uint32_t j = 0; j < NNV; j++) nn[j] = 0;
+    // ---- decode waves ----
+    uint64_t run[NU];
+#pragma unroll
+    for (uint32_t u = 0; u < NU; u++) run[u] = 0;
+    Lanes L;
+    L.blk = ~0u;
+#pragma unroll
+    for (uint32_t j = 0; j < NCW; j++) L.nacc[j] = 0, L.proj[j] = 0, L.isbool[j] = 0, L.vptr[j] = 0, L.bptr[j] = 0;
+#ifdef MJ_STAMPS
+    const uint64_t ct0 = __builtin_amdgcn_s_memtime();
+#endif
     lds_barrier();  // B_0
+    uint32_t prev_b = ~0u;
     for (uint32_t it = 0;; it++) {
+        const LAS uint8_t* info = infos + (it & 7) * 32;
+        if (!tile_valid(info)) break;
         LAS uint8_t* slot = lds + (it % NSLOT) * SLOT;
-        const Tile T = tile_info(cur, spans + (it & 7) * 16);
-        const LAS uint32_t* ro = (const LAS uint32_t*)(slot + (MJ_RO8 ? T.ro_shift : 0u));
-        if (!LEN && NUTF8 && T.seg_first && !T.first) seg_prefix(cur, run, lane);
-        if (T.hbm == 2) {  // a tile over 4 GiB of blob bytes (unsupported): report; prefixes undefined
+        const Tile T = tile_read(spans + (it & 7) * 16, info, stage);
+        const LAS uint32_t* ro = (const LAS uint32_t*)slot;
+        const uint32_t ph = tile_phase(info);
+        if (MODE == 0 && T.b != prev_b) {
+#pragma unroll
+            for (uint32_t u = 0; u < NU; u++) run[u] = 0;  // local mode: a new block starts at 0
+            prev_b = T.b;
+        }
+        if (T.hbm == 2) {  // a tile over 4 GiB of blob bytes (unsupported): report; keep the protocol going
             if (wave == 0 && lane == 0) report(args()->err, err_key(T.b, T.r0, 0, kStMalformed));
-            if (!LEN && NUTF8 && lane == 0) __hip_atomic_fetch_add(pcnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (NUTF8) {
+                if (lane == 0) __hip_atomic_fetch_add((LAS uint32_t*)ctl, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (MODE == 1 && ph == 1 && T.seg_last && wave == 0 && args()->emit) {
+                    for (uint32_t u = 0; u < NU; u++)
+                        if (lane == 0) publish(args()->flags + T.t * NU + u, kPre);
+                    if (lane == 0) __hip_atomic_store((LAS uint32_t*)ctl + 1, (uint32_t)T.t + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                }
+            }
         } else if (T.hbm) {
-            decode_tile<LEN>(HbmSrc{gp(T.data) + T.abase}, T, ro, wt, run, nn, wave, lane, pcnt, NC * (it + 1));
-            __builtin_amdgcn_s_waitcnt(0x0F70);
+            const HbmSrc src{gp(T.data) + T.abase};
+            if (MODE == 0) decode_tile<SH, 0>(src, T, ro, ctl, run, L, wave, lane, it);
+            else if (ph == 1) decode_tile<SH, 1>(src, T, ro, ctl, run, L, wave, lane, it);
+            else decode_tile<SH, 2>(src, T, ro, ctl, run, L, wave, lane, it);
             // drain the cold path's loads here (a compiler-visible vmcnt(0)),
             // so none is pending into a register the hot path reuses
             __builtin_amdgcn_s_waitcnt(0x0F70);
         } else {
-            decode_tile<LEN>(StageSrc{slot + RO_BYTES}, T, ro, wt, run, nn, wave, lane, pcnt, NC * (it + 1));
+            const StageSrc src{slot + SH::RO_BYTES};
+            MJ_TIC
+            if (MODE == 0) decode_tile<SH, 0>(src, T, ro, ctl, run, L, wave, lane, it);
+            else if (ph == 1) decode_tile<SH, 1>(src, T, ro, ctl, run, L, wave, lane, it);
+            else decode_tile<SH, 2>(src, T, ro, ctl, run, L, wave, lane, it);
+            MJ_TOC(ph == 0 ? 6 : ph == 1 ? 4 : 5)
         }
-        if (T.seg_last) {
-            if (LEN) {  // this wave's share of the segment's utf8 bytes
-                for (uint32_t u = 0; u < NUTF8; u++)
-                    if (lane == 0 && run[u])
-                        __hip_atomic_fetch_add(gp(args()->seg_tot) + (uint64_t)cur.k * NU + u, (unsigned long long)run[u],
-                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            } else {
-                flush_nulls(T.b, nn, lane);
-            }
-            for (uint32_t u = 0; u < (NUTF8 ? NUTF8 : 1); u++) run[u] = 0;
+        {
+            MJ_TIC
+            lds_barrier();  // B_it+1
+            MJ_TOC(0)
         }
-        cur_next(cur);
-        lds_barrier();  // B_it+1
-        if (!cur.ok) break;
     }
+    lanes_flush(L, lane);
+#ifdef MJ_STAMPS
+    if (lane == 0)
+        __hip_atomic_fetch_add((GAS unsigned long long*)args()->err + 2 + 9, (unsigned long long)(__builtin_amdgcn_s_memtime() - ct0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
 }
 
 }  // namespace mj
 
-extern "C" __global__ void __launch_bounds__(64 * MJ_NW) murr_jit_decode(mj::Args) { mj::kernel_body<false>(); }
-extern "C" __global__ void __launch_bounds__(64 * MJ_NW) murr_jit_lengths(mj::Args) { mj::kernel_body<true>(); }
+#define MJ_KERNEL(NW, R)                                                                                   \
+    extern "C" __global__ void __launch_bounds__(64 * NW) murr_jit_decode_##NW##x##R(mj::Args) {           \
+        mj::kernel_body<NW, R, 0>();                                                                       \
+    }                                                                                                      \
+    extern "C" __global__ void __launch_bounds__(64 * NW) murr_jit_decode_split_##NW##x##R(mj::Args) {     \
+        mj::kernel_body<NW, R, 1>();                                                                       \
+    }
+MJ_KERNEL(5, 2)
+MJ_KERNEL(5, 1)
+MJ_KERNEL(3, 1)

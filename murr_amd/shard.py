@@ -1,10 +1,22 @@
-"""Key-range sharding across GPUs: one process per GPU, each
-decoding its own contiguous key range; no data-path collective.
+"""Sharding across GPUs.
 
-torch.distributed (gloo, CPU tensors) carries only the start/stop barriers and
-the max-over-ranks time / sum-over-ranks bytes the bench reports, so the data
-path never touches RCCL: every output cell depends on exactly one input row
-(src/io/row/read.rs:85-91) and the utf8 offset prefix is local to a block.
+Bulk decode (mode 1, bench.py): one process per GPU, each decoding its own
+contiguous key range; no data-path collective.  torch.distributed (gloo, CPU
+tensors) carries only the start/stop barriers and the max-over-ranks time /
+sum-over-ranks bytes the bench reports: every output cell depends on exactly
+one input row (src/io/row/read.rs:85-91) and the utf8 offset prefix is local
+to a block.
+
+Random-key reads (mode 2) across one process per GPU (`merge_reads`,
+`ShardedResidentTable`): every rank reads the caller's keys against its own
+shard and the caller-order batch is the byte-wise sum of the ranks' buffers,
+three all-reduces per read (validity / fixed values / bool bitmaps, utf8
+lengths, utf8 bytes).  That sum is only correct when every key lives on
+exactly one rank, so writes are routed by key (`shard_of`) and `write_shard`
+refuses keys this rank does not own.  The collective-free form of mode 2 (one
+process driving every GPU: keys routed on the host, rows gathered on their
+shard's GPU, one peer-copy gather to the caller's GPU) is
+`murr_amd.multigpu.MultiDeviceTable`.
 """
 from __future__ import annotations
 

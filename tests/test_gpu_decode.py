@@ -203,19 +203,26 @@ def test_many_blocks_one_launch(ctx, kernel_mode, nblocks):
             check_padding(got[b][p], len(blocks[b][1]) - 1)
 
 
-@pytest.mark.parametrize("seg_tiles", [1, 2, 7])
-def test_split_blocks_utf8_prefix(ctx, kernel_mode, monkeypatch, seg_tiles):
-    # few large blocks: the JIT kernel cuts them into segments whose utf8
-    # starting offsets come from the length pass (murr_jit_lengths)
-    monkeypatch.setenv("MURR_JIT_SEGTILES", str(seg_tiles))
-    rng = np.random.default_rng(40 + seg_tiles)
+@pytest.mark.parametrize("mode,shape,segtiles", [("split", "5x2", 0), ("split", "5x1", 0), ("split", "3x1", 0),
+                                                 ("split", "5x2", 1), ("split", "3x1", 2),
+                                                 ("local", "5x2", 0), ("local", "3x1", 0)])
+def test_split_blocks_utf8_prefix(ctx, kernel_mode, monkeypatch, mode, shape, segtiles):
+    # few large blocks: in split mode the JIT kernel cuts them into segments
+    # (two passes each) and each segment's utf8 starting offsets come from
+    # the decoupled look-back over its predecessors; local mode walks every
+    # block in one workgroup (forced here to cover it on few blocks)
+    monkeypatch.setenv("MURR_JIT_MODE", mode)
+    monkeypatch.setenv("MURR_JIT_SHAPE", shape)
+    if segtiles:
+        monkeypatch.setenv("MURR_JIT_SEGTILES", str(segtiles))
+    rng = np.random.default_rng(40 + len(mode) + int(shape[0]) + segtiles)
     dtypes = [D.Utf8, D.Int16, D.Utf8, D.Bool, D.Float64]
     oseg = O.Segment([int(d) for d in dtypes])
     proj = [2, 0, 1, 3, 4, 0]
     blocks, wants = [], []
-    for n in [30000, 513, 7777]:
+    for n in [30000, 513, 0, 7777, 1]:
         cols = random_columns(rng, dtypes, n, null_p=0.15, max_str=30)
-        miss = set(rng.choice(n, size=n // 9, replace=False).tolist())
+        miss = set(rng.choice(n, size=n // 9, replace=False).tolist()) if n else set()
         _, data, off = oracle_block(dtypes, cols, n, miss)
         blocks.append((data, off))
         wants.append(O.decode_block(oseg, proj, data, off))
@@ -224,6 +231,26 @@ def test_split_blocks_utf8_prefix(ctx, kernel_mode, monkeypatch, seg_tiles):
     for b in range(len(blocks)):
         for p in range(len(proj)):
             assert_array_equal(got[b][p], wants[b][p], f"block {b} proj {p}")
+
+
+def test_split_many_segments_look_back(ctx, kernel_mode, monkeypatch):
+    # one block cut into more than 512 one-tile segments: look-backs that span
+    # several 512-segment windows and several rounds of the grid
+    monkeypatch.setenv("MURR_JIT_MODE", "split")
+    monkeypatch.setenv("MURR_JIT_SHAPE", "3x1")
+    monkeypatch.setenv("MURR_JIT_SEGTILES", "1")
+    rng = np.random.default_rng(4242)
+    dtypes = [D.Utf8, D.Int32, D.Utf8]
+    oseg = O.Segment([int(d) for d in dtypes])
+    proj = [0, 2, 1]
+    n = 150000
+    cols = random_columns(rng, dtypes, n, null_p=0.1, max_str=12)
+    miss = set(rng.choice(n, size=n // 50, replace=False).tolist())
+    _, data, off = oracle_block(dtypes, cols, n, miss)
+    got = gpu_decode(ctx, seg_of(dtypes), proj, [(data, off)])[0]
+    want = O.decode_block(oseg, proj, data, off)
+    for p in range(len(proj)):
+        assert_array_equal(got[p], want[p], f"proj {p}")
 
 
 def test_wide_schema_multi_byte_bitset(ctx, kernel_mode):

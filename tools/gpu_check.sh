@@ -16,7 +16,7 @@ step() {  # step <name> <timeout> <cmd...>
 rocm-smi --showproductname > gpurun_out/smi.log 2>&1 || true
 lscpu > gpurun_out/lscpu.log 2>&1 || true
 step smoke 180 python -c "import __graft_entry__ as g; g.smoke()"
-step pytest_gpu 600 python -m pytest tests -m gpu -x -q ${PYTEST_ARGS:-}
+step pytest_gpu 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread ${PYTEST_ARGS:-}
 step bench 380 python bench.py ${BENCH_ARGS:-}
 if [ -n "${PROFILE:-}" ]; then
   step rocprof 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o decode -- python3 bench.py --steps 5 --warmup 1 --no-cpu

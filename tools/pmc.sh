@@ -3,13 +3,14 @@
 # domains combined with --pmc).  Outputs under gpurun_out/pmc/.
 set -u
 export TMPDIR=/tmp
-mkdir -p gpurun_out/pmc
+OUT=${OUT:-gpurun_out/pmc}
+mkdir -p $OUT
 ARGS=${BENCH_ARGS:-"--steps 3 --warmup 1 --no-cpu"}
 i=0
 while read -r counters; do
   [ -z "$counters" ] && continue
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --pmc $counters --output-format csv -d gpurun_out/pmc -o pass$i -- python3 bench.py $ARGS > gpurun_out/pmc/pass$i.log 2>&1
+  timeout -k 10 300 rocprofv3 --pmc $counters --output-format csv -d $OUT -o pass$i -- python3 bench.py $ARGS > $OUT/pass$i.log 2>&1
   rc=$?
   echo "pass$i ($counters) exit=$rc"
   case $rc in 0) ;; *) exit $rc ;; esac
