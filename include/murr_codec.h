@@ -137,7 +137,18 @@ int murr_host_free(murr_ctx_t* ctx, void* p);
 int murr_memcpy_h2d(murr_ctx_t* ctx, void* dst, const void* src, uint64_t bytes);
 int murr_memcpy_d2h(murr_ctx_t* ctx, void* dst, const void* src, uint64_t bytes);
 int murr_memset_dev(murr_ctx_t* ctx, void* dst, int value, uint64_t bytes);
+int murr_memcpy_d2d(murr_ctx_t* ctx, void* dst, const void* src, uint64_t bytes);
 int murr_sync(murr_ctx_t* ctx);
+
+/* Compile (or load from the code-object cache) the decode and encode kernels
+ * of a segment layout on the context's device.  Table::create / Table::open
+ * (src/io/table/mod.rs:28-52, 131-154) are where a layout becomes known, so
+ * calling this there keeps run-time compilation off the read and write paths:
+ * the decode kernel is specialised on the layout only, and every projection
+ * of the table (Table::read's `columns`, src/io/table/mod.rs:114-123) runs
+ * the same code object.  Without it the first decode / encode of a layout
+ * compiles.  Synchronous. */
+int murr_segment_prepare(murr_ctx_t* ctx, const murr_segment_t* seg);
 
 /* ---- device-resident decode (row blobs -> Arrow) ------------------------- */
 
@@ -221,6 +232,16 @@ int murr_encode_batch(murr_ctx_t* ctx, const murr_segment_t* seg,
                       uint64_t* out_row_off, uint64_t* blob_len,
                       murr_error_t* err);
 
+/* murr_encode_batch writing row offsets from `row_base`: out_row_off[i] =
+ * row_base + (offset of row i in out_blob), so a batch can be encoded straight
+ * onto the tail of a growing blob arena whose offsets array already holds the
+ * earlier rows (MemoryStore::write appends, src/io/store/memory.rs:47-60).
+ * *blob_len = bytes written to out_blob. */
+int murr_encode_batch_at(murr_ctx_t* ctx, const murr_segment_t* seg,
+                         const murr_col_in_t* cols, uint64_t n_rows,
+                         uint8_t* out_blob, uint64_t blob_cap, uint64_t* out_row_off,
+                         uint64_t row_base, uint64_t* blob_len, murr_error_t* err);
+
 /* ---- host-memory path (pinned staging + hipMemcpyAsync both ways) -------- */
 
 /* Batched ReadBatchBuilder (src/io/row/read.rs:62-110) for the store-driven
@@ -290,6 +311,15 @@ typedef struct murr_index murr_index_t;
 int murr_index_build(murr_ctx_t* ctx, const uint8_t* key_data, const int32_t* key_offsets,
                      uint64_t key_offset, uint64_t n, murr_index_t** out, murr_error_t* err);
 void murr_index_free(murr_index_t* idx);
+/* Append n keys as rows idx.n .. idx.n + n - 1 (Table::write into a table that
+ * already holds rows, src/io/table/mod.rs:54-112 -> Store::write,
+ * src/io/store/memory.rs:47-60): a key written again now maps to its new
+ * row (later write wins).  The key copy grows by doubling and the slot table
+ * is rehashed only when the load would pass 1/2, so an append costs in
+ * proportion to the batch (amortised).  Synchronous. */
+int murr_index_append(murr_ctx_t* ctx, murr_index_t* idx, const uint8_t* key_data,
+                      const int32_t* key_offsets, uint64_t key_offset, uint64_t n,
+                      murr_error_t* err);
 /* Rows indexed (n at build) and hash-table slots. */
 int murr_index_info(const murr_index_t* idx, uint64_t* n, uint64_t* slots);
 
@@ -305,11 +335,20 @@ int murr_index_lookup(murr_ctx_t* ctx, const murr_index_t* idx, const uint8_t* q
  * lookup.  needed (optional, device u64) receives the block bytes; offsets
  * are clamped to out_cap, so when *needed > out_cap the block is cut short
  * (rows past the cap read as missing) -- size out_cap as nq * the longest row
- * to rule that out.  Feed the result to murr_decode_enqueue as one block. */
+ * to rule that out.  Feed the result to murr_decode_enqueue as one block.
+ * Two-phase form (exact sizing): out_data == NULL runs the lookup and the
+ * offsets only (rows and needed required, offsets not clamped); read
+ * *needed, allocate that many bytes, then murr_index_gather_copy. */
 int murr_index_gather(murr_ctx_t* ctx, const murr_index_t* idx, const uint8_t* q_data,
                       const int32_t* q_offsets, uint64_t nq, const uint8_t* blob,
                       const uint64_t* row_off, uint8_t* out_data, uint64_t out_cap,
                       uint64_t* out_row_off, uint32_t* rows, uint64_t* needed);
+
+/* Second phase of a two-phase gather: copy the rows the first phase looked up
+ * (rows[nq], out_row_off[nq + 1] from murr_index_gather with out_data NULL)
+ * into out_data (16-B aligned, *needed bytes).  Enqueue. */
+int murr_index_gather_copy(murr_ctx_t* ctx, const uint32_t* rows, uint64_t nq, const uint8_t* blob,
+                           const uint64_t* row_off, const uint64_t* out_row_off, uint8_t* out_data);
 
 /* ---- Arrow IPC framing --------------------------- */
 

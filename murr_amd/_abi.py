@@ -67,6 +67,7 @@ U32, U64, I32 = C.c_uint32, C.c_uint64, C.c_int
 SIGNATURES = {
     "murr_dtype_size": (I32, [U32]),
     "murr_segment_init": (I32, [C.POINTER(U32), U32, C.POINTER(Column), C.POINTER(Segment)]),
+    "murr_segment_prepare": (I32, [P, C.POINTER(Segment)]),
     "murr_bitmap_bytes": (U64, [U64]),
     "murr_ctx_create": (I32, [I32, PP]),
     "murr_ctx_destroy": (None, [P]),
@@ -80,6 +81,7 @@ SIGNATURES = {
     "murr_host_free": (I32, [P, P]),
     "murr_memcpy_h2d": (I32, [P, P, P, U64]),
     "murr_memcpy_d2h": (I32, [P, P, P, U64]),
+    "murr_memcpy_d2d": (I32, [P, P, P, U64]),
     "murr_memset_dev": (I32, [P, P, I32, U64]),
     "murr_sync": (I32, [P]),
     "murr_decode_blocks": (I32, [P, C.POINTER(Segment), C.POINTER(U32), U32, C.POINTER(Block), U32,
@@ -90,6 +92,8 @@ SIGNATURES = {
     "murr_encode_bound": (U64, [C.POINTER(Segment), U64, C.POINTER(U64)]),
     "murr_encode_batch": (I32, [P, C.POINTER(Segment), C.POINTER(ColIn), U64, P, U64, P,
                                 C.POINTER(U64), C.POINTER(Error)]),
+    "murr_encode_batch_at": (I32, [P, C.POINTER(Segment), C.POINTER(ColIn), U64, P, U64, P, U64,
+                                   C.POINTER(U64), C.POINTER(Error)]),
     "murr_builder_new": (I32, [P, C.POINTER(Segment), C.POINTER(U32), U32, U64, PP]),
     "murr_builder_add_row": (I32, [P, P, U64]),
     "murr_builder_add_empty": (I32, [P]),
@@ -103,9 +107,11 @@ SIGNATURES = {
                                C.POINTER(C.POINTER(C.c_uint64)), C.POINTER(Error)]),
     "murr_index_build": (I32, [P, P, P, U64, U64, PP, C.POINTER(Error)]),
     "murr_index_free": (None, [P]),
+    "murr_index_append": (I32, [P, P, P, P, U64, U64, C.POINTER(Error)]),
     "murr_index_info": (I32, [P, C.POINTER(U64), C.POINTER(U64)]),
     "murr_index_lookup": (I32, [P, P, P, P, U64, P]),
     "murr_index_gather": (I32, [P, P, P, P, U64, P, P, P, U64, P, P, P]),
+    "murr_index_gather_copy": (I32, [P, P, U64, P, P, P, P]),
     "murr_ipc_schema": (I32, [C.POINTER(Segment), C.POINTER(U32), U32, C.POINTER(C.c_char_p), U32, P, U64,
                               C.POINTER(U64)]),
     "murr_ipc_batch_host": (I32, [C.POINTER(Segment), C.POINTER(U32), U32, C.POINTER(HostArray), U64, U32, P,

@@ -97,12 +97,13 @@ struct murr_ctx {
 // Device key index (murr_index.hip): the keys' own copy and the slot table.
 struct murr_index {
     int device = 0;
-    uint8_t* key_data = nullptr;
-    int32_t* key_off = nullptr;
+    uint8_t* key_data = nullptr;    // the keys, back to back (grows by doubling)
+    int32_t* key_off = nullptr;     // n + 1 offsets into key_data (grows by doubling)
     uint64_t* slots = nullptr;
     uint64_t* loc = nullptr;
     unsigned long long* err = nullptr;
     uint64_t n = 0, mask = 0;
+    uint64_t key_bytes = 0, key_cap = 0, off_cap = 0;
 };
 
 namespace {
@@ -114,6 +115,23 @@ int hip_fail(murr_error_t* err, hipError_t e) { return set_err(err, MURR_E_HIP, 
         hipError_t _e = (expr);                             \
         if (_e != hipSuccess) return hip_fail(err, _e);     \
     } while (0)
+
+// Grow a device buffer to at least `need` bytes (doubling), keeping `keep` bytes.
+template <class T>
+int grow(murr_ctx* c, T** p, uint64_t* cap, uint64_t need, uint64_t keep, murr_error_t* err) {
+    if (need <= *cap && *p) return MURR_OK;
+    uint64_t ncap = std::max<uint64_t>(std::max<uint64_t>(need, 2 * *cap), 256);
+    T* q = nullptr;
+    HIPC(hipMalloc(&q, ncap));
+    if (keep && *p) HIPC(hipMemcpyAsync(q, *p, keep, hipMemcpyDeviceToDevice, c->stream));
+    if (*p) {
+        HIPC(hipStreamSynchronize(c->stream));
+        HIPC(hipFree(*p));
+    }
+    *p = q;
+    *cap = ncap;
+    return MURR_OK;
+}
 
 int ensure_ws(murr_ctx* c, uint64_t bytes, murr_error_t* err) {
     if (bytes <= c->ws_cap) return MURR_OK;
@@ -171,40 +189,73 @@ int murr_index_build(murr_ctx_t* c, const uint8_t* key_data, const int32_t* key_
     HIPC(hipSetDevice(c->device));
     std::unique_ptr<murr_index, void (*)(murr_index*)> x(new murr_index, murr_index_free);
     x->device = c->device;
-    x->n = n;
-    uint64_t slots = 64;
-    while (slots < 2 * n) slots <<= 1;
-    x->mask = slots - 1;
-    // the key bytes up to the last key's end (offsets keep their values)
-    int32_t last = 0;
-    if (n) {
-        HIPC(hipMemcpyAsync(&last, key_offsets + key_offset + n, 4, hipMemcpyDeviceToHost, c->stream));
-        HIPC(hipStreamSynchronize(c->stream));
-        if (last < 0) return set_err(err, MURR_E_ARGUMENT);
-    }
-    HIPC(hipMalloc(&x->key_data, std::max<uint64_t>((uint64_t)last, 16)));
-    HIPC(hipMalloc(&x->key_off, 4 * (n + 1)));
-    HIPC(hipMalloc(&x->slots, 8 * slots));
-    HIPC(hipMalloc(&x->loc, 8 * slots));
     HIPC(hipMalloc(&x->err, 8));
-    if (last) HIPC(hipMemcpyAsync(x->key_data, key_data, (uint64_t)last, hipMemcpyDeviceToDevice, c->stream));
-    if (n) HIPC(hipMemcpyAsync(x->key_off, key_offsets + key_offset, 4 * (n + 1), hipMemcpyDeviceToDevice, c->stream));
-    HIPC(hipMemsetAsync(x->slots, 0xFF, 8 * slots, c->stream));
     HIPC(hipMemsetAsync(x->err, 0, 8, c->stream));
+    const int st = murr_index_append(c, x.get(), key_data, key_offsets, key_offset, n, err);
+    if (st) return st;
+    *out = x.release();
+    return MURR_OK;
+}
+
+
+int murr_index_append(murr_ctx_t* c, murr_index_t* x, const uint8_t* key_data, const int32_t* key_offsets,
+                      uint64_t key_offset, uint64_t n, murr_error_t* err) {
+    if (!c || !x || x->device != c->device || c->pending || (n && (!key_data || !key_offsets)) ||
+        x->n + n >= kMissing)
+        return set_err(err, MURR_E_ARGUMENT);
+    HIPC(hipSetDevice(c->device));
+    // the appended keys' byte range [first, last) in key_data
+    int32_t ends[2] = {0, 0};
+    if (n) {
+        HIPC(hipMemcpyAsync(&ends[0], key_offsets + key_offset, 4, hipMemcpyDeviceToHost, c->stream));
+        HIPC(hipMemcpyAsync(&ends[1], key_offsets + key_offset + n, 4, hipMemcpyDeviceToHost, c->stream));
+        HIPC(hipStreamSynchronize(c->stream));
+        if (ends[0] < 0 || ends[1] < ends[0]) return set_err(err, MURR_E_ARGUMENT);
+    }
+    const uint64_t bytes = (uint64_t)(ends[1] - ends[0]);
+    if (x->key_bytes + bytes > 0x7FFFFFFFull) return set_err(err, MURR_E_OFFSET_OVERFLOW);
+    int st = grow(c, &x->key_data, &x->key_cap, x->key_bytes + bytes + 16, x->key_bytes, err);
+    if (!st) st = grow(c, &x->key_off, &x->off_cap, 4 * (x->n + n + 1), 4 * (x->n + 1), err);
+    if (st) return st;
+    if (x->n == 0) HIPC(hipMemsetAsync(x->key_off, 0, 4, c->stream));
+    if (bytes) HIPC(hipMemcpyAsync(x->key_data + x->key_bytes, key_data + ends[0], bytes, hipMemcpyDeviceToDevice, c->stream));
+    // offsets of keys n_old + 1 .. n_old + n, rebased onto the key copy
+    HIPC(launch_offsets_rebase(x->key_off + x->n + 1, key_offsets + key_offset + 1, n,
+                               (int64_t)x->key_bytes - ends[0], c->stream));
+    const uint64_t n0 = x->n, total = x->n + n;
     IndexArgs a{};
     a.key_data = x->key_data;
     a.key_off = x->key_off;
+    a.err = x->err;
+    uint64_t slots = x->mask + 1;
+    if (!x->slots || 2 * total > slots) {
+        // rehash: a table of >= 2 * total slots, every key inserted again
+        slots = 64;
+        while (slots < 2 * total) slots <<= 1;
+        if (x->slots) HIPC(hipFree(x->slots));
+        if (x->loc) HIPC(hipFree(x->loc));
+        x->slots = nullptr;
+        x->loc = nullptr;
+        HIPC(hipMalloc(&x->slots, 8 * slots));
+        HIPC(hipMalloc(&x->loc, 8 * slots));
+        HIPC(hipMemsetAsync(x->slots, 0xFF, 8 * slots, c->stream));
+        x->mask = slots - 1;
+        a.base = 0;
+        a.n = total;
+    } else {
+        a.base = n0;
+        a.n = n;
+    }
     a.slots = x->slots;
     a.loc = x->loc;
     a.mask = x->mask;
-    a.n = n;
-    a.err = x->err;
     HIPC(launch_index_insert(a, c->stream));
     unsigned long long word = 0;
     HIPC(hipMemcpyAsync(&word, x->err, 8, hipMemcpyDeviceToHost, c->stream));
     HIPC(hipStreamSynchronize(c->stream));
     if (word) return set_err(err, MURR_E_INTERNAL);
-    *out = x.release();
+    x->n = total;
+    x->key_bytes += bytes;
     return MURR_OK;
 }
 
@@ -247,8 +298,11 @@ int murr_index_gather(murr_ctx_t* c, const murr_index_t* x, const uint8_t* q_dat
                       uint64_t nq, const uint8_t* blob, const uint64_t* row_off, uint8_t* out_data,
                       uint64_t out_cap, uint64_t* out_row_off, uint32_t* rows, uint64_t* needed) {
     murr_error_t* err = nullptr;
+    // out_data == NULL: the first phase of a two-phase gather (lookup, sizes
+    // and their scan; offsets unclamped, *needed exact), rows required
+    const bool scan_only = out_data == nullptr;
     if (!c || !x || x->device != c->device || c->pending || !out_row_off ||
-        (nq && (!q_data || !q_offsets || !row_off || (x->n && !blob) || !out_data)))
+        (nq && (!q_data || !q_offsets || !row_off || (x->n && !blob))) || (scan_only && nq && (!rows || !needed)))
         return MURR_E_ARGUMENT;
     if (nq >= kMissing || ((uintptr_t)out_data & 15)) return MURR_E_ARGUMENT;
     HIPC(hipSetDevice(c->device));
@@ -272,7 +326,31 @@ int murr_index_gather(murr_ctx_t* c, const murr_index_t* x, const uint8_t* q_dat
     a.out_cap = out_cap;
     a.needed = needed;
     a.scratch = c->aux;
-    HIPC(launch_gather(a, c->stream));  // probe included
+    if (scan_only) {
+        a.out_cap = ~0ull;
+        HIPC(launch_gather_scan(a, c->stream));
+    } else {
+        HIPC(launch_gather(a, c->stream));  // probe included
+    }
+    return MURR_OK;
+}
+
+int murr_index_gather_copy(murr_ctx_t* c, const uint32_t* rows, uint64_t nq, const uint8_t* blob,
+                           const uint64_t* row_off, const uint64_t* out_row_off, uint8_t* out_data) {
+    murr_error_t* err = nullptr;
+    if (!c || c->pending || (nq && (!rows || !row_off || !out_row_off || !out_data)) || nq >= kMissing ||
+        ((uintptr_t)out_data & 15))
+        return MURR_E_ARGUMENT;
+    HIPC(hipSetDevice(c->device));
+    IndexArgs a{};
+    a.nq = nq;
+    a.rows = const_cast<uint32_t*>(rows);
+    a.blob = blob;
+    a.row_off = row_off;
+    a.sizes = const_cast<uint64_t*>(out_row_off);
+    a.out = out_data;
+    a.out_cap = ~0ull;
+    HIPC(launch_gather_copy(a, c->stream));
     return MURR_OK;
 }
 
@@ -420,6 +498,15 @@ int murr_memcpy_d2h(murr_ctx_t* c, void* dst, const void* src, uint64_t n) {
     if (!c) return MURR_E_ARGUMENT;
     if (!n) return MURR_OK;
     HIPC(hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToHost, c->stream));
+    HIPC(hipStreamSynchronize(c->stream));
+    return MURR_OK;
+}
+
+int murr_memcpy_d2d(murr_ctx_t* c, void* dst, const void* src, uint64_t n) {
+    murr_error_t* err = nullptr;
+    if (!c) return MURR_E_ARGUMENT;
+    if (!n) return MURR_OK;
+    HIPC(hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToDevice, c->stream));
     HIPC(hipStreamSynchronize(c->stream));
     return MURR_OK;
 }
@@ -666,6 +753,27 @@ int decode_enqueue_jit(murr_ctx* c, const murr_segment_t* seg, const JitLayout* 
 
 }  // namespace
 
+
+int murr_segment_prepare(murr_ctx_t* c, const murr_segment_t* seg) {
+    murr_error_t* err = nullptr;
+    if (!c || !valid_segment(seg)) return MURR_E_ARGUMENT;
+    HIPC(hipSetDevice(c->device));
+    std::string why;
+    if (seg->ncols && !jit_layout(c->device, seg, &why)) {
+        std::fprintf(stderr, "murr: JIT decode unavailable: %s\n", why.c_str());
+        return MURR_E_INTERNAL;
+    }
+    std::vector<EncCol> ec(seg->ncols);
+    for (uint32_t i = 0; i < seg->ncols; i++) {
+        const murr_column_t& col = seg->cols[i];
+        ec[i] = EncCol{nullptr, nullptr, nullptr, 0, col.dtype, col.index, col.offset, col.size};
+    }
+    if (seg->ncols && !jit_encode_kernel(c->device, seg->bitset_size, seg->capacity, ec.data(), seg->ncols, &why)) {
+        std::fprintf(stderr, "murr: JIT encode unavailable: %s\n", why.c_str());
+        return MURR_E_INTERNAL;
+    }
+    return MURR_OK;
+}
 
 int murr_decode_enqueue(murr_ctx_t* c, const murr_segment_t* seg, const uint32_t* proj,
                         uint32_t nproj, const murr_block_t* blocks, uint32_t nblocks,
@@ -963,6 +1071,12 @@ uint64_t murr_encode_bound(const murr_segment_t* seg, uint64_t n, const uint64_t
 int murr_encode_batch(murr_ctx_t* c, const murr_segment_t* seg, const murr_col_in_t* cols,
                       uint64_t n, uint8_t* out_blob, uint64_t blob_cap, uint64_t* out_row_off,
                       uint64_t* blob_len, murr_error_t* err) {
+    return murr_encode_batch_at(c, seg, cols, n, out_blob, blob_cap, out_row_off, 0, blob_len, err);
+}
+
+int murr_encode_batch_at(murr_ctx_t* c, const murr_segment_t* seg, const murr_col_in_t* cols,
+                         uint64_t n, uint8_t* out_blob, uint64_t blob_cap, uint64_t* out_row_off,
+                         uint64_t row_base, uint64_t* blob_len, murr_error_t* err) {
     if (!c || !valid_segment(seg) || (seg->ncols && !cols) || !out_row_off || c->pending)
         return set_err(err, MURR_E_ARGUMENT);
     if (n > 0xFFFFFFFFull * kTile) return set_err(err, MURR_E_ARGUMENT);
@@ -997,8 +1111,9 @@ int murr_encode_batch(murr_ctx_t* c, const murr_segment_t* seg, const murr_col_i
     HIPC(hipMemsetAsync(c->ws, 0, zbytes, c->stream));
     if (!ec.empty()) HIPC(hipMemcpyAsync(c->ws + d_cols, c->hs, sizeof(EncCol) * ec.size(),
                                          hipMemcpyHostToDevice, c->stream));
-    if (n == 0) HIPC(hipMemsetAsync(out_row_off, 0, 8, c->stream));
+    if (n == 0) HIPC(hipMemcpyAsync(out_row_off, &row_base, 8, hipMemcpyHostToDevice, c->stream));
     EncodeArgs a{};
+    a.row_base = row_base;
     a.cols = (const EncCol*)(c->ws + d_cols);
     a.out = out_blob;
     a.row_off = out_row_off;
@@ -1046,6 +1161,7 @@ int murr_encode_batch(murr_ctx_t* c, const murr_segment_t* seg, const murr_col_i
     uint64_t total;
     std::memcpy(&word, c->hs + rb, 8);
     std::memcpy(&total, c->hs + rb + 8, 8);
+    total -= row_base;
     if (blob_len) *blob_len = total;
     if (err) std::memset(err, 0, sizeof *err);
     st = unpack_err(word, err);

@@ -105,8 +105,8 @@ __device__ __forceinline__ bool key_eq(const GAS uint8_t* a, const KeyChunk& qc,
 }
 
 __global__ void __launch_bounds__(256) index_insert(IndexArgs A) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= A.n) return;
+    const uint64_t i = A.base + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;  // key i is row i
+    if (i >= A.base + A.n) return;
     const GAS int32_t* ko = gp(A.key_off);
     const int32_t k0 = ko[i], k1 = ko[i + 1];
     const uint32_t len = (uint32_t)(k1 - k0);
@@ -344,7 +344,7 @@ hipError_t launch_index_probe(const IndexArgs& a, hipStream_t s) {
 
 uint64_t gather_scan_groups(uint64_t nq) { return (nq + kScanGroup - 1) / kScanGroup; }
 
-hipError_t launch_gather(const IndexArgs& a, hipStream_t s) {
+hipError_t launch_gather_scan(const IndexArgs& a, hipStream_t s) {
     const uint64_t groups = gather_scan_groups(a.nq);
     if (a.nq <= kScanThreads) {
         hipLaunchKernelGGL(gather_probe_scan, dim3(1), dim3(kScanThreads), 0, s, a);
@@ -359,12 +359,37 @@ hipError_t launch_gather(const IndexArgs& a, hipStream_t s) {
             hipLaunchKernelGGL(gather_scan, dim3((uint32_t)groups), dim3(kScanThreads), 0, s, a, 1u);
         }
     }
+    return hipGetLastError();
+}
+
+hipError_t launch_gather_copy(const IndexArgs& a, hipStream_t s) {
     if (a.nq) {
         // eight lanes per row (measured best of 4 / 8 / 16 on config C rows)
         constexpr uint32_t rows_per_wg = 256 / 8;
         const dim3 grid((uint32_t)((a.nq + rows_per_wg - 1) / rows_per_wg));
         hipLaunchKernelGGL(gather_copy<8>, grid, dim3(256), 0, s, a);
     }
+    return hipGetLastError();
+}
+
+hipError_t launch_gather(const IndexArgs& a, hipStream_t s) {
+    const hipError_t e = launch_gather_scan(a, s);
+    if (e != hipSuccess) return e;
+    return launch_gather_copy(a, s);
+}
+
+namespace {
+__global__ void __launch_bounds__(256) offsets_rebase(int32_t* dst, const int32_t* src, uint64_t n, int64_t add) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) gp(dst)[i] = (int32_t)((int64_t)gp(src)[i] + add);
+}
+}  // namespace
+
+// dst[i] = src[i] + add for i < n (an appended key column's offsets into the
+// index's key copy).
+hipError_t launch_offsets_rebase(int32_t* dst, const int32_t* src, uint64_t n, int64_t add, hipStream_t s) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(offsets_rebase, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, dst, src, n, add);
     return hipGetLastError();
 }
 

@@ -82,11 +82,12 @@ struct EncCol {               // one Arrow input column, segment order
 struct EncodeArgs {
     const EncCol* cols;
     uint8_t* out;
-    uint64_t* row_off;           // n_rows + 1
+    uint64_t* row_off;           // n_rows + 1, written as row_base + offset in out
     uint64_t* lookback;          // [total_tiles]
     unsigned long long* err;     // max of ~key
     uint64_t n_rows, out_cap, total_tiles;
     uint32_t ncols, nutf8, bs, cap;
+    uint64_t row_base;
 };
 
 // Packed first-error key: block(18) | row(32) | column(10) | status(4); the
@@ -166,6 +167,7 @@ struct IndexArgs {
     uint64_t* loc;              // mask + 1 entries {key start:32 | key length:32}
     uint64_t mask;
     uint64_t n;
+    uint64_t base;              // insert: keys (and rows) base .. base + n - 1
     unsigned long long* err;
     const uint8_t* q_data;      // query keys (Arrow utf8)
     const int32_t* q_off;       // nq + 1
@@ -183,6 +185,9 @@ hipError_t launch_index_insert(const IndexArgs& a, hipStream_t s);
 hipError_t launch_index_probe(const IndexArgs& a, hipStream_t s);
 uint64_t gather_scan_groups(uint64_t nq);
 hipError_t launch_gather(const IndexArgs& a, hipStream_t s);
+hipError_t launch_gather_scan(const IndexArgs& a, hipStream_t s);  // probe + sizes + scan, no copy
+hipError_t launch_gather_copy(const IndexArgs& a, hipStream_t s);  // the copy of a scanned gather
+hipError_t launch_offsets_rebase(int32_t* dst, const int32_t* src, uint64_t n, int64_t add, hipStream_t s);
 
 // Arrow IPC framing (murr_ipc.cpp, murr_ipc.hip).
 enum : uint32_t { kIpcValidity = 0, kIpcOffsets = 1, kIpcValues = 2 };

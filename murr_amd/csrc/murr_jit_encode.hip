@@ -58,6 +58,7 @@ struct Args {  // = murr::EncodeArgs
     unsigned long long* err;
     uint64_t n_rows, out_cap, total_tiles;
     uint32_t ncols, nutf8, bs, cap;
+    uint64_t row_base;       // row_off values are row_base + offset in out
 };
 
 constexpr uint32_t TILE = 256, BS = MJE_BS, CAP = MJE_CAP, NCOLS = MJE_NCOLS, NUTF8 = MJE_NUTF8,
@@ -305,8 +306,8 @@ extern "C" __global__ void __launch_bounds__(256) murr_jit_encode(mje::Args) {
             span = agg;
         }
         if (active) {
-            gp(A->row_off)[row] = start;
-            if (row + 1 == n_rows) gp(A->row_off)[row + 1] = start + size;
+            gp(A->row_off)[row] = A->row_base + start;
+            if (row + 1 == n_rows) gp(A->row_off)[row + 1] = A->row_base + start + size;
         }
         if (tstart + span > out_cap) {
             if (tid == 0) report(A->err, err_key(0, r0, 0, kStCapacity));

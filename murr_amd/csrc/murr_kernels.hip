@@ -164,8 +164,8 @@ __global__ void __launch_bounds__(256) encode_kernel(EncodeArgs A) {
             span = agg;
         }
         if (active) {
-            A.row_off[row] = start;
-            if (row + 1 == A.n_rows) A.row_off[row + 1] = start + size;
+            A.row_off[row] = A.row_base + start;
+            if (row + 1 == A.n_rows) A.row_off[row + 1] = A.row_base + start + size;
         }
         if (tstart + span > A.out_cap) {
             if (tid == 0) report(A.err, err_key(0, r0, 0, kStCapacity));

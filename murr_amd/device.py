@@ -102,6 +102,12 @@ class DeviceBuffer:
                          what="d2h")
         return out
 
+    def copy_from(self, src: "DeviceBuffer", nbytes: int, dst_offset: int = 0, src_offset: int = 0):
+        """Device-to-device copy of nbytes (synchronous)."""
+        if nbytes:
+            raise_status(self.ctx.L.murr_memcpy_d2d(self.ctx.h, self.ptr + dst_offset, src.ptr + src_offset, nbytes),
+                         what="murr_memcpy_d2d")
+
     def memset(self, value: int = 0):
         raise_status(self.ctx.L.murr_memset_dev(self.ctx.h, self.ptr, value, self.nbytes), what="memset")
 

@@ -11,9 +11,11 @@ exactly as they do: request order, duplicates allowed, missing keys as all-null
 rows, later writes of a key win.
 
 `write` keeps Table::write's validation (src/io/table/mod.rs:54-96) and
-encodes on the device (murr_encode_batch).  A write appends to the resident
-set: the batches are re-encoded together and the index rebuilt, which suits a
-bulk-loaded hot set (one load, many reads) rather than a write-heavy table.
+appends like MemoryStore::write (src/io/store/memory.rs:47-60): the batch is
+encoded on the device straight onto the tail of a blob arena
+(murr_encode_batch_at; arena and row offsets grow by doubling) and only its
+keys go into the index (murr_index_append: a key written again maps to its
+new row, later write wins).  An append costs in proportion to the batch.
 """
 from __future__ import annotations
 
@@ -23,7 +25,7 @@ import numpy as np
 import pyarrow as pa
 
 from . import _abi
-from .device import Context, DecodeOutputs, DeviceBlock, decode_blocks, download_array, encode_batch
+from .device import Context, DecodeOutputs, DeviceBlock, decode_blocks, download_array
 from .errors import SegmentError, raise_status
 from .schema import DTypeName, TableSchema
 from .store import Store
@@ -81,6 +83,16 @@ class DeviceIndex:
         data.free()
         offs.free()
 
+    def append(self, keys: pa.Array):
+        """murr_index_append: rows n .. n + len(keys) - 1."""
+        data, offs = _upload_utf8(self.ctx, keys)
+        err = _abi.Error()
+        st = self.ctx.L.murr_index_append(self.ctx.h, self.h, data.ptr, offs.ptr, 0, len(keys), C.byref(err))
+        raise_status(st, err, "murr_index_append")
+        self.n += len(keys)
+        data.free()
+        offs.free()
+
     def info(self):
         n, slots = C.c_uint64(), C.c_uint64()
         raise_status(self.ctx.L.murr_index_info(self.h, C.byref(n), C.byref(slots)), what="murr_index_info")
@@ -107,6 +119,29 @@ class DeviceIndex:
             pass
 
 
+def row_sizes(segment, arrays) -> np.ndarray:
+    """Blob bytes of every row of a batch (WriteRow, src/io/row/write.rs:19-52):
+    bs + cap, plus 4 + len per non-null utf8 cell.  Host arithmetic on the Arrow
+    offsets and validity only."""
+    n = len(arrays[0]) if arrays else 0
+    size = np.full(n, segment.bitset_size + segment.capacity, np.int64)
+    for col, a in zip(segment.columns, arrays):
+        if col.dtype != DTypeName.Utf8 or n == 0:
+            continue
+        offs = np.frombuffer(a.buffers()[1], np.int32)[a.offset:a.offset + n + 1].astype(np.int64)
+        lens = np.diff(offs) + 4
+        if a.null_count:
+            valid = np.unpackbits(np.frombuffer(a.buffers()[0], np.uint8), bitorder="little")[a.offset:a.offset + n]
+            lens = lens * valid
+        size += lens
+    return size
+
+
+# Gathers whose worst case (keys x longest row) is above this size first look
+# the rows up and size the block exactly (one 8-byte read-back), then copy.
+TWO_PHASE_BYTES = 64 << 20
+
+
 class ResidentTable:
     """Table (src/io/table/mod.rs:20-155) whose rows stay in HBM."""
 
@@ -114,46 +149,103 @@ class ResidentTable:
         self.t = Table(Store(), name, table, ctx)  # schema, validation, column resolution
         self.ctx = self.t.ctx
         self.segment = self.t.segment
-        self.batches = []
+        self.t.prepare()  # kernels compiled at open, never on the read path
         self.index = None
-        self.blob = self.row_off = None
+        self.arena = None      # row blobs back to back
+        self.arena_cap = 0
+        self.used = 0          # arena bytes written
+        self.row_off = None    # n + 1 u64 offsets into the arena
+        self.off_cap = 0       # entries
         self.n = 0
         self.max_row = 0
 
+    @property
+    def blob(self):
+        return self.arena
+
+    def _grow(self, blob_need: int, rows_need: int):
+        """Arena and offsets room for blob_need more bytes and rows_need more
+        rows (doubling, old contents copied)."""
+        need = self.used + blob_need + 16
+        if need > self.arena_cap:
+            cap = max(need, 2 * self.arena_cap, 1 << 16)
+            arena = self.ctx.alloc(cap)
+            if self.arena is not None:
+                arena.copy_from(self.arena, self.used)
+                self.arena.free()
+            self.arena, self.arena_cap = arena, cap
+        need = self.n + rows_need + 1
+        if need > self.off_cap:
+            cap = max(need, 2 * self.off_cap, 1024)
+            offs = self.ctx.alloc(8 * cap)
+            if self.row_off is not None:
+                offs.copy_from(self.row_off, 8 * (self.n + 1))
+                self.row_off.free()
+            self.row_off, self.off_cap = offs, cap
+
     def write(self, batch: pa.RecordBatch):
-        """Table::write into the resident set (validation as table/mod.rs:54-96)."""
-        self.t.validate(batch)
-        batches = self.batches + [batch]
-        whole = pa.Table.from_batches(batches).combine_chunks()
-        merged = whole.to_batches()[0] if whole.num_rows else batch
-        keys, arrays = self.t.validate(merged)
-        n = merged.num_rows
+        """Table::write into the resident set (validation as table/mod.rs:54-96,
+        append as memory.rs:47-60)."""
+        keys, arrays = self.t.validate(batch)
+        m = batch.num_rows
+        if m == 0:
+            return
+        sizes = row_sizes(self.segment, arrays)
+        bound = int(sizes.sum())
+        self._grow(bound, m)
         cols = [_column_dict(self.ctx, a) for a in arrays]
-        blob, row_off, _ = encode_batch(self.ctx, self.segment, cols, n)
-        index = DeviceIndex(self.ctx, keys)
-        offs = row_off.download((n + 1) * 8).view(np.uint64)
-        self.batches = batches
-        self.blob, self.row_off, self.index, self.n = blob, row_off, index, n
-        self.max_row = int(np.diff(offs).max()) if n else 0
+        cin = (_abi.ColIn * max(len(cols), 1))()
+        for i, c in enumerate(cols):
+            cin[i].values = c["values"].ptr
+            cin[i].validity = c["validity"].ptr if c["validity"] is not None else None
+            cin[i].offsets = c["offsets"].ptr if c["offsets"] is not None else None
+            cin[i].offset = int(c["offset"])
+        blen = C.c_uint64()
+        err = _abi.Error()
+        st = self.ctx.L.murr_encode_batch_at(self.ctx.h, C.byref(self.segment.c), cin, m,
+                                             self.arena.ptr + self.used, self.arena_cap - self.used,
+                                             self.row_off.ptr + 8 * self.n, self.used, C.byref(blen),
+                                             C.byref(err))
+        raise_status(st, err, "murr_encode_batch_at")
+        assert blen.value == bound, (blen.value, bound)
+        if self.index is None:
+            self.index = DeviceIndex(self.ctx, keys)
+        else:
+            self.index.append(keys)
+        self.used += blen.value
+        self.n += m
+        self.max_row = max(self.max_row, int(sizes.max()))
 
     def gather(self, keys):
         """Lookup + gather on the device: a DeviceBlock of the rows of `keys` in
-        caller order (a miss = an empty row)."""
+        caller order (a miss = an empty row).  The block is sized from keys x
+        the longest row when that is small, else exactly (two phases)."""
+        if self.index is None:
+            raise SegmentError("resident table is empty")
         nq = len(keys)
         q = pa.array([k.encode() if isinstance(k, str) else bytes(k) for k in keys], pa.binary())
         qd, qo = _upload_utf8(self.ctx, q.view(pa.string()))
-        cap = max(nq * self.max_row, 16)
-        data = self.ctx.alloc(cap + 16)
         offs = self.ctx.alloc((nq + 1) * 8)
         needed = self.ctx.alloc(8)
-        blob = self.blob.ptr if self.blob is not None else None
-        row_off = self.row_off.ptr if self.row_off is not None else None
-        if self.index is None:
-            raise SegmentError("resident table is empty")
-        st = self.ctx.L.murr_index_gather(self.ctx.h, self.index.h, qd.ptr, qo.ptr, nq, blob, row_off,
-                                          data.ptr, cap, offs.ptr, None, needed.ptr)
+        bound = max(nq * self.max_row, 16)
+        L = self.ctx.L
+        if bound <= TWO_PHASE_BYTES:
+            data = self.ctx.alloc(bound + 16)
+            st = L.murr_index_gather(self.ctx.h, self.index.h, qd.ptr, qo.ptr, nq, self.arena.ptr, self.row_off.ptr,
+                                     data.ptr, bound, offs.ptr, None, needed.ptr)
+            raise_status(st, what="murr_index_gather")
+            # the decode's tile sizing hint: the mean row (data_bytes is never read past)
+            hint = min(bound, max(16, int(self.used / max(self.n, 1) * nq)))
+            return DeviceBlock(data, offs, nq, hint), (qd, qo)
+        rows = self.ctx.alloc(max(nq, 1) * 4)
+        st = L.murr_index_gather(self.ctx.h, self.index.h, qd.ptr, qo.ptr, nq, self.arena.ptr, self.row_off.ptr,
+                                 None, 0, offs.ptr, rows.ptr, needed.ptr)
         raise_status(st, what="murr_index_gather")
-        return DeviceBlock(data, offs, nq, 0), needed, (qd, qo)
+        nb = int(needed.download(8).view(np.uint64)[0])
+        data = self.ctx.alloc(max(nb, 16) + 16)
+        st = L.murr_index_gather_copy(self.ctx.h, rows.ptr, nq, self.arena.ptr, self.row_off.ptr, offs.ptr, data.ptr)
+        raise_status(st, what="murr_index_gather_copy")
+        return DeviceBlock(data, offs, nq, max(nb, 16)), (qd, qo, rows)
 
     def _resolve(self, columns):
         req = []
@@ -175,12 +267,10 @@ class ResidentTable:
         nq = len(keys)
         if self.index is None:
             return req, [_null_dict(c.dtype, nq) for c in req]
-        blk, needed, _keep = self.gather(keys)
-        blk.data_bytes = max(nq * self.max_row, 16)
+        blk, _keep = self.gather(keys)
         proj = [c.index for c in req]
         outs = DecodeOutputs(self.ctx, self.segment, proj, [blk])
         decode_blocks(self.ctx, self.segment, proj, [blk], outs)
-        assert int(needed.download(8).view(np.uint64)[0]) <= max(nq * self.max_row, 16)
         return req, [download_array(self.ctx, outs.array(0, p), int(c.dtype), nq) for p, c in enumerate(req)]
 
     def read(self, keys, columns) -> pa.RecordBatch:
@@ -207,8 +297,7 @@ class ResidentTable:
         schema = ipc.schema_message(self.segment, req, alignment)
         if self.index is None:
             return ipc.stream(schema, _all_null_message(self.segment, req, nq, alignment))
-        blk, needed, _keep = self.gather(keys)
-        blk.data_bytes = max(nq * self.max_row, 16)
+        blk, _keep = self.gather(keys)
         proj = [c.index for c in req]
         outs = DecodeOutputs(self.ctx, self.segment, proj, [blk])
         decode_blocks(self.ctx, self.segment, proj, [blk], outs)

@@ -45,6 +45,17 @@ class Table:
             self._ctx = default_context()
         return self._ctx
 
+    def prepare(self):
+        """Compile (or load from the code-object cache) the layout's decode and
+        encode kernels now (murr_segment_prepare), so no read or write pays
+        for it: the decode kernel is specialised on the segment layout only,
+        and every projection a read asks for runs the same code object."""
+        from .errors import raise_status
+        if not getattr(self, "_prepared", False):
+            raise_status(self.ctx.L.murr_segment_prepare(self.ctx.h, C.byref(self.segment.c)),
+                         what="murr_segment_prepare")
+            self._prepared = True
+
     @classmethod
     def create(cls, store: Store, name: str, table: TableSchema, ctx=None) -> "Table":
         store.create_table(name, table)

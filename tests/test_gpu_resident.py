@@ -217,3 +217,57 @@ def test_index_long_duplicate_keys():
     ix = DeviceIndex(ctx, pa.array(ks, pa.string()))
     assert ix.lookup([base + "a", base + "b", "z" * 64, "z" * 65, base + "c", "z" * 63]).tolist() == \
         [2, 4, 5, 6, ROW_MISSING, ROW_MISSING]
+
+
+def test_incremental_appends_keep_earlier_rows_and_later_write_wins():
+    # MemoryStore::write appends (src/io/store/memory.rs:47-60): each write
+    # encodes only its batch onto the arena tail (earlier rows' blobs and
+    # offsets stay byte-identical) and a key written again maps to its new row
+    ctx = default_context()
+    rt = ResidentTable(schema_c(), ctx)
+    batches = []
+    rng = np.random.default_rng(17)
+    prev_off = None
+    for w in range(6):
+        n = int(rng.integers(1, 3000))
+        # half new keys, half rewrites of keys from earlier batches
+        keys = [f"key{w * 100000 + i}" for i in range(n)]
+        if w:
+            for i in rng.choice(n, size=n // 2, replace=False):
+                keys[i] = f"key{int(rng.integers(0, w)) * 100000 + int(rng.integers(0, 50))}"
+        b = batch_c(n, start=w * 1000, seed=w, keys=keys)
+        n_before, used_before = rt.n, rt.used
+        rt.write(b)
+        batches.append(b)
+        assert rt.n == n_before + n
+        off = rt.row_off.download(8 * (rt.n + 1)).view(np.uint64)
+        assert int(off[n_before]) == used_before and int(off[-1]) == rt.used
+        if prev_off is not None:
+            assert np.array_equal(off[:len(prev_off)], prev_off)  # earlier rows untouched
+        prev_off = off.copy()
+        q = [f"key{int(x)}" for x in rng.integers(0, (w + 1) * 100000, size=300)]
+        q += [k for k in rng.choice(keys, size=200)]
+        cols = [f"c{i}" for i in rng.permutation(len(C_DTYPES))[:9]]
+        assert_same(rt.read(q, cols), expected(batches, q, cols))
+
+
+def test_oversized_row_sizes_the_gather_exactly():
+    # one 64 KiB string: keys x longest row is far above the single-phase
+    # bound, so the gather looks the rows up first and allocates exactly
+    ctx = default_context()
+    rt = ResidentTable(schema_c(), ctx)
+    n = 3000
+    b = batch_c(n, seed=3)
+    arrays = list(b.columns)
+    big = arrays[12].to_pylist()
+    big[7] = "x" * 65536
+    arrays[12] = pa.array(big, pa.string())
+    b = pa.RecordBatch.from_arrays(arrays, names=b.schema.names)
+    rt.write(b)
+    assert rt.max_row > 65536
+    rng = np.random.default_rng(9)
+    q = [f"key{int(x)}" for x in rng.integers(0, n + 100, size=5000)] + ["key7"] * 3
+    from murr_amd import resident
+    assert len(q) * rt.max_row > resident.TWO_PHASE_BYTES
+    cols = [f"c{i}" for i in range(len(C_DTYPES))]
+    assert_same(rt.read(q, cols), expected([b], q, cols))
