@@ -138,6 +138,9 @@ int murr_memcpy_h2d(murr_ctx_t* ctx, void* dst, const void* src, uint64_t bytes)
 int murr_memcpy_d2h(murr_ctx_t* ctx, void* dst, const void* src, uint64_t bytes);
 int murr_memset_dev(murr_ctx_t* ctx, void* dst, int value, uint64_t bytes);
 int murr_memcpy_d2d(murr_ctx_t* ctx, void* dst, const void* src, uint64_t bytes);
+/* dst on ctx's device <- src on device src_device (xGMI peer copy when they
+ * differ), enqueued on ctx's stream and waited for. */
+int murr_memcpy_peer(murr_ctx_t* ctx, void* dst, const void* src, int src_device, uint64_t bytes);
 int murr_sync(murr_ctx_t* ctx);
 
 /* Compile (or load from the code-object cache) the decode and encode kernels
@@ -349,6 +352,16 @@ int murr_index_gather(murr_ctx_t* ctx, const murr_index_t* idx, const uint8_t* q
  * into out_data (16-B aligned, *needed bytes).  Enqueue. */
 int murr_index_gather_copy(murr_ctx_t* ctx, const uint32_t* rows, uint64_t nq, const uint8_t* blob,
                            const uint64_t* row_off, const uint64_t* out_row_off, uint8_t* out_data);
+
+/* ---- sharding -------------------------------------------- */
+
+/* Owner shard of each of n keys (host Arrow utf8: key_offsets[key_offset ..
+ * key_offset + n], key_data): fmix64(FNV-1a 64 of the key bytes) mod nshards.
+ * Writes and reads route every key to its owner, so a key lives in exactly one
+ * shard and a later write of it lands where the earlier one did (later write
+ * wins, src/io/store/memory.rs:47-60).  Host function, no device. */
+int murr_shard_of(const uint8_t* key_data, const int32_t* key_offsets, uint64_t key_offset, uint64_t n,
+                  uint32_t nshards, uint32_t* out);
 
 /* ---- Arrow IPC framing --------------------------- */
 

@@ -82,6 +82,8 @@ SIGNATURES = {
     "murr_memcpy_h2d": (I32, [P, P, P, U64]),
     "murr_memcpy_d2h": (I32, [P, P, P, U64]),
     "murr_memcpy_d2d": (I32, [P, P, P, U64]),
+    "murr_memcpy_peer": (I32, [P, P, P, I32, U64]),
+    "murr_shard_of": (I32, [P, P, U64, U64, U32, P]),
     "murr_memset_dev": (I32, [P, P, I32, U64]),
     "murr_sync": (I32, [P]),
     "murr_decode_blocks": (I32, [P, C.POINTER(Segment), C.POINTER(U32), U32, C.POINTER(Block), U32,

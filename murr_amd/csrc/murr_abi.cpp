@@ -511,6 +511,35 @@ int murr_memcpy_d2d(murr_ctx_t* c, void* dst, const void* src, uint64_t n) {
     return MURR_OK;
 }
 
+int murr_memcpy_peer(murr_ctx_t* c, void* dst, const void* src, int src_device, uint64_t n) {
+    murr_error_t* err = nullptr;
+    if (!c) return MURR_E_ARGUMENT;
+    if (!n) return MURR_OK;
+    HIPC(hipSetDevice(c->device));
+    if (src_device == c->device) HIPC(hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToDevice, c->stream));
+    else HIPC(hipMemcpyPeerAsync(dst, c->device, src, src_device, n, c->stream));
+    HIPC(hipStreamSynchronize(c->stream));
+    return MURR_OK;
+}
+
+int murr_shard_of(const uint8_t* key_data, const int32_t* key_offsets, uint64_t key_offset, uint64_t n,
+                  uint32_t nshards, uint32_t* out) {
+    if (!nshards || (n && (!key_offsets || !out))) return MURR_E_ARGUMENT;
+    for (uint64_t i = 0; i < n; i++) {
+        const int32_t a = key_offsets[key_offset + i], b = key_offsets[key_offset + i + 1];
+        if (b < a || (b > a && !key_data)) return MURR_E_ARGUMENT;
+        uint64_t h = 0xcbf29ce484222325ull;
+        for (int32_t k = a; k < b; k++) h = (h ^ key_data[k]) * 0x100000001b3ull;
+        h ^= h >> 33;
+        h *= 0xff51afd7ed558ccdull;
+        h ^= h >> 33;
+        h *= 0xc4ceb9fe1a85ec53ull;
+        h ^= h >> 33;
+        out[i] = (uint32_t)(h % nshards);
+    }
+    return MURR_OK;
+}
+
 int murr_memset_dev(murr_ctx_t* c, void* dst, int v, uint64_t n) {
     murr_error_t* err = nullptr;
     if (!c) return MURR_E_ARGUMENT;

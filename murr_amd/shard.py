@@ -22,6 +22,49 @@ from __future__ import annotations
 
 import os
 
+import numpy as np
+
+
+def shard_of(keys, nshards: int) -> np.ndarray:
+    """Owner shard of every key (murr_shard_of: fmix64 of FNV-1a 64 over the
+    key bytes, mod nshards).  `keys`: a pyarrow string/binary array or a list
+    of str/bytes."""
+    import ctypes as C
+    import pyarrow as pa
+    from . import _abi
+    from .errors import raise_status
+    arr = keys if isinstance(keys, pa.Array) else pa.array(
+        [k.encode() if isinstance(k, str) else bytes(k) for k in keys], pa.binary())
+    if pa.types.is_string(arr.type):
+        arr = arr.view(pa.binary())
+    n = len(arr)
+    out = np.zeros(n, np.uint32)
+    if n == 0:
+        return out
+    bufs = arr.buffers()
+    offs = np.frombuffer(bufs[1], np.int32)
+    data = np.frombuffer(bufs[2], np.uint8) if bufs[2] is not None else np.zeros(1, np.uint8)
+    st = _abi.lib().murr_shard_of(data.ctypes.data, offs.ctypes.data, arr.offset, n, nshards, out.ctypes.data)
+    raise_status(st, what="murr_shard_of")
+    return out
+
+
+def check_owned(keys, rank: int, world: int):
+    """Raise ValueError unless every key's owner shard is `rank`."""
+    owner = shard_of(keys, world)
+    bad = np.flatnonzero(owner != rank)
+    if bad.size:
+        raise ValueError(f"{bad.size} keys belong to other shards (first: row {int(bad[0])} -> shard "
+                         f"{int(owner[bad[0]])}); route writes with route_batch")
+
+
+def route_batch(batch, key: str, nshards: int):
+    """Split a RecordBatch by the owner shard of its key column: one batch per
+    shard (rows keep their order)."""
+    import pyarrow as pa
+    owner = shard_of(batch.column(batch.schema.get_field_index(key)), nshards)
+    return [batch.take(pa.array(np.flatnonzero(owner == s))) for s in range(nshards)]
+
 
 def shard_rows(rank: int, world: int, total: int) -> tuple[int, int]:
     """Contiguous key range [start, start + count) of `rank` out of `world`
@@ -187,7 +230,12 @@ class ShardedResidentTable:
         self.local = ResidentTable(table, ctx, name)
 
     def write_shard(self, batch):
-        """Write this rank's key range (Table::write on its own shard)."""
+        """Write this rank's keys (Table::write on its own shard).  Every key
+        must be this rank's (shard_of): a key on two ranks would break the
+        byte-sum merge of reads (route a batch first with route_batch)."""
+        if self.group.world > 1:
+            key = self.local.t.table.key
+            check_owned(batch.column(batch.schema.get_field_index(key)), self.group.rank, self.group.world)
         self.local.write(batch)
 
     def read(self, keys, columns):

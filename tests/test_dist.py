@@ -175,3 +175,51 @@ def test_sharded_random_key_read_restores_caller_order(world):
             assert values == w["values"], (rank, p)
             if w["offsets"] is not None:
                 assert offsets == w["offsets"].tolist(), (rank, p)
+
+
+# ---- key routing (murr_shard_of) -----------------------------------------------------
+
+def _shard_of_py(key: bytes, n: int) -> int:
+    """Restatement of murr_shard_of: fmix64(FNV-1a 64) mod n."""
+    m = (1 << 64) - 1
+    h = 0xcbf29ce484222325
+    for b in key:
+        h = ((h ^ b) * 0x100000001b3) & m
+    h ^= h >> 33
+    h = (h * 0xff51afd7ed558ccd) & m
+    h ^= h >> 33
+    h = (h * 0xc4ceb9fe1a85ec53) & m
+    h ^= h >> 33
+    return h % n
+
+
+def test_shard_of_matches_restatement_and_balances():
+    import pyarrow as pa
+    from murr_amd.shard import shard_of
+    keys = [f"key{i}" for i in range(20000)] + ["", "é", "a" * 300]
+    for n in (1, 2, 3, 8):
+        got = shard_of(keys, n)
+        assert got.tolist() == [_shard_of_py(k.encode(), n) for k in keys]
+        if n > 1:
+            counts = np.bincount(got, minlength=n)
+            assert counts.min() > 0.9 * len(keys) / n  # balanced
+    # arrays with an offset, string or binary, give the same owners
+    arr = pa.array(keys, pa.string()).slice(5, 100)
+    assert shard_of(arr, 8).tolist() == shard_of(keys[5:105], 8).tolist()
+
+
+def test_route_batch_and_owned_check():
+    import pyarrow as pa
+    from murr_amd.shard import check_owned, route_batch, shard_of
+    keys = [f"k{i}" for i in range(5000)] + ["k7", "k7"]  # a repeated key lands on one shard
+    batch = pa.RecordBatch.from_arrays([pa.array(keys), pa.array(np.arange(len(keys)))], names=["key", "v"])
+    parts = route_batch(batch, "key", 3)
+    assert sum(p.num_rows for p in parts) == batch.num_rows
+    for r, p in enumerate(parts):
+        check_owned(p.column(0), r, 3)
+        assert p.column(1).to_pylist() == sorted(p.column(1).to_pylist())  # order kept
+    owners = {k: int(o) for k, o in zip(keys, shard_of(keys, 3))}
+    assert sum(1 for p in parts if "k7" in p.column(0).to_pylist()) == 1
+    other = (owners["k7"] + 1) % 3
+    with pytest.raises(ValueError, match="belong to other shards"):
+        check_owned(pa.array(["k7"]), other, 3)

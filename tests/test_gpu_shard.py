@@ -34,12 +34,11 @@ def _case():
 def _worker(rank, world, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
-    from murr_amd.shard import Group, ShardedResidentTable, shard_rows
+    from murr_amd.shard import Group, ShardedResidentTable, route_batch
     g = Group("gloo")
     ts, batch, keys = _case()
-    start, n = shard_rows(rank, world, ROWS)
     t = ShardedResidentTable(ts, g)
-    t.write_shard(batch.slice(start, n))
+    t.write_shard(route_batch(batch, "key", world)[rank])  # keys go to their owner shard
     rb = t.read(keys, COLS)
     sink = pa.BufferOutputStream()
     with pa.ipc.new_stream(sink, rb.schema) as w:
