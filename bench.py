@@ -336,52 +336,99 @@ def run_encode(args):
                       "GiB_s_blob_out": round(bytes_out / (k * 1e-3) / GIB, 2)}))
 
 
-def run_resident(args):
-    """Device-resident Table::read (SURVEY.md §8(f) rank 1): config C table of
-    args.rows rows in HBM, `--keys` random keys per read (about 5 % misses, as
-    config C), lookup + gather (murr_index_gather) + decode (murr_decode_blocks)
-    with no host round trip in between.  Reports the wall time per read
-    (host-synchronous, launches included) and the Arrow GiB/s."""
-    from murr_amd.resident import DeviceIndex, _upload_utf8
+def resident_table(ctx, kind: str, n: int, chunk: int = 10_000_000):
+    """A ResidentTable of n rows, written in chunks (ResidentTable.write appends).
+    kind "C": config C's 16 mixed nullable columns, keys "key{i}";
+    kind "ref": the reference bench dataset (benches/common/dataset.rs:24-55):
+    col_0..col_9 float32 = i, key = i.to_string()."""
     import pyarrow as pa
+    from murr_amd import ColumnSchema, TableSchema
+    from murr_amd.resident import ResidentTable
+    if kind == "ref":
+        ts = synth.ref_schema()
+    else:
+        cols_s = {"key": ColumnSchema(D.Utf8, False)}
+        cols_s.update({f"c{i}": ColumnSchema(c["dtype"]) for i, c in enumerate(synth.config_c(1))})
+        ts = TableSchema("key", cols_s)
+    rt = ResidentTable(ts, ctx)
+    names = [c for c in ts.columns if c != "key"]
+    for start in range(0, n, chunk):
+        m = min(chunk, n - start)
+        if kind == "ref":
+            rt.write(synth.ref_batch(start, m))
+            continue
+        cols = synth.config_c(m, start=start)
+        keys = pa.array([f"key{i}" for i in range(start, start + m)], pa.string())
+        rt.write(pa.RecordBatch.from_arrays([keys] + [synth.to_arrow(c) for c in cols], names=["key"] + names))
+    return rt, names
+
+
+def ref_keys(kind: str, rows: int, nq: int, k: int):
+    """Key set k of a bench: kind "ref" samples like run_read_bench
+    (benches/common/read_bench.rs:89-98: seed num_keys * 2_000_000 + k, uniform
+    over [0, rows), key = i.to_string(); numpy's generator in place of rand's
+    StdRng, so the same distribution, not the same keys); kind "C" draws over
+    1.05 x rows, so about 5 % miss."""
+    if kind == "ref":
+        ids = np.random.default_rng(nq * 2_000_000 + k).integers(0, rows, size=nq)
+        return [str(int(i)) for i in ids]
+    ids = np.random.default_rng(44 + k).integers(0, int(rows * 1.05), size=nq)
+    return [f"key{int(i)}" for i in ids]
+
+
+def run_resident(args):
+    """Device-resident Table::read (SURVEY.md §8(f) rank 1) on a table of
+    args.rows rows in HBM: `--table C` (config C) or `--table ref` (the
+    reference read benches' dataset: --rows 100000000 is benches/read_block.rs,
+    10000000 benches/read_plain.rs).  `--keys` keys per read.  Two timings,
+    medians over --steps reads on rotating key sets:
+      device: lookup + gather (murr_index_gather) + decode (murr_decode_blocks),
+        keys already in HBM, no host round trip (host-synchronous wall time);
+      host: ResidentTable.read, keys from Python to a RecordBatch on the host
+        (what benches/common/read_bench.rs times around Table::read)."""
+    import pyarrow as pa
+    from murr_amd.resident import _upload_utf8
     ctx = Context(0)
     n, nq = args.rows, args.keys
-    cols = make_columns("C", n, 0)
-    seg = SegmentSchema([(f"c{i}", c["dtype"]) for i, c in enumerate(cols)])
-    dblob, doff, blen = encode_batch(ctx, seg, synth.upload_columns(ctx, cols), n)
-    offs = doff.download((n + 1) * 8).view(np.uint64)
-    max_row = int(np.diff(offs).max())
-    ix = DeviceIndex(ctx, pa.array([f"key{i}" for i in range(n)], pa.string()))
-    rng = np.random.default_rng(44)
-    qsets = []
-    for _ in range(4):
-        ids = rng.integers(0, int(n * 1.05), size=nq)
-        qsets.append(_upload_utf8(ctx, pa.array([f"key{i}" for i in ids], pa.string())))
-    cap = nq * max_row
+    t0 = time.perf_counter()
+    rt, names = resident_table(ctx, args.table, n)
+    build_s = time.perf_counter() - t0
+    seg = rt.segment
+    qsets = [ref_keys(args.table, n, nq, k) for k in range(4)]
+    dq = [_upload_utf8(ctx, pa.array(q, pa.string())) for q in qsets]
+    cap = max(nq * rt.max_row, 16)
     data, roff, needed = ctx.alloc(cap + 16), ctx.alloc((nq + 1) * 8), ctx.alloc(8)
-    blk = DeviceBlock(data, roff, nq, cap)
-    proj = list(range(len(cols)))
+    blk = DeviceBlock(data, roff, nq, min(cap, max(16, int(rt.used / max(rt.n, 1) * nq))))
+    proj = list(range(len(seg.columns)))
     outs = DecodeOutputs(ctx, seg, proj, [blk])
     cb = (_abi.Block * 1)()
-    cb[0].data, cb[0].row_off, cb[0].n_rows, cb[0].data_bytes = data.ptr, roff.ptr, nq, cap
+    cb[0].data, cb[0].row_off, cb[0].n_rows, cb[0].data_bytes = data.ptr, roff.ptr, nq, blk.data_bytes
     pj = (C.c_uint32 * len(proj))(*proj)
     err = _abi.Error()
     L = ctx.L
 
     def read(q):
-        st = L.murr_index_gather(ctx.h, ix.h, q[0].ptr, q[1].ptr, nq, dblob.ptr, doff.ptr, data.ptr, cap,
-                                 roff.ptr, None, needed.ptr)
+        st = L.murr_index_gather(ctx.h, rt.index.h, q[0].ptr, q[1].ptr, nq, rt.arena.ptr, rt.row_off.ptr,
+                                 data.ptr, cap, roff.ptr, None, needed.ptr)
         assert st == 0, st
         st = L.murr_decode_blocks(ctx.h, C.byref(seg.c), pj, len(proj), cb, 1, outs.arrays, C.byref(err))
         assert st == 0, (st, err.status)
 
     for i in range(args.warmup):
-        read(qsets[i % 4])
+        read(dq[i % 4])
     ts = []
     for i in range(args.steps):
         t0 = time.perf_counter()
-        read(qsets[i % 4])
+        read(dq[i % 4])
         ts.append(time.perf_counter() - t0)
+    for i in range(args.warmup):
+        rt.read(qsets[i % 4], names)
+    th = []
+    for i in range(args.steps):
+        t0 = time.perf_counter()
+        rb = rt.read(qsets[i % 4], names)
+        th.append(time.perf_counter() - t0)
+    out_bytes = sum(sum(b.size for b in col.buffers() if b is not None) for col in rb.columns)
     ipc_res = {}
     if args.ipc:
         # + Arrow IPC record-batch message packed in HBM (murr_ipc_batch_device)
@@ -404,32 +451,26 @@ def run_resident(args):
             assert L.murr_memcpy_d2h(ctx.h, hmsg, dmsg.ptr, mlen.value) == 0
 
         for i in range(args.warmup):
-            read_ipc(qsets[i % 4])
+            read_ipc(dq[i % 4])
         ti = []
         for i in range(args.steps):
             t0 = time.perf_counter()
-            read_ipc(qsets[i % 4])
+            read_ipc(dq[i % 4])
             ti.append(time.perf_counter() - t0)
         L.murr_host_free(ctx.h, hmsg)
         ipc_res = {"ipc_message_bytes": int(mlen.value),
                    "us_per_read_ipc_median": round(float(np.median(ti)) * 1e6, 1),
                    "ipc_path": "gather + decode + ipc_pack + one D2H (pinned)"}
-    nb = int(needed.download(8).view(np.uint64)[0])
-    assert nb <= cap
-    out_bytes = 0
-    for p in range(len(proj)):
-        a = outs.array(0, p)
-        dt = cols[p]["dtype"]
-        bm = (nq + 7) // 8
-        out_bytes += (a.data_len + 4 * (nq + 1)) if dt == D.Utf8 else a.data_len
-        out_bytes += bm if a.null_count else 0
     med = float(np.median(ts))
-    print(json.dumps({"mode": "resident", "config": "C", "table_rows": n, "keys_per_read": nq,
-                      "gathered_bytes": nb, "arrow_bytes_out": out_bytes,
-                      "us_per_read_median": round(med * 1e6, 1),
-                      "us_per_read_p95": round(float(np.percentile(ts, 95)) * 1e6, 1),
-                      "GiB_s_arrow_out": round(out_bytes / med / GIB, 3),
-                      "kernels": "index_probe, gather_scan, gather_copy, " + ctx.last_kernel(), **ipc_res}))
+    shape = {100_000_000: "benches/read_block.rs", 10_000_000: "benches/read_plain.rs"}.get(n, "")
+    print(json.dumps({"mode": "resident", "table": args.table, "bench_shape": shape if args.table == "ref" else "",
+                      "table_rows": n, "keys_per_read": nq, "columns": len(proj), "build_s": round(build_s, 2),
+                      "arrow_bytes_out": out_bytes,
+                      "us_per_read_device_median": round(med * 1e6, 1),
+                      "us_per_read_device_p95": round(float(np.percentile(ts, 95)) * 1e6, 1),
+                      "us_per_read_host_median": round(float(np.median(th)) * 1e6, 1),
+                      "GiB_s_arrow_out_device": round(out_bytes / med / GIB, 3),
+                      "kernels": "index_probe/gather_scan, gather_copy, " + ctx.last_kernel(), **ipc_res}))
 
 
 def main():
@@ -443,6 +484,8 @@ def main():
     ap.add_argument("--mode", default="decode", choices=["decode", "host", "encode", "resident"])
     ap.add_argument("--keys", type=int, default=1000, help="resident mode: keys per read")
     ap.add_argument("--ipc", action="store_true", help="resident mode: also time the Arrow IPC message path")
+    ap.add_argument("--table", default="C", choices=["C", "ref"],
+                    help="resident mode: config C table, or the reference read benches' dataset (10 x f32)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--pmc-csv", default=None)

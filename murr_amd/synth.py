@@ -32,12 +32,25 @@ def pack_bits(mask: np.ndarray) -> np.ndarray:
 
 
 def int_strings(start: int, n: int):
-    """`i.to_string()` for i in [start, start+n): (offsets int32, data uint8)."""
-    s = "".join(str(i) for i in range(start, start + n)).encode()
-    lens = np.array([len(str(i)) for i in range(start, start + n)], dtype=np.int64)
+    """`i.to_string()` for i in [start, start+n): (offsets int32, data uint8).
+    Vectorised: the numbers with the same digit count form contiguous runs,
+    each written as a [run, width] digit matrix, so 1e8 keys take seconds."""
     offs = np.zeros(n + 1, dtype=np.int64)
-    np.cumsum(lens, out=offs[1:])
-    return offs.astype(np.int32), np.frombuffer(s, dtype=np.uint8).copy()
+    parts = []
+    i, at = start, 0
+    while i < start + n:
+        width = len(str(i))
+        hi = min(start + n, 10 ** width)  # numbers below 10**width have `width` digits
+        v = np.arange(i, hi, dtype=np.int64)
+        m = v.size
+        digits = np.empty((m, width), dtype=np.uint8)
+        for j in range(width):
+            digits[:, j] = (v // 10 ** (width - 1 - j)) % 10 + 48
+        parts.append(digits.ravel())
+        offs[at + 1:at + m + 1] = offs[at] + width * np.arange(1, m + 1, dtype=np.int64)
+        i, at = hi, at + m
+    data = np.concatenate(parts) if parts else np.zeros(0, np.uint8)
+    return offs.astype(np.int32), data
 
 
 def random_ascii(rng, n: int, max_len: int = 32):
@@ -126,8 +139,24 @@ def config_c(n: int, start: int = 0, null_frac: float = 0.10, seed_nulls: int = 
 
 def config_e(n: int, ncols: int = 10, start: int = 0):
     """{col_0..col_{ncols-1}: f32 = i} (benches/write.rs:21-22, data.rs:54-56)."""
-    v = np.arange(start, start + n, dtype=np.float32)
+    v = np.arange(start, start + n, dtype=np.int64).astype(np.float32)  # `i as f32`
     return [column(D.Float32, v) for _ in range(ncols)]
+
+
+def ref_batch(start: int, n: int, ncols: int = 10) -> pa.RecordBatch:
+    """Rows [start, start+n) of the reference benches' dataset
+    (benches/common/dataset.rs:24-55): key = i.to_string(), col_j = i as f32."""
+    ko, kd = int_strings(start, n)
+    keys = pa.Array.from_buffers(pa.string(), n, [None, pa.py_buffer(ko), pa.py_buffer(kd)])
+    v = pa.array(np.arange(start, start + n, dtype=np.int64).astype(np.float32))
+    return pa.RecordBatch.from_arrays([keys] + [v] * ncols, names=["key"] + [f"col_{j}" for j in range(ncols)])
+
+
+def ref_schema(ncols: int = 10):
+    from .schema import ColumnSchema, TableSchema
+    cols = {"key": ColumnSchema(D.Utf8, False)}
+    cols.update({f"col_{j}": ColumnSchema(D.Float32) for j in range(ncols)})
+    return TableSchema("key", cols)
 
 
 def utf8_bytes(cols):

@@ -271,3 +271,29 @@ def test_oversized_row_sizes_the_gather_exactly():
     assert len(q) * rt.max_row > resident.TWO_PHASE_BYTES
     cols = [f"c{i}" for i in range(len(C_DTYPES))]
     assert_same(rt.read(q, cols), expected([b], q, cols))
+
+
+def test_reference_bench_dataset_chunked_reads():
+    """The read benches' table (benches/common/dataset.rs:24-55, col_j = i as f32,
+    key = i.to_string()) written in chunks like bench.py --mode resident --table ref,
+    read with keys sampled as benches/common/read_bench.rs:89-98 (1000 keys per
+    read, uniform over the rows): every key hits and every column is `i as f32`."""
+    n, chunk = 250_000, 60_000
+    t = ResidentTable(synth.ref_schema())
+    batches = []
+    for s in range(0, n, chunk):
+        batches.append(synth.ref_batch(s, min(chunk, n - s)))
+        t.write(batches[-1])
+    cols = [f"col_{j}" for j in range(10)]
+    for k in range(3):
+        ids = np.random.default_rng(1000 * 2_000_000 + k).integers(0, n, size=1000)
+        keys = [str(int(i)) for i in ids]
+        got = t.read(keys, cols)
+        want = ids.astype(np.float32)
+        for c in got.columns:
+            assert c.null_count == 0
+            assert np.array_equal(c.to_numpy(), want)
+        assert_same(got, expected(batches, keys, cols))
+    # projection subset and the largest key
+    got = t.read([str(n - 1), "0", str(n)], ["col_9", "col_0"])
+    assert got.column(0).to_pylist() == [float(n - 1), 0.0, None]
