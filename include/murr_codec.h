@@ -353,6 +353,29 @@ int murr_index_gather(murr_ctx_t* ctx, const murr_index_t* idx, const uint8_t* q
 int murr_index_gather_copy(murr_ctx_t* ctx, const uint32_t* rows, uint64_t nq, const uint8_t* blob,
                            const uint64_t* row_off, const uint64_t* out_row_off, uint8_t* out_data);
 
+/* ---- resident read: host keys in, host Arrow arrays out ------------------- */
+
+/* Table::read (src/io/table/mod.rs:114-129) over a table whose row blobs live
+ * in HBM, as one call: replaces RocksDBStore::read's MultiGet + the
+ * ReadBatchBuilder feed (src/io/store/rocksdb/mod.rs:241-267) for a resident
+ * table.  The reader keeps its pinned and device scratch between reads. */
+typedef struct murr_reader murr_reader_t;
+
+int murr_reader_new(murr_ctx_t* ctx, const murr_segment_t* seg, murr_reader_t** out);
+/* Keys: host Arrow utf8 (key_offsets[key_offset .. key_offset + nq], key_data).
+ * The table: idx over its keys, (blob, row_off) its rows in HBM, blob_bytes
+ * their total size, max_row the longest row.  One H2D of the keys, lookup +
+ * gather + decode on the ctx stream, one D2H when the arrays fit 1 MiB (else
+ * one per buffer, exact sizes).  outs[nproj] point into the reader's pinned
+ * memory, valid until its next read or free.  A missing key is an all-null
+ * row (add_empty, rocksdb/mod.rs:262-263).  Synchronous. */
+int murr_reader_read(murr_reader_t* r, const murr_index_t* idx, const uint8_t* blob,
+                     const uint64_t* row_off, uint64_t blob_bytes, uint64_t max_row,
+                     const uint8_t* key_data, const int32_t* key_offsets, uint64_t key_offset,
+                     uint64_t nq, const uint32_t* proj, uint32_t nproj,
+                     murr_host_array_t* outs, murr_error_t* err);
+void murr_reader_free(murr_reader_t* r);
+
 /* ---- sharding -------------------------------------------- */
 
 /* Owner shard of each of n keys (host Arrow utf8: key_offsets[key_offset ..

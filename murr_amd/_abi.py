@@ -104,6 +104,10 @@ SIGNATURES = {
     "murr_builder_last_timing": (I32, [P, C.POINTER(C.c_double), C.POINTER(C.c_float),
                                        C.POINTER(C.c_float), C.POINTER(C.c_float)]),
     "murr_builder_free": (None, [P]),
+    "murr_reader_new": (I32, [P, C.POINTER(Segment), PP]),
+    "murr_reader_read": (I32, [P, P, P, P, U64, U64, P, P, U64, U64, C.POINTER(U32), U32,
+                               C.POINTER(HostArray), C.POINTER(Error)]),
+    "murr_reader_free": (None, [P]),
     "murr_encode_host": (I32, [P, C.POINTER(Segment), C.POINTER(HostColIn), U64,
                                C.POINTER(C.POINTER(C.c_uint8)), C.POINTER(U64),
                                C.POINTER(C.POINTER(C.c_uint64)), C.POINTER(Error)]),

@@ -1203,6 +1203,18 @@ int murr_encode_batch_at(murr_ctx_t* c, const murr_segment_t* seg, const murr_co
 
 // ---- host-memory path --------------------------------------------------------
 
+// Decoded outputs of one block on their way to the host: one device region and
+// one pinned region with the same layout (per column values, validity, utf8
+// offsets; 64-B aligned parts), grown on demand and reused.
+struct HostOut {
+    uint8_t* dout = nullptr;
+    uint64_t dout_cap = 0;
+    uint8_t* hout = nullptr;
+    uint64_t hout_cap = 0;
+    std::vector<murr_array_t> arr;
+    std::vector<uint64_t> off;  // per column: values, validity, offsets
+};
+
 struct murr_builder {
     murr_ctx* ctx = nullptr;
     std::vector<murr_column_t> cols;
@@ -1217,13 +1229,7 @@ struct murr_builder {
     // device buffers (grow-only)
     uint8_t* ddata = nullptr;
     uint64_t ddata_cap = 0;
-    uint8_t* dout = nullptr;
-    uint64_t dout_cap = 0;
-    // host outputs (pinned)
-    uint8_t* hout = nullptr;
-    uint64_t hout_cap = 0;
-    std::vector<murr_array_t> arr;
-    std::vector<uint64_t> out_off;  // per column: values, validity, offsets offsets in dout/hout
+    HostOut out;  // decoded outputs (device + pinned host)
     hipEvent_t e0 = nullptr, e1 = nullptr, e2 = nullptr, e3 = nullptr;
     double total_ms = 0;
     float h2d_ms = 0, k_ms = 0, d2h_ms = 0;
@@ -1282,6 +1288,86 @@ bool grow_dev(murr_ctx* c, uint8_t** p, uint64_t* cap, uint64_t need) {
     const uint64_t nc = round_up(std::max<uint64_t>(need, 1 << 16), 1 << 16);
     if (!pool_take(c, false, need, nc, p, cap)) { *cap = 0; return false; }
     return true;
+}
+
+// Decode one device block (enqueued behind whatever is on the stream) into
+// o.dout and bring the projected arrays to o.hout; outs[p] point into o.hout.
+// A small batch (the point-lookup case) copies its whole output region back
+// in one D2H right behind the decode, with no round trip to learn the sizes;
+// a large one waits for the sizes and copies exactly the bytes.  utf8_cap
+// bounds the string bytes of any one utf8 column.  e2/e3 (optional) bracket
+// the D2H.
+int decode_to_host(murr_ctx* c, const murr_segment_t* seg, const uint32_t* proj, uint32_t np,
+                   murr_block_t blk, uint64_t utf8_cap, HostOut& o, hipEvent_t e2, hipEvent_t e3,
+                   murr_host_array_t* outs, murr_error_t* err) {
+    const uint64_t n = blk.n_rows;
+    const uint64_t bm = murr_bitmap_bytes(n);
+    o.off.assign((size_t)np * 3, 0);
+    uint64_t off = 0;
+    for (uint32_t p = 0; p < np; p++) {
+        const murr_column_t& col = seg->cols[proj[p]];
+        uint64_t vb = col.dtype == MURR_UTF8 ? utf8_cap : col.dtype == MURR_BOOL ? bm : n * col.size;
+        o.off[3 * p] = off;
+        off = round_up(off + std::max<uint64_t>(vb, 8), 64);
+        o.off[3 * p + 1] = off;
+        off = round_up(off + std::max<uint64_t>(bm, 8), 64);
+        o.off[3 * p + 2] = off;
+        if (col.dtype == MURR_UTF8) off = round_up(off + (n + 1) * 4, 64);
+    }
+    const uint64_t total_out = std::max<uint64_t>(off, 64);
+    if (!grow_dev(c, &o.dout, &o.dout_cap, total_out) || !grow_pinned(c, &o.hout, &o.hout_cap, total_out, 0))
+        return set_err(err, MURR_E_HIP);
+    o.arr.assign(np, murr_array_t{});
+    for (uint32_t p = 0; p < np; p++) {
+        murr_array_t& a = o.arr[p];
+        a.values = o.dout + o.off[3 * p];
+        a.validity = o.dout + o.off[3 * p + 1];
+        a.offsets = seg->cols[proj[p]].dtype == MURR_UTF8 ? (int32_t*)(o.dout + o.off[3 * p + 2]) : nullptr;
+        a.values_cap = utf8_cap;
+    }
+    constexpr uint64_t kOneCopy = 1 << 20;
+    int st = murr_decode_enqueue(c, seg, proj, np, &blk, 1, o.arr.data());
+    if (st) {
+        if (err && st != MURR_E_HIP) set_err(err, st);
+        else if (err) set_err(err, st, (int)hipGetLastError());
+        return st;
+    }
+    if (total_out <= kOneCopy) {
+        if (e2) HIPC(hipEventRecord(e2, c->stream));
+        HIPC(hipMemcpyAsync(o.hout, o.dout, total_out, hipMemcpyDeviceToHost, c->stream));
+        if (e3) HIPC(hipEventRecord(e3, c->stream));
+        st = murr_decode_wait(c, err);
+        if (st) return st;
+    } else {
+        st = murr_decode_wait(c, err);
+        if (st) return st;
+        if (e2) HIPC(hipEventRecord(e2, c->stream));
+        for (uint32_t p = 0; p < np; p++) {
+            const murr_array_t& a = o.arr[p];
+            if (a.data_len)
+                HIPC(hipMemcpyAsync(o.hout + o.off[3 * p], a.values, a.data_len, hipMemcpyDeviceToHost, c->stream));
+            if (a.null_count)
+                HIPC(hipMemcpyAsync(o.hout + o.off[3 * p + 1], a.validity, bm, hipMemcpyDeviceToHost, c->stream));
+            if (a.offsets)
+                HIPC(hipMemcpyAsync(o.hout + o.off[3 * p + 2], a.offsets, (n + 1) * 4, hipMemcpyDeviceToHost,
+                                    c->stream));
+        }
+        if (e3) HIPC(hipEventRecord(e3, c->stream));
+        HIPC(hipStreamSynchronize(c->stream));
+    }
+    for (uint32_t p = 0; p < np; p++) {
+        const murr_array_t& a = o.arr[p];
+        murr_host_array_t& h = outs[p];
+        h.values = o.hout + o.off[3 * p];
+        h.validity = a.null_count ? o.hout + o.off[3 * p + 1] : nullptr;
+        h.offsets = a.offsets ? (const int32_t*)(o.hout + o.off[3 * p + 2]) : nullptr;
+        h.length = n;
+        h.null_count = a.null_count;
+        h.values_len = a.data_len;
+        h.dtype = seg->cols[proj[p]].dtype;
+        h._pad = 0;
+    }
+    return MURR_OK;
 }
 
 bool push_off(murr_builder* b) {
@@ -1374,28 +1460,9 @@ int murr_builder_build(murr_builder_t* b, murr_host_array_t* outs, murr_error_t*
     const uint64_t n = b->n, np = b->proj.size();
     const uint64_t dbytes = round_up(b->hdata_len, 16) + 16;
     const uint64_t obytes = (n + 1) * 8;
-    // Output layout in one device (and one pinned host) buffer, 64-B aligned parts.
-    const uint64_t bm = murr_bitmap_bytes(n);
-    const uint64_t utf8_cap = b->hdata_len > b->present * ((uint64_t)b->seg.bitset_size + b->seg.capacity)
-                                  ? b->hdata_len - b->present * ((uint64_t)b->seg.bitset_size + b->seg.capacity)
-                                  : 0;
-    b->out_off.assign(np * 3, 0);
-    uint64_t off = 0;
-    for (uint64_t p = 0; p < np; p++) {
-        const murr_column_t& col = b->cols[b->proj[p]];
-        uint64_t vb = col.dtype == MURR_UTF8 ? utf8_cap : col.dtype == MURR_BOOL ? bm : n * col.size;
-        b->out_off[3 * p] = off;
-        off = round_up(off + std::max<uint64_t>(vb, 8), 64);
-        b->out_off[3 * p + 1] = off;
-        off = round_up(off + std::max<uint64_t>(bm, 8), 64);
-        b->out_off[3 * p + 2] = off;
-        if (col.dtype == MURR_UTF8) off = round_up(off + (n + 1) * 4, 64);
-    }
-    const uint64_t total_out = std::max<uint64_t>(off, 64);
-    if (!grow_dev(c, &b->ddata, &b->ddata_cap, dbytes + obytes + 64) ||
-        !grow_dev(c, &b->dout, &b->dout_cap, total_out) ||
-        !grow_pinned(c, &b->hout, &b->hout_cap, total_out, 0))
-        return set_err(err, MURR_E_HIP);
+    const uint64_t fixed = (uint64_t)b->seg.bitset_size + b->seg.capacity;
+    const uint64_t utf8_cap = b->hdata_len > b->present * fixed ? b->hdata_len - b->present * fixed : 0;
+    if (!grow_dev(c, &b->ddata, &b->ddata_cap, dbytes + obytes + 64)) return set_err(err, MURR_E_HIP);
     uint8_t* ddata = b->ddata;
     uint64_t* doff = (uint64_t*)(b->ddata + round_up(dbytes, 64));
     HIPC(hipEventRecord(b->e0, c->stream));
@@ -1403,63 +1470,8 @@ int murr_builder_build(murr_builder_t* b, murr_host_array_t* outs, murr_error_t*
     HIPC(hipMemcpyAsync(doff, b->hoff, obytes, hipMemcpyHostToDevice, c->stream));
     HIPC(hipEventRecord(b->e1, c->stream));
     murr_block_t blk{ddata, doff, n, b->hdata_len};
-    b->arr.assign(np, murr_array_t{});
-    for (uint64_t p = 0; p < np; p++) {
-        const murr_column_t& col = b->cols[b->proj[p]];
-        murr_array_t& a = b->arr[p];
-        a.values = b->dout + b->out_off[3 * p];
-        a.validity = b->dout + b->out_off[3 * p + 1];
-        a.offsets = col.dtype == MURR_UTF8 ? (int32_t*)(b->dout + b->out_off[3 * p + 2]) : nullptr;
-        a.values_cap = utf8_cap;
-    }
-    // A small batch (the point-lookup case) copies its whole output region
-    // back in one D2H right behind the decode, with no round trip to learn
-    // the sizes; a large one waits for the sizes and copies exactly the bytes.
-    constexpr uint64_t kOneCopy = 1 << 20;
-    int st = murr_decode_enqueue(c, &b->seg, b->proj.data(), (uint32_t)np, &blk, 1, b->arr.data());
-    if (st) {
-        if (err && st != MURR_E_HIP) set_err(err, st);
-        else if (err) set_err(err, st, (int)hipGetLastError());
-        return st;
-    }
-    if (total_out <= kOneCopy) {
-        HIPC(hipEventRecord(b->e2, c->stream));
-        HIPC(hipMemcpyAsync(b->hout, b->dout, total_out, hipMemcpyDeviceToHost, c->stream));
-        HIPC(hipEventRecord(b->e3, c->stream));
-        st = murr_decode_wait(c, err);
-        if (st) return st;
-    } else {
-        st = murr_decode_wait(c, err);
-        if (st) return st;
-        HIPC(hipEventRecord(b->e2, c->stream));
-        for (uint64_t p = 0; p < np; p++) {
-            const murr_column_t& col = b->cols[b->proj[p]];
-            const murr_array_t& a = b->arr[p];
-            uint64_t vlen = a.data_len;
-            if (vlen) HIPC(hipMemcpyAsync(b->hout + b->out_off[3 * p], a.values, vlen, hipMemcpyDeviceToHost, c->stream));
-            if (a.null_count)
-                HIPC(hipMemcpyAsync(b->hout + b->out_off[3 * p + 1], a.validity, (n + 7) / 8,
-                                    hipMemcpyDeviceToHost, c->stream));
-            if (col.dtype == MURR_UTF8)
-                HIPC(hipMemcpyAsync(b->hout + b->out_off[3 * p + 2], a.offsets, (n + 1) * 4,
-                                    hipMemcpyDeviceToHost, c->stream));
-        }
-        HIPC(hipEventRecord(b->e3, c->stream));
-        HIPC(hipStreamSynchronize(c->stream));
-    }
-    for (uint64_t p = 0; p < np; p++) {
-        const murr_column_t& col = b->cols[b->proj[p]];
-        const murr_array_t& a = b->arr[p];
-        murr_host_array_t& h = outs[p];
-        h.values = b->hout + b->out_off[3 * p];
-        h.validity = a.null_count ? b->hout + b->out_off[3 * p + 1] : nullptr;
-        h.offsets = col.dtype == MURR_UTF8 ? (const int32_t*)(b->hout + b->out_off[3 * p + 2]) : nullptr;
-        h.length = n;
-        h.null_count = a.null_count;
-        h.values_len = a.data_len;
-        h.dtype = col.dtype;
-        h._pad = 0;
-    }
+    int st = decode_to_host(c, &b->seg, b->proj.data(), (uint32_t)np, blk, utf8_cap, b->out, b->e2, b->e3, outs, err);
+    if (st) return st;
     hipEventElapsedTime(&b->h2d_ms, b->e0, b->e1);
     murr_ctx_last_kernel_ms(c, &b->k_ms);
     hipEventElapsedTime(&b->d2h_ms, b->e2, b->e3);
@@ -1484,15 +1496,141 @@ void murr_builder_free(murr_builder_t* b) {
     // buffers and events go back to the context's pool for the next builder
     pool_give(c, true, b->hdata, b->hdata_cap);
     pool_give(c, true, (uint8_t*)b->hoff, b->hoff_cap * 8);
-    pool_give(c, true, b->hout, b->hout_cap);
+    pool_give(c, true, b->out.hout, b->out.hout_cap);
     pool_give(c, false, b->ddata, b->ddata_cap);
-    pool_give(c, false, b->dout, b->dout_cap);
+    pool_give(c, false, b->out.dout, b->out.dout_cap);
     for (hipEvent_t e : {b->e0, b->e1, b->e2, b->e3}) {
         if (!e) continue;
         if (c) c->event_pool.push_back(e);
         else (void)hipEventDestroy(e);
     }
     delete b;
+}
+
+}  // extern "C"
+
+// ---- resident read, host keys in, host arrays out ---------------------------
+
+// Reads whose worst case (keys x longest row) passes this size the gather
+// exactly (two phases); resident.py's TWO_PHASE_BYTES is the same bound.
+constexpr uint64_t kTwoPhaseBytes = 64ull << 20;
+
+struct murr_reader {
+    murr_ctx* ctx = nullptr;
+    std::vector<murr_column_t> cols;
+    murr_segment_t seg{};
+    uint8_t* hkeys = nullptr;   // pinned: rebased key offsets, then the key bytes
+    uint64_t hkeys_cap = 0;
+    uint8_t* dwork = nullptr;   // device: keys, gather offsets, rows, needed, gathered rows
+    uint64_t dwork_cap = 0;
+    HostOut out;
+};
+
+extern "C" {
+
+int murr_reader_new(murr_ctx_t* c, const murr_segment_t* seg, murr_reader_t** out) {
+    if (!c || !out || !valid_segment(seg)) return MURR_E_ARGUMENT;
+    murr_reader* r = new (std::nothrow) murr_reader();
+    if (!r) return MURR_E_INTERNAL;
+    r->ctx = c;
+    r->cols.assign(seg->cols, seg->cols + seg->ncols);
+    r->seg = *seg;
+    r->seg.cols = r->cols.data();
+    *out = r;
+    return MURR_OK;
+}
+
+// Table::read (src/io/table/mod.rs:114-129) over a device-resident table in
+// one call: the keys go up in one H2D, lookup + gather + decode run on the
+// stream, the arrays come back in one D2H (small reads) -- the per-key
+// MultiGet + ReadBatchBuilder of RocksDBStore::read (rocksdb/mod.rs:241-267)
+// with no host work per key.
+int murr_reader_read(murr_reader_t* r, const murr_index_t* x, const uint8_t* blob, const uint64_t* row_off,
+                     uint64_t blob_bytes, uint64_t max_row, const uint8_t* key_data, const int32_t* key_offsets,
+                     uint64_t key_offset, uint64_t nq, const uint32_t* proj, uint32_t nproj,
+                     murr_host_array_t* outs, murr_error_t* err) {
+    if (err) std::memset(err, 0, sizeof *err);
+    if (!r || !x || (nproj && (!proj || !outs)) || (nq && (!key_offsets || !key_data)))
+        return set_err(err, MURR_E_ARGUMENT);
+    if (!nproj) return set_err(err, MURR_E_ARROW);  // no columns and no row count (table/mod.rs:124)
+    for (uint32_t p = 0; p < nproj; p++)
+        if (proj[p] >= r->seg.ncols) return set_err(err, MURR_E_BAD_COLUMN);
+    murr_ctx* c = r->ctx;
+    if (x->device != c->device || c->pending) return set_err(err, MURR_E_ARGUMENT);
+    if (nq >= kMissing) return set_err(err, MURR_E_ARGUMENT);
+    HIPC(hipSetDevice(c->device));
+    // 1. keys: rebased offsets + bytes in pinned staging, one H2D
+    const int32_t k0 = nq ? key_offsets[key_offset] : 0;
+    const uint64_t kbytes = nq ? (uint64_t)(key_offsets[key_offset + nq] - k0) : 0;
+    const uint64_t offb = round_up((nq + 1) * 4, 64);
+    const uint64_t hk = offb + round_up(kbytes, 16) + 16;
+    if (!grow_pinned(c, &r->hkeys, &r->hkeys_cap, hk, 0)) return set_err(err, MURR_E_HIP);
+    int32_t* ho = (int32_t*)r->hkeys;
+    ho[0] = 0;
+    for (uint64_t i = 1; i <= nq; i++) ho[i] = key_offsets[key_offset + i] - k0;
+    if (kbytes) std::memcpy(r->hkeys + offb, key_data + k0, kbytes);
+    // 2. device work: keys | out_row_off | rows | needed | gathered rows
+    const uint64_t fixed = (uint64_t)r->seg.bitset_size + r->seg.capacity;
+    const uint64_t bound = std::max<uint64_t>(nq * max_row, 16);
+    const bool two_phase = bound > kTwoPhaseBytes;
+    const uint64_t o_off = round_up(hk, 256), o_rows = round_up(o_off + (nq + 1) * 8, 256),
+                   o_need = round_up(o_rows + (nq + 1) * 4, 256), o_data = o_need + 256;
+    uint64_t data_cap = two_phase ? 0 : bound;
+    if (!grow_dev(c, &r->dwork, &r->dwork_cap, o_data + data_cap + 16)) return set_err(err, MURR_E_HIP);
+    uint8_t* w = r->dwork;
+    HIPC(hipMemcpyAsync(w, r->hkeys, hk, hipMemcpyHostToDevice, c->stream));
+    const int32_t* dq_off = (const int32_t*)w;
+    const uint8_t* dq_data = w + offb;
+    uint64_t* doff = (uint64_t*)(w + o_off);
+    uint32_t* drows = (uint32_t*)(w + o_rows);
+    uint64_t* dneed = (uint64_t*)(w + o_need);
+    uint64_t gathered = bound;
+    int st;
+    if (!two_phase) {
+        st = murr_index_gather(c, x, dq_data, dq_off, nq, blob, row_off, w + o_data, data_cap, doff, nullptr, dneed);
+        if (st) return set_err(err, st);
+    } else {
+        // exact sizing: lookup + offsets, one 8-byte read-back, then the copy
+        st = murr_index_gather(c, x, dq_data, dq_off, nq, blob, row_off, nullptr, 0, doff, drows, dneed);
+        if (st) return set_err(err, st);
+        HIPC(hipMemcpyAsync(&gathered, dneed, 8, hipMemcpyDeviceToHost, c->stream));
+        HIPC(hipStreamSynchronize(c->stream));
+        if (!grow_dev(c, &r->dwork, &r->dwork_cap, o_data + gathered + 16)) {
+            // grow_dev does not keep contents: redo the first phase on the new buffer
+            return set_err(err, MURR_E_HIP);
+        }
+        if (r->dwork != w) {
+            w = r->dwork;
+            HIPC(hipMemcpyAsync(w, r->hkeys, hk, hipMemcpyHostToDevice, c->stream));
+            dq_off = (const int32_t*)w;
+            dq_data = w + offb;
+            doff = (uint64_t*)(w + o_off);
+            drows = (uint32_t*)(w + o_rows);
+            dneed = (uint64_t*)(w + o_need);
+            st = murr_index_gather(c, x, dq_data, dq_off, nq, blob, row_off, nullptr, 0, doff, drows, dneed);
+            if (st) return set_err(err, st);
+        }
+        st = murr_index_gather_copy(c, drows, nq, blob, row_off, doff, w + o_data);
+        if (st) return set_err(err, st);
+    }
+    // 3. decode + D2H.  The tile-sizing hint is the table's mean row x keys
+    // (never read past: rows end at doff[nq]).
+    const uint64_t mean = x->n ? blob_bytes / x->n : fixed;
+    const uint64_t hint = std::min<uint64_t>(gathered, std::max<uint64_t>(16, mean * nq));
+    murr_block_t blk{w + o_data, doff, nq, two_phase ? std::max<uint64_t>(gathered, 16) : hint};
+    const uint64_t utf8_cap = two_phase ? gathered : (max_row > fixed ? nq * (max_row - fixed) : 0);
+    return decode_to_host(c, &r->seg, proj, nproj, blk, utf8_cap, r->out, nullptr, nullptr, outs, err);
+}
+
+void murr_reader_free(murr_reader_t* r) {
+    if (!r) return;
+    murr_ctx* c = r->ctx;
+    if (c) (void)hipSetDevice(c->device);
+    pool_give(c, true, r->hkeys, r->hkeys_cap);
+    pool_give(c, false, r->dwork, r->dwork_cap);
+    pool_give(c, true, r->out.hout, r->out.hout_cap);
+    pool_give(c, false, r->out.dout, r->out.dout_cap);
+    delete r;
 }
 
 // Host-memory encode: H2D Arrow buffers, murr_encode_batch, D2H blobs + offsets.

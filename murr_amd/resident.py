@@ -27,6 +27,7 @@ import pyarrow as pa
 from . import _abi
 from .device import Context, DecodeOutputs, DeviceBlock, decode_blocks, download_array
 from .errors import SegmentError, raise_status
+from .row import host_array_to_arrow
 from .schema import DTypeName, TableSchema
 from .store import Store
 from .table import Table
@@ -137,6 +138,14 @@ def row_sizes(segment, arrays) -> np.ndarray:
     return size
 
 
+def _key_array(keys) -> pa.Array:
+    """Query keys as an Arrow utf8/binary array (the bytes are what is hashed)."""
+    try:
+        return pa.array(keys, pa.string())
+    except (TypeError, pa.ArrowInvalid):
+        return pa.array([k.encode() if isinstance(k, str) else bytes(k) for k in keys], pa.binary())
+
+
 # Gathers whose worst case (keys x longest row) is above this size first look
 # the rows up and size the block exactly (one 8-byte read-back), then copy.
 TWO_PHASE_BYTES = 64 << 20
@@ -158,6 +167,15 @@ class ResidentTable:
         self.off_cap = 0       # entries
         self.n = 0
         self.max_row = 0
+        self._reader = None    # murr_reader_t: scratch of the one-call host read
+
+    def __del__(self):
+        try:
+            if self._reader is not None and self.ctx.h:
+                self.ctx.L.murr_reader_free(self._reader)
+                self._reader = None
+        except Exception:
+            pass
 
     @property
     def blob(self):
@@ -274,9 +292,30 @@ class ResidentTable:
         return req, [download_array(self.ctx, outs.array(0, p), int(c.dtype), nq) for p, c in enumerate(req)]
 
     def read(self, keys, columns) -> pa.RecordBatch:
-        """Table::read (table/mod.rs:114-129) with the store lookup on the device."""
-        req, hs = self.read_host(keys, columns)
-        return host_batch(req, hs)
+        """Table::read (table/mod.rs:114-129) with the store lookup on the
+        device, in one native call (murr_reader_read: one H2D of the keys,
+        lookup + gather + decode, one D2H of the arrays)."""
+        req = self._resolve(columns)
+        nq = len(keys)
+        if self.index is None:
+            return host_batch(req, [_null_dict(c.dtype, nq) for c in req])
+        L = self.ctx.L
+        if self._reader is None:
+            h = C.c_void_p()
+            raise_status(L.murr_reader_new(self.ctx.h, C.byref(self.segment.c), C.byref(h)), what="murr_reader_new")
+            self._reader = h
+        q = keys if isinstance(keys, pa.Array) else _key_array(keys)
+        kb = q.buffers()
+        proj = (C.c_uint32 * len(req))(*[c.index for c in req])
+        outs = (_abi.HostArray * len(req))()
+        err = _abi.Error()
+        st = L.murr_reader_read(self._reader, self.index.h, self.arena.ptr, self.row_off.ptr, self.used,
+                                self.max_row, kb[2].address if nq and kb[2] is not None else None,
+                                kb[1].address if nq else None, q.offset, nq, proj, len(req), outs, C.byref(err))
+        raise_status(st, err, "murr_reader_read")
+        arrays = [host_array_to_arrow(outs[p]) for p in range(len(req))]
+        fields = [pa.field(c.name, c.dtype.arrow_dtype(), True) for c in req]
+        return pa.RecordBatch.from_arrays(arrays, schema=pa.schema(fields))
 
     def read_ipc(self, keys, columns, alignment: int = 64) -> bytes:
         """read() as the Arrow IPC stream of the HTTP fetch handler's StreamWriter
