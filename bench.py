@@ -187,6 +187,10 @@ def cpu_baseline_threads(seg, proj, host_blob, host_off, rows, target_s, threads
                       f"threads, oracle/libmurr_oracle.so, {dt:.1f} s"}
 
 
+def L_len(ctx, seg, rows, stride):
+    return ctx.L.murr_utf8_index_len(C.byref(seg.c), rows, stride)
+
+
 def run_decode(args, dist, rank, world, local_rank):
     ndev = device_count()
     if local_rank >= ndev:
@@ -207,6 +211,14 @@ def run_decode(args, dist, rank, world, local_rank):
     host_off = doff.download((rows + 1) * 8).view(np.uint64).copy()
     del dblob, doff
     blocks = [DeviceBlock.upload(ctx, host_blob, host_off) for _ in range(K)]
+    # each block's utf8 index, written with the block (murr_utf8_index; not timed,
+    # like the encode): one large block decodes on the whole GPU in one pass
+    ix_bytes = 0
+    if args.uidx_stride:
+        for b in blocks:
+            b.index_utf8(ctx, seg, args.uidx_stride)
+        ix_bytes = 8 * int(L_len(ctx, seg, rows, args.uidx_stride)) if blocks[0].uidx is not None else 0
+        ctx.sync()
     outs = DecodeOutputs(ctx, seg, proj, blocks)
     cb = (_abi.Block * K)()
     for i, b in enumerate(blocks):
@@ -215,9 +227,14 @@ def run_decode(args, dist, rank, world, local_rank):
     pj = (C.c_uint32 * len(proj))(*proj)
     err = _abi.Error()
     L = ctx.L
+    ux = (C.c_void_p * K)(*[b.uidx.ptr if b.uidx is not None else None for b in blocks]) if ix_bytes else None
 
     def step():
-        st = L.murr_decode_blocks(ctx.h, C.byref(seg.c), pj, len(proj), cb, K, outs.arrays, C.byref(err))
+        if ux is not None:
+            st = L.murr_decode_blocks_ix(ctx.h, C.byref(seg.c), pj, len(proj), cb, K, ux, args.uidx_stride,
+                                         outs.arrays, C.byref(err))
+        else:
+            st = L.murr_decode_blocks(ctx.h, C.byref(seg.c), pj, len(proj), cb, K, outs.arrays, C.byref(err))
         if st:
             raise RuntimeError(f"decode failed: {_abi.status_str(st)} row {err.row} col {err.column}")
 
@@ -238,7 +255,7 @@ def run_decode(args, dist, rank, world, local_rank):
     a0 = [outs.array(0, p) for p in range(len(proj))]
     out_block = arrow_out_bytes(seg, proj, rows, [a.null_count for a in a0],
                                 [a.data_len for a in a0])
-    in_block = int(host_blob.size) + 8 * (rows + 1)
+    in_block = int(host_blob.size) + 8 * (rows + 1) + ix_bytes  # blobs, row offsets, utf8 index
     out_step = out_block * K
     total_out = sum_over_ranks(dist, out_step * args.steps)
     value = total_out / elapsed / GIB
@@ -255,6 +272,7 @@ def run_decode(args, dist, rank, world, local_rank):
                                 "D": "configs[3] shard: 16-col mixed nullable, key-range shard per GPU"
                                 }.get(args.config, args.config),
                    "rows_per_block": rows, "blocks_per_step": K, "columns": len(proj),
+                   "utf8_index_stride": args.uidx_stride if ix_bytes else None,
                    "bytes_in_per_step": in_block * K, "bytes_out_per_step": out_step,
                    "parallelism": f"{world} key-range shard(s), no collective"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
@@ -484,6 +502,8 @@ def main():
     ap.add_argument("--mode", default="decode", choices=["decode", "host", "encode", "resident"])
     ap.add_argument("--keys", type=int, default=1000, help="resident mode: keys per read")
     ap.add_argument("--ipc", action="store_true", help="resident mode: also time the Arrow IPC message path")
+    ap.add_argument("--uidx-stride", type=int, default=512,
+                    help="decode mode: utf8 index stride of each block (0 = no index)")
     ap.add_argument("--table", default="C", choices=["C", "ref"],
                     help="resident mode: config C table, or the reference read benches' dataset (10 x f32)")
     ap.add_argument("--no-cpu", action="store_true")

@@ -205,6 +205,30 @@ int murr_decode_enqueue(murr_ctx_t* ctx, const murr_segment_t* seg,
                         murr_array_t* outs);
 int murr_decode_wait(murr_ctx_t* ctx, murr_error_t* err);
 
+/* ---- utf8 index of a block (optional) --------------------------------------
+ * For every utf8 column of the layout (column order), the string bytes of the
+ * rows before row j * stride, j = 0 .. ceil(n_rows / stride): the offsets the
+ * decode's utf8 arrays reach at those rows (Utf8Encoder::add_row,
+ * src/io/codec/utf8.rs:86-96, with the cell rules of read.rs:45-55).  u64
+ * entries, [j][nutf8].  Built once when a block is written; passed to the
+ * decode beside the block, it lets many workgroups decode one large block,
+ * each from a known starting offset, in one pass.  stride: a power of two in
+ * [64, 2^30].  A layout without utf8 columns needs no index (len 0). */
+uint64_t murr_utf8_index_len(const murr_segment_t* seg, uint64_t n_rows, uint32_t stride);
+int murr_utf8_index(murr_ctx_t* ctx, const murr_segment_t* seg, const murr_block_t* block,
+                    uint32_t stride, uint64_t* out /* device, murr_utf8_index_len entries */);  /* enqueue */
+/* murr_decode_enqueue / murr_decode_blocks with an index per block (uidx[b]
+ * null: block b has none; uidx null: no block has one).  Same outputs. */
+int murr_decode_enqueue_ix(murr_ctx_t* ctx, const murr_segment_t* seg,
+                           const uint32_t* proj, uint32_t nproj,
+                           const murr_block_t* blocks, uint32_t nblocks,
+                           const uint64_t* const* uidx, uint32_t stride, murr_array_t* outs);
+int murr_decode_blocks_ix(murr_ctx_t* ctx, const murr_segment_t* seg,
+                          const uint32_t* proj, uint32_t nproj,
+                          const murr_block_t* blocks, uint32_t nblocks,
+                          const uint64_t* const* uidx, uint32_t stride, murr_array_t* outs,
+                          murr_error_t* err);
+
 /* ---- device-resident encode (Arrow -> row blobs) -------------------------- */
 
 /* One Arrow input column (device pointers).  `offset` is the Arrow array

@@ -91,6 +91,12 @@ SIGNATURES = {
     "murr_decode_enqueue": (I32, [P, C.POINTER(Segment), C.POINTER(U32), U32, C.POINTER(Block), U32,
                                   C.POINTER(Array)]),
     "murr_decode_wait": (I32, [P, C.POINTER(Error)]),
+    "murr_decode_blocks_ix": (I32, [P, C.POINTER(Segment), C.POINTER(U32), U32, C.POINTER(Block), U32,
+                                    C.POINTER(C.c_void_p), U32, C.POINTER(Array), C.POINTER(Error)]),
+    "murr_decode_enqueue_ix": (I32, [P, C.POINTER(Segment), C.POINTER(U32), U32, C.POINTER(Block), U32,
+                                     C.POINTER(C.c_void_p), U32, C.POINTER(Array)]),
+    "murr_utf8_index_len": (U64, [C.POINTER(Segment), U64, U32]),
+    "murr_utf8_index": (I32, [P, C.POINTER(Segment), C.POINTER(Block), U32, P]),
     "murr_encode_bound": (U64, [C.POINTER(Segment), U64, C.POINTER(U64)]),
     "murr_encode_batch": (I32, [P, C.POINTER(Segment), C.POINTER(ColIn), U64, P, U64, P,
                                 C.POINTER(U64), C.POINTER(Error)]),

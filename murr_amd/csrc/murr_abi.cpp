@@ -575,15 +575,21 @@ int pending_set(murr_ctx* c, murr_array_t* outs, const murr_block_t* blocks, uin
     return MURR_OK;
 }
 
+// A utf8 index stride: a power of two in [64, 2^30].
+bool stride_ok(uint64_t s) { return s >= 64 && s <= (1ull << 30) && (s & (s - 1)) == 0; }
+
 // The layout-specialised decode (murr_jit_kernel.hip).  Tile shape from the
-// mean row size; local mode (a workgroup owns whole blocks) when the blocks
-// fill the co-resident grid, else stream mode (tiles round-robin, utf8
-// prefixes by decoupled look-back).  A projection naming a column twice runs
-// one launch per occurrence round (the later rounds only fill the duplicate
-// outputs, so they report no errors).
+// mean row size.  Local mode (a workgroup owns whole blocks) when the blocks
+// fill the co-resident grid; or, when every block can be cut (it has a utf8
+// index, or the layout has no utf8 column), local mode over virtual blocks
+// of a few tiles, each starting at its index entry; else split mode
+// (segments, two passes, decoupled look-back).  A projection naming a column
+// twice runs one launch per occurrence round (the later rounds only fill the
+// duplicate outputs, so they report no errors).
 int decode_enqueue_jit(murr_ctx* c, const murr_segment_t* seg, const JitLayout* jl, const uint32_t* proj,
                        uint32_t nproj, const murr_block_t* blocks, uint32_t nblocks, murr_array_t* outs,
-                       const std::vector<DecProj>& dp, double est_row, bool force_local = false) {
+                       const std::vector<DecProj>& dp, double est_row, bool force_local = false,
+                       const uint64_t* const* uidx = nullptr, uint32_t stride = 0) {
     murr_error_t* err = nullptr;
     const bool verbose = std::getenv("MURR_DECODE_VERBOSE") != nullptr;
     uint32_t nu_layout = 0;
@@ -639,23 +645,44 @@ int decode_enqueue_jit(murr_ctx* c, const murr_segment_t* seg, const JitLayout* 
     const uint64_t G = (uint64_t)c->cus * bpc;
 
     std::vector<DecBlock> db(nblocks);
-    std::vector<uint32_t> order;
-    uint64_t tiles = 0;
+    uint64_t tiles = 0, nonempty = 0, total_rows = 0;
+    bool cuttable = true;  // every block can be cut into virtual blocks
     for (uint32_t b = 0; b < nblocks; b++) {
-        db[b] = DecBlock{blocks[b].data, blocks[b].row_off, blocks[b].n_rows, tiles};
+        const uint64_t* ux = uidx ? uidx[b] : nullptr;
+        db[b] = DecBlock{blocks[b].data, blocks[b].row_off, blocks[b].n_rows, tiles, ux};
         tiles += (blocks[b].n_rows + K.tr - 1) / K.tr;
-        if (blocks[b].n_rows) order.push_back(b);
+        nonempty += blocks[b].n_rows != 0;
+        total_rows += blocks[b].n_rows;
+        cuttable &= nu_layout == 0 || ux != nullptr || blocks[b].n_rows == 0;
     }
-    const uint64_t nonempty = order.size();
     // local mode when whole blocks keep >= 75 % of the grid busy
-    bool local = false;
-    (void)bpc_safe;
+    bool local = false, cut = false;
     if (nonempty) {
         const uint64_t rounds = (nonempty + G - 1) / G;
         local = nonempty * 4 >= rounds * G * 3;
+        if (!local && cuttable && stride_ok(nu_layout ? stride : 64)) local = cut = true;
     }
-    if (const char* e = std::getenv("MURR_JIT_MODE")) local = std::string(e) == "local";  // tuning
+    if (const char* e = std::getenv("MURR_JIT_MODE")) {  // tuning
+        local = std::string(e) == "local";
+        cut = cut && local;
+    }
     if (force_local) local = true;
+    // (virtual) blocks of local mode: whole blocks, or cuts every V rows (a
+    // multiple of the index stride, about 8 per workgroup for balance)
+    std::vector<JitSeg> lsegs;
+    if (local) {
+        const uint64_t S = nu_layout ? std::max<uint32_t>(stride, 1) : K.tr;  // (stride checked when cut)
+        uint64_t V = std::max<uint64_t>(K.tr, (total_rows + 8 * G - 1) / (8 * G));
+        V = (V + S - 1) / S * S;
+        if (const char* e = std::getenv("MURR_JIT_VROWS")) V = std::max<uint64_t>(S, (uint64_t)std::atoll(e) / S * S);
+        for (uint32_t b = 0; b < nblocks; b++) {
+            const uint64_t n = blocks[b].n_rows;
+            if (!n) continue;
+            if (!cut) lsegs.push_back(JitSeg{b, 0, 0, n});
+            else
+                for (uint64_t r = 0; r < n; r += V) lsegs.push_back(JitSeg{b, 0, r, std::min(n, r + V)});
+        }
+    }
     // Split mode: segments of seg_tiles tiles dealt round-robin over a
     // co-resident grid; a grid round of segments (the distance between a
     // segment's two passes) is kept near 96 MiB so the second pass still
@@ -675,7 +702,7 @@ int decode_enqueue_jit(murr_ctx* c, const murr_segment_t* seg, const JitLayout* 
         }
     }
     const uint64_t nseg = jsegs.size();
-    const uint64_t grid = std::max<uint64_t>(1, local ? std::min<uint64_t>(G, nonempty) : std::min<uint64_t>(G_split, nseg));
+    const uint64_t grid = std::max<uint64_t>(1, local ? std::min<uint64_t>(G, lsegs.size()) : std::min<uint64_t>(G_split, nseg));
     bool emit = false;
     for (uint32_t p = 0; p < nproj; p++) emit |= dp[p].is_utf8;
 
@@ -696,9 +723,9 @@ int decode_enqueue_jit(murr_ctx* c, const murr_segment_t* seg, const JitLayout* 
     const uint64_t zbytes = round_up(z_flags + flag_bytes * rounds, 16);
     const uint64_t d_blocks = zbytes;
     const uint64_t d_outs = round_up(d_blocks + sizeof(DecBlock) * nblocks, 16);
-    const uint64_t d_order = round_up(d_outs + sizeof(DecOut) * dout.size(), 16);
-    const uint64_t d_segs = round_up(d_order + 4 * order.size(), 16);
-    const uint64_t d_slots = round_up(d_segs + sizeof(JitSeg) * nseg, 16);
+    const std::vector<JitSeg>& segs_out = local ? lsegs : jsegs;
+    const uint64_t d_segs = round_up(d_outs + sizeof(DecOut) * dout.size(), 16);
+    const uint64_t d_slots = round_up(d_segs + sizeof(JitSeg) * segs_out.size(), 16);
     const uint64_t d_projc = round_up(d_slots + 2 * (uint64_t)npad * rounds, 16);
     const uint64_t d_sink = round_up(d_projc + 2 * (uint64_t)nproj, 256);
     const uint64_t dend = d_sink + 1024;
@@ -713,8 +740,7 @@ int decode_enqueue_jit(murr_ctx* c, const murr_segment_t* seg, const JitLayout* 
     if (hz) std::memset(c->hs, 0, hz);
     std::memcpy(hd + (d_blocks - zbytes), db.data(), sizeof(DecBlock) * nblocks);
     std::memcpy(hd + (d_outs - zbytes), dout.data(), sizeof(DecOut) * dout.size());
-    if (!order.empty()) std::memcpy(hd + (d_order - zbytes), order.data(), 4 * order.size());
-    if (nseg) std::memcpy(hd + (d_segs - zbytes), jsegs.data(), sizeof(JitSeg) * nseg);
+    if (!segs_out.empty()) std::memcpy(hd + (d_segs - zbytes), segs_out.data(), sizeof(JitSeg) * segs_out.size());
     std::vector<uint16_t> slots((uint64_t)npad * rounds, 0xFFFF);
     for (uint32_t col = 0; col < ncols; col++)
         for (uint32_t r = 0; r < occ[col].size(); r++) slots[(uint64_t)r * npad + col] = (uint16_t)occ[col][r];
@@ -734,7 +760,7 @@ int decode_enqueue_jit(murr_ctx* c, const murr_segment_t* seg, const JitLayout* 
     JitArgsHead h{};
     h.blocks = (const DecBlock*)(c->ws + d_blocks);
     h.outs = (const DecOut*)(c->ws + d_outs);
-    h.order = (const uint32_t*)(c->ws + d_order);
+    h.order = nullptr;
     h.segs = (const JitSeg*)(c->ws + d_segs);
     h.projcols = (const uint16_t*)(c->ws + d_projc);
     h.nulls = (unsigned long long*)(c->ws + z_nulls);
@@ -745,12 +771,14 @@ int decode_enqueue_jit(murr_ctx* c, const murr_segment_t* seg, const JitLayout* 
     h.emit = emit;
     h.nblocks = nblocks;
     h.nproj = nproj;
-    h.norder = (uint32_t)order.size();
+    h.norder = (uint32_t)lsegs.size();
+    h.ulog = cut && nu_layout ? (uint32_t)__builtin_ctzll(stride) : 0;
     h.mode = local ? 0 : 1;
     h.stage = stage;
     if (verbose)
         std::fprintf(stderr, "decode launch (jit %ux%u): %s grid %llu (%d/CU, %d split) blocks %llu tiles %llu segments %llu (%llu tiles) rows/tile %u stage %u lds %u rounds %u\n",
-                     K.nw, K.r, local ? "local" : "split", (unsigned long long)grid, bpc, bpc_safe, (unsigned long long)nonempty,
+                     K.nw, K.r, cut ? "local-cut" : local ? "local" : "split", (unsigned long long)grid, bpc, bpc_safe,
+                     (unsigned long long)(local ? lsegs.size() : nonempty),
                      (unsigned long long)tiles, (unsigned long long)nseg, (unsigned long long)seg_tiles, K.tr, stage, lds, rounds);
     HIPC(hipEventRecord(c->k0, c->stream));
     if (tiles) {
@@ -807,10 +835,17 @@ int murr_segment_prepare(murr_ctx_t* c, const murr_segment_t* seg) {
 int murr_decode_enqueue(murr_ctx_t* c, const murr_segment_t* seg, const uint32_t* proj,
                         uint32_t nproj, const murr_block_t* blocks, uint32_t nblocks,
                         murr_array_t* outs) {
+    return murr_decode_enqueue_ix(c, seg, proj, nproj, blocks, nblocks, nullptr, 0, outs);
+}
+
+int murr_decode_enqueue_ix(murr_ctx_t* c, const murr_segment_t* seg, const uint32_t* proj,
+                           uint32_t nproj, const murr_block_t* blocks, uint32_t nblocks,
+                           const uint64_t* const* uidx, uint32_t stride, murr_array_t* outs) {
     murr_error_t* err = nullptr;
     if (!c || !valid_segment(seg) || (nblocks && (!blocks || !outs)) || (nproj && !proj) ||
         c->pending)
         return MURR_E_ARGUMENT;
+    if (uidx && !stride_ok(stride)) return MURR_E_ARGUMENT;
     if (nproj == 0) return MURR_E_ARROW;  // RecordBatch::try_new, read.rs:106-108
     if (nproj > kMaxProj || nblocks > 0x3FFFF) return MURR_E_ARGUMENT;
     for (uint32_t p = 0; p < nproj; p++)
@@ -913,7 +948,8 @@ int murr_decode_enqueue(murr_ctx_t* c, const murr_segment_t* seg, const uint32_t
         if (jmode != 0 && max_rows < 0x7FFFFFFFull) {
             std::string why;
             const JitLayout* jl = jit_layout(c->device, seg, &why);
-            if (jl) return decode_enqueue_jit(c, seg, jl, proj, nproj, blocks, nblocks, outs, dp, est_row);
+            if (jl) return decode_enqueue_jit(c, seg, jl, proj, nproj, blocks, nblocks, outs, dp, est_row, false, uidx,
+                                              stride);
             if (jmode == 1) {
                 std::fprintf(stderr, "murr: JIT decode unavailable: %s\n", why.c_str());
                 return MURR_E_INTERNAL;
@@ -1013,6 +1049,38 @@ int murr_decode_enqueue(murr_ctx_t* c, const murr_segment_t* seg, const uint32_t
     return pending_set(c, outs, blocks, nblocks, nproj, dp, rb);
 }
 
+uint64_t murr_utf8_index_len(const murr_segment_t* seg, uint64_t n_rows, uint32_t stride) {
+    if (!valid_segment(seg) || !stride_ok(stride)) return 0;
+    uint64_t nu = 0;
+    for (uint32_t i = 0; i < seg->ncols; i++) nu += seg->cols[i].dtype == MURR_UTF8;
+    return nu ? ((n_rows + stride - 1) / stride + 1) * nu : 0;
+}
+
+int murr_utf8_index(murr_ctx_t* c, const murr_segment_t* seg, const murr_block_t* block, uint32_t stride,
+                    uint64_t* out) {
+    murr_error_t* err = nullptr;
+    if (!c || !valid_segment(seg) || !block || !stride_ok(stride) || c->pending) return MURR_E_ARGUMENT;
+    Utf8IndexArgs a{};
+    for (uint32_t i = 0; i < seg->ncols; i++) {
+        if (seg->cols[i].dtype != MURR_UTF8) continue;
+        if (a.nu == kMaxUidxCols) return MURR_E_ARGUMENT;
+        a.col[a.nu] = seg->cols[i].index;
+        a.fo[a.nu] = seg->bitset_size + seg->cols[i].offset;
+        a.nu++;
+    }
+    if (!a.nu) return MURR_OK;  // no utf8 column: nothing to index
+    if (!out || (block->n_rows && (!block->data || !block->row_off))) return MURR_E_ARGUMENT;
+    HIPC(hipSetDevice(c->device));
+    a.data = block->data;
+    a.row_off = block->row_off;
+    a.out = out;
+    a.n = block->n_rows;
+    a.stride = stride;
+    a.bs = seg->bitset_size;
+    HIPC(launch_utf8_index(a, c->stream));
+    return MURR_OK;
+}
+
 int murr_decode_wait(murr_ctx_t* c, murr_error_t* err) {
     if (!c || !c->pending) return set_err(err, MURR_E_ARGUMENT);
     c->pending = false;
@@ -1078,7 +1146,13 @@ int murr_decode_wait(murr_ctx_t* c, murr_error_t* err) {
 int murr_decode_blocks(murr_ctx_t* c, const murr_segment_t* seg, const uint32_t* proj,
                        uint32_t nproj, const murr_block_t* blocks, uint32_t nblocks,
                        murr_array_t* outs, murr_error_t* err) {
-    int st = murr_decode_enqueue(c, seg, proj, nproj, blocks, nblocks, outs);
+    return murr_decode_blocks_ix(c, seg, proj, nproj, blocks, nblocks, nullptr, 0, outs, err);
+}
+
+int murr_decode_blocks_ix(murr_ctx_t* c, const murr_segment_t* seg, const uint32_t* proj,
+                          uint32_t nproj, const murr_block_t* blocks, uint32_t nblocks,
+                          const uint64_t* const* uidx, uint32_t stride, murr_array_t* outs, murr_error_t* err) {
+    int st = murr_decode_enqueue_ix(c, seg, proj, nproj, blocks, nblocks, uidx, stride, outs);
     if (st) {
         if (err && st != MURR_E_HIP) set_err(err, st);
         else if (err && st == MURR_E_HIP) set_err(err, st, (int)hipGetLastError());

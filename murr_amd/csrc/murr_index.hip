@@ -393,4 +393,87 @@ hipError_t launch_offsets_rebase(int32_t* dst, const int32_t* src, uint64_t n, i
     return hipGetLastError();
 }
 
+// ---- utf8 index of a block (murr_utf8_index) -------------------------------------
+// For every utf8 column u of the layout, the string bytes of the rows before
+// row j * stride: what the decode's utf8 offsets reach at that row
+// (Utf8Encoder::add_row, src/io/codec/utf8.rs:86-96), by the decode's own
+// cell rules (read.rs:45-55 bounds; a null, missing, short or malformed cell
+// adds nothing).  With it, a block can be decoded by many workgroups at once,
+// each from a known starting offset.
+namespace {
+__device__ __forceinline__ uint32_t ld32u(const uint8_t* p) {
+    return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+
+// One workgroup per stride of rows: the stride's string bytes per column.
+__global__ void __launch_bounds__(256) uidx_sums(Utf8IndexArgs A) {
+    __shared__ uint64_t part[4];
+    const uint64_t r0 = (uint64_t)blockIdx.x * A.stride, r1 = r0 + A.stride < A.n ? r0 + A.stride : A.n;
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (uint32_t u = 0; u < A.nu; u++) {
+        const uint32_t c = A.col[u], fo = A.fo[u];
+        uint64_t sum = 0;
+        for (uint64_t i = r0 + threadIdx.x; i < r1; i += 256) {
+            const uint64_t a = gp(A.row_off)[i], e = gp(A.row_off)[i + 1];
+            if (e < a || e - a > 0xFFFFFFFFull) continue;  // the decode reports such a row
+            const uint32_t rl = (uint32_t)(e - a);
+            const uint8_t* row = A.data + a;
+            if (rl < A.bs || ((row[c >> 3] >> (c & 7)) & 1)) continue;  // short row / null cell
+            if (fo + 4 > rl) continue;
+            const uint32_t sl = ld32u(row + fo), vlen = rl - A.bs;
+            if (sl > vlen - 4) continue;
+            const uint32_t l = ld32u(row + A.bs + sl);
+            if (l > vlen - 4 - sl) continue;
+            sum += l;
+        }
+        for (int m = 32; m >= 1; m >>= 1) sum += (uint64_t)__shfl_xor((unsigned long long)sum, m, 64);
+        if (lane == 0) part[wave] = sum;
+        __syncthreads();
+        if (threadIdx.x == 0) gp(A.out)[(uint64_t)blockIdx.x * A.nu + u] = part[0] + part[1] + part[2] + part[3];
+        __syncthreads();
+    }
+}
+
+// One workgroup: the strides' sums -> exclusive prefixes in place, plus the
+// block total at entry nstrides.
+__global__ void __launch_bounds__(1024) uidx_scan(uint64_t* out, uint64_t nstrides, uint32_t nu) {
+    __shared__ uint64_t wsum[16];
+    __shared__ uint64_t carry_s;
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (uint32_t u = 0; u < nu; u++) {
+        uint64_t carry = 0;
+        for (uint64_t base = 0; base < nstrides; base += 1024) {
+            const uint64_t j = base + threadIdx.x;
+            const uint64_t v = j < nstrides ? gp(out)[j * nu + u] : 0;
+            uint64_t inc = v;
+            for (int d = 1; d < 64; d <<= 1) {
+                const uint64_t o = (uint64_t)__shfl_up((unsigned long long)inc, d, 64);
+                if (lane >= (uint32_t)d) inc += o;
+            }
+            if (lane == 63) wsum[wave] = inc;
+            __syncthreads();
+            uint64_t before = 0, total = 0;
+            for (uint32_t w = 0; w < 16; w++) {
+                before += w < wave ? wsum[w] : 0;
+                total += wsum[w];
+            }
+            if (j < nstrides) gp(out)[j * nu + u] = carry + before + inc - v;
+            carry += total;
+            __syncthreads();
+        }
+        if (threadIdx.x == 0) carry_s = carry;
+        __syncthreads();
+        if (threadIdx.x == 0) gp(out)[nstrides * nu + u] = carry_s;
+        __syncthreads();
+    }
+}
+}  // namespace
+
+hipError_t launch_utf8_index(const Utf8IndexArgs& a, hipStream_t s) {
+    const uint64_t nstrides = (a.n + a.stride - 1) / a.stride;
+    if (nstrides) hipLaunchKernelGGL(uidx_sums, dim3((uint32_t)nstrides), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(uidx_scan, dim3(1), dim3(1024), 0, s, a.out, nstrides, a.nu);
+    return hipGetLastError();
+}
+
 }  // namespace murr

@@ -31,6 +31,7 @@ struct DecBlock {             // one block (batch read) of row blobs
     const uint64_t* row_off;  // n_rows + 1
     uint64_t n_rows;
     uint64_t tile_base;       // first global tile of this block
+    const uint64_t* uidx;     // its utf8 index (murr_utf8_index) or null (JIT kernel only)
 };
 
 struct DecProj {              // one projected column
@@ -119,8 +120,8 @@ struct JitSeg {                    // = mj::Seg: rows [r_begin, r_end) of block 
 struct JitArgsHead {               // = mj::Args without its trailing slot[] (murr_jit_kernel.hip)
     const DecBlock* blocks;
     const DecOut* outs;            // [nblocks][nproj]
-    const uint32_t* order;         // local mode: non-empty blocks
-    const JitSeg* segs;            // split mode: segments
+    const uint32_t* order;         // unused
+    const JitSeg* segs;            // split mode: segments; local mode: (virtual) blocks
     const uint16_t* slot_tab;      // [ncols] output position per column (0xFFFF = not decoded)
     const uint16_t* projcols;      // [nproj] column per output position
     unsigned long long* nulls;
@@ -131,7 +132,8 @@ struct JitArgsHead {               // = mj::Args without its trailing slot[] (mu
     uint64_t nseg;
     uint32_t nblocks, nproj, norder, mode;  // mode: 0 local, 1 split
     uint32_t stage, report;
-    uint32_t emit, pad1;           // split mode: a second pass writes utf8 cells
+    uint32_t emit;                 // split mode: a second pass writes utf8 cells
+    uint32_t ulog;                 // log2 of the utf8 index stride
     unsigned int* abort_word;      // split mode: a timed-out wait aborts the launch (zeroed)
 };
 static_assert(sizeof(JitArgsHead) == 136, "mj::Args layout");
@@ -157,6 +159,19 @@ hipError_t launch_decode(const DecodeArgs& a, uint32_t nw, uint32_t kc, uint32_t
 int decode_blocks_per_cu(uint32_t nw, uint32_t kc, uint32_t lds);
 hipError_t launch_encode(const EncodeArgs& a, uint32_t grid, hipStream_t s);
 int encode_blocks_per_cu();
+
+// utf8 index of a block (murr_index.hip, murr_utf8_index).
+constexpr uint32_t kMaxUidxCols = 64;
+struct Utf8IndexArgs {
+    const uint8_t* data;
+    const uint64_t* row_off;
+    uint64_t* out;                 // [(n + stride - 1) / stride + 1][nu]
+    uint64_t n, stride;
+    uint32_t bs, nu;
+    uint32_t col[kMaxUidxCols];    // segment column index of utf8 column u
+    uint32_t fo[kMaxUidxCols];     // its slot's row offset (bitset_size + offset)
+};
+hipError_t launch_utf8_index(const Utf8IndexArgs& a, hipStream_t s);
 
 // Device key index + row gather (murr_index.hip).
 constexpr uint32_t kMissing = 0xFFFFFFFFu;

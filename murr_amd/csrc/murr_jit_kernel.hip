@@ -69,10 +69,13 @@ struct Blk {  // = murr::DecBlock
     const uint8_t* data;
     const uint64_t* row_off;
     uint64_t n_rows;
-    uint64_t tile_base;  // first global tile of this block (stream mode)
+    uint64_t tile_base;    // first global tile of this block (stream mode)
+    const uint64_t* uidx;  // utf8 index (murr_utf8_index) or null: [row / 2^ulog][NU] starting offsets
 };
-// A segment: rows [r_begin, r_end) of block b (split mode); `first` is the
-// index of the block's first segment.
+// A segment: rows [r_begin, r_end) of block b; `first` is the index of the
+// block's first segment (split mode).  Local mode walks a table of them too:
+// whole blocks, or virtual blocks of an indexed block (their utf8 offsets
+// start at the index's entry for r_begin).
 struct Seg {  // = murr::JitSeg
     uint32_t b, first;
     uint64_t r_begin, r_end;
@@ -89,8 +92,8 @@ constexpr uint32_t NCW = (NCOLS + 63) / 64;  // 64-column lane groups
 struct Args {
     const Blk* blocks;
     const Out* outs;              // [nblocks][nproj]
-    const uint32_t* order;        // local mode: non-empty blocks in launch order
-    const void* segs;             // split mode: Seg[nseg]
+    const uint32_t* order;        // unused
+    const void* segs;             // Seg[nseg] (split mode) or Seg[norder] (local mode)
     const uint16_t* slot_tab;     // = slot[], in memory (per-lane reads)
     const uint16_t* projcols;     // [nproj]: segment column of projection position p
     unsigned long long* nulls;    // [nblocks][nproj]
@@ -102,7 +105,8 @@ struct Args {
     uint32_t nblocks, nproj, norder, mode;
     uint32_t stage;               // stage bytes per ring slot (multiple of 1 KiB)
     uint32_t report;              // report malformed rows (the first projection round)
-    uint32_t emit, pad1;          // split mode: some utf8 column is projected (second pass)
+    uint32_t emit;                // split mode: some utf8 column is projected (second pass)
+    uint32_t ulog;                // log2 of the utf8 index stride
     unsigned int* abort_word;     // split mode: set when a wait timed out (every wait then gives up)
     uint16_t slot[(NCOLS + 1) & ~1u];  // output position of column c, 0xFFFF = not decoded
 };
@@ -338,12 +342,13 @@ DEV Cur cur_make(uint32_t ok, uint32_t k, uint32_t b, uint32_t first, uint32_t p
     c.r_end = ok && r_end == ~0ull ? c.n_rows : r_end;
     return c;
 }
-// local mode: the k-th entry of the launch's block order (whole blocks)
+// local mode: the k-th (virtual) block of the launch
 DEV Cur cur_local(uint32_t k) {
     k = sgpr(k);
     const uint32_t ok = k < args()->norder;
-    const uint32_t b = ok ? sgpr(((const CAS uint32_t*)args()->order)[k]) : 0u;
-    return cur_make(ok, k, b, 0, 0, 0, ~0ull, 0);
+    const CAS Seg* sp = (const CAS Seg*)args()->segs + (ok ? k : 0u);
+    const uint64_t rb = ok ? sgpr64(sp->r_begin) : 0, re = ok ? sgpr64(sp->r_end) : 0;
+    return cur_make(ok, k, ok ? sgpr(sp->b) : 0u, 0, 0, rb, re, rb);
 }
 // split mode: segment k, first pass
 DEV Cur cur_seg(uint32_t k) {
@@ -1129,7 +1134,6 @@ DEV void kernel_body() {
     const uint64_t ct0 = __builtin_amdgcn_s_memtime();
 #endif
     lds_barrier();  // B_0
-    uint32_t prev_b = ~0u;
     for (uint32_t it = 0;; it++) {
         const LAS uint8_t* info = infos + (it & 7) * 32;
         if (!tile_valid(info)) break;
@@ -1137,10 +1141,12 @@ DEV void kernel_body() {
         const Tile T = tile_read(spans + (it & 7) * 16, info, stage);
         const LAS uint32_t* ro = (const LAS uint32_t*)slot;
         const uint32_t ph = tile_phase(info);
-        if (MODE == 0 && T.b != prev_b) {
+        if (MODE == 0 && T.seg_first) {
+            // local mode: a (virtual) block starts at 0, or at its utf8 index entry
+            const uint64_t* ux = (const uint64_t*)sgpr64((uint64_t)((const CAS Blk*)args()->blocks + T.b)->uidx);
 #pragma unroll
-            for (uint32_t u = 0; u < NU; u++) run[u] = 0;  // local mode: a new block starts at 0
-            prev_b = T.b;
+            for (uint32_t u = 0; u < NU; u++)
+                run[u] = NUTF8 && T.r0 ? sgpr64(((const CAS uint64_t*)ux)[(T.r0 >> args()->ulog) * NU + u]) : 0;
         }
         if (T.hbm == 2) {  // a tile over 4 GiB of blob bytes (unsupported): report; keep the protocol going
             if (wave == 0 && lane == 0) report(args()->err, err_key(T.b, T.r0, 0, kStMalformed));

@@ -114,11 +114,29 @@ class DeviceBuffer:
 
 @dataclass
 class DeviceBlock:
-    """murr_block_t: row blobs back to back + row offsets (n_rows + 1)."""
+    """murr_block_t: row blobs back to back + row offsets (n_rows + 1), and
+    optionally its utf8 index (murr_utf8_index, built by `index_utf8`)."""
     data: DeviceBuffer
     row_off: DeviceBuffer
     n_rows: int
     data_bytes: int
+    uidx: "DeviceBuffer | None" = None
+    stride: int = 0
+
+    def index_utf8(self, ctx: "Context", segment: SegmentSchema, stride: int = 512) -> "DeviceBlock":
+        """Build the block's utf8 index (per `stride` rows, every utf8 column's
+        string bytes before it): lets one large block be decoded by the whole
+        GPU in one pass.  A layout without utf8 columns needs none."""
+        n = int(ctx.L.murr_utf8_index_len(C.byref(segment.c), self.n_rows, stride))
+        if n == 0:
+            self.uidx, self.stride = None, 0
+            return self
+        buf = ctx.alloc(8 * n)
+        cb = _abi.Block(self.data.ptr, self.row_off.ptr, self.n_rows, self.data_bytes)
+        raise_status(ctx.L.murr_utf8_index(ctx.h, C.byref(segment.c), C.byref(cb), stride, buf.ptr),
+                     what="murr_utf8_index")
+        self.uidx, self.stride = buf, stride
+        return self
 
     @classmethod
     def upload(cls, ctx: Context, data: np.ndarray, row_off: np.ndarray) -> "DeviceBlock":
@@ -180,8 +198,17 @@ def decode_blocks(ctx: Context, segment: SegmentSchema, proj, blocks, outs: Deco
         cb[i].data_bytes = blk.data_bytes
     pj = (C.c_uint32 * max(len(proj), 1))(*proj)
     err = _abi.Error()
-    st = ctx.L.murr_decode_blocks(ctx.h, C.byref(segment.c), pj, len(proj), cb, len(blocks),
-                                  outs.arrays, C.byref(err))
+    ix = [b.uidx for b in blocks]
+    if any(u is not None for u in ix):
+        strides = {b.stride for b in blocks if b.uidx is not None}
+        if len(strides) != 1:
+            raise ValueError("blocks of one decode share one utf8 index stride")
+        up = (C.c_void_p * len(blocks))(*[u.ptr if u is not None else None for u in ix])
+        st = ctx.L.murr_decode_blocks_ix(ctx.h, C.byref(segment.c), pj, len(proj), cb, len(blocks), up,
+                                         strides.pop(), outs.arrays, C.byref(err))
+    else:
+        st = ctx.L.murr_decode_blocks(ctx.h, C.byref(segment.c), pj, len(proj), cb, len(blocks),
+                                      outs.arrays, C.byref(err))
     raise_status(st, err, "murr_decode_blocks")
     return outs
 

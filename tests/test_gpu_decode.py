@@ -293,3 +293,112 @@ def test_validity_first_null_late(ctx, kernel_mode, first_null):
         for p in range(len(proj)):
             assert_array_equal(got[b][p], want[p], f"block {b} proj {p}")
             check_padding(got[b][p], len(oo) - 1)
+
+
+# ---- utf8 index (murr_utf8_index) and the decode of cut blocks ----------------
+
+def utf8_cols(dtypes):
+    return [i for i, d in enumerate(dtypes) if d == D.Utf8]
+
+
+def expected_index(oseg, dtypes, data, off, n, stride):
+    """Index entries from the oracle's own decode: column u's utf8 offsets at
+    rows 0, stride, 2 stride, ..., and n (the block total)."""
+    uc = utf8_cols(dtypes)
+    want = O.decode_block(oseg, uc, data, off)
+    js = list(range(0, n, stride)) + [n]
+    return np.array([[int(want[u]["offsets"][j]) for u in range(len(uc))] for j in js], np.uint64)
+
+
+@pytest.mark.parametrize("seed,n,stride", [(41, 1, 64), (42, 1000, 64), (43, 4099, 512), (44, 20000, 256),
+                                           (45, 70000, 4096)])
+def test_utf8_index_matches_oracle_offsets(ctx, seed, n, stride):
+    rng = np.random.default_rng(seed)
+    dtypes = [D.Utf8, D.Int32, D.Utf8, D.Bool, D.Utf8]
+    cols = random_columns(rng, dtypes, n, null_p=0.2, max_str=30)
+    oseg, data, off = oracle_block(dtypes, cols, n, set(rng.choice(n, size=n // 9, replace=False).tolist()))
+    seg = seg_of(dtypes)
+    blk = DeviceBlock.upload(ctx, data, off).index_utf8(ctx, seg, stride)
+    got = blk.uidx.download().view(np.uint64).reshape(-1, 3)
+    assert np.array_equal(got, expected_index(oseg, dtypes, data, off, n, stride))
+
+
+def test_utf8_index_rows_the_decode_rejects_count_zero(ctx):
+    # a malformed cell (slot past the row) and a short row add nothing, as in the decode
+    dtypes = [D.Utf8, D.Float32]
+    n = 300
+    rng = np.random.default_rng(46)
+    cols = random_columns(rng, dtypes, n, null_p=0.0, max_str=10)
+    oseg, data, off = oracle_block(dtypes, cols, n)
+    data = data.copy()
+    a = int(off[100])
+    data[a + 1: a + 5] = np.frombuffer((10 ** 6).to_bytes(4, "little"), np.uint8)  # slot of row 100
+    blk = DeviceBlock.upload(ctx, data, off).index_utf8(ctx, seg_of(dtypes), 64)
+    got = blk.uidx.download().view(np.uint64)
+    lens = np.diff(cols[0]["offsets"].astype(np.int64))
+    lens[100] = 0
+    want = [int(lens[:j].sum()) for j in list(range(0, n, 64)) + [n]]
+    assert got.tolist() == want
+
+
+@pytest.mark.parametrize("seed,n,nblocks,vrows", [(51, 50000, 1, 0), (52, 30000, 3, 512), (53, 9000, 2, 1024),
+                                                  (54, 257, 1, 0)])
+def test_cut_blocks_decode_bit_exact(ctx, kernel_mode, monkeypatch, seed, n, nblocks, vrows):
+    # few large blocks with a utf8 index: local mode over virtual blocks, each
+    # starting at its index entry; same buffers as the oracle
+    if vrows:
+        monkeypatch.setenv("MURR_JIT_VROWS", str(vrows))
+    rng = np.random.default_rng(seed)
+    dtypes = [D.Utf8, D.Int64, D.Bool, D.Utf8, D.Float32, D.UInt8, D.Utf8]
+    oseg = O.Segment([int(d) for d in dtypes])
+    proj = [3, 0, 4, 2, 1, 5, 6, 0]
+    seg = seg_of(dtypes)
+    dblocks, wants = [], []
+    for b in range(nblocks):
+        cols = random_columns(rng, dtypes, n, null_p=0.15, max_str=20)
+        _, data, off = oracle_block(dtypes, cols, n, set(rng.choice(n, size=n // 11, replace=False).tolist()))
+        dblocks.append(DeviceBlock.upload(ctx, data, off).index_utf8(ctx, seg, 512))
+        wants.append(O.decode_block(oseg, proj, data, off))
+    outs = decode_blocks(ctx, seg, proj, dblocks)
+    for b, blk in enumerate(dblocks):
+        for p, ci in enumerate(proj):
+            got = download_array(ctx, outs.array(b, p), int(seg.columns[ci].dtype), n)
+            assert_array_equal(got, wants[b][p], f"block {b} proj {p}")
+            check_padding(got, n)
+
+
+def test_cut_blocks_first_error_is_row_major(ctx, kernel_mode):
+    dtypes = [D.Utf8, D.Utf8]
+    n = 40000
+    rng = np.random.default_rng(55)
+    cols = random_columns(rng, dtypes, n, null_p=0.0, unicode=False)
+    oseg, data, off = oracle_block(dtypes, cols, n)
+    data = data.copy()
+    lens = [np.diff(c["offsets"].astype(np.int64)) for c in cols]
+    for r0, c in ((31000, 0), (23000, 1)):
+        r = r0 + int(np.argmax(lens[c][r0:] > 0))
+        a = int(off[r])
+        slot = int.from_bytes(data[a + 1 + 4 * c: a + 5 + 4 * c].tobytes(), "little")
+        data[a + 1 + slot + 4] = 0xFF
+    with pytest.raises(O.OracleError) as oe:
+        O.decode_block(oseg, [0, 1], data, off)
+    seg = seg_of(dtypes)
+    blk = DeviceBlock.upload(ctx, data, off).index_utf8(ctx, seg, 256)
+    with pytest.raises(SegmentError, match=r"row %d, column %d" % (oe.value.row, oe.value.column)):
+        decode_blocks(ctx, seg, [0, 1], [blk])
+
+
+def test_layout_without_utf8_cuts_without_index(ctx, kernel_mode):
+    dtypes = [D.Int64, D.Float32, D.Bool, D.UInt16]
+    n = 60000
+    rng = np.random.default_rng(56)
+    cols = random_columns(rng, dtypes, n, null_p=0.3)
+    oseg, data, off = oracle_block(dtypes, cols, n, {5, 6, 59999})
+    seg = seg_of(dtypes)
+    blk = DeviceBlock.upload(ctx, data, off).index_utf8(ctx, seg, 512)
+    assert blk.uidx is None  # nothing to index
+    proj = [3, 2, 1, 0]
+    outs = decode_blocks(ctx, seg, proj, [blk])
+    want = O.decode_block(oseg, proj, data, off)
+    for p, ci in enumerate(proj):
+        assert_array_equal(download_array(ctx, outs.array(0, p), int(seg.columns[ci].dtype), n), want[p], f"proj {p}")
