@@ -601,25 +601,27 @@ int decode_enqueue_jit(murr_ctx* c, const murr_segment_t* seg, const JitLayout* 
     auto lds_for = [&](uint32_t s, double slack) {
         const JitShapeK& k = jl->shapes[s];
         const uint32_t st = (uint32_t)round_up((uint64_t)(k.tr * est_row * slack) + 64, 1024);
-        return jit_lds_bytes(k.nw, k.r, st, nu_layout);
+        return jit_lds_bytes(k.nw, k.r, k.nslot, st, nu_layout);
     };
     uint32_t si = 2;
     double slack = 1.08;
     uint32_t budget = 65536;
     if (lds_for(0, 1.15) <= 40960) { si = 0; slack = 1.15; budget = 40960; }
     else if (lds_for(1, 1.08) <= 65536) si = 1;
-    if (const char* e = std::getenv("MURR_JIT_SHAPE")) {  // tuning: "NWxR"
-        uint32_t w = 0, r = 0;
-        if (std::sscanf(e, "%ux%u", &w, &r) == 2)
+    if (const char* e = std::getenv("MURR_JIT_SHAPE")) {  // tuning: "NWxR" or "NWxRs3"
+        uint32_t w = 0, r = 0, ns = 2;
+        if (std::sscanf(e, "%ux%us%u", &w, &r, &ns) >= 2)
             for (uint32_t s = 0; s < kJitShapes; s++)
-                if (jl->shapes[s].nw == w && jl->shapes[s].r == r) si = s;
+                if (jl->shapes[s].nw == w && jl->shapes[s].r == r && jl->shapes[s].nslot == ns) si = s;
     }
     if (const char* e = std::getenv("MURR_JIT_LDS")) budget = (uint32_t)std::atoi(e);  // tuning
+    if (const char* e = std::getenv("MURR_JIT_SLACK")) slack = std::atof(e);  // tuning
     const JitShapeK& K = jl->shapes[si];
-    const uint32_t smax = std::max<uint32_t>(1024, ((budget - std::min(budget, jit_lds_bytes(K.nw, K.r, 0, nu_layout))) / 2) & ~1023u);
+    const uint32_t smax = std::max<uint32_t>(
+        1024, ((budget - std::min(budget, jit_lds_bytes(K.nw, K.r, K.nslot, 0, nu_layout))) / K.nslot) & ~1023u);
     uint32_t stage = (uint32_t)std::min<uint64_t>(round_up((uint64_t)(K.tr * est_row * slack) + 64, 1024), smax);
     if (const char* e = std::getenv("MURR_JIT_STAGE")) stage = (uint32_t)round_up((uint64_t)std::atof(e), 1024);
-    const uint32_t lds = jit_lds_bytes(K.nw, K.r, stage, nu_layout);
+    const uint32_t lds = jit_lds_bytes(K.nw, K.r, K.nslot, stage, nu_layout);
 
     // Workgroups per CU: the occupancy answer, never above the LDS bound.
     // Stream mode needs the whole grid resident at once (workgroups wait on
@@ -776,8 +778,8 @@ int decode_enqueue_jit(murr_ctx* c, const murr_segment_t* seg, const JitLayout* 
     h.mode = local ? 0 : 1;
     h.stage = stage;
     if (verbose)
-        std::fprintf(stderr, "decode launch (jit %ux%u): %s grid %llu (%d/CU, %d split) blocks %llu tiles %llu segments %llu (%llu tiles) rows/tile %u stage %u lds %u rounds %u\n",
-                     K.nw, K.r, cut ? "local-cut" : local ? "local" : "split", (unsigned long long)grid, bpc, bpc_safe,
+        std::fprintf(stderr, "decode launch (jit %ux%us%u): %s grid %llu (%d/CU, %d split) blocks %llu tiles %llu segments %llu (%llu tiles) rows/tile %u stage %u lds %u rounds %u\n",
+                     K.nw, K.r, K.nslot, cut ? "local-cut" : local ? "local" : "split", (unsigned long long)grid, bpc, bpc_safe,
                      (unsigned long long)(local ? lsegs.size() : nonempty),
                      (unsigned long long)tiles, (unsigned long long)nseg, (unsigned long long)seg_tiles, K.tr, stage, lds, rounds);
     HIPC(hipEventRecord(c->k0, c->stream));

@@ -104,10 +104,13 @@ __host__ __device__ inline uint64_t err_key(uint64_t block, uint64_t row, uint32
 // module per segment layout holds every tile shape; the projection is a
 // kernel argument.
 constexpr uint32_t kJitShapes = 3;
-constexpr uint32_t kJitShapeTab[kJitShapes][2] = {{5, 2}, {5, 1}, {3, 1}};  // waves x 64-row chunks per wave
+// waves x 64-row chunks per decode wave x LDS ring slots (murr_jit_kernel.hip
+// MJ_KERNEL instantiates each; a 3-slot ring measured no faster on B or C)
+constexpr uint32_t kJitShapeTab[kJitShapes][3] = {{5, 2, 2}, {5, 1, 2}, {3, 1, 2}};
 struct JitShapeK {
     hipFunction_t fn = nullptr, fn_split = nullptr;  // local / split mode kernels
     uint32_t nw = 0, r = 0, tr = 0;  // waves (nw-1 decode, 1 loads), chunks per decode wave, rows per tile
+    uint32_t nslot = 2;              // LDS ring slots (nslot - 1 tiles in flight)
 };
 struct JitLayout {
     JitShapeK shapes[kJitShapes];
@@ -138,7 +141,7 @@ struct JitArgsHead {               // = mj::Args without its trailing slot[] (mu
 };
 static_assert(sizeof(JitArgsHead) == 136, "mj::Args layout");
 const JitLayout* jit_layout(int device, const murr_segment_t* seg, std::string* why);
-uint32_t jit_lds_bytes(uint32_t nw, uint32_t r, uint32_t stage, uint32_t nutf8);
+uint32_t jit_lds_bytes(uint32_t nw, uint32_t r, uint32_t nslot, uint32_t stage, uint32_t nutf8);
 hipError_t jit_decode_launch(const JitShapeK& k, bool split, const void* args, size_t bytes, uint32_t grid,
                              uint32_t lds, hipStream_t s);
 

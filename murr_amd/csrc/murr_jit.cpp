@@ -195,12 +195,11 @@ bool compile(Entry& e, const std::string& pre, int device) {
         JitShapeK& k = e.k.shapes[s];
         k.nw = kJitShapeTab[s][0];
         k.r = kJitShapeTab[s][1];
+        k.nslot = kJitShapeTab[s][2];
         k.tr = 64 * (k.nw - 1) * k.r;
-        const std::string name = "murr_jit_decode_" + std::to_string(k.nw) + "x" + std::to_string(k.r);
-        he = hipModuleGetFunction(&k.fn, e.mod, name.c_str());
-        if (he == hipSuccess)
-            he = hipModuleGetFunction(&k.fn_split, e.mod,
-                                      ("murr_jit_decode_split_" + std::to_string(k.nw) + "x" + std::to_string(k.r)).c_str());
+        const std::string sh = std::to_string(k.nw) + "x" + std::to_string(k.r) + (k.nslot == 2 ? "" : "s3");
+        he = hipModuleGetFunction(&k.fn, e.mod, ("murr_jit_decode_" + sh).c_str());
+        if (he == hipSuccess) he = hipModuleGetFunction(&k.fn_split, e.mod, ("murr_jit_decode_split_" + sh).c_str());
     }
     (void)hipSetDevice(cur);
     if (he != hipSuccess) {
@@ -212,14 +211,14 @@ bool compile(Entry& e, const std::string& pre, int device) {
 
 }  // namespace
 
-// LDS bytes of a shape (murr_jit_kernel.hip Shape): two ring slots [row
+// LDS bytes of a shape (murr_jit_kernel.hip Shape): nslot ring slots [row
 // offsets | stage], the span and tile rings, counters, tile prefixes, the
 // decode waves' utf8 totals and the loader's 1 KiB prefetch scratch.
-uint32_t jit_lds_bytes(uint32_t nw, uint32_t r, uint32_t stage, uint32_t nutf8) {
+uint32_t jit_lds_bytes(uint32_t nw, uint32_t r, uint32_t nslot, uint32_t stage, uint32_t nutf8) {
     const uint32_t tr = 64 * (nw - 1) * r;
     const uint32_t ro = ((tr + 1) * 4 + 16 + 15) & ~15u;
     const uint32_t nu = std::max<uint32_t>(nutf8, 1);
-    return 2 * (ro + stage + 64) + 128 + 256 + 16 + 8 * nu + ((4 * nu * (nw - 1) + 15) & ~15u) + 1024;
+    return nslot * (ro + stage + 64) + 128 + 256 + 16 + 8 * nu + ((4 * nu * (nw - 1) + 15) & ~15u) + 1024;
 }
 
 const JitLayout* jit_layout(int device, const murr_segment_t* seg, std::string* why) {

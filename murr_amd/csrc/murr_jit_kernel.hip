@@ -293,12 +293,14 @@ DEV void wait_vmcnt(uint32_t n) {
 }
 
 // ---- shape ---------------------------------------------------------------------
-template <uint32_t NW_, uint32_t R_>
+template <uint32_t NW_, uint32_t R_, uint32_t NSLOT_>
 struct Shape {
     static constexpr uint32_t NW = NW_, NC = NW_ - 1, R = R_, TR = 64 * (NW_ - 1) * R_;
     // LDS slot: [row offsets, low dwords: (TR+1)*4 + 16][stage + 64 pad]
     static constexpr uint32_t RO_BYTES = ((TR + 1) * 4 + 16 + 15) & ~15u;
-    static constexpr uint32_t NSLOT = 2;
+    // ring slots: 2 (one tile in flight while one decodes) or 3 (two in flight)
+    static constexpr uint32_t NSLOT = NSLOT_;
+    static_assert(NSLOT == 2 || NSLOT == 3, "ring of 2 or 3 slots");
     // after the slots: span ring [8][16 B] | tile ring [8][32 B] | counters |
     // tile prefixes [NU] u64 | wave totals [NU][NC] u32 | prefetch scratch 1 KiB
     static constexpr uint32_t SPAN_B = 128, INFO_B = 256, CNT_B = 16, PF_B = 1024;
@@ -1053,9 +1055,9 @@ DEV void decode_tile(const Src& src, const Tile& T, const LAS uint32_t* ro, LAS 
 // ---- kernel body ---------------------------------------------------------------------
 // MODE 0: local, 1: split (separate kernels: the split path's look-back
 // registers would otherwise cost the local kernel occupancy).
-template <uint32_t NW, uint32_t R, uint32_t MODE>
+template <uint32_t NW, uint32_t R, uint32_t NS, uint32_t MODE>
 DEV void kernel_body() {
-    using SH = Shape<NW, R>;
+    using SH = Shape<NW, R, NS>;
     constexpr uint32_t NC = SH::NC, TR = SH::TR, NSLOT = SH::NSLOT;
     extern __shared__ __attribute__((aligned(16))) uint8_t lds_[];
     LAS uint8_t* lds = (LAS uint8_t*)lds_;
@@ -1070,10 +1072,11 @@ DEV void kernel_body() {
     if (threadIdx.x < 2) ((LAS uint32_t*)ctl)[threadIdx.x] = 0;
 
     if (wave == NC) {
-        // ---- loader: one tile in flight.  At iteration i (after barrier B_i
-        // freed slot (i+1) % 2) it DMAs tile i+1 and announces tile i+4 (its
-        // identity and span).  It issues no other vector-memory instruction,
-        // so its counted vmcnt waits for exactly the DMA it needs.
+        // ---- loader: NSLOT - 1 tiles in flight.  At iteration i (after
+        // barrier B_i freed the slot of tile i - 1) it DMAs tile i + NSLOT - 1
+        // and announces tile i + NSLOT + 2 (its identity and span), then waits
+        // for tile i + 1.  It issues no other vector-memory instruction, so
+        // its counted vmcnt waits for exactly the DMA it needs.
         Cur cs = cur_first<MODE>();  // next tile to announce
 #pragma unroll
         for (uint32_t k = 0; k <= NSLOT + 1; k++) {
@@ -1085,15 +1088,25 @@ DEV void kernel_body() {
         uint64_t lwait = 0;
 #endif
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-        if (tile_valid(infos)) tile_dma<TR, SH::RO_BYTES>(tile_read(spans, infos, stage), lds, lane);
-        wait_vmcnt(0);
-        lds_barrier();  // B_0: tile 0 and the spans of tiles 0 .. 3 landed
+        // tiles 0 .. NSLOT - 2 into their slots; B_0 once tile 0 landed
+        uint32_t after0 = 0;  // ops issued after tile 0's DMA
+#pragma unroll
+        for (uint32_t j = 0; j + 1 < NSLOT; j++) {
+            uint32_t n = 0;
+            if (tile_valid(infos + j * 32))
+                n = tile_dma<TR, SH::RO_BYTES>(tile_read(spans + j * 16, infos + j * 32, stage), lds + j * SLOT, lane);
+            after0 += j ? n : 0;
+        }
+        wait_vmcnt(after0);
+        lds_barrier();  // B_0: tile 0 and the spans of tiles 0 .. NSLOT + 1 landed
+        uint32_t pend = 0;  // NSLOT 3: ops issued after tile it+1's DMA before this iteration
         for (uint32_t it = 0;; it++) {
             if (!tile_valid(infos + (it & 7) * 32)) break;  // the decode waves leave too
-            const uint32_t t1 = it + 1, k = it + NSLOT + 2;
-            if (tile_valid(infos + (t1 & 7) * 32))
-                tile_dma<TR, SH::RO_BYTES>(tile_read(spans + (t1 & 7) * 16, infos + (t1 & 7) * 32, stage),
-                                           lds + (t1 % NSLOT) * SLOT, lane);
+            const uint32_t tn = it + NSLOT - 1, k = it + NSLOT + 2;
+            uint32_t nd = 0;
+            if (tile_valid(infos + (tn & 7) * 32))
+                nd = tile_dma<TR, SH::RO_BYTES>(tile_read(spans + (tn & 7) * 16, infos + (tn & 7) * 32, stage),
+                                                lds + (tn % NSLOT) * SLOT, lane);
             // tile it+2 into L2 (tuning: MJ_PREFETCH=1; measured slower on configs C/D)
             uint32_t np = 0;
 #if MJ_PREFETCH
@@ -1106,7 +1119,10 @@ DEV void kernel_body() {
 #ifdef MJ_STAMPS
             const uint64_t w0 = __builtin_amdgcn_s_memtime();
 #endif
-            wait_vmcnt(ns);
+            // tile it+1's DMA: the one just issued (NSLOT 2), or the one issued
+            // an iteration ago, with `pend` ops behind it then (NSLOT 3)
+            wait_vmcnt((NSLOT == 2 ? 0u : pend + nd) + ns);
+            pend = ns;
             lds_barrier();  // B_it+1: tile it+1 landed, tile it decoded
 #ifdef MJ_STAMPS
             lwait += __builtin_amdgcn_s_memtime() - w0;
@@ -1189,13 +1205,13 @@ DEV void kernel_body() {
 
 }  // namespace mj
 
-#define MJ_KERNEL(NW, R)                                                                                   \
-    extern "C" __global__ void __launch_bounds__(64 * NW) murr_jit_decode_##NW##x##R(mj::Args) {           \
-        mj::kernel_body<NW, R, 0>();                                                                       \
+#define MJ_KERNEL(NW, R, NS, SFX)                                                                         \
+    extern "C" __global__ void __launch_bounds__(64 * NW) murr_jit_decode_##NW##x##R##SFX(mj::Args) {      \
+        mj::kernel_body<NW, R, NS, 0>();                                                                   \
     }                                                                                                      \
-    extern "C" __global__ void __launch_bounds__(64 * NW) murr_jit_decode_split_##NW##x##R(mj::Args) {     \
-        mj::kernel_body<NW, R, 1>();                                                                       \
+    extern "C" __global__ void __launch_bounds__(64 * NW) murr_jit_decode_split_##NW##x##R##SFX(mj::Args) {\
+        mj::kernel_body<NW, R, NS, 1>();                                                                   \
     }
-MJ_KERNEL(5, 2)
-MJ_KERNEL(5, 1)
-MJ_KERNEL(3, 1)
+MJ_KERNEL(5, 2, 2, )
+MJ_KERNEL(5, 1, 2, )
+MJ_KERNEL(3, 1, 2, )
