@@ -663,6 +663,8 @@ int decode_enqueue_jit(murr_ctx* c, const murr_segment_t* seg, const JitLayout* 
         const uint64_t rounds = (nonempty + G - 1) / G;
         local = nonempty * 4 >= rounds * G * 3;
         if (!local && cuttable && stride_ok(nu_layout ? stride : 64)) local = cut = true;
+        // tuning: cut whenever possible (whole blocks may leave workgroup slots idle)
+        if (std::getenv("MURR_JIT_CUT") && cuttable && stride_ok(nu_layout ? stride : 64)) local = cut = true;
     }
     if (const char* e = std::getenv("MURR_JIT_MODE")) {  // tuning
         local = std::string(e) == "local";
