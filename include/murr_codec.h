@@ -400,6 +400,46 @@ int murr_reader_read(murr_reader_t* r, const murr_index_t* idx, const uint8_t* b
                      murr_host_array_t* outs, murr_error_t* err);
 void murr_reader_free(murr_reader_t* r);
 
+/* ---- RocksDB data blocks --------------------------- */
+
+/* The data blocks of the block-based SSTs the reference's store writes
+ * (src/io/store/rocksdb/block.rs:97-121: block_size 512, restart interval 8,
+ * BinaryAndHash data-block index, default compression) decoded on the device
+ * into their entries: the bulk read a warm-up or rehydration does before the
+ * row blobs go to murr_decode_* and the keys to murr_index_build.  A block is
+ * its contents as stored (the BlockHandle's bytes, without the 5-byte
+ * trailer) with the trailer's compression type: 0 none, 1 Snappy (raw
+ * format), 4 / 5 LZ4 / LZ4HC (varint32 length + LZ4 block); other types are
+ * MURR_E_MALFORMED_ROW.  Entries come out in block order: user keys (the internal key less
+ * its 8-byte trailer) as Arrow utf8, values as a decode block (values 16-B
+ * aligned, value_offsets[n + 1] from 0), and each trailer's sequence number
+ * and value type.  Blocks that do not parse are MURR_E_MALFORMED_ROW with the
+ * first such block in err->row.  Outputs are allocated by the library (device
+ * memory) and freed with murr_sst_result_free, or one by one with
+ * murr_dev_free (to keep, e.g., values and value_offsets as a table's
+ * arena).  Synchronous. */
+typedef struct {
+    const uint8_t* data;   /* device */
+    uint64_t size;
+    uint32_t compression;  /* RocksDB CompressionType: 0 none, 1 Snappy, 4 LZ4, 5 LZ4HC */
+    uint32_t _pad;
+} murr_sst_block_t;
+
+typedef struct {
+    uint64_t n;                /* entries */
+    uint8_t* keys;             /* user key bytes */
+    int32_t* key_offsets;      /* n + 1 */
+    uint8_t* values;           /* value bytes (row blobs) */
+    uint64_t* value_offsets;   /* n + 1 */
+    uint64_t* seqs;            /* n */
+    uint8_t* types;            /* n (1 = value, 0 = deletion, ...) */
+    uint64_t key_bytes, value_bytes;
+} murr_sst_result_t;
+
+int murr_sst_decode(murr_ctx_t* ctx, const murr_sst_block_t* blocks, uint32_t nblocks,
+                    murr_sst_result_t* out, murr_error_t* err);
+void murr_sst_result_free(murr_ctx_t* ctx, murr_sst_result_t* r);
+
 /* ---- sharding -------------------------------------------- */
 
 /* Owner shard of each of n keys (host Arrow utf8: key_offsets[key_offset ..

@@ -49,6 +49,16 @@ class ColIn(C.Structure):
                 ("offset", C.c_uint64)]
 
 
+class SstBlock(C.Structure):
+    _fields_ = [("data", C.c_void_p), ("size", C.c_uint64), ("compression", C.c_uint32), ("_pad", C.c_uint32)]
+
+
+class SstResult(C.Structure):
+    _fields_ = [("n", C.c_uint64), ("keys", C.c_void_p), ("key_offsets", C.c_void_p), ("values", C.c_void_p),
+                ("value_offsets", C.c_void_p), ("seqs", C.c_void_p), ("types", C.c_void_p),
+                ("key_bytes", C.c_uint64), ("value_bytes", C.c_uint64)]
+
+
 class HostArray(C.Structure):
     _fields_ = [("values", C.c_void_p), ("validity", C.c_void_p), ("offsets", C.c_void_p),
                 ("length", C.c_uint64), ("null_count", C.c_uint64), ("values_len", C.c_uint64),
@@ -96,6 +106,8 @@ SIGNATURES = {
     "murr_decode_enqueue_ix": (I32, [P, C.POINTER(Segment), C.POINTER(U32), U32, C.POINTER(Block), U32,
                                      C.POINTER(C.c_void_p), U32, C.POINTER(Array)]),
     "murr_utf8_index_len": (U64, [C.POINTER(Segment), U64, U32]),
+    "murr_sst_decode": (I32, [P, C.POINTER(SstBlock), U32, C.POINTER(SstResult), C.POINTER(Error)]),
+    "murr_sst_result_free": (None, [P, C.POINTER(SstResult)]),
     "murr_utf8_index": (I32, [P, C.POINTER(Segment), C.POINTER(Block), U32, P]),
     "murr_encode_bound": (U64, [C.POINTER(Segment), U64, C.POINTER(U64)]),
     "murr_encode_batch": (I32, [P, C.POINTER(Segment), C.POINTER(ColIn), U64, P, U64, P,

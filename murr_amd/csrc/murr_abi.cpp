@@ -1711,6 +1711,118 @@ void murr_reader_free(murr_reader_t* r) {
     delete r;
 }
 
+// ---- RocksDB data blocks (murr_sst.hip) --------------
+
+void murr_sst_result_free(murr_ctx_t* c, murr_sst_result_t* r) {
+    if (!r) return;
+    if (c) (void)hipSetDevice(c->device);
+    for (void* p : {(void*)r->keys, (void*)r->key_offsets, (void*)r->values, (void*)r->value_offsets,
+                    (void*)r->seqs, (void*)r->types})
+        if (p) (void)hipFree(p);
+    std::memset(r, 0, sizeof *r);
+}
+
+// Decode data blocks into entries: uncompressed sizes, their scan, the
+// decompression, the entry counts, their scans, the entry decode; two 8-byte
+// (then 32-byte) read-backs size the outputs.  Synchronous.
+int murr_sst_decode(murr_ctx_t* c, const murr_sst_block_t* blocks, uint32_t nblocks, murr_sst_result_t* out,
+                    murr_error_t* err) {
+    if (err) std::memset(err, 0, sizeof *err);
+    if (!c || !out || (nblocks && !blocks) || c->pending) return set_err(err, MURR_E_ARGUMENT);
+    std::memset(out, 0, sizeof *out);
+    for (uint32_t b = 0; b < nblocks; b++)
+        if (blocks[b].size && !blocks[b].data) return set_err(err, MURR_E_ARGUMENT);
+    HIPC(hipSetDevice(c->device));
+    const uint64_t nb = nblocks, nparts = (nb + 1023) / 1024;
+    // scratch: err | totals[4] | descriptors | ulen | uoff | ne | kb | vb | parts
+    const uint64_t o_tot = 8, o_desc = 64, o_ulen = round_up(o_desc + sizeof(SstBlock) * nb, 16);
+    const uint64_t o_uoff = o_ulen + 8 * nb, o_ne = o_uoff + 8 * nb, o_kb = o_ne + 8 * nb, o_vb = o_kb + 8 * nb;
+    const uint64_t o_part = o_vb + 8 * nb, scratch_bytes = o_part + 8 * std::max<uint64_t>(nparts, 1) + 64;
+    uint8_t* w = nullptr;
+    uint8_t* raw = nullptr;
+    HIPC(hipMalloc(&w, scratch_bytes));
+    auto fail = [&](int st) {
+        if (w) (void)hipFree(w);
+        if (raw) (void)hipFree(raw);
+        murr_sst_result_free(c, out);
+        return st;
+    };
+#define SSTC(expr)                                                           \
+    do {                                                                     \
+        hipError_t _e = (expr);                                              \
+        if (_e != hipSuccess) return fail(set_err(err, MURR_E_HIP, (int)_e)); \
+    } while (0)
+    std::vector<SstBlock> desc(nb);
+    for (uint64_t b = 0; b < nb; b++) desc[b] = SstBlock{blocks[b].data, blocks[b].size, blocks[b].compression, 0};
+    SSTC(hipMemsetAsync(w, 0, 64, c->stream));
+    if (nb) SSTC(hipMemcpyAsync(w + o_desc, desc.data(), sizeof(SstBlock) * nb, hipMemcpyHostToDevice, c->stream));
+    SstArgs a{};
+    a.blocks = (const SstBlock*)(w + o_desc);
+    a.nblocks = nb;
+    a.ulen = (uint64_t*)(w + o_ulen);
+    a.uoff = (uint64_t*)(w + o_uoff);
+    a.ne = (uint64_t*)(w + o_ne);
+    a.kb = (uint64_t*)(w + o_kb);
+    a.vb = (uint64_t*)(w + o_vb);
+    a.err = (unsigned long long*)w;
+    uint64_t* tot = (uint64_t*)(w + o_tot);
+    uint64_t* part = (uint64_t*)(w + o_part);
+    uint64_t host[5] = {0, 0, 0, 0, 0};
+    if (nb) {
+        // 1. uncompressed sizes and their placement
+        SSTC(launch_sst_len(a, c->stream));
+        SSTC(hipMemcpyAsync(a.uoff, a.ulen, 8 * nb, hipMemcpyDeviceToDevice, c->stream));
+        SSTC(launch_scan_u64(a.uoff, nb, part, tot, c->stream));
+        SSTC(hipMemcpyAsync(host, w, 16, hipMemcpyDeviceToHost, c->stream));
+        SSTC(hipStreamSynchronize(c->stream));
+        // a block already found corrupt inflates to nothing and is reported
+        // again below, so the error names the lowest corrupt block of any pass
+        // 2. decompress, 3. count
+        SSTC(hipMalloc(&raw, host[1] + 16));
+        a.raw = raw;
+        SSTC(launch_sst_inflate(a, c->stream));
+        SSTC(launch_sst_count(a, c->stream));
+        SSTC(launch_scan_u64(a.ne, nb, part, tot + 1, c->stream));
+        SSTC(launch_scan_u64(a.kb, nb, part, tot + 2, c->stream));
+        SSTC(launch_scan_u64(a.vb, nb, part, tot + 3, c->stream));
+        SSTC(hipMemcpyAsync(host, w, 40, hipMemcpyDeviceToHost, c->stream));
+        SSTC(hipStreamSynchronize(c->stream));
+        if (host[0]) return fail(unpack_err(host[0], err));
+    }
+    const uint64_t n = host[2], kbytes = host[3], vbytes = host[4];
+    if (kbytes > 0x7FFFFFFFull) return fail(set_err(err, MURR_E_OFFSET_OVERFLOW));
+    // 4. outputs, then the entries
+    SSTC(hipMalloc((void**)&out->keys, kbytes + 16));
+    SSTC(hipMalloc((void**)&out->key_offsets, 4 * (n + 1)));
+    SSTC(hipMalloc((void**)&out->values, vbytes + 16));
+    SSTC(hipMalloc((void**)&out->value_offsets, 8 * (n + 1)));
+    SSTC(hipMalloc((void**)&out->seqs, 8 * std::max<uint64_t>(n, 1)));
+    SSTC(hipMalloc((void**)&out->types, std::max<uint64_t>(n, 1)));
+    SSTC(hipMemsetAsync(out->key_offsets, 0, 4, c->stream));
+    SSTC(hipMemsetAsync(out->value_offsets, 0, 8, c->stream));
+    out->n = n;
+    out->key_bytes = kbytes;
+    out->value_bytes = vbytes;
+    if (n) {
+        a.keys = out->keys;
+        a.key_off = out->key_offsets;
+        a.vals = out->values;
+        a.val_off = out->value_offsets;
+        a.seqs = out->seqs;
+        a.types = out->types;
+        SSTC(hipEventRecord(c->k0, c->stream));
+        SSTC(launch_sst_decode(a, c->stream));
+        SSTC(hipEventRecord(c->k1, c->stream));
+        c->timed = true;
+        c->last_kernel = "sst_decode";
+    }
+    SSTC(hipStreamSynchronize(c->stream));
+#undef SSTC
+    (void)hipFree(w);
+    if (raw) (void)hipFree(raw);
+    return MURR_OK;
+}
+
 // Host-memory encode: H2D Arrow buffers, murr_encode_batch, D2H blobs + offsets.
 int murr_encode_host(murr_ctx_t* c, const murr_segment_t* seg, const murr_host_col_in_t* cols,
                      uint64_t n, uint8_t** out_blob, uint64_t* blob_len, uint64_t** out_row_off,

@@ -163,6 +163,33 @@ int decode_blocks_per_cu(uint32_t nw, uint32_t kc, uint32_t lds);
 hipError_t launch_encode(const EncodeArgs& a, uint32_t grid, hipStream_t s);
 int encode_blocks_per_cu();
 
+// RocksDB data blocks (murr_sst.hip, murr_sst_decode).
+struct SstBlock {                  // = murr_sst_block_t
+    const uint8_t* data;
+    uint64_t size;
+    uint32_t compression, pad;
+};
+struct SstArgs {
+    const SstBlock* blocks;
+    uint64_t nblocks;
+    uint64_t* ulen;                // [nblocks] uncompressed sizes
+    uint64_t* uoff;                // [nblocks] their placement in raw
+    uint8_t* raw;                  // uncompressed blocks back to back
+    uint64_t *ne, *kb, *vb;        // [nblocks] entries / key bytes / value bytes, then their prefixes
+    uint8_t* keys;                 // user keys back to back
+    int32_t* key_off;              // [entries + 1]
+    uint8_t* vals;                 // values (row blobs) back to back
+    uint64_t* val_off;             // [entries + 1]
+    uint64_t* seqs;
+    uint8_t* types;
+    unsigned long long* err;
+};
+hipError_t launch_sst_len(const SstArgs& a, hipStream_t s);
+hipError_t launch_sst_inflate(const SstArgs& a, hipStream_t s);
+hipError_t launch_sst_count(const SstArgs& a, hipStream_t s);
+hipError_t launch_sst_decode(const SstArgs& a, hipStream_t s);
+hipError_t launch_scan_u64(uint64_t* x, uint64_t n, uint64_t* part, uint64_t* total, hipStream_t s);
+
 // utf8 index of a block (murr_index.hip, murr_utf8_index).
 constexpr uint32_t kMaxUidxCols = 64;
 struct Utf8IndexArgs {

@@ -72,17 +72,23 @@ def _column_dict(ctx: Context, arr: pa.Array) -> dict:
 class DeviceIndex:
     """murr_index_t: hash index over a device utf8 key column."""
 
-    def __init__(self, ctx: Context, keys: pa.Array):
+    def __init__(self, ctx: Context, keys: pa.Array | None = None, *, device_keys=None):
+        """Over a host key column, or device_keys = (data DeviceBuffer, int32
+        offsets DeviceBuffer, n) already in HBM."""
         self.ctx = ctx
-        self.n = len(keys)
-        data, offs = _upload_utf8(ctx, keys)
+        if device_keys is not None:
+            data, offs, self.n = device_keys
+        else:
+            self.n = len(keys)
+            data, offs = _upload_utf8(ctx, keys)
         h = C.c_void_p()
         err = _abi.Error()
         st = ctx.L.murr_index_build(ctx.h, data.ptr, offs.ptr, 0, self.n, C.byref(h), C.byref(err))
         raise_status(st, err, "murr_index_build")
         self.h = h.value
-        data.free()
-        offs.free()
+        if device_keys is None:
+            data.free()
+            offs.free()
 
     def append(self, keys: pa.Array):
         """murr_index_append: rows n .. n + len(keys) - 1."""
@@ -233,6 +239,29 @@ class ResidentTable:
         self.used += blen.value
         self.n += m
         self.max_row = max(self.max_row, int(sizes.max()))
+
+    def load_sst(self, entries):
+        """Rehydrate an empty table from SST entries decoded on the device
+        (murr_amd.sst.decode): the values are the table's row blobs and become
+        the arena as they lie, the user keys go into the device index.  The
+        entries must be live rows (value type kTypeValue, as in a compacted
+        bottommost file); a key seen twice maps to its later entry, as with
+        write().  Nothing but the value lengths and types crosses to the host."""
+        if self.n:
+            raise SegmentError("load_sst rehydrates an empty resident table")
+        n = entries.n
+        if n == 0:
+            return
+        types = entries.types.download(n)
+        if (types != 1).any():
+            i = int(np.flatnonzero(types != 1)[0])
+            raise SegmentError(f"entry {i} has value type {int(types[i])}: only live values (type 1) rehydrate")
+        lens = np.diff(entries.value_offsets.download(8 * (n + 1)).view(np.uint64))
+        self.index = DeviceIndex(self.ctx, device_keys=(entries.keys, entries.key_offsets, n))
+        self.arena, self.arena_cap = entries.values, entries.value_bytes + 16
+        self.row_off, self.off_cap = entries.value_offsets, n + 1
+        self.used, self.n = entries.value_bytes, n
+        self.max_row = int(lens.max())
 
     def gather(self, keys):
         """Lookup + gather on the device: a DeviceBlock of the rows of `keys` in

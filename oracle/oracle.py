@@ -72,6 +72,13 @@ def lib():
         L.oc_free.argtypes = [C.c_void_p]
         L.oc_utf8_valid.argtypes = [C.c_char_p, C.c_uint64, C.POINTER(C.c_uint64),
                                     C.POINTER(C.c_int)]
+        L.oc_snappy_uncompressed_len.argtypes = [C.c_char_p, C.c_uint64, C.POINTER(C.c_uint64)]
+        L.oc_snappy_decompress.argtypes = [C.c_char_p, C.c_uint64, C.c_void_p, C.c_uint64, C.POINTER(C.c_uint64)]
+        L.oc_lz4_decompress.argtypes = [C.c_char_p, C.c_uint64, C.c_void_p, C.c_uint64, C.POINTER(C.c_uint64)]
+        L.oc_block_count.argtypes = [C.c_char_p, C.c_uint64, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
+                                     C.POINTER(C.c_uint64)]
+        L.oc_block_decode.argtypes = [C.c_char_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                      C.c_void_p, C.c_void_p]
         _lib = L
     return _lib
 
@@ -175,3 +182,65 @@ def utf8_valid(b: bytes):
     el = C.c_int()
     ok = lib().oc_utf8_valid(b, len(b), C.byref(vut), C.byref(el))
     return bool(ok), vut.value, el.value
+
+
+# ---- RocksDB data blocks (murr_sst.c) ------------------------------------------
+
+SST_E_CORRUPT = 12
+
+
+def _inflate(fn, src: bytes, what: str) -> bytes:
+    n = C.c_uint64()
+    st = lib().oc_snappy_uncompressed_len(src, len(src), C.byref(n))
+    if st:
+        raise OracleError(st, 0, 0, what)
+    out = C.create_string_buffer(max(n.value, 1))
+    got = C.c_uint64()
+    st = fn(src, len(src), out, n.value, C.byref(got))
+    if st:
+        raise OracleError(st, 0, 0, what)
+    return out.raw[:got.value]
+
+
+def snappy_decompress(src: bytes) -> bytes:
+    """Raw Snappy (the restatement in murr_sst.c)."""
+    return _inflate(lib().oc_snappy_decompress, src, "corrupt snappy")
+
+
+def lz4_decompress(src: bytes) -> bytes:
+    """varint32 length + LZ4 block, as RocksDB stores LZ4 blocks (murr_sst.c)."""
+    return _inflate(lib().oc_lz4_decompress, src, "corrupt lz4")
+
+
+def block_contents(stored: bytes, compression: int) -> bytes:
+    """A stored data block's uncompressed contents (0 none, 1 Snappy, 4/5 LZ4)."""
+    if compression == 0:
+        return stored
+    if compression == 1:
+        return snappy_decompress(stored)
+    if compression in (4, 5):
+        return lz4_decompress(stored)
+    raise OracleError(12, 0, 0, f"unsupported compression {compression}")
+
+
+def block_decode(block: bytes):
+    """Entries of one uncompressed RocksDB data block, in block order:
+    (user keys, values, sequence numbers, value types)."""
+    ne, kb, vb = C.c_uint64(), C.c_uint64(), C.c_uint64()
+    st = lib().oc_block_count(block, len(block), C.byref(ne), C.byref(kb), C.byref(vb))
+    if st:
+        raise OracleError(st, 0, 0, "corrupt block")
+    n = ne.value
+    keys = C.create_string_buffer(max(kb.value, 1))
+    vals = C.create_string_buffer(max(vb.value, 1))
+    koff = np.zeros(n + 1, np.int32)
+    voff = np.zeros(n + 1, np.uint64)
+    seqs = np.zeros(max(n, 1), np.uint64)
+    types = np.zeros(max(n, 1), np.uint8)
+    st = lib().oc_block_decode(block, len(block), keys, koff.ctypes.data, vals, voff.ctypes.data,
+                               seqs.ctypes.data, types.ctypes.data)
+    if st:
+        raise OracleError(st, 0, 0, "corrupt block")
+    kr, vr = keys.raw, vals.raw
+    return ([kr[koff[i]:koff[i + 1]] for i in range(n)], [vr[int(voff[i]):int(voff[i + 1])] for i in range(n)],
+            seqs[:n].copy(), types[:n].copy())

@@ -1,0 +1,150 @@
+"""RocksDB data-block decode on the device (murr_sst_decode through the C ABI)
+against the CPU restatement (oracle/murr_sst.c, itself checked against
+pyarrow's Snappy / LZ4 codecs and the BlockBuilder restatement in
+tests/sstgen.py): bit-exact keys, values, sequence numbers and types, the
+first corrupt block named, and a table rehydrated from its SST blocks reading
+exactly as the table it came from."""
+import numpy as np
+import pyarrow as pa
+import pytest
+
+import oracle as O
+import sstgen as G
+from murr_amd import SegmentError, sst
+from murr_amd.resident import ResidentTable
+from murr_amd.row import default_context
+
+from test_gpu_resident import assert_same, batch_c, expected, schema_c
+
+pytestmark = pytest.mark.gpu
+
+
+def oracle_entries(stored):
+    keys, vals, seqs, types = [], [], [], []
+    for data, comp in stored:
+        k, v, s, t = O.block_decode(O.block_contents(data, comp))
+        keys += k
+        vals += v
+        seqs += s.tolist()
+        types += t.tolist()
+    return keys, vals, seqs, types
+
+
+def check(stored):
+    ctx = default_context()
+    e = sst.decode_host(ctx, stored)
+    keys, vals, seqs, types = e.to_host()
+    wk, wv, ws, wt = oracle_entries(stored)
+    assert e.n == len(wk)
+    assert keys == wk
+    assert vals == wv
+    assert seqs.tolist() == ws
+    assert types.tolist() == wt
+    assert e.key_bytes == sum(map(len, wk)) and e.value_bytes == sum(map(len, wv))
+    return e
+
+
+@pytest.mark.parametrize("comp", [G.NONE, G.SNAPPY, G.LZ4])
+@pytest.mark.parametrize("restart,hash_index", [(1, False), (8, True), (16, False)])
+def test_blocks_bit_exact(comp, restart, hash_index):
+    rng = np.random.default_rng(comp * 100 + restart + hash_index)
+    entries = G.random_entries(rng, 3000, max_val=300, dup_p=0.2, del_p=0.1)
+    blocks = G.blocks_of(entries, restart_interval=restart, hash_index=hash_index)
+    check([(G.compress(b, comp), comp) for b in blocks])
+
+
+def test_mixed_compression_and_block_sizes():
+    rng = np.random.default_rng(11)
+    entries = G.random_entries(rng, 4000, max_key=60, max_val=2000, dup_p=0.1)
+    stored = []
+    for i, b in enumerate(G.blocks_of(entries, block_size=int(rng.integers(64, 16384)))):
+        comp = (G.NONE, G.SNAPPY, G.LZ4, 5)[i % 4]  # 5 = LZ4HC, the same stored format
+        stored.append((G.compress(b, comp if comp != 5 else G.LZ4), comp))
+    check(stored)
+
+
+def test_edge_blocks():
+    empty = G.build_block([])
+    one = G.build_block([(b"", 7, G.TYPE_VALUE, b"")])  # empty user key and value
+    versions = G.build_block([(b"k", 100 - i, G.TYPE_VALUE, bytes([i]) * i) for i in range(30)])
+    big = G.build_block([(b"big", 1, G.TYPE_VALUE, bytes(range(256)) * 400)])
+    check([(empty, 0), (one, 0), (G.snappy(versions), 1), (G.lz4(big), 4), (G.snappy(empty), 1)])
+    e = sst.decode_host(default_context(), [])
+    assert e.n == 0
+
+
+def test_many_blocks_scan_carry():
+    # > 1024 x 1024 blocks: the block scans run their multi-pass carry
+    blk = G.snappy(G.build_block([(b"user-key-%d" % 7, 5, G.TYPE_VALUE, b"v" * 11)]))
+    nb = 1024 * 1024 + 4321
+    ctx = default_context()
+    host = np.tile(np.frombuffer(blk, np.uint8), nb)
+    buf = ctx.upload(np.concatenate([host, np.zeros(16, np.uint8)]))
+    e = sst.decode(ctx, buf, [(i * len(blk), len(blk), 1) for i in range(nb)])
+    assert e.n == nb and e.key_bytes == nb * 10 and e.value_bytes == nb * 11
+    ko = e.key_offsets.download(4 * (nb + 1)).view(np.int32)
+    vo = e.value_offsets.download(8 * (nb + 1)).view(np.uint64)
+    assert np.array_equal(ko, np.arange(nb + 1, dtype=np.int32) * 10)
+    assert np.array_equal(vo, np.arange(nb + 1, dtype=np.uint64) * 11)
+    assert e.keys.download(e.key_bytes).tobytes() == b"user-key-7" * nb
+    assert np.all(e.seqs.download(8 * nb).view(np.uint64) == 5)
+
+
+@pytest.mark.parametrize("bad", ["truncated_snappy", "lz4_cut", "unknown_type", "footer", "varint", "shared"])
+def test_first_corrupt_block_is_named(bad):
+    rng = np.random.default_rng(3)
+    blocks = G.blocks_of(G.random_entries(rng, 600), restart_interval=8)
+    stored = [(G.snappy(b), G.SNAPPY) for b in blocks]
+    assert len(stored) > 20
+    raw = blocks[9]
+    if bad == "truncated_snappy":
+        broken = (G.snappy(raw)[:-3], G.SNAPPY)
+    elif bad == "lz4_cut":
+        broken = (G.lz4(raw)[:-1], G.LZ4)
+    elif bad == "unknown_type":
+        broken = (raw, 7)  # ZSTD: not inflated on the device
+    elif bad == "footer":
+        broken = (raw[:-4] + (0x7FFFFFFF).to_bytes(4, "little"), G.NONE)
+    elif bad == "varint":
+        broken = (b"\xff\xff\xff\xff\xff\xff" + raw[6:], G.NONE)
+    else:
+        b = bytearray(raw)
+        b[0] = 3  # a restart entry claiming shared bytes
+        broken = (bytes(b), G.NONE)
+    stored[9] = broken
+    stored[15] = broken
+    stored[4] = (raw, 7) if bad != "unknown_type" else (G.snappy(raw)[:-3], G.SNAPPY)  # another pass's error
+    with pytest.raises(SegmentError, match=r"malformed.*row 4,"):
+        sst.decode_host(default_context(), stored)
+    stored[4] = (G.snappy(blocks[4]), G.SNAPPY)
+    with pytest.raises(SegmentError, match=r"row 9,"):
+        sst.decode_host(default_context(), stored)
+
+
+def test_rehydrate_resident_table_from_sst():
+    src = ResidentTable(schema_c())
+    b0 = batch_c(6000, seed=42)
+    src.write(b0)
+    arena = src.arena.download(src.used).tobytes()
+    offs = src.row_off.download(8 * (src.n + 1)).view(np.uint64)
+    keys = b0.column(0).to_pylist()
+    order = sorted(range(len(keys)), key=lambda i: keys[i].encode())
+    entries = [(keys[i].encode(), 1000 + i, G.TYPE_VALUE, arena[offs[i]:offs[i + 1]]) for i in order]
+    stored = [(G.snappy(b), G.SNAPPY) for b in G.blocks_of(entries)]
+    t = ResidentTable(schema_c())
+    t.load_sst(sst.decode_host(t.ctx, stored))
+    rng = np.random.default_rng(8)
+    q = [f"key{i}" for i in rng.integers(0, 6500, size=2000)]
+    cols = [f"c{i}" for i in range(16)]
+    assert_same(t.read(q, cols), expected([b0], q, cols))
+    # appends after a rehydration grow the adopted arena
+    b1 = batch_c(500, start=5900, seed=7)
+    t.write(b1)
+    assert_same(t.read(q, cols), expected([b0, b1], q, cols))
+
+
+def test_rehydrate_rejects_tombstones():
+    blk = G.build_block([(b"a", 2, G.TYPE_VALUE, b""), (b"b", 1, G.TYPE_DELETION, b"")])
+    t = ResidentTable(schema_c())
+    with pytest.raises(SegmentError, match="entry 1"):
+        t.load_sst(sst.decode_host(t.ctx, [(blk, 0)]))
