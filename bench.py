@@ -491,6 +491,85 @@ def run_resident(args):
                       "kernels": "index_probe/gather_scan, gather_copy, " + ctx.last_kernel(), **ipc_res}))
 
 
+def sst_blocks(rows: int, comp: int, block_size: int = 512):
+    """The SST data blocks the reference's store would hold for the read
+    benches' dataset (keys i.to_string(), 10 x f32 row blobs), in key order,
+    cut at block_size with restart interval 8 and BinaryAndHash
+    (src/io/store/rocksdb/block.rs:83-111); blocks stored with `comp`."""
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "tests"))
+    import sstgen as G
+    ctx = Context(0)
+    rt, _ = resident_table(ctx, "ref", rows)
+    arena = rt.arena.download(rt.used).tobytes()
+    off = rt.row_off.download(8 * (rows + 1)).view(np.uint64)
+    order = sorted(range(rows), key=lambda i: str(i))
+    entries = [(str(i).encode(), rows + i, G.TYPE_VALUE, arena[off[i]:off[i + 1]]) for i in order]
+    return [(G.compress(b, comp), comp) for b in G.blocks_of(entries, block_size=block_size)]
+
+
+def run_sst(args):
+    """§8(f) rank 4: a whole SST's data blocks (resident in HBM) -> entries in
+    HBM (murr_sst_decode: inflate, count, scans, entry decode).  Wall time per
+    call (host-synchronous, the library's output allocations included) and the
+    entry-decode kernel's event time; rates over the stored bytes read plus the
+    entry bytes written."""
+    from murr_amd import sst
+    comp = {"none": 0, "snappy": 1, "lz4": 4}[args.sst_compression]
+    t0 = time.perf_counter()
+    stored = sst_blocks(args.rows, comp)
+    gen_s = time.perf_counter() - t0
+    ctx = Context(0)
+    buf, handles = sst.upload_blocks(ctx, stored)
+    in_bytes = sum(len(d) for d, _ in stored)
+    t0 = time.perf_counter()
+    table = sst.block_table(buf, handles)  # once per file: murr_sst_block_t[]
+    table_ms = (time.perf_counter() - t0) * 1e3
+    for _ in range(args.warmup):
+        e = sst.decode(ctx, buf, table)
+        del e
+    ts, ks = [], []
+    for _ in range(args.steps):
+        t0 = time.perf_counter()
+        e = sst.decode(ctx, buf, table)
+        ts.append(time.perf_counter() - t0)
+        ks.append(ctx.last_kernel_ms())
+        n, kb, vb = e.n, e.key_bytes, e.value_bytes
+        del e
+    out_bytes = kb + vb + 4 * (n + 1) + 8 * (n + 1) + 9 * n
+    med = float(np.median(ts))
+    cpu = None if args.no_cpu else sst_cpu_baseline(stored, args.cpu_seconds)
+    print(json.dumps({"mode": "sst", "compression": args.sst_compression, "rows": args.rows, "blocks": len(stored),
+                      "stored_bytes": in_bytes, "entry_bytes_out": out_bytes, "gen_s": round(gen_s, 1),
+                      "block_table_ms_once": round(table_ms, 3),
+                      "ms_per_call_median": round(med * 1e3, 3),
+                      "entry_decode_kernel_ms": round(float(np.median(ks)), 4),
+                      "GB_s_stored_in": round(in_bytes / med / 1e9, 2),
+                      "GB_s_in_plus_out": round((in_bytes + out_bytes) / med / 1e9, 2),
+                      "entries_per_s": round(n / med, 0), "cpu_baseline": cpu}))
+
+
+def sst_cpu_baseline(stored, target_s):
+    """The oracle's restatement (oracle/murr_sst.c: Snappy/LZ4 + block walk,
+    1 thread) over the same stored blocks, repeated for about target_s."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    data = np.frombuffer(b"".join(d for d, _ in stored), np.uint8)
+    sizes = np.array([len(d) for d, _ in stored], np.int64)
+    h = np.stack([np.cumsum(sizes) - sizes, sizes, np.array([c for _, c in stored], np.int64)], axis=1)
+    n_entries, reps = 0, 0
+    t = time.perf_counter()
+    while True:
+        n_entries += O.sst_decode_all(data, h)[0]
+        reps += 1
+        dt = time.perf_counter() - t
+        if dt >= target_s:
+            break
+    return {"value": round(n_entries / dt, 0), "unit": "entries/s", "cores": 1, "kind": "port",
+            "cpu_model": cpu_model(),
+            "sample": f"{reps} pass(es) over the {len(stored)} stored blocks (inflate + entry decode) in "
+                      f"oracle/libmurr_oracle.so oc_sst_decode_all, {dt:.1f} s"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -499,7 +578,9 @@ def main():
     ap.add_argument("--config", default="B", choices=["B", "C", "D", "E"])
     ap.add_argument("--rows", type=int, default=None, help="rows per block")
     ap.add_argument("--blocks", type=int, default=None, help="blocks per launch")
-    ap.add_argument("--mode", default="decode", choices=["decode", "host", "encode", "resident"])
+    ap.add_argument("--mode", default="decode", choices=["decode", "host", "encode", "resident", "sst"])
+    ap.add_argument("--sst-compression", default="snappy", choices=["none", "snappy", "lz4"],
+                    help="sst mode: stored block compression")
     ap.add_argument("--keys", type=int, default=1000, help="resident mode: keys per read")
     ap.add_argument("--ipc", action="store_true", help="resident mode: also time the Arrow IPC message path")
     ap.add_argument("--uidx-stride", type=int, default=512,
@@ -516,7 +597,7 @@ def main():
         args.rows = {"B": 100_000, "C": 1_000_000, "D": 1_250_000, "E": 20_000_000}[args.config]
         if args.mode == "encode":
             args.rows = 20_000_000
-        if args.mode == "resident":
+        if args.mode in ("resident", "sst"):
             args.rows = 1_000_000
     if args.blocks is None:
         args.blocks = {"B": 1000, "C": 1, "D": 1, "E": 1}[args.config]
@@ -526,6 +607,8 @@ def main():
         return run_encode(args)
     if args.mode == "resident":
         return run_resident(args)
+    if args.mode == "sst":
+        return run_sst(args)
     dist, rank, world, local_rank = dist_init(args)
     if world != args.gpus and rank == 0:
         print(f"note: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)

@@ -428,16 +428,16 @@ int murr_ctx_create(int device, murr_ctx_t** out) {
 
 void murr_ctx_destroy(murr_ctx_t* c) {
     if (!c) return;
-    hipSetDevice(c->device);
-    if (c->stream) hipStreamSynchronize(c->stream);
-    if (c->ws) hipFree(c->ws);
-    if (c->aux) hipFree(c->aux);
-    if (c->hs) hipHostFree(c->hs);
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->ws) (void)hipFree(c->ws);
+    if (c->aux) (void)hipFree(c->aux);
+    if (c->hs) (void)hipHostFree(c->hs);
     for (const auto& b : c->pool) (void)(b.pinned ? hipHostFree(b.p) : hipFree(b.p));
     for (hipEvent_t e : c->event_pool) (void)hipEventDestroy(e);
-    if (c->k0) hipEventDestroy(c->k0);
-    if (c->k1) hipEventDestroy(c->k1);
-    if (c->stream) hipStreamDestroy(c->stream);
+    if (c->k0) (void)hipEventDestroy(c->k0);
+    if (c->k1) (void)hipEventDestroy(c->k1);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
 
@@ -971,7 +971,7 @@ int murr_decode_enqueue_ix(murr_ctx_t* c, const murr_segment_t* seg, const uint3
     uint64_t tiles = 0;
     uint32_t nonempty = 0;
     for (uint32_t b = 0; b < nblocks; b++) {
-        db[b] = DecBlock{blocks[b].data, blocks[b].row_off, blocks[b].n_rows, tiles};
+        db[b] = DecBlock{blocks[b].data, blocks[b].row_off, blocks[b].n_rows, tiles, nullptr};
         tiles += (blocks[b].n_rows + R - 1) / R;
         nonempty += blocks[b].n_rows != 0;
     }
@@ -1125,7 +1125,7 @@ int murr_decode_wait(murr_ctx_t* c, murr_error_t* err) {
         const unsigned long long* stp = (const unsigned long long*)(rb + 16);
         if (stp[0] | stp[4]) {
             std::fprintf(stderr, "stamps (Gcycles, sum over waves; murr_jit_kernel.hip / murr_decode.hip Stamps):");
-            for (int i = 0; i < kStampSlots; i++) std::fprintf(stderr, "%s %.3f", i == 4 ? " |" : "", stp[i] * 1e-9);
+            for (uint32_t i = 0; i < kStampSlots; i++) std::fprintf(stderr, "%s %.3f", i == 4 ? " |" : "", stp[i] * 1e-9);
             std::fprintf(stderr, "\n");
         }
     }
@@ -1476,7 +1476,7 @@ int murr_builder_new(murr_ctx_t* c, const murr_segment_t* seg, const uint32_t* p
     b->seg = *seg;
     b->seg.cols = b->cols.data();
     b->proj.assign(proj, proj + nproj);
-    hipSetDevice(c->device);
+    (void)hipSetDevice(c->device);
     uint64_t cap = std::max<uint64_t>(capacity, 16);
     uint64_t capb = 0;
     uint8_t* p = nullptr;
@@ -1550,9 +1550,9 @@ int murr_builder_build(murr_builder_t* b, murr_host_array_t* outs, murr_error_t*
     murr_block_t blk{ddata, doff, n, b->hdata_len};
     int st = decode_to_host(c, &b->seg, b->proj.data(), (uint32_t)np, blk, utf8_cap, b->out, b->e2, b->e3, outs, err);
     if (st) return st;
-    hipEventElapsedTime(&b->h2d_ms, b->e0, b->e1);
+    (void)hipEventElapsedTime(&b->h2d_ms, b->e0, b->e1);
     murr_ctx_last_kernel_ms(c, &b->k_ms);
-    hipEventElapsedTime(&b->d2h_ms, b->e2, b->e3);
+    (void)hipEventElapsedTime(&b->d2h_ms, b->e2, b->e3);
     b->total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     return MURR_OK;
 }
@@ -1722,9 +1722,12 @@ void murr_sst_result_free(murr_ctx_t* c, murr_sst_result_t* r) {
     std::memset(r, 0, sizeof *r);
 }
 
-// Decode data blocks into entries: uncompressed sizes, their scan, the
-// decompression, the entry counts, their scans, the entry decode; two 8-byte
-// (then 32-byte) read-backs size the outputs.  Synchronous.
+// Decode data blocks into entries: sst_count (a lane group per block inflates
+// it in LDS, counts its entries and keeps a tier-0 block in its HBM slot;
+// blocks too large for LDS are flagged tier 2), the scans placing every
+// block's entries, one 40-byte read-back that sizes the outputs, sst_decode.
+// Tier-2 blocks add a raw buffer, sst_big_count and a second read-back.
+// Scratch comes from the context pool.  Synchronous.
 int murr_sst_decode(murr_ctx_t* c, const murr_sst_block_t* blocks, uint32_t nblocks, murr_sst_result_t* out,
                     murr_error_t* err) {
     if (err) std::memset(err, 0, sizeof *err);
@@ -1734,16 +1737,24 @@ int murr_sst_decode(murr_ctx_t* c, const murr_sst_block_t* blocks, uint32_t nblo
         if (blocks[b].size && !blocks[b].data) return set_err(err, MURR_E_ARGUMENT);
     HIPC(hipSetDevice(c->device));
     const uint64_t nb = nblocks, nparts = (nb + 1023) / 1024;
-    // scratch: err | totals[4] | descriptors | ulen | uoff | ne | kb | vb | parts
-    const uint64_t o_tot = 8, o_desc = 64, o_ulen = round_up(o_desc + sizeof(SstBlock) * nb, 16);
-    const uint64_t o_uoff = o_ulen + 8 * nb, o_ne = o_uoff + 8 * nb, o_kb = o_ne + 8 * nb, o_vb = o_kb + 8 * nb;
-    const uint64_t o_part = o_vb + 8 * nb, scratch_bytes = o_part + 8 * std::max<uint64_t>(nparts, 1) + 64;
-    uint8_t* w = nullptr;
-    uint8_t* raw = nullptr;
-    HIPC(hipMalloc(&w, scratch_bytes));
+    // scratch: err | totals[5] | nlist | descriptors | tier rlen list | ulen uoff ne kb vb eoff koff voff | parts
+    const uint64_t o_tot = 8, o_nlist = 56, o_desc = 64, o_tier = round_up(o_desc + sizeof(SstBlock) * nb, 16);
+    const uint64_t o_arr = round_up(o_tier + 3 * 4 * nb, 16), o_part = o_arr + 8 * 8 * nb;
+    const uint64_t scratch_bytes = o_part + 8 * std::max<uint64_t>(nparts, 1) + 64;
+    const uint64_t slot_bytes = 1024 * nb + 64;  // tier-0 blocks between sst_count and sst_decode
+    uint8_t *w = nullptr, *raw = nullptr, *slots = nullptr;
+    uint64_t w_cap = 0, raw_cap = 0, slots_cap = 0;
+    if (!pool_take(c, false, scratch_bytes, round_up(scratch_bytes, 1 << 20), &w, &w_cap))
+        return set_err(err, MURR_E_HIP, (int)hipErrorOutOfMemory);
+    if (!pool_take(c, false, slot_bytes, round_up(slot_bytes, 1 << 20), &slots, &slots_cap)) {
+        pool_give(c, false, w, w_cap);
+        return set_err(err, MURR_E_HIP, (int)hipErrorOutOfMemory);
+    }
     auto fail = [&](int st) {
-        if (w) (void)hipFree(w);
-        if (raw) (void)hipFree(raw);
+        (void)hipStreamSynchronize(c->stream);
+        pool_give(c, false, w, w_cap);
+        pool_give(c, false, slots, slots_cap);
+        pool_give(c, false, raw, raw_cap);
         murr_sst_result_free(c, out);
         return st;
     };
@@ -1752,46 +1763,54 @@ int murr_sst_decode(murr_ctx_t* c, const murr_sst_block_t* blocks, uint32_t nblo
         hipError_t _e = (expr);                                              \
         if (_e != hipSuccess) return fail(set_err(err, MURR_E_HIP, (int)_e)); \
     } while (0)
-    std::vector<SstBlock> desc(nb);
-    for (uint64_t b = 0; b < nb; b++) desc[b] = SstBlock{blocks[b].data, blocks[b].size, blocks[b].compression, 0};
+    static_assert(sizeof(SstBlock) == sizeof(murr_sst_block_t), "murr_sst_block_t is the device descriptor");
     SSTC(hipMemsetAsync(w, 0, 64, c->stream));
-    if (nb) SSTC(hipMemcpyAsync(w + o_desc, desc.data(), sizeof(SstBlock) * nb, hipMemcpyHostToDevice, c->stream));
+    if (nb) SSTC(hipMemcpyAsync(w + o_desc, blocks, sizeof(SstBlock) * nb, hipMemcpyHostToDevice, c->stream));
     SstArgs a{};
     a.blocks = (const SstBlock*)(w + o_desc);
     a.nblocks = nb;
-    a.ulen = (uint64_t*)(w + o_ulen);
-    a.uoff = (uint64_t*)(w + o_uoff);
-    a.ne = (uint64_t*)(w + o_ne);
-    a.kb = (uint64_t*)(w + o_kb);
-    a.vb = (uint64_t*)(w + o_vb);
+    a.tier = (uint32_t*)(w + o_tier);
+    a.rlen = a.tier + nb;
+    a.list = a.tier + 2 * nb;
+    a.nlist = (uint32_t*)(w + o_nlist);
+    a.slots = slots;
+    uint64_t* arr = (uint64_t*)(w + o_arr);
+    a.ulen = arr;
+    a.uoff = arr + nb;
+    a.ne = arr + 2 * nb;
+    a.kb = arr + 3 * nb;
+    a.vb = arr + 4 * nb;
+    a.eoff = arr + 5 * nb;
+    a.koff = arr + 6 * nb;
+    a.voff = arr + 7 * nb;
     a.err = (unsigned long long*)w;
-    uint64_t* tot = (uint64_t*)(w + o_tot);
+    uint64_t* tot = (uint64_t*)(w + o_tot);  // [0] entries [1] key bytes [2] value bytes [3] big bytes
     uint64_t* part = (uint64_t*)(w + o_part);
-    uint64_t host[5] = {0, 0, 0, 0, 0};
+    uint64_t host[5] = {0, 0, 0, 0, 0};  // err, totals
+    auto scans = [&]() -> hipError_t {
+        hipError_t e;
+        if ((e = launch_scan_u64(a.ne, a.eoff, nb, part, tot, c->stream)) != hipSuccess) return e;
+        if ((e = launch_scan_u64(a.kb, a.koff, nb, part, tot + 1, c->stream)) != hipSuccess) return e;
+        if ((e = launch_scan_u64(a.vb, a.voff, nb, part, tot + 2, c->stream)) != hipSuccess) return e;
+        if ((e = hipMemcpyAsync(host, w, 40, hipMemcpyDeviceToHost, c->stream)) != hipSuccess) return e;
+        return hipStreamSynchronize(c->stream);
+    };
     if (nb) {
-        // 1. uncompressed sizes and their placement
-        SSTC(launch_sst_len(a, c->stream));
-        SSTC(hipMemcpyAsync(a.uoff, a.ulen, 8 * nb, hipMemcpyDeviceToDevice, c->stream));
-        SSTC(launch_scan_u64(a.uoff, nb, part, tot, c->stream));
-        SSTC(hipMemcpyAsync(host, w, 16, hipMemcpyDeviceToHost, c->stream));
-        SSTC(hipStreamSynchronize(c->stream));
-        // a block already found corrupt inflates to nothing and is reported
-        // again below, so the error names the lowest corrupt block of any pass
-        // 2. decompress, 3. count
-        SSTC(hipMalloc(&raw, host[1] + 16));
-        a.raw = raw;
-        SSTC(launch_sst_inflate(a, c->stream));
         SSTC(launch_sst_count(a, c->stream));
-        SSTC(launch_scan_u64(a.ne, nb, part, tot + 1, c->stream));
-        SSTC(launch_scan_u64(a.kb, nb, part, tot + 2, c->stream));
-        SSTC(launch_scan_u64(a.vb, nb, part, tot + 3, c->stream));
-        SSTC(hipMemcpyAsync(host, w, 40, hipMemcpyDeviceToHost, c->stream));
-        SSTC(hipStreamSynchronize(c->stream));
+        SSTC(launch_scan_u64(a.ulen, a.uoff, nb, part, tot + 3, c->stream));
+        SSTC(scans());
+        if (host[4]) {  // big blocks: inflated to raw by one thread each, counted, placed again
+            if (!pool_take(c, false, host[4] + 16, round_up(host[4] + 16, 1 << 20), &raw, &raw_cap))
+                return fail(set_err(err, MURR_E_HIP, (int)hipErrorOutOfMemory));
+            a.raw = raw;
+            SSTC(launch_sst_big_count(a, c->stream));
+            SSTC(scans());
+        }
         if (host[0]) return fail(unpack_err(host[0], err));
     }
-    const uint64_t n = host[2], kbytes = host[3], vbytes = host[4];
+    const uint64_t n = host[1], kbytes = host[2], vbytes = host[3];
     if (kbytes > 0x7FFFFFFFull) return fail(set_err(err, MURR_E_OFFSET_OVERFLOW));
-    // 4. outputs, then the entries
+    // outputs (the caller's), then the entries
     SSTC(hipMalloc((void**)&out->keys, kbytes + 16));
     SSTC(hipMalloc((void**)&out->key_offsets, 4 * (n + 1)));
     SSTC(hipMalloc((void**)&out->values, vbytes + 16));
@@ -1812,14 +1831,16 @@ int murr_sst_decode(murr_ctx_t* c, const murr_sst_block_t* blocks, uint32_t nblo
         a.types = out->types;
         SSTC(hipEventRecord(c->k0, c->stream));
         SSTC(launch_sst_decode(a, c->stream));
+        if (raw) SSTC(launch_sst_big_decode(a, c->stream));
         SSTC(hipEventRecord(c->k1, c->stream));
         c->timed = true;
         c->last_kernel = "sst_decode";
     }
     SSTC(hipStreamSynchronize(c->stream));
 #undef SSTC
-    (void)hipFree(w);
-    if (raw) (void)hipFree(raw);
+    pool_give(c, false, w, w_cap);
+    pool_give(c, false, slots, slots_cap);
+    pool_give(c, false, raw, raw_cap);
     return MURR_OK;
 }
 
@@ -1831,7 +1852,7 @@ int murr_encode_host(murr_ctx_t* c, const murr_segment_t* seg, const murr_host_c
         return set_err(err, MURR_E_ARGUMENT);
     HIPC(hipSetDevice(c->device));
     std::vector<void*> dbufs;
-    auto cleanup = [&]() { for (void* p : dbufs) hipFree(p); };
+    auto cleanup = [&]() { for (void* p : dbufs) (void)hipFree(p); };
     std::vector<murr_col_in_t> din(seg->ncols);
     std::vector<uint64_t> utf8_bytes(seg->ncols, 0);
     auto up = [&](const void* h, uint64_t bytes, const void** d) -> int {
@@ -1862,7 +1883,7 @@ int murr_encode_host(murr_ctx_t* c, const murr_segment_t* seg, const murr_host_c
     uint64_t* doff = nullptr;
     if (hipMalloc(&dblob, round_up(cap + 16, 16)) != hipSuccess ||
         hipMalloc(&doff, (n + 1) * 8) != hipSuccess) {
-        if (dblob) hipFree(dblob);
+        if (dblob) (void)hipFree(dblob);
         cleanup();
         return set_err(err, MURR_E_HIP);
     }
@@ -1875,7 +1896,7 @@ int murr_encode_host(murr_ctx_t* c, const murr_segment_t* seg, const murr_host_c
     uint64_t* ho = nullptr;
     if (hipHostMalloc(&hb, round_up(len + 16, 16), hipHostMallocDefault) != hipSuccess ||
         hipHostMalloc(&ho, (n + 1) * 8, hipHostMallocDefault) != hipSuccess) {
-        if (hb) hipHostFree(hb);
+        if (hb) (void)hipHostFree(hb);
         cleanup();
         return set_err(err, MURR_E_HIP);
     }
@@ -1884,8 +1905,8 @@ int murr_encode_host(murr_ctx_t* c, const murr_segment_t* seg, const murr_host_c
     hipError_t e3 = hipStreamSynchronize(c->stream);
     cleanup();
     if (e1 != hipSuccess || e2 != hipSuccess || e3 != hipSuccess) {
-        hipHostFree(hb);
-        hipHostFree(ho);
+        (void)hipHostFree(hb);
+        (void)hipHostFree(ho);
         return set_err(err, MURR_E_HIP, (int)(e1 ? e1 : e2 ? e2 : e3));
     }
     *out_blob = hb;

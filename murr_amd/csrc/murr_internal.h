@@ -172,10 +172,16 @@ struct SstBlock {                  // = murr_sst_block_t
 struct SstArgs {
     const SstBlock* blocks;
     uint64_t nblocks;
-    uint64_t* ulen;                // [nblocks] uncompressed sizes
-    uint64_t* uoff;                // [nblocks] their placement in raw
-    uint8_t* raw;                  // uncompressed blocks back to back
-    uint64_t *ne, *kb, *vb;        // [nblocks] entries / key bytes / value bytes, then their prefixes
+    uint32_t* tier;                // [nblocks] 0 / 1: LDS slot tier; 2: one thread, through raw
+    uint64_t* ulen;                // [nblocks] uncompressed size of a tier-2 block (0 otherwise)
+    uint64_t* uoff;                // [nblocks] its placement in raw (prefix of ulen)
+    uint8_t* raw;                  // tier-2 blocks uncompressed, back to back
+    uint8_t* slots;                // [nblocks][1024] compressed tier-0 blocks, inflated by sst_count
+    uint32_t* rlen;                // [nblocks] uncompressed size of a tier-0/1 block
+    uint32_t* list;                // tier-1 blocks, *nlist of them
+    uint32_t* nlist;
+    uint64_t *ne, *kb, *vb;        // [nblocks] entries / key bytes / value bytes
+    uint64_t *eoff, *koff, *voff;  // [nblocks] their exclusive prefixes
     uint8_t* keys;                 // user keys back to back
     int32_t* key_off;              // [entries + 1]
     uint8_t* vals;                 // values (row blobs) back to back
@@ -184,11 +190,13 @@ struct SstArgs {
     uint8_t* types;
     unsigned long long* err;
 };
-hipError_t launch_sst_len(const SstArgs& a, hipStream_t s);
-hipError_t launch_sst_inflate(const SstArgs& a, hipStream_t s);
-hipError_t launch_sst_count(const SstArgs& a, hipStream_t s);
-hipError_t launch_sst_decode(const SstArgs& a, hipStream_t s);
-hipError_t launch_scan_u64(uint64_t* x, uint64_t n, uint64_t* part, uint64_t* total, hipStream_t s);
+hipError_t launch_sst_count(const SstArgs& a, hipStream_t s);      // tiers 0 and 1; flags tier 2
+hipError_t launch_sst_big_count(const SstArgs& a, hipStream_t s);  // tier 2: inflate to raw, count
+hipError_t launch_sst_decode(const SstArgs& a, hipStream_t s);     // tiers 0 and 1, after the scans
+hipError_t launch_sst_big_decode(const SstArgs& a, hipStream_t s); // tier 2
+// y[0..n) = exclusive prefix of x[0..n) (y may be x), total -> *total; part: ceil(n / 1024) scratch.
+hipError_t launch_scan_u64(const uint64_t* x, uint64_t* y, uint64_t n, uint64_t* part, uint64_t* total,
+                           hipStream_t s);
 
 // utf8 index of a block (murr_index.hip, murr_utf8_index).
 constexpr uint32_t kMaxUidxCols = 64;

@@ -14,11 +14,22 @@
 // their count (u16), and a u32 footer num_restarts | index_type << 31.  Keys
 // are internal keys: user key + 8-byte LE trailer (sequence << 8 | type).
 //
-// One thread per block (blocks are ~512 B and a launch holds many): the
-// uncompressed length, the decompression, the entry count and the entry
-// decode are four passes, with device scans between them placing every
-// block's bytes and entries.  HBM-bound in principle; byte-serial per thread
-// in practice.
+// A lane group per block.  The stored block is staged into
+// the group's LDS slot, inflated there (tags parsed wave-uniformly from 8-byte LDS
+// windows, every literal and match copied by the group's lanes at once; a match
+// longer than its offset repeats its pattern by i % offset), and the entries
+// are walked from LDS: headers uniformly, key deltas and values copied by the
+// lanes, the internal key rebuilt in place in an LDS key buffer as the block
+// format defines it.  sst_count inflates from the stored bytes and keeps each inflated tier-0 block in a fixed 1 KiB HBM slot
+// for sst_decode, which stages it back instead of inflating again.  Slots come
+// in two tiers:
+// blocks up to 1 KiB uncompressed (16 lanes each, 8 per workgroup: the
+// reference's 512-byte blocks) and up to 4 KiB (a wave each); a block larger
+// than that, or with an internal key > kKeyCap, is tier 2: one thread
+// inflates it into a raw buffer and walks it serially (sst_big_count,
+// sst_big_decode).
+#include <cstdlib>
+
 #include "murr_device.h"
 
 namespace murr {
@@ -28,6 +39,24 @@ namespace {
 using namespace dev;
 
 constexpr uint32_t kSstCorrupt = 5;  // err_key status: MURR_E_MALFORMED_ROW (row = block index)
+constexpr uint32_t kThreads = 128;   // threads per workgroup (kThreads / G blocks)
+constexpr uint32_t kKeyCap = 256;    // internal key bytes
+constexpr uint32_t kPad = 32;        // the 16-B staging shift + window reads 11 bytes past a position
+
+// A block slot in LDS for blocks of up to RAW uncompressed bytes (stored bytes
+// up to Snappy's bound for RAW).  Tier 0: RAW 1024 (the reference's 512-byte
+// blocks plus their last entry), 16 lanes per block; tier 1: RAW 4096, a
+// wave per block; larger blocks (tier 2) go thread-serial through HBM.
+template <uint32_t RAW, bool COMP = true>  // COMP false: no stored-block region (tier-0 decode)
+struct alignas(16) BlockLds {
+    static constexpr uint32_t kRaw = RAW;
+    static constexpr uint32_t kComp = (RAW + RAW / 6 + 32 + 15) & ~15u;
+    uint8_t raw[RAW + kPad];
+    uint8_t comp[COMP ? kComp + kPad : 16];
+    uint8_t key[kKeyCap + kPad];
+};
+static_assert(sizeof(BlockLds<1024>) % 16 == 0 && sizeof(BlockLds<4096>) % 16 == 0, "LDS slots stay aligned");
+constexpr uint32_t kTier0Raw = 1024, kTier1Raw = 4096;
 
 // unaligned little-endian u32 (byte loads: blocks are byte-packed)
 __device__ __forceinline__ uint32_t ld_u32u(const uint8_t* p) {
@@ -46,6 +75,17 @@ __device__ __forceinline__ SstBlock ldblock(const SstBlock* b) {
     return r;
 }
 
+// Lanes of one wave exchange bytes through LDS: order this wave's LDS
+// accesses (the LDS serves a wave's instructions in issue order; this keeps
+// the compiler from moving them across).
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// ---- thread-serial path (big blocks) -------------------------------------------
+
 // varint32 at p (bounded by end); false when malformed.
 __device__ __forceinline__ bool varint32(const uint8_t*& p, const uint8_t* end, uint32_t& v) {
     uint32_t r = 0;
@@ -60,27 +100,6 @@ __device__ __forceinline__ bool varint32(const uint8_t*& p, const uint8_t* end, 
         }
     }
     return false;
-}
-
-// Pass 1: uncompressed length of every block.
-__global__ void __launch_bounds__(256) sst_len(SstArgs A) {
-    const uint64_t b = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    if (b >= A.nblocks) return;
-    const SstBlock blk = ldblock(A.blocks + b);
-    uint64_t len = blk.size;
-    if (blk.compression == 1 || blk.compression == 4 || blk.compression == 5) {  // Snappy, LZ4, LZ4HC
-        const uint8_t* p = blk.data;
-        uint32_t v = 0;
-        if (!varint32(p, blk.data + blk.size, v)) {
-            sst_report(A.err, b);
-            v = 0;
-        }
-        len = v;
-    } else if (blk.compression != 0) {
-        sst_report(A.err, b);
-        len = 0;
-    }
-    gp(A.ulen)[b] = len;
 }
 
 // Raw Snappy into dst[0, ulen); false when malformed.
@@ -171,24 +190,6 @@ __device__ bool inflate_lz4(const uint8_t* p, const uint8_t* end, GAS uint8_t* d
     return o == ulen;
 }
 
-// Pass 2: decompress (or copy) block b to raw + uoff[b].
-__global__ void __launch_bounds__(256) sst_inflate(SstArgs A) {
-    const uint64_t b = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    if (b >= A.nblocks) return;
-    const SstBlock blk = ldblock(A.blocks + b);
-    GAS uint8_t* dst = gp(A.raw) + gp(A.uoff)[b];
-    const uint64_t ulen = gp(A.ulen)[b];
-    bool ok = true;
-    if (blk.compression == 0)
-        for (uint64_t i = 0; i < ulen; i++) dst[i] = gp(blk.data)[i];
-    else if (blk.compression == 1)
-        ok = inflate_snappy(blk.data, blk.data + blk.size, dst, ulen);
-    else if (blk.compression == 4 || blk.compression == 5)
-        ok = inflate_lz4(blk.data, blk.data + blk.size, dst, ulen);
-    // other types were reported by sst_len
-    if (!ok) sst_report(A.err, b);
-}
-
 // The entry region [0, limit) of an uncompressed block from its footer.
 __device__ __forceinline__ bool block_layout(const uint8_t* blk, uint64_t n, uint64_t& limit) {
     if (n < 4) return false;
@@ -205,15 +206,14 @@ __device__ __forceinline__ bool block_layout(const uint8_t* blk, uint64_t n, uin
     return true;
 }
 
-// Passes 3 and 4: walk block b's entries; count (emit false) or write them.
+// Walk big block b's entries from raw; count (EMIT false) or write them.
 template <bool EMIT>
-__device__ void sst_walk(const SstArgs& A, uint64_t b) {
+__device__ void big_walk(const SstArgs& A, uint64_t b) {
     const uint8_t* blk = A.raw + gp(A.uoff)[b];
     const uint64_t n = gp(A.ulen)[b];
     uint64_t limit = 0;
     if (!block_layout(blk, n, limit)) {
         if (!EMIT) sst_report(A.err, b);
-        if (!EMIT) gp(A.ne)[b] = gp(A.kb)[b] = gp(A.vb)[b] = 0;
         return;
     }
     const uint8_t* p = blk;
@@ -221,11 +221,11 @@ __device__ void sst_walk(const SstArgs& A, uint64_t b) {
     uint64_t cnt = 0, kbytes = 0, vbytes = 0;
     uint64_t e0 = 0, k0 = 0, v0 = 0;
     if (EMIT) {
-        e0 = gp(A.ne)[b];
-        k0 = gp(A.kb)[b];
-        v0 = gp(A.vb)[b];
+        e0 = gp(A.eoff)[b];
+        k0 = gp(A.koff)[b];
+        v0 = gp(A.voff)[b];
     }
-    uint64_t pstart = 0;     // previous user key: output position and length
+    uint64_t pstart = 0;  // previous user key: output position and length
     uint32_t plen = 0, pilen = 0;
     uint64_t ptrailer = 0;  // previous trailer
     bool bad = false;
@@ -276,16 +276,406 @@ __device__ void sst_walk(const SstArgs& A, uint64_t b) {
     }
 }
 
-__global__ void __launch_bounds__(256) sst_count(SstArgs A) {
+// Big blocks: inflate (or copy) into raw + uoff[b], then count.
+__global__ void __launch_bounds__(256) sst_big_count(SstArgs A) {
     const uint64_t b = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    if (b < A.nblocks) sst_walk<false>(A, b);
-}
-__global__ void __launch_bounds__(256) sst_decode(SstArgs A) {
-    const uint64_t b = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    if (b < A.nblocks) sst_walk<true>(A, b);
+    if (b >= A.nblocks || gp(A.tier)[b] != 2) return;
+    const SstBlock blk = ldblock(A.blocks + b);
+    GAS uint8_t* dst = gp(A.raw) + gp(A.uoff)[b];
+    const uint64_t ulen = gp(A.ulen)[b];
+    bool ok = true;
+    if (blk.compression == 0)
+        for (uint64_t i = 0; i < ulen; i++) dst[i] = gp(blk.data)[i];
+    else if (blk.compression == 1)
+        ok = inflate_snappy(blk.data, blk.data + blk.size, dst, ulen);
+    else
+        ok = inflate_lz4(blk.data, blk.data + blk.size, dst, ulen);
+    if (!ok) {
+        sst_report(A.err, b);
+        return;
+    }
+    big_walk<false>(A, b);
 }
 
-// Exclusive scan of u64 x[0..n) in place, total at x[n]: chunk scans of 1024
+__global__ void __launch_bounds__(256) sst_big_decode(SstArgs A) {
+    const uint64_t b = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (b < A.nblocks && gp(A.tier)[b] == 2) big_walk<true>(A, b);
+}
+
+// ---- wave-per-block path -------------------------------------------------------
+
+// 8 bytes of an LDS region from byte p (any alignment; reads to p + 11).
+__device__ __forceinline__ uint64_t win8(const uint8_t* s, uint32_t p) {
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(s + (p & ~3u));
+    const uint64_t lo = (uint64_t)w[0] | ((uint64_t)w[1] << 32);
+    const uint32_t sh = (p & 3u) * 8;
+    return sh ? (lo >> sh) | ((uint64_t)w[2] << (64 - sh)) : lo;
+}
+
+// varint32 at s[p] (p < end) from one window: its length, 0 = malformed.
+__device__ __forceinline__ uint32_t wvarint(const uint8_t* s, uint32_t p, uint32_t end, uint32_t& v) {
+    const uint64_t w = win8(s, p);
+    uint32_t r = 0;
+    for (uint32_t i = 0; i < 5; i++) {
+        if (p + i >= end) return 0;
+        const uint32_t b = (uint32_t)(w >> (8 * i)) & 0xFFu;
+        r |= (b & 0x7Fu) << (7 * i);
+        if (!(b & 0x80u)) {
+            v = r;
+            return i + 1;
+        }
+    }
+    return 0;
+}
+
+// An entry header (three varint32s, at most 15 bytes) from one 16-byte
+// window at s[p] (p < end): bytes consumed, 0 = malformed.
+__device__ __forceinline__ uint32_t hdr3(const uint8_t* s, uint32_t p, uint32_t end, uint32_t& a, uint32_t& b,
+                                         uint32_t& c) {
+    const uint64_t w0 = win8(s, p), w1 = win8(s, p + 8);
+    uint32_t v[3], i = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 3; k++) {
+        uint32_t r = 0;
+        bool done = false;
+#pragma unroll
+        for (uint32_t j = 0; j < 5; j++) {
+            if (!done) {
+                if (p + i >= end) return 0;
+                const uint32_t byte = (uint32_t)(i < 8 ? w0 >> (8 * i) : w1 >> (8 * (i - 8))) & 0xFFu;
+                r |= (byte & 0x7Fu) << (7 * j);
+                done = !(byte & 0x80u);
+                i++;
+            }
+        }
+        if (!done) return 0;
+        v[k] = r;
+    }
+    a = v[0];
+    b = v[1];
+    c = v[2];
+    return i;
+}
+
+// Stage n bytes from src into LDS with 16-byte loads from src's 16-B aligned
+// base, four per lane in flight: the block lands at dst + the returned shift.
+template <uint32_t G>
+__device__ __forceinline__ uint32_t stage(uint8_t* dst, const uint8_t* src, uint32_t n, uint32_t lane) {
+    const uint64_t a = reinterpret_cast<uint64_t>(src);
+    const uint32_t shift = (uint32_t)(a & 15u);
+    const GAS u32x4* s16 = reinterpret_cast<const GAS u32x4*>(a - shift);
+    u32x4* d16 = reinterpret_cast<u32x4*>(dst);
+    const uint32_t chunks = (shift + n + 15) >> 4;
+    for (uint32_t c = lane; c < chunks; c += 4 * G) {
+        u32x4 v[4];
+#pragma unroll
+        for (uint32_t u = 0; u < 4; u++)
+            if (c + u * G < chunks) v[u] = s16[c + u * G];
+#pragma unroll
+        for (uint32_t u = 0; u < 4; u++)
+            if (c + u * G < chunks) d16[c + u * G] = v[u];
+    }
+    return shift;
+}
+
+// Lane-group copies inside the group's LDS.
+template <uint32_t G>
+__device__ __forceinline__ void wcopy(uint8_t* dst, const uint8_t* src, uint32_t n, uint32_t lane) {
+    for (uint32_t i = lane; i < n; i += G) dst[i] = src[i];
+}
+// out[o, o + len) = out[o - off + (i % off)]: a match repeats its last `off` bytes
+template <uint32_t G>
+__device__ __forceinline__ void wmatch(uint8_t* out, uint32_t o, uint32_t off, uint32_t len, uint32_t lane) {
+    if (off >= len) {
+        for (uint32_t i = lane; i < len; i += G) out[o + i] = out[o - off + i];
+    } else {
+        for (uint32_t i = lane; i < len; i += G) out[o + i] = out[o - off + i % off];
+    }
+}
+
+// Snappy from c[p, n) into r[0, ulen) (wave-uniform parse); false when malformed.
+template <uint32_t G>
+__device__ __forceinline__ bool winflate_snappy(const uint8_t* c, uint32_t p, uint32_t n, uint8_t* r, uint32_t ulen,
+                                                uint32_t lane) {
+    uint32_t o = 0;
+    while (p < n) {
+        const uint64_t w = win8(c, p);
+        const uint32_t tag = (uint32_t)w & 0xFFu;
+        p++;
+        uint32_t len, off;
+        const uint32_t kind = tag & 3u;
+        if (kind == 0) {
+            len = tag >> 2;
+            if (len >= 60) {
+                const uint32_t nb = len - 59;
+                if (n - p < nb) return false;
+                len = (uint32_t)(w >> 8) & (nb == 4 ? 0xFFFFFFFFu : ((1u << (8 * nb)) - 1));
+                p += nb;
+            }
+            len += 1;
+            if (n - p < len || o + len > ulen) return false;
+            wcopy<G>(r + o, c + p, len, lane);
+            p += len;
+            o += len;
+            wave_sync();
+            continue;
+        }
+        if (kind == 1) {
+            if (p >= n) return false;
+            len = 4 + ((tag >> 2) & 7u);
+            off = ((tag >> 5) << 8) | ((uint32_t)(w >> 8) & 0xFFu);
+            p += 1;
+        } else if (kind == 2) {
+            if (n - p < 2) return false;
+            len = 1 + (tag >> 2);
+            off = (uint32_t)(w >> 8) & 0xFFFFu;
+            p += 2;
+        } else {
+            if (n - p < 4) return false;
+            len = 1 + (tag >> 2);
+            off = (uint32_t)(w >> 8);
+            p += 4;
+        }
+        if (off == 0 || off > o || o + len > ulen) return false;
+        wmatch<G>(r, o, off, len, lane);
+        o += len;
+        wave_sync();
+    }
+    return o == ulen;
+}
+
+// LZ4 length extension from LDS.
+__device__ __forceinline__ bool wlz4_ext(const uint8_t* c, uint32_t& p, uint32_t n, uint32_t& v) {
+    uint32_t b;
+    do {
+        if (p >= n) return false;
+        b = c[p++];
+        v += b;
+    } while (b == 255);
+    return true;
+}
+
+// LZ4 block from c[p, n) into r[0, ulen) (wave-uniform parse).
+template <uint32_t G>
+__device__ __forceinline__ bool winflate_lz4(const uint8_t* c, uint32_t p, uint32_t n, uint8_t* r, uint32_t ulen,
+                                             uint32_t lane) {
+    uint32_t o = 0;
+    for (;;) {
+        if (p >= n) return false;
+        const uint32_t tok = c[p++];
+        uint32_t lit = tok >> 4;
+        if (lit == 15 && !wlz4_ext(c, p, n, lit)) return false;
+        if (n - p < lit || o + lit > ulen) return false;
+        wcopy<G>(r + o, c + p, lit, lane);
+        p += lit;
+        o += lit;
+        wave_sync();
+        if (p == n) break;
+        if (n - p < 2) return false;
+        const uint32_t off = (uint32_t)win8(c, p) & 0xFFFFu;
+        p += 2;
+        uint32_t ml = tok & 15u;
+        if (ml == 15 && !wlz4_ext(c, p, n, ml)) return false;
+        ml += 4;
+        if (off == 0 || off > o || o + ml > ulen) return false;
+        wmatch<G>(r, o, off, ml, lane);
+        o += ml;
+        wave_sync();
+    }
+    return o == ulen;
+}
+
+// Stage + inflate a block into L.raw: 1 ok, 0 malformed, 2 larger than the
+// slot (big_len = its uncompressed size).  The block is L.raw[r0, r0 + ulen).
+template <uint32_t G, class Lds>
+__device__ __forceinline__ int wave_inflate(const SstBlock& blk, Lds& L, uint32_t& r0, uint32_t& ulen,
+                                            uint64_t& big_len, uint32_t lane) {
+    if (blk.compression == 0) {
+        big_len = blk.size;
+        if (blk.size > Lds::kRaw) return 2;
+        ulen = (uint32_t)blk.size;
+        r0 = stage<G>(L.raw, blk.data, ulen, lane);
+        wave_sync();
+        return 1;
+    }
+    if (blk.size > Lds::kComp) {  // sized from the length prefix, read from HBM
+        const uint8_t* p = blk.data;
+        uint32_t v = 0;
+        if (!varint32(p, blk.data + blk.size, v)) return 0;
+        big_len = v;
+        return 2;
+    }
+    const uint32_t n = (uint32_t)blk.size;
+    const uint32_t c0 = stage<G>(L.comp, blk.data, n, lane);
+    wave_sync();
+    // the varint32 length prefix (Snappy's own, RocksDB's for LZ4)
+    uint32_t v = 0;
+    const uint32_t hl = n ? wvarint(L.comp, c0, c0 + n, v) : 0;
+    if (!hl) return 0;
+    big_len = v;
+    if (v > Lds::kRaw) return 2;
+    ulen = v;
+    r0 = 0;
+    const bool ok = blk.compression == 1 ? winflate_snappy<G>(L.comp, c0 + hl, c0 + n, L.raw, ulen, lane)
+                                         : winflate_lz4<G>(L.comp, c0 + hl, c0 + n, L.raw, ulen, lane);
+    return ok ? 1 : 0;
+}
+
+// Walk the entries of the block in L.raw[0, n); EMIT writes them at (e0, k0,
+// v0).  1 ok, 0 malformed, 3 an internal key longer than the key buffer.
+template <uint32_t G, bool EMIT, class Lds>
+__device__ __forceinline__ int wave_walk(const SstArgs& A, Lds& L, uint32_t r0, uint32_t n, uint32_t lane,
+                                         uint64_t& cnt, uint64_t& kbytes, uint64_t& vbytes, uint64_t e0, uint64_t k0,
+                                         uint64_t v0) {
+    cnt = kbytes = vbytes = 0;
+    if (n < 4) return 0;
+    const uint32_t footer = (uint32_t)win8(L.raw, r0 + n - 4);
+    const uint32_t nr = footer & 0x7FFFFFFFu;
+    uint64_t tail = 4;
+    if (footer >> 31) {
+        if (n < 6) return 0;
+        tail += 2 + ((uint32_t)win8(L.raw, r0 + n - 6) & 0xFFFFu);
+    }
+    tail += 4ull * nr;
+    if (nr == 0 || tail > n) return 0;
+    const uint32_t end = r0 + n - (uint32_t)tail;
+    uint32_t p = r0, pilen = 0;
+    while (p < end) {
+        uint32_t shared = 0, nonshared = 0, vlen = 0;
+        const uint32_t k = hdr3(L.raw, p, end, shared, nonshared, vlen);
+        if (!k) return 0;
+        p += k;
+        const uint64_t ilen = (uint64_t)shared + nonshared;
+        if (shared > pilen || ilen < 8 || (uint64_t)(end - p) < (uint64_t)nonshared + vlen) return 0;
+        if (ilen > kKeyCap) return 3;
+        const uint32_t ul = (uint32_t)ilen - 8;
+        if (EMIT) {
+            wcopy<G>(L.key + shared, L.raw + p, nonshared, lane);  // the internal key, rebuilt in place
+            wave_sync();
+            const uint64_t e = e0 + cnt;
+            GAS uint8_t* ko = gp(A.keys) + k0 + kbytes;
+            for (uint32_t q = lane; q < ul; q += G) ko[q] = L.key[q];
+            GAS uint8_t* vo = gp(A.vals) + v0 + vbytes;
+            const uint8_t* vs = L.raw + p + nonshared;
+            for (uint32_t q = lane; q < vlen; q += G) vo[q] = vs[q];
+            if (lane == 0) {
+                const uint64_t trailer = win8(L.key, ul);
+                gp(A.key_off)[e + 1] = (int32_t)(k0 + kbytes + ul);
+                gp(A.seqs)[e] = trailer >> 8;
+                gp(A.types)[e] = (uint8_t)(trailer & 0xFFu);
+                gp(A.val_off)[e + 1] = v0 + vbytes + vlen;
+            }
+            wave_sync();
+        }
+        p += nonshared + vlen;
+        pilen = (uint32_t)ilen;
+        kbytes += ul;
+        vbytes += vlen;
+        cnt++;
+    }
+    return 1;
+}
+
+// Tier-0 blocks inflated by sst_count wait for sst_decode in a fixed HBM slot
+// (kTier0Raw bytes each, 16-byte stores), so the decode does not inflate again.
+template <uint32_t G>
+__device__ __forceinline__ void store_slot(GAS uint8_t* dst, const uint8_t* src, uint32_t n, uint32_t lane) {
+    GAS u32x4* d16 = reinterpret_cast<GAS u32x4*>(dst);
+    const u32x4* s16 = reinterpret_cast<const u32x4*>(src);
+    for (uint32_t c = lane; c < (n + 15) / 16; c += G) d16[c] = s16[c];
+}
+
+// Count the blocks of tier TIER (tier 0: every block; tier 1: those on the
+// tier-1 list) with G lanes per block in RAW-byte LDS slots.  A block larger
+// than the slot moves to tier 1 if it fits there, else to tier 2 (as does
+// one with a key past the key buffer).
+template <uint32_t G, uint32_t RAW, uint32_t TIER>
+__device__ __forceinline__ void count_block(const SstArgs& A, BlockLds<RAW>& L, uint64_t b, uint32_t lane) {
+    const SstBlock blk = ldblock(A.blocks + b);
+    uint64_t cnt = 0, kbytes = 0, vbytes = 0, big_len = 0;
+    uint32_t ulen = 0, r0 = 0;
+    int st = 0;  // unknown compression types are malformed
+    if (blk.compression == 0 || blk.compression == 1 || blk.compression == 4 || blk.compression == 5) {
+        st = wave_inflate<G>(blk, L, r0, ulen, big_len, lane);
+        if (st == 1) st = wave_walk<G, false>(A, L, r0, ulen, lane, cnt, kbytes, vbytes, 0, 0, 0);
+    }
+    if (TIER == 0 && st == 1 && blk.compression != 0)
+        store_slot<G>(gp(A.slots) + b * kTier0Raw, L.raw, ulen, lane);
+    if (lane == 0) {
+        if (st == 0) sst_report(A.err, b);
+        uint32_t tier = TIER;
+        if (st == 3) tier = 2;
+        if (st == 2)
+            tier = (TIER == 0 && big_len <= kTier1Raw && blk.size <= BlockLds<kTier1Raw>::kComp) ? 1 : 2;
+        if (TIER == 0 && tier == 1)
+            gp(A.list)[__hip_atomic_fetch_add(gp(A.nlist), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)] =
+                (uint32_t)b;
+        gp(A.tier)[b] = tier;
+        gp(A.rlen)[b] = st == 1 ? ulen : 0;
+        gp(A.ulen)[b] = tier == 2 ? (big_len ? big_len : 1) : 0;  // a tier-2 block owns >= 1 raw byte
+        gp(A.ne)[b] = st == 1 ? cnt : 0;
+        gp(A.kb)[b] = st == 1 ? kbytes : 0;
+        gp(A.vb)[b] = st == 1 ? vbytes : 0;
+    }
+}
+
+template <uint32_t G>
+__global__ void __launch_bounds__(kThreads) sst_count0(SstArgs A) {
+    __shared__ BlockLds<kTier0Raw> lds[kThreads / G];
+    const uint32_t lane = threadIdx.x % G, slot = threadIdx.x / G;
+    const uint64_t b = (uint64_t)blockIdx.x * (kThreads / G) + slot;
+    if (b < A.nblocks) count_block<G, kTier0Raw, 0>(A, lds[slot], b, lane);
+}
+
+// Tier 1: a wave per block over the tier-1 list (a fixed grid; no work when
+// the list is empty).
+constexpr uint32_t kTier1Grid = 1024;
+__global__ void __launch_bounds__(kThreads) sst_count1(SstArgs A) {
+    __shared__ BlockLds<kTier1Raw> lds[kThreads / 64];
+    const uint32_t lane = threadIdx.x % 64, slot = threadIdx.x / 64;
+    const uint32_t nl = __hip_atomic_load(gp(A.nlist), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (uint32_t i = blockIdx.x * (kThreads / 64) + slot; i < nl; i += gridDim.x * (kThreads / 64))
+        count_block<64, kTier1Raw, 1>(A, lds[slot], gp(A.list)[i], lane);
+}
+
+template <uint32_t G, class Lds, bool FROM_SLOT>
+__device__ __forceinline__ void decode_block(const SstArgs& A, Lds& L, uint64_t b, uint32_t lane) {
+    const SstBlock blk = ldblock(A.blocks + b);
+    uint64_t cnt, kbytes, vbytes, big_len;
+    uint32_t ulen = 0, r0 = 0;
+    int st = 1;
+    if (FROM_SLOT) {  // tier 0: the stored block if plain, else its slot (inflated by sst_count)
+        ulen = gp(A.rlen)[b];
+        r0 = stage<G>(L.raw, blk.compression == 0 ? blk.data : A.slots + b * kTier0Raw, ulen, lane);
+        wave_sync();
+    } else {
+        st = wave_inflate<G>(blk, L, r0, ulen, big_len, lane);
+    }
+    // sst_count accepted the block: this walk repeats it and writes the entries
+    if (st == 1)
+        (void)wave_walk<G, true>(A, L, r0, ulen, lane, cnt, kbytes, vbytes, gp(A.eoff)[b], gp(A.koff)[b],
+                                 gp(A.voff)[b]);
+}
+
+template <uint32_t G>
+__global__ void __launch_bounds__(kThreads) sst_decode0(SstArgs A) {
+    __shared__ BlockLds<kTier0Raw, false> lds[kThreads / G];
+    const uint32_t lane = threadIdx.x % G, slot = threadIdx.x / G;
+    const uint64_t b = (uint64_t)blockIdx.x * (kThreads / G) + slot;
+    if (b < A.nblocks && gp(A.tier)[b] == 0) decode_block<G, BlockLds<kTier0Raw, false>, true>(A, lds[slot], b, lane);
+}
+
+__global__ void __launch_bounds__(kThreads) sst_decode1(SstArgs A) {
+    __shared__ BlockLds<kTier1Raw> lds[kThreads / 64];
+    const uint32_t lane = threadIdx.x % 64, slot = threadIdx.x / 64;
+    const uint32_t nl = __hip_atomic_load(gp(A.nlist), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (uint32_t i = blockIdx.x * (kThreads / 64) + slot; i < nl; i += gridDim.x * (kThreads / 64)) {
+        const uint32_t b = gp(A.list)[i];
+        if (gp(A.tier)[b] == 1) decode_block<64, BlockLds<kTier1Raw>, false>(A, lds[slot], b, lane);
+    }
+}
+
+// Exclusive scan of u64 x[0..n) into y, total at *total: chunk scans of 1024
 // (sums into part[]), one workgroup over the chunk sums, then the add-back.
 __device__ uint64_t block_scan1024(uint64_t v, uint64_t* s_w, uint64_t* total) {
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -305,13 +695,13 @@ __device__ uint64_t block_scan1024(uint64_t v, uint64_t* s_w, uint64_t* total) {
     *total = all;
     return before + inc - v;
 }
-__global__ void __launch_bounds__(1024) scan_chunks(uint64_t* x, uint64_t n, uint64_t* part) {
+__global__ void __launch_bounds__(1024) scan_chunks(const uint64_t* x, uint64_t* y, uint64_t n, uint64_t* part) {
     __shared__ uint64_t s_w[16];
     const uint64_t i = (uint64_t)blockIdx.x * 1024 + threadIdx.x;
     const uint64_t v = i < n ? gp(x)[i] : 0;
     uint64_t tot;
     const uint64_t ex = block_scan1024(v, s_w, &tot);
-    if (i < n) gp(x)[i] = ex;
+    if (i < n) gp(y)[i] = ex;
     if (threadIdx.x == 0) gp(part)[blockIdx.x] = tot;
 }
 __global__ void __launch_bounds__(1024) scan_parts(uint64_t* part, uint64_t nparts, uint64_t* total) {
@@ -327,35 +717,61 @@ __global__ void __launch_bounds__(1024) scan_parts(uint64_t* part, uint64_t npar
     }
     if (threadIdx.x == 0) gp(total)[0] = carry;
 }
-__global__ void __launch_bounds__(1024) scan_add(uint64_t* x, uint64_t n, const uint64_t* part) {
+__global__ void __launch_bounds__(1024) scan_add(uint64_t* y, uint64_t n, const uint64_t* part) {
     const uint64_t i = (uint64_t)blockIdx.x * 1024 + threadIdx.x;
-    if (i < n) gp(x)[i] += gp(part)[blockIdx.x];
+    if (i < n) gp(y)[i] += gp(part)[blockIdx.x];
 }
 
 }  // namespace
 
-hipError_t launch_sst_len(const SstArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(sst_len, dim3((uint32_t)((a.nblocks + 255) / 256)), dim3(256), 0, s, a);
+// Lanes per tier-0 block: MURR_SST_LANES for sst_count, MURR_SST_DLANES for
+// sst_decode (4, 8, 16, 32 or 64; tuning), defaults kCountLanes / kDecodeLanes.
+constexpr uint32_t kCountLanes = 16, kDecodeLanes = 8;
+uint32_t lanes_env(const char* name, uint32_t dflt) {
+    const char* e = std::getenv(name);
+    const uint32_t v = e ? (uint32_t)std::atoi(e) : dflt;
+    return (v == 4 || v == 8 || v == 16 || v == 32 || v == 64) ? v : dflt;
+}
+template <uint32_t G>
+hipError_t launch_tier0(bool decode, const SstArgs& a, hipStream_t s) {
+    const dim3 grid((uint32_t)((a.nblocks + kThreads / G - 1) / (kThreads / G)));
+    if (decode) hipLaunchKernelGGL(sst_decode0<G>, grid, dim3(kThreads), 0, s, a);
+    else hipLaunchKernelGGL(sst_count0<G>, grid, dim3(kThreads), 0, s, a);
     return hipGetLastError();
 }
-hipError_t launch_sst_inflate(const SstArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(sst_inflate, dim3((uint32_t)((a.nblocks + 255) / 256)), dim3(256), 0, s, a);
+hipError_t launch_tiers(bool decode, const SstArgs& a, hipStream_t s) {
+    static const uint32_t gc = lanes_env("MURR_SST_LANES", kCountLanes);
+    static const uint32_t gd = lanes_env("MURR_SST_DLANES", kDecodeLanes);
+    hipError_t e;
+    switch (decode ? gd : gc) {
+    case 4: e = launch_tier0<4>(decode, a, s); break;
+    case 8: e = launch_tier0<8>(decode, a, s); break;
+    case 32: e = launch_tier0<32>(decode, a, s); break;
+    case 64: e = launch_tier0<64>(decode, a, s); break;
+    default: e = launch_tier0<16>(decode, a, s); break;
+    }
+    if (e != hipSuccess) return e;
+    // tier 1 right behind tier 0, over the list tier 0's count made
+    if (decode) hipLaunchKernelGGL(sst_decode1, dim3(kTier1Grid), dim3(kThreads), 0, s, a);
+    else hipLaunchKernelGGL(sst_count1, dim3(kTier1Grid), dim3(kThreads), 0, s, a);
     return hipGetLastError();
 }
-hipError_t launch_sst_count(const SstArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(sst_count, dim3((uint32_t)((a.nblocks + 255) / 256)), dim3(256), 0, s, a);
+hipError_t launch_sst_count(const SstArgs& a, hipStream_t s) { return launch_tiers(false, a, s); }
+hipError_t launch_sst_big_count(const SstArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(sst_big_count, dim3((uint32_t)((a.nblocks + 255) / 256)), dim3(256), 0, s, a);
     return hipGetLastError();
 }
-hipError_t launch_sst_decode(const SstArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(sst_decode, dim3((uint32_t)((a.nblocks + 255) / 256)), dim3(256), 0, s, a);
+hipError_t launch_sst_decode(const SstArgs& a, hipStream_t s) { return launch_tiers(true, a, s); }
+hipError_t launch_sst_big_decode(const SstArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(sst_big_decode, dim3((uint32_t)((a.nblocks + 255) / 256)), dim3(256), 0, s, a);
     return hipGetLastError();
 }
-// x[0..n) -> exclusive prefix, total -> *total; part: ceil(n / 1024) scratch.
-hipError_t launch_scan_u64(uint64_t* x, uint64_t n, uint64_t* part, uint64_t* total, hipStream_t s) {
+hipError_t launch_scan_u64(const uint64_t* x, uint64_t* y, uint64_t n, uint64_t* part, uint64_t* total,
+                           hipStream_t s) {
     const uint64_t nparts = (n + 1023) / 1024;
-    if (nparts) hipLaunchKernelGGL(scan_chunks, dim3((uint32_t)nparts), dim3(1024), 0, s, x, n, part);
+    if (nparts) hipLaunchKernelGGL(scan_chunks, dim3((uint32_t)nparts), dim3(1024), 0, s, x, y, n, part);
     hipLaunchKernelGGL(scan_parts, dim3(1), dim3(1024), 0, s, part, nparts, total);
-    if (nparts) hipLaunchKernelGGL(scan_add, dim3((uint32_t)nparts), dim3(1024), 0, s, x, n, (const uint64_t*)part);
+    if (nparts) hipLaunchKernelGGL(scan_add, dim3((uint32_t)nparts), dim3(1024), 0, s, y, n, (const uint64_t*)part);
     return hipGetLastError();
 }
 

@@ -26,6 +26,8 @@ from .errors import raise_status
 # RocksDB CompressionType values the device inflates.
 NONE, SNAPPY, LZ4, LZ4HC = 0, 1, 4, 5
 TYPE_DELETION, TYPE_VALUE = 0, 1
+_SST_BLOCK = np.dtype([("data", np.uint64), ("size", np.uint64), ("compression", np.uint32), ("_pad", np.uint32)])
+assert _SST_BLOCK.itemsize == C.sizeof(_abi.SstBlock)
 
 
 @dataclass
@@ -61,30 +63,42 @@ class SstEntries:
 def upload_blocks(ctx: Context, blocks):
     """Stored blocks [(bytes, compression)] back to back in one device buffer
     (the layout of the file's data region): (buffer, [(offset, size,
-    compression)])."""
-    offs, pos = [], 0
-    for data, comp in blocks:
-        offs.append((pos, len(data), int(comp)))
-        pos += len(data)
+    compression)] as an int64 array)."""
+    sizes = np.array([len(d) for d, _ in blocks], np.int64)
+    h = np.zeros((len(blocks), 3), np.int64)
+    h[:, 0] = np.cumsum(sizes) - sizes
+    h[:, 1] = sizes
+    h[:, 2] = [int(c) for _, c in blocks]
     host = np.frombuffer(b"".join(bytes(d) for d, _ in blocks) + bytes(16), np.uint8)
-    return ctx.upload(host), offs
+    return ctx.upload(host), h
+
+
+def block_table(buf: DeviceBuffer, handles) -> np.ndarray:
+    """murr_sst_block_t[] for blocks at buf + offset (handles: [(offset, size,
+    compression)]), bounds-checked against the buffer."""
+    h = np.asarray(handles, dtype=np.int64).reshape(-1, 3)
+    nb = h.shape[0]
+    bad = (h[:, 0] < 0) | (h[:, 1] < 0) | (h[:, 0] + h[:, 1] > buf.nbytes)
+    if bad.any():
+        i = int(np.flatnonzero(bad)[0])
+        raise ValueError(f"block {i} {tuple(int(x) for x in h[i, :2])} lies outside the {buf.nbytes}-byte buffer")
+    desc = np.zeros(max(nb, 1), dtype=_SST_BLOCK)
+    desc["data"][:nb] = np.uint64(buf.ptr) + h[:, 0].astype(np.uint64)
+    desc["size"][:nb] = h[:, 1]
+    desc["compression"][:nb] = h[:, 2]
+    return desc[:nb]
 
 
 def decode(ctx: Context, buf: DeviceBuffer, handles) -> SstEntries:
     """murr_sst_decode over blocks at buf + offset (handles: [(offset, size,
-    compression)]).  A block that does not parse raises SegmentError
+    compression)], or the block_table() made from them once for a file that is
+    decoded again).  A block that does not parse raises SegmentError
     (MURR_E_MALFORMED_ROW) naming the first such block."""
-    nb = len(handles)
-    desc = (_abi.SstBlock * max(nb, 1))()
-    for i, (off, size, comp) in enumerate(handles):
-        if off < 0 or off + size > buf.nbytes:
-            raise ValueError(f"block {i} ({off}, {size}) lies outside the {buf.nbytes}-byte buffer")
-        desc[i].data = buf.ptr + off
-        desc[i].size = size
-        desc[i].compression = comp
+    desc = handles if isinstance(handles, np.ndarray) and handles.dtype == _SST_BLOCK else block_table(buf, handles)
     res = _abi.SstResult()
     err = _abi.Error()
-    st = ctx.L.murr_sst_decode(ctx.h, desc, nb, C.byref(res), C.byref(err))
+    st = ctx.L.murr_sst_decode(ctx.h, desc.ctypes.data_as(C.POINTER(_abi.SstBlock)), len(desc),
+                               C.byref(res), C.byref(err))
     raise_status(st, err, "murr_sst_decode")
     n = res.n
     # each output is its own allocation: ownership moves to DeviceBuffers (murr_dev_free)

@@ -40,6 +40,7 @@
  */
 #include "murr_sst.h"
 
+#include <stdlib.h>
 #include <string.h>
 
 static int get_varint32(const uint8_t** p, const uint8_t* end, uint32_t* v) {
@@ -237,4 +238,40 @@ int oc_block_decode(const uint8_t* b, uint64_t n, uint8_t* keys, int32_t* key_of
     key_off[0] = 0;
     val_off[0] = 0;
     return block_walk(b, n, &ne, &kb, &vb, keys, key_off, vals, val_off, seqs, types, scratch, sizeof scratch);
+}
+
+/* Bulk form for the bench's CPU baseline: every block of a buffer inflated and
+ * decoded (entries written to scratch and discarded), one thread; totals out. */
+int oc_sst_decode_all(const uint8_t* data, const uint64_t* off, const uint64_t* size, const uint32_t* comp,
+                      uint64_t nb, uint64_t* entries, uint64_t* key_bytes, uint64_t* value_bytes) {
+    uint64_t cap = 1 << 16;
+    uint8_t* raw = malloc(cap);
+    uint8_t *keys = malloc(cap), *vals = malloc(cap);
+    int32_t* koff = malloc(sizeof(int32_t) * (cap + 1));
+    uint64_t *voff = malloc(8 * (cap + 1)), *seqs = malloc(8 * cap);
+    uint8_t* types = malloc(cap);
+    int st = OC_OK;
+    *entries = *key_bytes = *value_bytes = 0;
+    for (uint64_t b = 0; b < nb && st == OC_OK; b++) {
+        const uint8_t* src = data + off[b];
+        uint64_t n = size[b];
+        if (comp[b] != 0) {
+            uint64_t ulen = 0, got = 0;
+            if ((st = oc_snappy_uncompressed_len(src, n, &ulen))) break;
+            if (ulen > cap) { st = OC_SST_E_CORRUPT; break; }
+            st = comp[b] == 1 ? oc_snappy_decompress(src, n, raw, cap, &got) : oc_lz4_decompress(src, n, raw, cap, &got);
+            if (st) break;
+            src = raw;
+            n = got;
+        }
+        if (n > cap) { st = OC_SST_E_CORRUPT; break; }
+        uint64_t ne, kb, vb;
+        if ((st = oc_block_count(src, n, &ne, &kb, &vb))) break;
+        if ((st = oc_block_decode(src, n, keys, koff, vals, voff, seqs, types))) break;
+        *entries += ne;
+        *key_bytes += kb;
+        *value_bytes += vb;
+    }
+    free(raw); free(keys); free(vals); free(koff); free(voff); free(seqs); free(types);
+    return st;
 }

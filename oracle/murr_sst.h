@@ -28,6 +28,11 @@ int oc_block_count(const uint8_t* b, uint64_t n, uint64_t* nentries, uint64_t* k
 int oc_block_decode(const uint8_t* b, uint64_t n, uint8_t* keys, int32_t* key_off, uint8_t* vals,
                     uint64_t* val_off, uint64_t* seqs, uint8_t* types);
 
+/* Every block of a buffer (blocks up to 64 KiB uncompressed), one thread:
+ * the bench's CPU baseline.  Totals of entries, key and value bytes. */
+int oc_sst_decode_all(const uint8_t* data, const uint64_t* off, const uint64_t* size, const uint32_t* comp,
+                      uint64_t nb, uint64_t* entries, uint64_t* key_bytes, uint64_t* value_bytes);
+
 #ifdef __cplusplus
 }
 #endif

@@ -75,6 +75,8 @@ def lib():
         L.oc_snappy_uncompressed_len.argtypes = [C.c_char_p, C.c_uint64, C.POINTER(C.c_uint64)]
         L.oc_snappy_decompress.argtypes = [C.c_char_p, C.c_uint64, C.c_void_p, C.c_uint64, C.POINTER(C.c_uint64)]
         L.oc_lz4_decompress.argtypes = [C.c_char_p, C.c_uint64, C.c_void_p, C.c_uint64, C.POINTER(C.c_uint64)]
+        L.oc_sst_decode_all.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64,
+                                         C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
         L.oc_block_count.argtypes = [C.c_char_p, C.c_uint64, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
                                      C.POINTER(C.c_uint64)]
         L.oc_block_decode.argtypes = [C.c_char_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
@@ -210,6 +212,21 @@ def snappy_decompress(src: bytes) -> bytes:
 def lz4_decompress(src: bytes) -> bytes:
     """varint32 length + LZ4 block, as RocksDB stores LZ4 blocks (murr_sst.c)."""
     return _inflate(lib().oc_lz4_decompress, src, "corrupt lz4")
+
+
+def sst_decode_all(data: np.ndarray, handles: np.ndarray):
+    """Every block of `data` (handles: int64 [nb, 3] offset, size, compression)
+    inflated and decoded in C, one thread: (entries, key bytes, value bytes)."""
+    data = np.ascontiguousarray(data, np.uint8)
+    off = np.ascontiguousarray(handles[:, 0], np.uint64)
+    size = np.ascontiguousarray(handles[:, 1], np.uint64)
+    comp = np.ascontiguousarray(handles[:, 2], np.uint32)
+    ne, kb, vb = C.c_uint64(), C.c_uint64(), C.c_uint64()
+    st = lib().oc_sst_decode_all(data.ctypes.data, off.ctypes.data, size.ctypes.data, comp.ctypes.data, len(off),
+                                 C.byref(ne), C.byref(kb), C.byref(vb))
+    if st:
+        raise OracleError(st, 0, 0, "corrupt block")
+    return ne.value, kb.value, vb.value
 
 
 def block_contents(stored: bytes, compression: int) -> bytes:

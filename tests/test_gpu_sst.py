@@ -73,6 +73,26 @@ def test_edge_blocks():
     assert e.n == 0
 
 
+def test_long_keys_and_block_size_boundaries():
+    # internal keys past the LDS key buffer (256 B), blocks at and around the
+    # LDS slot tiers (1 KiB, 4 KiB uncompressed) and the thread-serial tier
+    rng = np.random.default_rng(21)
+    stored = []
+    for klen in (240, 248, 249, 300, 1000):
+        entries = sorted((bytes(rng.integers(97, 100, size=klen, dtype=np.uint8)) + b"%03d" % i, 9, 1, b"v" * i)
+                         for i in range(12))
+        stored.append((G.snappy(G.build_block(entries, restart_interval=4)), G.SNAPPY))
+    for target in (1000, 1023, 1024, 1025, 2048, 4095, 4096, 4097, 5000):
+        for comp in (G.NONE, G.SNAPPY, G.LZ4):
+            e1 = [(b"a", 5, 1, b"")]
+            base = len(G.build_block(e1 + [(b"b", 4, 1, b"")], hash_index=False))
+            e2 = e1 + [(b"b", 4, 1, bytes(rng.integers(0, 256, size=target - base - 1, dtype=np.uint8)))]
+            raw = G.build_block(e2, hash_index=False)
+            assert abs(len(raw) - target) <= 2
+            stored.append((G.compress(raw, comp), comp))
+    check(stored)
+
+
 def test_many_blocks_scan_carry():
     # > 1024 x 1024 blocks: the block scans run their multi-pass carry
     blk = G.snappy(G.build_block([(b"user-key-%d" % 7, 5, G.TYPE_VALUE, b"v" * 11)]))

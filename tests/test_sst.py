@@ -109,3 +109,18 @@ def test_corrupt_blocks_are_errors():
     bad[0] = 5  # shared bytes at a restart point
     with pytest.raises(O.OracleError):
         O.block_decode(bytes(bad))
+
+
+def test_bulk_decode_totals_match_per_block():
+    rng = np.random.default_rng(13)
+    blocks = G.blocks_of(G.random_entries(rng, 3000, dup_p=0.1))
+    stored = [(G.compress(b, (G.NONE, G.SNAPPY, G.LZ4)[i % 3]), (G.NONE, G.SNAPPY, G.LZ4)[i % 3])
+              for i, b in enumerate(blocks)]
+    data = np.frombuffer(b"".join(d for d, _ in stored), np.uint8)
+    sizes = np.array([len(d) for d, _ in stored], np.int64)
+    h = np.stack([np.cumsum(sizes) - sizes, sizes, np.array([c for _, c in stored], np.int64)], axis=1)
+    ne = kb = vb = 0
+    for d, c in stored:
+        k, v, _, _ = O.block_decode(O.block_contents(d, c))
+        ne, kb, vb = ne + len(k), kb + sum(map(len, k)), vb + sum(map(len, v))
+    assert O.sst_decode_all(data, h) == (ne, kb, vb)
