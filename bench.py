@@ -60,6 +60,8 @@ def sum_over_ranks(g, x: float) -> float:
 
 
 def make_columns(config: str, rows: int, start: int):
+    if config == "A":
+        return synth.config_a(rows, start=start)
     if config == "B":
         return synth.config_b(rows, start=start)
     if config in ("C", "D"):
@@ -575,7 +577,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="B", choices=["B", "C", "D", "E"])
+    ap.add_argument("--config", default="B", choices=["A", "B", "C", "D", "E"])
     ap.add_argument("--rows", type=int, default=None, help="rows per block")
     ap.add_argument("--blocks", type=int, default=None, help="blocks per launch")
     ap.add_argument("--mode", default="decode", choices=["decode", "host", "encode", "resident", "sst"])
@@ -594,13 +596,13 @@ def main():
     ap.add_argument("--proj", default=None, help="comma-separated projected columns (default all)")
     args = ap.parse_args()
     if args.rows is None:
-        args.rows = {"B": 100_000, "C": 1_000_000, "D": 1_250_000, "E": 20_000_000}[args.config]
+        args.rows = {"A": 1000, "B": 100_000, "C": 1_000_000, "D": 1_250_000, "E": 20_000_000}[args.config]
         if args.mode == "encode":
             args.rows = 20_000_000
         if args.mode in ("resident", "sst"):
             args.rows = 1_000_000
     if args.blocks is None:
-        args.blocks = {"B": 1000, "C": 1, "D": 1, "E": 1}[args.config]
+        args.blocks = {"A": 1, "B": 1000, "C": 1, "D": 1, "E": 1}[args.config]
     if args.mode == "host":
         return run_host(args)
     if args.mode == "encode":

@@ -90,6 +90,12 @@ def to_arrow(c) -> pa.Array:
     return pa.Array.from_buffers(dt.arrow_dtype(), n, [valid, pa.py_buffer(c["values"].tobytes())])
 
 
+def config_a(n: int = 1000, start: int = 0):
+    """configs[0], benches/read_plain.rs on CPU at its plumbing size: one
+    FLOAT32 column, f = i, no nulls."""
+    return [column(D.Float32, np.arange(start, start + n).astype(np.float32))]
+
+
 def config_b(n: int, start: int = 0, null_frac: float = 0.0, seed: int = 42):
     """{f: f32 = i, s: utf8 = i.to_string()} (key column omitted: not in the blob)."""
     i = np.arange(start, start + n)

@@ -1,6 +1,6 @@
 """BASELINE.json sizes through size-independent properties: encode -> decode is
 the identity on Arrow buffers, the device encode equals the oracle / the closed
-form, and a 1000-key random read equals the oracle.  (configs B, C/D, E)"""
+form, and a 1000-key random read equals the oracle.  (configs A, B, C/D, E)"""
 import numpy as np
 import pytest
 
@@ -71,6 +71,25 @@ def roundtrip(ctx, cols, n, check_oracle_encode=True):
         got = download_array(ctx, outs.array(0, p), int(c["dtype"]), n)
         assert_array_equal(got, as_expected(c), f"column {p}")
     return seg, blob, row_off, blen
+
+
+def test_config_a_1k_rows_single_f32(ctx):
+    # configs[0]: benches/read_plain.rs's plumbing size, one f32 column, f = i;
+    # device decode and the host path (pinned H2D -> decode -> D2H) through
+    # ReadBatchBuilder, both against the oracle and the closed form
+    import pyarrow as pa
+    from murr_amd.row import ReadBatchBuilder
+    cols = synth.config_a(1000)
+    seg, blob, row_off, blen = roundtrip(ctx, cols, 1000)
+    host_blob = blob.download(blen).tobytes()
+    offs = row_off.download(8 * 1001).view(np.uint64)
+    b = ReadBatchBuilder(seg, seg.columns, 1000, ctx)
+    for i in range(1000):
+        b.add_row(host_blob[offs[i]:offs[i + 1]])
+    rb = b.build()
+    assert rb.column(0).equals(pa.array(np.arange(1000, dtype=np.float32)))
+    want = O.decode_block(O.Segment([int(D.Float32)]), [0], np.frombuffer(host_blob, np.uint8), offs)
+    assert want[0]["values"] == rb.column(0).buffers()[1].to_pybytes()[:4000]
 
 
 def test_config_b_100k_rows(ctx):
