@@ -829,7 +829,8 @@ int murr_segment_prepare(murr_ctx_t* c, const murr_segment_t* seg) {
         const murr_column_t& col = seg->cols[i];
         ec[i] = EncCol{nullptr, nullptr, nullptr, 0, col.dtype, col.index, col.offset, col.size};
     }
-    if (seg->ncols && !jit_encode_kernel(c->device, seg->bitset_size, seg->capacity, ec.data(), seg->ncols, &why)) {
+    if (seg->ncols &&
+        !jit_encode_kernel(c->device, seg->bitset_size, seg->capacity, ec.data(), seg->ncols, 32768, &why)) {
         std::fprintf(stderr, "murr: JIT encode unavailable: %s\n", why.c_str());
         return MURR_E_INTERNAL;
     }
@@ -1240,7 +1241,8 @@ int murr_encode_batch_at(murr_ctx_t* c, const murr_segment_t* seg, const murr_co
         const char* je = std::getenv("MURR_ENCODE_JIT");
         if (!(je && std::atoi(je) == 0) && seg->ncols) {
             std::string why;
-            ek = jit_encode_kernel(c->device, seg->bitset_size, seg->capacity, ec.data(), seg->ncols, &why);
+            ek = jit_encode_kernel(c->device, seg->bitset_size, seg->capacity, ec.data(), seg->ncols,
+                                   jit_encode_stage(n, blob_cap), &why);
             if (!ek && (std::getenv("MURR_DECODE_VERBOSE") || (je && std::atoi(je) == 1)))
                 std::fprintf(stderr, "murr: JIT encode unavailable: %s\n", why.c_str());
             if (!ek && je && std::atoi(je) == 1) return set_err(err, MURR_E_INTERNAL);

@@ -151,8 +151,10 @@ struct JitEncKernel {
     int bpc;  // resident workgroups per CU
 };
 struct EncCol;
+// stage: LDS bytes of a tile's blobs (jit_encode_stage), a compile-time size.
+uint32_t jit_encode_stage(uint64_t n_rows, uint64_t blob_cap);
 const JitEncKernel* jit_encode_kernel(int device, uint32_t bs, uint32_t cap, const EncCol* cols, uint32_t ncols,
-                                      std::string* why);
+                                      uint32_t stage, std::string* why);
 struct EncodeArgs;
 hipError_t jit_encode_launch(const JitEncKernel* k, const EncodeArgs& a, uint32_t grid, hipStream_t s);
 

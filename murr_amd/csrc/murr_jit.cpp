@@ -279,9 +279,19 @@ std::string enc_prelude(uint32_t bs, uint32_t cap, const EncCol* cols, uint32_t 
 
 }  // namespace
 
+// LDS stage of one 256-row tile: 8, 16 or 32 KiB, the smallest that holds
+// the mean blob (blob_cap / n_rows, the bound the caller sized) with a quarter
+// of headroom.  Small stages let eight workgroups share a CU; a tile over its
+// stage is written straight to HBM (correct, slower).  Three variants per
+// layout at most (each one compile, cached).
+uint32_t jit_encode_stage(uint64_t n_rows, uint64_t blob_cap) {
+    const uint64_t mean = n_rows ? (blob_cap + n_rows - 1) / n_rows : 128;
+    const uint64_t want = 256 * mean * 5 / 4 + 64;
+    return want <= 8192 ? 8192u : want <= 16384 ? 16384u : 32768u;
+}
+
 const JitEncKernel* jit_encode_kernel(int device, uint32_t bs, uint32_t cap, const EncCol* cols, uint32_t ncols,
-                                      std::string* why) {
-    const uint32_t stage = 32768;
+                                      uint32_t stage, std::string* why) {
     const std::string pre = enc_prelude(bs, cap, cols, ncols, stage);
     const std::string key = std::to_string(device) + "\n" + pre;
     std::lock_guard<std::mutex> lk(g_mu);

@@ -163,12 +163,17 @@ DEV void write_out(const LAS uint8_t* buf, GAS uint8_t* out, uint64_t g0, uint64
 
 // One row's fixed part and payload sizes.  `pos` = payload append position
 // (write.rs:44-52), starting at bs + cap.
+#ifndef MJE_PF
+#define MJE_PF 3
+#endif
+constexpr uint32_t PF = MJE_PF;  // aligned dwords of each string loaded with the row (the rest later)
 struct RowBuild {
     Row r;
     uint32_t vmask[(NCOLS + 31) / 32 ? (NCOLS + 31) / 32 : 1];  // valid bits, segment order
     uint32_t pos;
     uint32_t ulen[NUTF8 ? NUTF8 : 1];
     uint64_t ustart[NUTF8 ? NUTF8 : 1];  // Arrow data offset of the string
+    uint32_t pre[NUTF8 ? NUTF8 : 1][PF];  // its first PF aligned dwords
 };
 
 template <uint32_t C, uint32_t KIND, uint32_t SOFF, uint32_t U>
@@ -190,6 +195,14 @@ DEV void build_col(RowBuild& B, uint64_t row) {
         B.ulen[U] = v ? len : 0u;
         B.ustart[U] = a;
         if (v) B.pos += 4 + len;
+        // the string's first aligned dwords now, so their latency overlaps the
+        // rest of the row and the tile scan (an aligned dword never crosses a
+        // page: bytes around the string are safe to load and masked later)
+        const uintptr_t sp = (uintptr_t)(gp(c.values) + a);
+        const GAS uint32_t* w = (const GAS uint32_t*)(sp & ~(uintptr_t)3);
+        const uint32_t nd = v ? (len + (uint32_t)(sp & 3) + 3) / 4 : 0u;
+#pragma unroll
+        for (uint32_t i = 0; i < PF; i++) B.pre[U][i] = i < nd ? w[i] : 0u;
     } else if constexpr (KIND == 9) {  // bool: b as u8 (bool_.rs:111-117)
         const uint32_t b = v ? (gp(c.values)[e >> 3] >> (e & 7)) & 1u : 0u;
         put8<OFF>(B.r, b);
@@ -237,8 +250,7 @@ DEV void put_payload(const RowBuild& B, LAS uint32_t* stw, uint32_t rb, uint32_t
     const uint32_t sa = (uint32_t)(sa_ptr & 3);
     const GAS uint32_t* w = (const GAS uint32_t*)(sa_ptr - sa);
     const uint32_t d0 = rb + p - sa;  // stage byte of w[0]'s first byte
-    for (uint32_t i = 0; 4 * i < n + sa; i++) {
-        uint32_t v = w[i];
+    auto merge = [&](uint32_t v, uint32_t i) {
         // keep the bytes b with 0 <= 4i + b - sa < n
         const int32_t lo = (int32_t)sa - 4 * (int32_t)i, hi = (int32_t)(n + sa) - 4 * (int32_t)i;
         if (lo > 0) v &= ~0u << (8 * lo);
@@ -248,7 +260,11 @@ DEV void put_payload(const RowBuild& B, LAS uint32_t* stw, uint32_t rb, uint32_t
             __hip_atomic_fetch_or(stw + dw, v << (8 * sh), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         if (sh && (v >> (32 - 8 * sh)))
             __hip_atomic_fetch_or(stw + dw + 1, v >> (32 - 8 * sh), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
+    };
+#pragma unroll
+    for (uint32_t i = 0; i < PF; i++)
+        if (4 * i < n + sa) merge(B.pre[U][i], i);  // loaded with the row
+    for (uint32_t i = PF; 4 * i < n + sa; i++) merge(w[i], i);
     p += n;
 }
 
@@ -268,6 +284,9 @@ extern "C" __global__ void __launch_bounds__(256) murr_jit_encode(mje::Args) {
         const uint32_t nr = (uint32_t)min((uint64_t)TILE, n_rows - r0);
         const bool active = tid < nr;
         const uint64_t row = r0 + (active ? tid : 0u);
+        // the tile's start (murr_jit_encode_sizes + murr_jit_encode_scan left the
+        // exclusive prefix of the tile totals in lookback[t]), loaded up front
+        const uint64_t t_pre = NUTF8 ? ((const GAS uint64_t*)A->lookback)[t] : 0;
 
         RowBuild B;
 #pragma unroll
@@ -299,9 +318,7 @@ extern "C" __global__ void __launch_bounds__(256) murr_jit_encode(mje::Args) {
                 agg += v;
             }
             __syncthreads();
-            // the tile's start: murr_jit_encode_sizes + murr_jit_encode_scan
-            // left the exclusive prefix of the tile totals in lookback[t]
-            tstart = ((const GAS uint64_t*)A->lookback)[t];
+            tstart = t_pre;
             start = tstart + before + inc - size;
             span = agg;
         }

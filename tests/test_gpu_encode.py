@@ -92,6 +92,25 @@ def test_long_strings_take_the_hbm_path(ctx):
     assert np.array_equal(off, woff) and blob.tobytes() == wblob.tobytes()
 
 
+def test_tiles_over_a_small_stage(ctx):
+    # short strings keep the mean blob small (an 8 KiB LDS stage per 256-row
+    # tile), while a few tiles of 120-byte strings overflow it: those tiles go
+    # straight to HBM, the rest through the stage
+    n = 20_000
+    rng = np.random.default_rng(33)
+    lens = np.full(n, 3, np.int64)
+    lens[2560:3072] = 120  # tiles 10 and 11
+    lens[7000:7100] = 120  # part of tile 27
+    offs = np.zeros(n + 1, np.int64)
+    np.cumsum(lens, out=offs[1:])
+    data = rng.integers(97, 123, size=int(offs[-1]), dtype=np.uint8)
+    cols = [synth.column(D.Float32, np.arange(n, dtype=np.float32)),
+            synth.column(D.Utf8, offsets=offs.astype(np.int32), data=data)]
+    blob, off = gpu_encode(ctx, [D.Float32, D.Utf8], cols, n)
+    wblob, woff = O.encode_batch(O.Segment([int(D.Float32), int(D.Utf8)]), synth.oracle_cols(cols), n)
+    assert np.array_equal(off, woff) and blob.tobytes() == wblob.tobytes()
+
+
 def test_sliced_arrow_inputs(ctx):
     # Arrow arrays with a non-zero offset (RecordBatch::slice, dataset.rs:73-80)
     rng = np.random.default_rng(32)
