@@ -1254,7 +1254,9 @@ int murr_encode_batch_at(murr_ctx_t* c, const murr_segment_t* seg, const murr_co
         const int per_cu = ek ? std::max(1, ek->bpc - 1) : c->enc_grid_per_cu;
         uint64_t grid = std::min<uint64_t>(tiles, (uint64_t)c->cus * per_cu);
         if (ek) {
-            HIPC(jit_encode_launch(ek, a, (uint32_t)grid, c->stream));
+            bool inl = true;
+            for (const EncCol& e : ec) inl = inl && (e.dtype != MURR_UTF8 || e.validity == nullptr);
+            HIPC(jit_encode_launch(ek, a, (uint32_t)grid, c->stream, inl));
             c->last_kernel = "murr_jit_encode";
         } else {
             HIPC(launch_encode(a, (uint32_t)grid, c->stream));

@@ -156,7 +156,10 @@ uint32_t jit_encode_stage(uint64_t n_rows, uint64_t blob_cap);
 const JitEncKernel* jit_encode_kernel(int device, uint32_t bs, uint32_t cap, const EncCol* cols, uint32_t ncols,
                                       uint32_t stage, std::string* why);
 struct EncodeArgs;
-hipError_t jit_encode_launch(const JitEncKernel* k, const EncodeArgs& a, uint32_t grid, hipStream_t s);
+// inline_sizes: no utf8 column has a validity buffer (the scan computes the
+// tile totals; no sizes pass).
+hipError_t jit_encode_launch(const JitEncKernel* k, const EncodeArgs& a, uint32_t grid, hipStream_t s,
+                             bool inline_sizes);
 
 void decode_lds_plan(DecodeArgs& a, uint32_t nw, uint32_t kc, uint32_t slots, uint32_t depth);
 bool decode_shape_ok(uint32_t nw, uint32_t kc);

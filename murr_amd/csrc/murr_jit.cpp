@@ -325,7 +325,8 @@ const JitEncKernel* jit_encode_kernel(int device, uint32_t bs, uint32_t cap, con
     return &it->second->k;
 }
 
-hipError_t jit_encode_launch(const JitEncKernel* k, const EncodeArgs& a, uint32_t grid, hipStream_t s) {
+hipError_t jit_encode_launch(const JitEncKernel* k, const EncodeArgs& a, uint32_t grid, hipStream_t s,
+                             bool inline_sizes) {
     EncodeArgs args = a;
     size_t sz = sizeof(args);
     void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &args, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
@@ -334,7 +335,10 @@ hipError_t jit_encode_launch(const JitEncKernel* k, const EncodeArgs& a, uint32_
         // scan over 4096-tile groups (sums, one-workgroup scan of the sums, prefixes)
         const uint32_t tiles = (uint32_t)std::min<uint64_t>(a.total_tiles, 0x7FFFFFFFull);
         const uint32_t groups = (uint32_t)((a.total_tiles + 4095) / 4096);
-        hipError_t e = hipModuleLaunchKernel(k->fn_sizes, tiles, 1, 1, 256, 1, 1, 0, s, nullptr, cfg);
+        // (no utf8 column with a validity buffer: the scan derives the tile
+        // totals from the offsets itself, murr_jit_encode.hip sizes_inline)
+        hipError_t e = inline_sizes ? hipSuccess
+                                    : hipModuleLaunchKernel(k->fn_sizes, tiles, 1, 1, 256, 1, 1, 0, s, nullptr, cfg);
         struct {
             EncodeArgs a;
             uint32_t pass;

@@ -261,18 +261,49 @@ struct HbmSrc {
     DEV uint32_t u32(uint32_t a) const { return *(const GAS u32u*)(g + a); }
 };
 
+// Projection slots loaded once per tile (MJ_HOIST >= 1) and output
+// descriptors kept in per-lane registers (>= 2) instead of kernel-argument
+// and descriptor loads at every use (0; tuning).
+#ifndef MJ_HOIST
+#define MJ_HOIST 2
+#endif
+// Ablations (tuning only, MURR_JIT_DEFS): skip the string byte stores / the
+// fixed-width value stores, to price them.
+#ifndef MJ_ABL_NOSTR
+#define MJ_ABL_NOSTR 0
+#endif
+#ifndef MJ_ABL_NOFIX
+#define MJ_ABL_NOFIX 0
+#endif
+// Output stores (written once, read by the caller later): plain, or
+// non-temporal under MJ_OUT_NT (tuning).
+template <class T> DEV void ost(GAS T* p, T v) {
+#if defined(MJ_OUT_NT) && MJ_OUT_NT
+    __builtin_nontemporal_store(v, p);
+#else
+    *p = v;
+#endif
+}
+
 // ---- LDS-DMA (inline asm: kept out of the compiler's waitcnt bookkeeping;
 // the loader wave waits for exactly its own DMA with counted vmcnt) ----------
+// Cache policy of the blob stream (read once): MJ_BLOB_POL, e.g. " nt"
+// (tuning: MURR_JIT_DEFS=MJ_BLOB_NT=1).
+#if defined(MJ_BLOB_NT) && MJ_BLOB_NT
+#define MJ_BLOB_POL " nt"
+#else
+#define MJ_BLOB_POL ""
+#endif
 DEV void glds16(const GAS void* src, LAS void* dst) {
     uint32_t keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" MJ_BLOB_POL "\n\ts_mov_b32 m0, %0"
                  : "=&s"(keep)
                  : "v"(src), "s"(__builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)dst))
                  : "memory");
 }
 DEV void glds4(const GAS void* src, LAS void* dst) {
     uint32_t keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off" MJ_BLOB_POL "\n\ts_mov_b32 m0, %0"
                  : "=&s"(keep)
                  : "v"(src), "s"(__builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)dst))
                  : "memory");
@@ -567,6 +598,9 @@ struct Lanes {
     uint32_t isbool[NCW];
     uint32_t nacc[NCW];             // nulls of column c since the last flush
     uint32_t blk;                   // block the pointers belong to (~0 = none)
+#if MJ_HOIST >= 2
+    uint64_t optr[NCW], ocap[NCW];  // utf8 offsets pointer / values capacity of column c
+#endif
 };
 
 DEV const Out* outs_of(uint32_t b) {
@@ -581,6 +615,26 @@ DEV Out ldout(const Out* base, uint32_t p) {
     Out r;
     r.values = q->values; r.validity = q->validity; r.offsets = q->offsets; r.values_cap = q->values_cap;
     return r;
+}
+
+// Column C's output descriptor for the current block from the lane table
+// (v_readlane, no memory round trip; MJ_HOIST >= 2), or from memory.
+template <uint32_t C> DEV Out lane_out(const Lanes& L, const Out* ob, uint32_t p) {
+#if MJ_HOIST >= 2
+    auto rl64 = [](uint64_t v) {
+        // (readlane returns int: cast before widening, or the low word sign-extends)
+        return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(v >> 32), C % 64) << 32) |
+               (uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)v, C % 64);
+    };
+    Out r;
+    r.values = (uint8_t*)rl64(L.bptr[C / 64]);
+    r.validity = nullptr;  // (validity words go through store_words)
+    r.offsets = (int32_t*)rl64(L.optr[C / 64]);
+    r.values_cap = rl64(L.ocap[C / 64]);
+    return r;
+#else
+    return ldout(ob, p);
+#endif
 }
 
 // Per-lane output pointers of block b (lane c: column c's validity and bool
@@ -612,7 +666,16 @@ DEV void lanes_block(Lanes& L, uint32_t b, uint32_t lane) {
         const GAS Out* o = (const GAS Out*)ob + (s != kNone ? s : 0u);
         L.vptr[j] = s != kNone ? (uint64_t)o->validity : 0;
         L.bptr[j] = s != kNone ? (uint64_t)o->values : 0;
+#if MJ_HOIST >= 2
+        L.optr[j] = s != kNone ? (uint64_t)o->offsets : 0;
+        L.ocap[j] = s != kNone ? (uint64_t)o->values_cap : 0;
+#endif
     }
+    // Wait for these loads here, on the (rare) block-change path.  Left
+    // pending, they make the compiler put a vmcnt(0) where this path rejoins
+    // the tile loop -- every tile would then wait for all of the previous
+    // tile's stores to be acknowledged.
+    __builtin_amdgcn_s_waitcnt(0x0F70);
 }
 
 // Validity (and bool values) words of one chunk for every decoded column: one
@@ -662,19 +725,30 @@ DEV uint32_t copy_str(const Src& src, GAS uint8_t* vb, uint32_t pay, uint32_t n)
             }
             return 0u;
         }
-        // 8-byte steps from realigned dword pairs, the last one overlapping
+        // 8-byte steps from realigned dword pairs, the last one overlapping;
+        // two steps per iteration with their LDS reads issued together (one
+        // LDS round trip per 16 bytes)
         uint32_t hib = 0;
         const uint32_t sh = pay & 3u;
         const LAS uint32_t* p = (const LAS uint32_t*)(src.s + (pay & ~3u));
 #pragma unroll 1
-        for (uint32_t q = 0;; q += 8) {
-            const uint32_t at = q + 8 <= n ? q : n - 8;
-            const uint32_t b = sh + at, d = b >> 2, s2 = b & 3u;
-            const uint32_t x0 = p[d], x1 = p[d + 1], x2 = p[d + 2];
-            const uint32_t lo = __builtin_amdgcn_alignbyte(x1, x0, s2), hi = __builtin_amdgcn_alignbyte(x2, x1, s2);
-            *(GAS u64u*)(vb + at) = ((uint64_t)hi << 32) | lo;
-            hib |= lo | hi;
-            if (q + 8 >= n) break;
+        for (uint32_t q = 0;; q += 16) {
+            const bool two = q + 8 < n;  // a second step in this iteration
+            const uint32_t at0 = q + 8 <= n ? q : n - 8;
+            const uint32_t at1 = q + 16 <= n ? q + 8 : n - 8;
+            const uint32_t b0 = sh + at0, d0 = b0 >> 2, s0 = b0 & 3u;
+            const uint32_t b1 = sh + at1, d1 = b1 >> 2, s1 = b1 & 3u;
+            const uint32_t x0 = p[d0], x1 = p[d0 + 1], x2 = p[d0 + 2];
+            const uint32_t y0 = p[d1], y1 = p[d1 + 1], y2 = p[d1 + 2];
+            const uint32_t lo0 = __builtin_amdgcn_alignbyte(x1, x0, s0), hi0 = __builtin_amdgcn_alignbyte(x2, x1, s0);
+            const uint32_t lo1 = __builtin_amdgcn_alignbyte(y1, y0, s1), hi1 = __builtin_amdgcn_alignbyte(y2, y1, s1);
+            *(GAS u64u*)(vb + at0) = ((uint64_t)hi0 << 32) | lo0;
+            hib |= lo0 | hi0;
+            if (two) {
+                *(GAS u64u*)(vb + at1) = ((uint64_t)hi1 << 32) | lo1;
+                hib |= lo1 | hi1;
+            }
+            if (q + 16 >= n) break;
         }
         return hib;
     }
@@ -811,6 +885,19 @@ DEV void decode_tile(const Src& src, const Tile& T, const LAS uint32_t* ro, LAS 
     LAS uint64_t* tpre = (LAS uint64_t*)(ctl + SH::CNT_B);
     LAS uint32_t* wt = (LAS uint32_t*)(ctl + SH::CNT_B + 8 * NU);
     lanes_block(L, T.b, lane);
+#if MJ_HOIST
+    // the projection's slot words, once per tile (one batched scalar load;
+    // slot_of would wait on a kernel-argument load per use)
+    uint32_t slw[(NCOLS + 1) / 2];
+    {
+        const CAS uint32_t* w = (const CAS uint32_t*)args()->slot;
+#pragma unroll
+        for (uint32_t j = 0; j < (NCOLS + 1) / 2; j++) slw[j] = w[j];
+    }
+#define MJ_SLOT(C) ((slw[(C) >> 1] >> (16 * ((C) & 1))) & 0xFFFFu)
+#else
+#define MJ_SLOT(C) slot_of(C)
+#endif
 
     Rows<R> W;
     uint32_t badk = 0, partial = 0;
@@ -858,7 +945,7 @@ DEV void decode_tile(const Src& src, const Tile& T, const LAS uint32_t* ro, LAS 
     for (uint32_t u = 0; u < NU; u++) utot[u] = 0;
 #define MJ_U(C, W_, FO, U)                                                                              \
     if constexpr (W_ == 0) {                                                                            \
-        if (slot_of(C) != kNone) {                                                                      \
+        if (MJ_SLOT(C) != kNone) {                                                                      \
             uint32_t wtot = 0;                                                                          \
             _Pragma("unroll") for (uint32_t k = 0; k < R; k++) {                                        \
                 const uint32_t rl = W.rl[k];                                                            \
@@ -875,7 +962,7 @@ DEV void decode_tile(const Src& src, const Tile& T, const LAS uint32_t* ro, LAS 
                 upay[U][k] = pa + 4;                                                                    \
                 ulen[U][k] = good ? l : 0u;                                                             \
                 uinc[U][k] = wave_scan(ulen[U][k]) + wtot;                                              \
-                wtot = __builtin_amdgcn_readlane(uinc[U][k], 63);                                       \
+                wtot = (uint32_t)__builtin_amdgcn_readlane(uinc[U][k], 63);                                       \
                 if constexpr (PH != 2) stash<C>(vlo[k], vhi[k], valid);                                 \
             }                                                                                           \
             utot[U] = wtot;                                                                             \
@@ -895,9 +982,9 @@ DEV void decode_tile(const Src& src, const Tile& T, const LAS uint32_t* ro, LAS 
     // ---- fixed-width and bool columns (primitive.rs:43-56, bool_.rs:86-99)
 #define MJ_F(C, W_, FO, U)                                                                              \
     if constexpr (W_ != 0 && PH != 2) {                                                                 \
-        if (slot_of(C) != kNone) {                                                                      \
+        if (MJ_SLOT(C) != kNone) {                                                                      \
             constexpr uint32_t WW = W_ == 9 ? 1u : W_;                                                  \
-            const Out o = ldout(ob, slot_of(C));                                                        \
+            const Out o = lane_out<C>(L, ob, MJ_SLOT(C));                                               \
             _Pragma("unroll") for (uint32_t k = 0; k < R; k++) {                                        \
                 const uint32_t i = rbase + k * 64 + lane;                                               \
                 bool valid = (W.vb[k][C / 32] >> (C % 32)) & 1u;                                        \
@@ -914,12 +1001,12 @@ DEV void decode_tile(const Src& src, const Tile& T, const LAS uint32_t* ro, LAS 
                 stash<C>(vlo[k], vhi[k], (W.vb[k][C / 32] >> (C % 32)) & 1u);                           \
                 if constexpr (W_ == 9) {                                                                \
                     stash<C>(blo[k], bhi[k], lo != 0);                                                  \
-                } else if (i < T.nr) {                                                                  \
+                } else if (i < T.nr && !MJ_ABL_NOFIX) {                                                 \
                     const uint64_t row = T.r0 + i;                                                      \
-                    if constexpr (W_ == 8) gp((uint64_t*)o.values)[row] = ((uint64_t)hi << 32) | lo;    \
-                    else if constexpr (W_ == 4) gp((uint32_t*)o.values)[row] = lo;                      \
-                    else if constexpr (W_ == 2) gp((uint16_t*)o.values)[row] = (uint16_t)lo;            \
-                    else gp((uint8_t*)o.values)[row] = (uint8_t)lo;                                     \
+                    if constexpr (W_ == 8) ost(gp((uint64_t*)o.values) + row, ((uint64_t)hi << 32) | lo); \
+                    else if constexpr (W_ == 4) ost(gp((uint32_t*)o.values) + row, lo);                 \
+                    else if constexpr (W_ == 2) ost(gp((uint16_t*)o.values) + row, (uint16_t)lo);       \
+                    else ost(gp((uint8_t*)o.values) + row, (uint8_t)lo);                                \
                 }                                                                                       \
             }                                                                                           \
         }                                                                                               \
@@ -1017,9 +1104,9 @@ DEV void decode_tile(const Src& src, const Tile& T, const LAS uint32_t* ro, LAS 
     // ---- offsets and string bytes (utf8.rs:86-96 append_value)
 #define MJ_E(C, W_, FO, U)                                                                              \
     if constexpr (W_ == 0 && PH != 1) {                                                                 \
-        if (slot_of(C) != kNone) {                                                                      \
-            const uint32_t P = slot_of(C);                                                              \
-            const Out o = ldout(ob, P);                                                                 \
+        if (MJ_SLOT(C) != kNone) {                                                                      \
+            const uint32_t P = MJ_SLOT(C);                                                              \
+            const Out o = lane_out<C>(L, ob, P);                                                        \
             const uint64_t base = tile_pre[U] + before[U];                                              \
             if (T.first && wave == 0 && lane == 0) gp(o.offsets)[0] = 0;                                \
             if (T.last && wave == 0 && lane == 0)                                                       \
@@ -1030,11 +1117,11 @@ DEV void decode_tile(const Src& src, const Tile& T, const LAS uint32_t* ro, LAS 
                 const bool act = i < T.nr;                                                              \
                 const uint32_t n = ulen[U][k];                                                          \
                 const uint64_t e = base + uinc[U][k];                                                   \
-                const uint64_t cend = base + __builtin_amdgcn_readlane(uinc[U][k], 63);                 \
+                const uint64_t cend = base + (uint32_t)__builtin_amdgcn_readlane(uinc[U][k], 63);                 \
                 uint32_t hib = 0;                                                                       \
                 if (cend <= 0x7FFFFFFFull && cend <= o.values_cap) { /* wave-uniform fast path */       \
-                    if (act) obf[i] = (int32_t)e;                                                       \
-                    if (n) hib = copy_str(src, gp(o.values) + (e - n), upay[U][k], n);                  \
+                    if (act) ost(obf + i, (int32_t)e);                                                  \
+                    if (n && !MJ_ABL_NOSTR) hib = copy_str(src, gp(o.values) + (e - n), upay[U][k], n); \
                 } else {                                                                                \
                     if (act) {                                                                          \
                         if (e > 0x7FFFFFFFull) report(err, err_key(T.b, T.r0 + i, P, kStOverflow));     \
@@ -1050,6 +1137,7 @@ DEV void decode_tile(const Src& src, const Tile& T, const LAS uint32_t* ro, LAS 
     }
     MJ_COLS(MJ_E)
 #undef MJ_E
+#undef MJ_SLOT
 }
 
 // ---- kernel body ---------------------------------------------------------------------
@@ -1205,8 +1293,15 @@ DEV void kernel_body() {
 
 }  // namespace mj
 
+// Local-mode kernels may ask the compiler for a register budget that admits
+// MJ_WPE waves per SIMD (SGPRs: 7 waves at <= 96, 8 at <= 80; tuning).
+#if defined(MJ_WPE) && MJ_WPE
+#define MJ_WPE_ATTR __attribute__((amdgpu_waves_per_eu(MJ_WPE)))
+#else
+#define MJ_WPE_ATTR
+#endif
 #define MJ_KERNEL(NW, R, NS, SFX)                                                                         \
-    extern "C" __global__ void __launch_bounds__(64 * NW) murr_jit_decode_##NW##x##R##SFX(mj::Args) {      \
+    extern "C" __global__ void __launch_bounds__(64 * NW) MJ_WPE_ATTR murr_jit_decode_##NW##x##R##SFX(mj::Args) { \
         mj::kernel_body<NW, R, NS, 0>();                                                                   \
     }                                                                                                      \
     extern "C" __global__ void __launch_bounds__(64 * NW) murr_jit_decode_split_##NW##x##R##SFX(mj::Args) {\
