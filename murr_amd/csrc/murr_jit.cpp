@@ -143,6 +143,23 @@ void evict() {
     }
 }
 
+// tuning: MURR_JIT_DEFS="NAME=VALUE,..." extra #defines (ablation builds of
+// the decode and encode kernels)
+void tuning_defs(std::ostringstream& o) {
+    if (const char* e = std::getenv("MURR_JIT_DEFS")) {
+        std::string d(e);
+        size_t pos = 0;
+        while (pos < d.size()) {
+            size_t end = d.find(',', pos);
+            if (end == std::string::npos) end = d.size();
+            std::string kv = d.substr(pos, end - pos);
+            const size_t eq = kv.find('=');
+            if (!kv.empty()) o << "#define " << (eq == std::string::npos ? kv : kv.substr(0, eq) + " " + kv.substr(eq + 1)) << "\n";
+            pos = end + 1;
+        }
+    }
+}
+
 // Prelude: the segment layout (src/io/schema.rs:23-54), nothing of the
 // projection.  MJ_COLS(X) lists every column as X(index, width, row offset of
 // its field, utf8 ordinal); width 0 = utf8 slot, 9 = bool byte.
@@ -159,19 +176,7 @@ std::string prelude(const murr_segment_t* seg) {
           << (w == 0 ? u++ : 0u) << ")";
     }
     o << "\n";
-    // tuning: MURR_JIT_DEFS="NAME=VALUE,..." extra #defines (ablation builds)
-    if (const char* e = std::getenv("MURR_JIT_DEFS")) {
-        std::string d(e);
-        size_t pos = 0;
-        while (pos < d.size()) {
-            size_t end = d.find(',', pos);
-            if (end == std::string::npos) end = d.size();
-            std::string kv = d.substr(pos, end - pos);
-            const size_t eq = kv.find('=');
-            if (!kv.empty()) o << "#define " << (eq == std::string::npos ? kv : kv.substr(0, eq) + " " + kv.substr(eq + 1)) << "\n";
-            pos = end + 1;
-        }
-    }
+    tuning_defs(o);
     return o.str();
 }
 
@@ -274,6 +279,7 @@ std::string enc_prelude(uint32_t bs, uint32_t cap, const EncCol* cols, uint32_t 
         o << " X(" << c << ", " << kind << ", " << cols[c].soff << ", " << (kind == 0 ? u++ : 0u) << ")";
     }
     o << "\n";
+    tuning_defs(o);
     return o.str();
 }
 

@@ -77,6 +77,7 @@ DEV void report(unsigned long long* err, uint64_t key) {
     __hip_atomic_fetch_max((GAS unsigned long long*)err, (unsigned long long)~key, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
 }
+DEV uint32_t umin(uint32_t a, uint32_t b) { return a < b ? a : b; }
 template <class T> DEV GAS T* gp(T* p) { return (GAS T*)p; }
 template <class T> DEV const GAS T* gp(const T* p) { return (const GAS T*)p; }
 
@@ -275,9 +276,81 @@ DEV void put_payload(const RowBuild& B, LAS uint32_t* stw, uint32_t rb, uint32_t
     p += n;
 }
 
+// The bytes of one row written to the stage in order, as whole dwords: the
+// dwords wholly inside the row are plain LDS stores; the first (when the row
+// starts mid-dword) and the last partial one are shared with the neighbouring
+// rows and are OR-merged into the zeroed stage.
+#ifndef MJE_STREAM
+#define MJE_STREAM 1
+#endif
+struct Emit {
+    LAS uint32_t* stw;
+    uint32_t d, d0, sh;  // next stage dword, the row's first dword, its byte offset in it
+    uint64_t acc;        // pending bytes, lowest first
+    uint32_t nb;         // how many (< 4 between puts)
+    DEV void start(LAS uint32_t* s, uint32_t rb) {
+        stw = s;
+        d = d0 = rb >> 2;
+        sh = rb & 3u;
+        acc = 0;
+        nb = sh;  // the first dword's leading bytes are the previous row's (zero here)
+    }
+    DEV void emit(uint32_t w) {
+        if (d == d0 && sh) __hip_atomic_fetch_or(stw + d, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        else stw[d] = w;
+        d++;
+    }
+    DEV void put(uint32_t v, uint32_t m) {  // the low m (1..4) bytes of v
+        if (m < 4) v &= (1u << (8 * m)) - 1u;
+        acc |= (uint64_t)v << (8 * nb);
+        nb += m;
+        if (nb >= 4) {
+            emit((uint32_t)acc);
+            acc >>= 32;
+            nb -= 4;
+        }
+    }
+    DEV void finish() {
+        if (nb) __hip_atomic_fetch_or(stw + d, (uint32_t)acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+};
+
+// Utf8 payload of column C into the emitter: u32 len, then the string in
+// 4-byte chunks realigned from the aligned dwords that cover it (dwords past
+// the string are never loaded; they read as 0).
+template <uint32_t C, uint32_t U> DEV void emit_payload(const RowBuild& B, Emit& E) {
+    if (!((B.vmask[C / 32] >> (C % 32)) & 1)) return;
+    const uint32_t n = B.ulen[U];
+    E.put(n, 4);
+    const Col c = ldcol(C);
+    const uintptr_t sa_ptr = (uintptr_t)(gp(c.values) + B.ustart[U]);
+    const uint32_t sa = (uint32_t)(sa_ptr & 3);
+    const GAS uint32_t* w = (const GAS uint32_t*)(sa_ptr - sa);
+    // chunk q = string bytes [4q, 4q + 4) = alignbyte(w[q + 1], w[q], sa)
+#pragma unroll
+    for (uint32_t q = 0; q + 1 < PF; q++)
+        if (4 * q < n) E.put(__builtin_amdgcn_alignbyte(B.pre[U][q + 1], B.pre[U][q], sa), umin(4u, n - 4 * q));
+    uint32_t cur = B.pre[U][PF - 1];
+    for (uint32_t q = PF - 1; 4 * q < n; q += 4) {
+        uint32_t x[4];
+#pragma unroll
+        for (uint32_t k = 0; k < 4; k++) x[k] = 4 * (q + 1 + k) < n + sa ? w[q + 1 + k] : 0u;
+#pragma unroll
+        for (uint32_t k = 0; k < 4; k++)
+            if (4 * (q + k) < n) E.put(__builtin_amdgcn_alignbyte(x[k], k ? x[k - 1] : cur, sa), umin(4u, n - 4 * (q + k)));
+        cur = x[3];
+    }
+}
+
 }  // namespace mje
 
-extern "C" __global__ void __launch_bounds__(256) murr_jit_encode(mje::Args) {
+// MJE_WPE (tuning): a register budget admitting that many waves per SIMD.
+#if defined(MJE_WPE) && MJE_WPE
+#define MJE_WPE_ATTR __attribute__((amdgpu_waves_per_eu(MJE_WPE)))
+#else
+#define MJE_WPE_ATTR
+#endif
+extern "C" __global__ void __launch_bounds__(256) MJE_WPE_ATTR murr_jit_encode(mje::Args) {
     using namespace mje;
     __shared__ __attribute__((aligned(16))) uint32_t stage[STAGE / 4 + 8];
     __shared__ uint64_t s_w[8];
@@ -341,6 +414,18 @@ extern "C" __global__ void __launch_bounds__(256) murr_jit_encode(mje::Args) {
             // zero the stage, merge the rows, write it out
             for (uint32_t k = tid; k < (uint32_t)((span + 7) >> 2) + 1; k += TILE) stw[k] = 0;
             __syncthreads();
+#if MJE_STREAM
+            if (active && NUTF8) {
+                Emit E;
+                E.start(stw, (uint32_t)(start - tstart));
+#pragma unroll
+                for (uint32_t k = 0; k < NR; k++) E.put(B.r.w[k], k + 1 < NR ? 4u : FIXED - 4 * (NR - 1));
+#define MJE_DO_EMIT(C, KIND, SOFF, U) if (KIND == 0) emit_payload<C, U>(B, E);
+                MJE_COLS(MJE_DO_EMIT)
+#undef MJE_DO_EMIT
+                E.finish();
+            } else
+#endif
             if (active) {
                 const uint32_t rb = (uint32_t)(start - tstart), sh = rb & 3u, d0 = rb >> 2;
 #pragma unroll
@@ -425,18 +510,27 @@ DEV bool sizes_inline() {
 #undef MJE_NOVAL
     return ok;
 }
-DEV uint64_t tile_bytes_inline(uint64_t t) {
-    const uint64_t r0 = t * TILE, nr = min((uint64_t)TILE, args()->n_rows - r0);
-    uint64_t b = nr * (FIXED + 4 * NUTF8);
+// Totals of the N consecutive tiles t0 .. t0 + N - 1 (those below hi); each
+// column's descriptor is read once, every offset load issued together.
+template <uint32_t N> DEV void tile_bytes_inline(uint64_t t0, uint64_t hi, uint64_t (&x)[N]) {
+    const uint64_t n_rows = args()->n_rows;
+    uint64_t nr[N];
+#pragma unroll
+    for (uint32_t q = 0; q < N; q++) {
+        const uint64_t r0 = (t0 + q) * TILE;
+        nr[q] = t0 + q < hi ? min((uint64_t)TILE, n_rows - r0) : 0;
+        x[q] = nr[q] * (FIXED + 4 * NUTF8);
+    }
 #define MJE_TB(C, KIND, SOFF, U)                                                            \
     if (KIND == 0) {                                                                        \
         const Col c = ldcol(C);                                                             \
-        const uint64_t e = c.offset + r0;                                                   \
-        b += (uint64_t)(int64_t)(gp(c.offsets)[e + nr] - gp(c.offsets)[e]);                 \
+        _Pragma("unroll") for (uint32_t q = 0; q < N; q++) {                                \
+            const uint64_t e = c.offset + (t0 + q) * TILE;                                  \
+            if (nr[q]) x[q] += (uint64_t)(int64_t)(gp(c.offsets)[e + nr[q]] - gp(c.offsets)[e]); \
+        }                                                                                   \
     }
     MJE_COLS(MJE_TB)
 #undef MJE_TB
-    return b;
 }
 }  // namespace mje
 
@@ -487,14 +581,22 @@ extern "C" __global__ void __launch_bounds__(1024) murr_jit_encode_scan(mje::Arg
     }
     const uint64_t g = blockIdx.x, lo = g * SCAN_PER, hi = min(T, lo + SCAN_PER);
     constexpr uint32_t PER = SCAN_PER / 1024;  // 4 per thread, contiguous
-    const bool inl = sizes_inline();
     uint64_t x[PER], s = 0;
+    if (pass == 0 && sizes_inline()) {
+        // tile totals from the offsets (no sizes pass), kept for pass 1
+        tile_bytes_inline<PER>(lo + tid * PER, hi, x);
 #pragma unroll
-    for (uint32_t q = 0; q < PER; q++) {
-        const uint64_t j = lo + tid * PER + q;
-        x[q] = j < hi ? (inl ? tile_bytes_inline(j) : v[j]) : 0;
-        s += x[q];
+        for (uint32_t q = 0; q < PER; q++)
+            if (lo + tid * PER + q < hi) v[lo + tid * PER + q] = x[q];
+    } else {
+#pragma unroll
+        for (uint32_t q = 0; q < PER; q++) {
+            const uint64_t j = lo + tid * PER + q;
+            x[q] = j < hi ? v[j] : 0;
+        }
     }
+#pragma unroll
+    for (uint32_t q = 0; q < PER; q++) s += x[q];
     uint64_t tot;
     const uint64_t ex = block_excl(s, (LAS uint64_t*)s_t, &tot);
     if (pass == 0) {
