@@ -102,6 +102,29 @@ def test_random_all_dtypes_vs_oracle(ctx, seed, n):
         check_padding(got[p], n)
 
 
+@pytest.mark.parametrize("max_str,null_p", [(1, 0.0), (3, 0.3), (6, 0.0), (8, 0.1), (8, 0.0), (11, 0.2)])
+@pytest.mark.parametrize("n", [1, 7, 64, 129, 3001])
+def test_short_strings_packed_stores(ctx, max_str, null_p, n):
+    """Short strings (the overlapping head/tail stores of copy_str for 1-8
+    bytes; max_str 11 mixes in the 8-byte-step path), nulls and missing rows,
+    duplicate projections, several blocks in one launch so chunk edges fall at
+    every alignment of the output buffer."""
+    rng = np.random.default_rng(1000 * max_str + n)
+    dtypes = [D.Utf8, D.Int8, D.Utf8]
+    blocks, want = [], []
+    for b in range(3):
+        cols = random_columns(rng, dtypes, n, null_p=null_p, max_str=max_str, unicode=max_str >= 3)
+        missing = set(rng.choice(n, size=n // 7, replace=False).tolist()) if n > 7 else set()
+        oseg, data, off = oracle_block(dtypes, cols, n, missing)
+        blocks.append((data, off))
+        want.append(O.decode_block(oseg, [2, 0, 1, 0], data, off))
+    got = gpu_decode(ctx, seg_of(dtypes), [2, 0, 1, 0], blocks)
+    for b in range(3):
+        for p in range(4):
+            assert_array_equal(got[b][p], want[b][p], f"block {b} proj {p}")
+            check_padding(got[b][p], n)
+
+
 def test_long_strings_take_the_hbm_path(ctx):
     # tiles whose blob span exceeds the 32 KiB LDS stage read HBM directly
     rng = np.random.default_rng(11)
