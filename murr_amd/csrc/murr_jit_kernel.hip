@@ -352,6 +352,7 @@ struct TileInfo {
 struct Cur {
     const uint8_t* data;
     const uint64_t* row_off;
+    const uint64_t* uidx;
     uint64_t n_rows, r0, r_begin, r_end;
     uint32_t k, b, first, phase, ok;
 };
@@ -371,6 +372,7 @@ DEV Cur cur_make(uint32_t ok, uint32_t k, uint32_t b, uint32_t first, uint32_t p
     c.data = ok ? (const uint8_t*)sgpr64((uint64_t)bp->data) : nullptr;
     c.row_off = ok ? (const uint64_t*)sgpr64((uint64_t)bp->row_off) : nullptr;
     c.n_rows = ok ? sgpr64(bp->n_rows) : 0;
+    c.uidx = ok ? (const uint64_t*)sgpr64((uint64_t)bp->uidx) : nullptr;
     c.r_begin = r_begin;
     c.r_end = ok && r_end == ~0ull ? c.n_rows : r_end;
     return c;
@@ -415,8 +417,21 @@ template <uint32_t TR> DEV uint32_t cur_nr(const Cur& c) { return (uint32_t)umin
 
 // The loader publishes tile i's identity (ring entry i & 7, lane 0) and
 // fetches its span (row_off[r0], row_off[r0 + nr]) by LDS-DMA (lanes 0-3).
+// Local mode: the utf8 index entry that starts a (virtual) block, fetched by
+// the loader with the tile's announcement into a ring beside the tile ring
+// (the prefetch scratch), so the decode waves read it from LDS instead of two
+// dependent scalar loads at the block's first tile.
+#ifndef MJ_PREFETCH
+#define MJ_PREFETCH 0
+#endif
+#if MJ_PREFETCH || MJ_NUTF8 == 0 || MJ_NUTF8 > 16
+constexpr bool UPRE = false;
+#else
+constexpr bool UPRE = true;
+#endif
 template <uint32_t TR>
-DEV uint32_t tile_announce(const Cur& c, LAS uint8_t* span_ent, LAS uint8_t* info_ent, uint32_t lane) {
+DEV uint32_t tile_announce(const Cur& c, LAS uint8_t* span_ent, LAS uint8_t* info_ent, uint32_t lane,
+                           LAS uint8_t* upre_ent) {
     if (lane == 0) {
         LAS TileInfo* ti = (LAS TileInfo*)info_ent;
         if (c.ok) {
@@ -436,6 +451,13 @@ DEV uint32_t tile_announce(const Cur& c, LAS uint8_t* span_ent, LAS uint8_t* inf
     if (lane < 4) {
         const uint64_t r = c.r0 + (lane < 2 ? 0u : cur_nr<TR>(c));
         glds4((const GAS uint8_t*)(c.row_off + r) + (lane & 1) * 4, span_ent);
+    }
+    if constexpr (UPRE) {
+        if (c.phase == 0 && c.r0 == c.r_begin && c.r0 != 0 && c.uidx) {
+            const GAS uint32_t* ux = (const GAS uint32_t*)(c.uidx + (c.r0 >> args()->ulog) * NU);
+            if (lane < 2 * NU) glds4(ux + lane, upre_ent);
+            return 2;
+        }
     }
     return 1;
 }
@@ -1168,7 +1190,7 @@ DEV void kernel_body() {
         Cur cs = cur_first<MODE>();  // next tile to announce
 #pragma unroll
         for (uint32_t k = 0; k <= NSLOT + 1; k++) {
-            tile_announce<TR>(cs, spans + (k & 7) * 16, infos + (k & 7) * 32, lane);
+            tile_announce<TR>(cs, spans + (k & 7) * 16, infos + (k & 7) * 32, lane, pf + (k & 7) * 8 * NU);
             cs = cur_next<TR>(cs);
         }
 #ifdef MJ_STAMPS
@@ -1202,7 +1224,8 @@ DEV void kernel_body() {
             if (tile_valid(infos + (t2 & 7) * 32))
                 np = tile_prefetch(tile_read(spans + (t2 & 7) * 16, infos + (t2 & 7) * 32, stage), pf, lane);
 #endif
-            const uint32_t ns = tile_announce<TR>(cs, spans + (k & 7) * 16, infos + (k & 7) * 32, lane) + np;
+            const uint32_t ns = tile_announce<TR>(cs, spans + (k & 7) * 16, infos + (k & 7) * 32, lane,
+                                                  pf + (k & 7) * 8 * NU) + np;
             cs = cur_next<TR>(cs);
 #ifdef MJ_STAMPS
             const uint64_t w0 = __builtin_amdgcn_s_memtime();
@@ -1246,11 +1269,18 @@ DEV void kernel_body() {
         const LAS uint32_t* ro = (const LAS uint32_t*)slot;
         const uint32_t ph = tile_phase(info);
         if (MODE == 0 && T.seg_first) {
-            // local mode: a (virtual) block starts at 0, or at its utf8 index entry
-            const uint64_t* ux = (const uint64_t*)sgpr64((uint64_t)((const CAS Blk*)args()->blocks + T.b)->uidx);
+            // local mode: a (virtual) block starts at 0, or at its utf8 index
+            // entry (in LDS, fetched by the loader with the announcement)
+            if constexpr (UPRE) {
+                const LAS uint64_t* up = (const LAS uint64_t*)(pf + (it & 7) * 8 * NU);
 #pragma unroll
-            for (uint32_t u = 0; u < NU; u++)
-                run[u] = NUTF8 && T.r0 ? sgpr64(((const CAS uint64_t*)ux)[(T.r0 >> args()->ulog) * NU + u]) : 0;
+                for (uint32_t u = 0; u < NU; u++) run[u] = T.r0 ? sgpr64(up[u]) : 0;
+            } else {
+                const uint64_t* ux = (const uint64_t*)sgpr64((uint64_t)((const CAS Blk*)args()->blocks + T.b)->uidx);
+#pragma unroll
+                for (uint32_t u = 0; u < NU; u++)
+                    run[u] = NUTF8 && T.r0 ? sgpr64(((const CAS uint64_t*)ux)[(T.r0 >> args()->ulog) * NU + u]) : 0;
+            }
         }
         if (T.hbm == 2) {  // a tile over 4 GiB of blob bytes (unsupported): report; keep the protocol going
             if (wave == 0 && lane == 0) report(args()->err, err_key(T.b, T.r0, 0, kStMalformed));
