@@ -40,4 +40,8 @@ if [ -z "${QUICK:-}" ]; then
   run resident_1000 300 python3 bench.py --mode resident --keys 1000 --steps 30 --warmup 5
   run resident_read_plain 300 python3 bench.py --mode resident --table ref --rows 10000000 --keys 1000 --steps 200 --warmup 20 --ipc
   run resident_read_block 400 python3 bench.py --mode resident --table ref --rows 100000000 --keys 1000 --steps 200 --warmup 20
+  # one-block config D at 2x / 4x the shard: fixed cost per launch (fit over rows)
+  run decode_D1x2 300 python3 bench.py --config D --rows 2500000 --steps 10 --warmup 2 --no-cpu
+  run decode_D1x4 300 python3 bench.py --config D --rows 5000000 --steps 10 --warmup 2 --no-cpu
+  run encode_prof 300 bash tools/enc_prof.sh
 fi
