@@ -595,11 +595,13 @@ int decode_enqueue_jit(murr_ctx* c, const murr_segment_t* seg, const JitLayout* 
     uint32_t nu_layout = 0;
     for (uint32_t i = 0; i < seg->ncols; i++) nu_layout += seg->cols[i].dtype == MURR_UTF8;
     const uint32_t nu = std::max<uint32_t>(nu_layout, 1);
-    // Shape: 5 waves x 2 chunks (512 rows) when its two LDS slots fit 40 KiB
-    // with 15 % slack over the mean row (four workgroups per CU); else 3 x 1
-    // (128 rows) when that fits 40 KiB with 8 % slack (four or five per CU:
-    // config C 0.51 -> 0.54 against 5 x 1 at two per CU); else 5 x 1 (256
-    // rows) within 64 KiB; else 3 x 1.
+    // Shape: 5 waves x 3 chunks (768 rows) when its two LDS slots fit 40 KiB
+    // with 15 % slack over the mean row (four workgroups per CU; config B 0.62
+    // -> 0.65 against 5 x 2: the per-tile overheads spread over more rows);
+    // else 5 x 2 (512 rows) within the same 40 KiB; else 3 x 1 (128 rows)
+    // when that fits 40 KiB with 8 % slack (four or five per CU: config C
+    // 0.51 -> 0.54 against 5 x 1 at two per CU); else 5 x 1 (256 rows) within
+    // 64 KiB; else 3 x 1.
     auto lds_for = [&](uint32_t s, double slack) {
         const JitShapeK& k = jl->shapes[s];
         const uint32_t st = (uint32_t)round_up((uint64_t)(k.tr * est_row * slack) + 64, 1024);
@@ -608,7 +610,8 @@ int decode_enqueue_jit(murr_ctx* c, const murr_segment_t* seg, const JitLayout* 
     uint32_t si = 2;
     double slack = 1.08;
     uint32_t budget = 65536;
-    if (lds_for(0, 1.15) <= 40960) { si = 0; slack = 1.15; budget = 40960; }
+    if (lds_for(3, 1.15) <= 40960) { si = 3; slack = 1.15; budget = 40960; }
+    else if (lds_for(0, 1.15) <= 40960) { si = 0; slack = 1.15; budget = 40960; }
     else if (lds_for(2, 1.08) <= 40960) { si = 2; budget = 40960; }
     else if (lds_for(1, 1.08) <= 65536) si = 1;
     if (const char* e = std::getenv("MURR_JIT_SHAPE")) {  // tuning: "NWxR" or "NWxRs3"

@@ -103,10 +103,11 @@ __host__ __device__ inline uint64_t err_key(uint64_t block, uint64_t row, uint32
 // Layout-specialised decode kernel (murr_jit.cpp, murr_jit_kernel.hip): one
 // module per segment layout holds every tile shape; the projection is a
 // kernel argument.
-constexpr uint32_t kJitShapes = 3;
+constexpr uint32_t kJitShapes = 4;
 // waves x 64-row chunks per decode wave x LDS ring slots (murr_jit_kernel.hip
-// MJ_KERNEL instantiates each; a 3-slot ring measured no faster on B or C)
-constexpr uint32_t kJitShapeTab[kJitShapes][3] = {{5, 2, 2}, {5, 1, 2}, {3, 1, 2}};
+// MJ_KERNEL instantiates each; a 3-slot ring measured no faster on B or C;
+// 5x4 and 7x2 measured slower on B than 5x3)
+constexpr uint32_t kJitShapeTab[kJitShapes][3] = {{5, 2, 2}, {5, 1, 2}, {3, 1, 2}, {5, 3, 2}};
 struct JitShapeK {
     hipFunction_t fn = nullptr, fn_split = nullptr;  // local / split mode kernels
     uint32_t nw = 0, r = 0, tr = 0;  // waves (nw-1 decode, 1 loads), chunks per decode wave, rows per tile

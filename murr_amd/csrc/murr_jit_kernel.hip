@@ -1340,3 +1340,4 @@ DEV void kernel_body() {
 MJ_KERNEL(5, 2, 2, )
 MJ_KERNEL(5, 1, 2, )
 MJ_KERNEL(3, 1, 2, )
+MJ_KERNEL(5, 3, 2, )

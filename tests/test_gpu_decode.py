@@ -227,8 +227,8 @@ def test_many_blocks_one_launch(ctx, kernel_mode, nblocks):
 
 
 @pytest.mark.parametrize("mode,shape,segtiles", [("split", "5x2", 0), ("split", "5x1", 0), ("split", "3x1", 0),
-                                                 ("split", "5x2", 1), ("split", "3x1", 2),
-                                                 ("local", "5x2", 0), ("local", "3x1", 0)])
+                                                 ("split", "5x3", 0), ("split", "5x2", 1), ("split", "3x1", 2),
+                                                 ("local", "5x2", 0), ("local", "3x1", 0), ("local", "5x3", 0)])
 def test_split_blocks_utf8_prefix(ctx, kernel_mode, monkeypatch, mode, shape, segtiles):
     # few large blocks: in split mode the JIT kernel cuts them into segments
     # (two passes each) and each segment's utf8 starting offsets come from
