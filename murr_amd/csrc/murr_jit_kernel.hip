@@ -117,7 +117,8 @@ enum : uint32_t { kStUtf8 = 1, kStOverflow = 4, kStMalformed = 5, kStCapacity = 
 // summed over waves into err[2 + k] (murr_abi.cpp prints them with
 // MURR_DECODE_VERBOSE).  k: 0 decode-wave tile barrier, 1 wave-total wait,
 // 2 segment-prefix wait, 3 look-back, 4 first-pass tiles, 5 second-pass
-// tiles, 6 local tiles, 7 loader waits, 8 loader total, 9 decode-wave total.
+// tiles, 6 local tiles, 7 loader waits, 8 loader total, 9 decode-wave total,
+// 10 the loader's vmcnt waits (part of 7).
 #ifdef MJ_STAMPS
 #define MJ_TIC const uint64_t mj_t0_ = __builtin_amdgcn_s_memtime();
 #define MJ_TOC(k)                                                                                             \
@@ -1195,7 +1196,7 @@ DEV void kernel_body() {
         }
 #ifdef MJ_STAMPS
         const uint64_t lt0 = __builtin_amdgcn_s_memtime();
-        uint64_t lwait = 0;
+        uint64_t lwait = 0, lvm = 0;  // loader waits: all / the vmcnt part (slot 10)
 #endif
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
         // tiles 0 .. NSLOT - 2 into their slots; B_0 once tile 0 landed
@@ -1234,6 +1235,10 @@ DEV void kernel_body() {
             // an iteration ago, with `pend` ops behind it then (NSLOT 3)
             wait_vmcnt((NSLOT == 2 ? 0u : pend + nd) + ns);
             pend = ns;
+#ifdef MJ_STAMPS
+            const uint64_t w1 = __builtin_amdgcn_s_memtime();
+            lvm += w1 - w0;
+#endif
             lds_barrier();  // B_it+1: tile it+1 landed, tile it decoded
 #ifdef MJ_STAMPS
             lwait += __builtin_amdgcn_s_memtime() - w0;
@@ -1243,6 +1248,7 @@ DEV void kernel_body() {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (lane == 0) {
             __hip_atomic_fetch_add((GAS unsigned long long*)args()->err + 2 + 7, (unsigned long long)lwait, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_add((GAS unsigned long long*)args()->err + 2 + 10, (unsigned long long)lvm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_fetch_add((GAS unsigned long long*)args()->err + 2 + 8, (unsigned long long)(__builtin_amdgcn_s_memtime() - lt0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
 #endif
