@@ -125,6 +125,32 @@ def test_sliced_arrow_inputs(ctx):
     assert np.array_equal(off, woff) and blob.tobytes() == wblob.tobytes()
 
 
+def test_sliced_inputs_without_validity(ctx):
+    # no utf8 validity buffer: tile totals come from the offsets inside the
+    # scan (murr_jit_encode.hip sizes_inline), from a slice's offset
+    rng = np.random.default_rng(34)
+    dtypes = [D.Utf8, D.Float32, D.Utf8]
+    full = 3000
+    cols = random_columns(rng, dtypes, full, null_p=0.0)
+    k, n = 129, 2600
+    for c in cols:
+        assert c["validity"] is None
+        c["offset"] = k
+    blob, off = gpu_encode(ctx, dtypes, cols, n)
+    wblob, woff = O.encode_batch(O.Segment([int(d) for d in dtypes]), synth.oracle_cols(cols), n)
+    assert np.array_equal(off, woff) and blob.tobytes() == wblob.tobytes()
+
+
+def test_inline_tile_totals_over_several_scan_groups(ctx):
+    # 1.2 M rows = 4688 tiles: two 4096-tile scan groups on the inline path,
+    # and a ragged last tile
+    n = 1_200_000 + 77
+    cols = synth.config_b(n)
+    blob, off = gpu_encode(ctx, [D.Float32, D.Utf8], cols, n)
+    wblob, woff = O.encode_batch(O.Segment([int(D.Float32), int(D.Utf8)]), synth.oracle_cols(cols), n)
+    assert np.array_equal(off, woff) and blob.tobytes() == wblob.tobytes()
+
+
 def test_empty_batch(ctx):
     dtypes = [D.Utf8, D.Float32]
     cols = random_columns(np.random.default_rng(0), dtypes, 0)
