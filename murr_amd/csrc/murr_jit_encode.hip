@@ -98,6 +98,28 @@ DEV bool valid(const Col& c, uint64_t e) {
     if (!c.validity) return true;
     return (gp(c.validity)[e >> 3] >> (e & 7)) & 1;
 }
+// Bit (ew + lane) of an Arrow bitmap for the 64 rows of a wave (ew uniform):
+// three scalar dwords cover the wave's 64 bits, so the texture data path --
+// the encode's bound -- sees no load; a window that would
+// reach past the bitmap's bytes (nbytes = ceil((offset + n) / 8)) takes the
+// per-lane byte load.
+DEV bool bit_of_wave(const uint8_t* bm, uint64_t ew, uint32_t lane, uint64_t nbytes) {
+    const uint64_t d = ew >> 5;
+    if ((d + 3) * 4 <= nbytes) {
+        const CAS uint32_t* p = (const CAS uint32_t*)bm + d;
+        const uint32_t x0 = p[0], x1 = p[1], x2 = p[2];
+        const uint32_t sh = (uint32_t)ew & 31u;
+        const uint64_t lo = ((uint64_t)x1 << 32) | x0;
+        const uint64_t w = sh ? (lo >> sh) | ((uint64_t)x2 << (64 - sh)) : lo;
+        return (w >> lane) & 1;
+    }
+    const uint64_t e = ew + lane;
+    return (gp(bm)[e >> 3] >> (e & 7)) & 1;
+}
+DEV bool valid_wave(const Col& c, uint64_t ew, uint32_t lane, uint64_t nbytes) {
+    if (!c.validity) return true;
+    return bit_of_wave(c.validity, ew, lane, nbytes);
+}
 
 // The fixed part of one row as dwords, byte placement at compile time.
 struct Row {
@@ -177,11 +199,19 @@ struct RowBuild {
     uint32_t pre[NUTF8 ? NUTF8 : 1][PF];  // its first PF aligned dwords
 };
 
+// rw: the wave's first row (uniform); row = rw + lane for the active lanes
 template <uint32_t C, uint32_t KIND, uint32_t SOFF, uint32_t U>
-DEV void build_col(RowBuild& B, uint64_t row) {
+DEV void build_col(RowBuild& B, uint64_t row, uint64_t rw, uint32_t lane) {
     const Col c = ldcol(C);
     const uint64_t e = c.offset + row;
-    const bool v = valid(c, e);
+    // the wave's first element and the bitmaps' byte length (used only with a
+    // validity buffer or for bool values)
+    auto wave_ew = [&]() {
+        return (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(c.offset + rw)) |
+               ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)((c.offset + rw) >> 32)) << 32);
+    };
+    auto bm_bytes = [&]() { return (c.offset + args()->n_rows + 7) >> 3; };
+    const bool v = c.validity ? bit_of_wave(c.validity, wave_ew(), lane, bm_bytes()) : true;
     B.vmask[C / 32] |= (uint32_t)v << (C % 32);
     constexpr uint32_t OFF = BS + SOFF;
     // Every load below is unconditional (in bounds for any row < n_rows) and
@@ -204,7 +234,7 @@ DEV void build_col(RowBuild& B, uint64_t row) {
 #pragma unroll
         for (uint32_t i = 0; i < PF; i++) B.pre[U][i] = i < nd ? w[i] : 0u;
     } else if constexpr (KIND == 9) {  // bool: b as u8 (bool_.rs:111-117)
-        const uint32_t b = (gp(c.values)[e >> 3] >> (e & 7)) & 1u;
+        const uint32_t b = bit_of_wave(c.values, wave_ew(), lane, bm_bytes());
         put8<OFF>(B.r, v ? b : 0u);
     } else if constexpr (KIND == 8) {
         const GAS uint32_t* p = (const GAS uint32_t*)(gp(c.values) + e * 8);
@@ -374,7 +404,7 @@ extern "C" __global__ void __launch_bounds__(256) MJE_WPE_ATTR murr_jit_encode(m
 #pragma unroll
         for (uint32_t k = 0; k < sizeof(B.vmask) / 4; k++) B.vmask[k] = 0;
         B.pos = FIXED;
-#define MJE_DO_COL(C, KIND, SOFF, U) build_col<C, KIND, SOFF, U>(B, row);
+#define MJE_DO_COL(C, KIND, SOFF, U) build_col<C, KIND, SOFF, U>(B, row, r0 + 64 * wave, lane);
         MJE_COLS(MJE_DO_COL)
 #undef MJE_DO_COL
         put_bitset(B);
@@ -485,7 +515,8 @@ extern "C" __global__ void __launch_bounds__(256) murr_jit_encode_sizes(mje::Arg
                 const Col c = ldcol(C);                                                      \
                 const uint64_t e = c.offset + row;                                           \
                 const uint32_t l = (uint32_t)(gp(c.offsets)[e + 1] - gp(c.offsets)[e]);      \
-                if (valid(c, e)) size += 4 + l;                                              \
+                const uint64_t ew = c.offset + t * TILE + 64 * wave;                         \
+                if (valid_wave(c, ew, lane, (c.offset + n_rows + 7) >> 3)) size += 4 + l;    \
             }
             MJE_COLS(MJE_DO_SIZE)
 #undef MJE_DO_SIZE
