@@ -489,9 +489,21 @@ DEV Tile tile_read(const LAS uint8_t* span_ent, const LAS uint8_t* info_ent, uin
     const uint64_t span = ((end + 15) & ~15ull) - T.abase;
     T.hbm = end < base || end - T.abase > 0xFFFFFF00ull ? 2u : span > stage ? 1u : 0u;
     T.span = T.hbm ? 0u : (uint32_t)span;
+    T.data = nullptr;
+    T.row_off = nullptr;
+    return T;
+}
+// The block's blob and row-offset pointers: the loader needs them for every
+// tile, the decode waves only for a tile decoded from HBM (two dependent
+// scalar loads kept off their per-tile path).
+DEV void tile_ptrs(Tile& T) {
     const CAS Blk* bp = (const CAS Blk*)args()->blocks + T.b;
     T.data = (const uint8_t*)sgpr64((uint64_t)bp->data);
     T.row_off = (const uint64_t*)sgpr64((uint64_t)bp->row_off);
+}
+DEV Tile tile_read_ptrs(const LAS uint8_t* span_ent, const LAS uint8_t* info_ent, uint32_t stage) {
+    Tile T = tile_read(span_ent, info_ent, stage);
+    tile_ptrs(T);
     return T;
 }
 DEV uint32_t tile_valid(const LAS uint8_t* info_ent) { return sgpr(((const LAS TileInfo*)info_ent)->flags) & 4u; }
@@ -1205,7 +1217,7 @@ DEV void kernel_body() {
         for (uint32_t j = 0; j + 1 < NSLOT; j++) {
             uint32_t n = 0;
             if (tile_valid(infos + j * 32))
-                n = tile_dma<TR, SH::RO_BYTES>(tile_read(spans + j * 16, infos + j * 32, stage), lds + j * SLOT, lane);
+                n = tile_dma<TR, SH::RO_BYTES>(tile_read_ptrs(spans + j * 16, infos + j * 32, stage), lds + j * SLOT, lane);
             after0 += j ? n : 0;
         }
         wait_vmcnt(after0);
@@ -1216,14 +1228,14 @@ DEV void kernel_body() {
             const uint32_t tn = it + NSLOT - 1, k = it + NSLOT + 2;
             uint32_t nd = 0;
             if (tile_valid(infos + (tn & 7) * 32))
-                nd = tile_dma<TR, SH::RO_BYTES>(tile_read(spans + (tn & 7) * 16, infos + (tn & 7) * 32, stage),
+                nd = tile_dma<TR, SH::RO_BYTES>(tile_read_ptrs(spans + (tn & 7) * 16, infos + (tn & 7) * 32, stage),
                                                 lds + (tn % NSLOT) * SLOT, lane);
             // tile it+2 into L2 (tuning: MJ_PREFETCH=1; measured slower on configs C/D)
             uint32_t np = 0;
 #if MJ_PREFETCH
             const uint32_t t2 = it + 2;
             if (tile_valid(infos + (t2 & 7) * 32))
-                np = tile_prefetch(tile_read(spans + (t2 & 7) * 16, infos + (t2 & 7) * 32, stage), pf, lane);
+                np = tile_prefetch(tile_read_ptrs(spans + (t2 & 7) * 16, infos + (t2 & 7) * 32, stage), pf, lane);
 #endif
             const uint32_t ns = tile_announce<TR>(cs, spans + (k & 7) * 16, infos + (k & 7) * 32, lane,
                                                   pf + (k & 7) * 8 * NU) + np;
@@ -1299,7 +1311,9 @@ DEV void kernel_body() {
                 }
             }
         } else if (T.hbm) {
-            const HbmSrc src{gp(T.data) + T.abase};
+            Tile Th = T;
+            tile_ptrs(Th);
+            const HbmSrc src{gp(Th.data) + Th.abase};
             if (MODE == 0) decode_tile<SH, 0>(src, T, ro, ctl, run, L, wave, lane, it);
             else if (ph == 1) decode_tile<SH, 1>(src, T, ro, ctl, run, L, wave, lane, it);
             else decode_tile<SH, 2>(src, T, ro, ctl, run, L, wave, lane, it);
