@@ -1213,8 +1213,9 @@ int murr_encode_batch_at(murr_ctx_t* c, const murr_segment_t* seg, const murr_co
     }
     if (n && !out_blob) return set_err(err, MURR_E_ARGUMENT);
     const uint64_t tiles = (n + kTile - 1) / kTile;
-    // utf8 layouts: tile totals / starts, then the 4096-tile group sums (JIT scan)
-    const uint64_t z_lb = 16, zbytes = round_up(z_lb + 8 * (nutf8 ? tiles + 1 + (tiles + 4095) / 4096 : 0), 16);
+    // utf8 layouts: tile totals / starts, then the group sums (JIT scan)
+    const uint64_t z_lb = 16,
+                   zbytes = round_up(z_lb + 8 * (nutf8 ? tiles + 1 + (tiles + kEncScanPer - 1) / kEncScanPer : 0), 16);
     const uint64_t d_cols = zbytes, dend = round_up(d_cols + sizeof(EncCol) * ec.size(), 16);
     int st = ensure_ws(c, dend, err);
     if (st) return st;

@@ -13,6 +13,10 @@ namespace murr {
 
 // Threads per encode workgroup (4 waves).
 constexpr uint32_t kTile = 256;
+// JIT encode scan: tiles per workgroup of its group passes (a multiple of
+// 1024; murr_jit_encode.hip MJE_SCAN_PER).  1024 spreads the pass that also
+// derives tile totals from the offsets over more CUs than 4096 did.
+constexpr uint32_t kEncScanPer = 1024;
 // Bytes of assembled rows an encode tile stages through LDS.  Tiles whose
 // byte span exceeds the stage read / write HBM directly (the "global" path).
 constexpr uint32_t kStage = 32768;

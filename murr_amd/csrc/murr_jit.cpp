@@ -273,7 +273,8 @@ std::string enc_prelude(uint32_t bs, uint32_t cap, const EncCol* cols, uint32_t 
     uint32_t nutf8 = 0;
     for (uint32_t c = 0; c < ncols; c++) nutf8 += cols[c].dtype == MURR_UTF8;
     o << "#define MJE_BS " << bs << "\n#define MJE_CAP " << cap << "\n#define MJE_NCOLS " << ncols
-      << "\n#define MJE_NUTF8 " << nutf8 << "\n#define MJE_STAGE " << stage << "\n#define MJE_COLS(X)";
+      << "\n#define MJE_NUTF8 " << nutf8 << "\n#define MJE_STAGE " << stage << "\n#define MJE_SCAN_PER " << kEncScanPer
+      << "\n#define MJE_COLS(X)";
     for (uint32_t c = 0, u = 0; c < ncols; c++) {
         const uint32_t kind = cols[c].dtype == MURR_UTF8 ? 0u : cols[c].dtype == MURR_BOOL ? 9u : cols[c].width;
         o << " X(" << c << ", " << kind << ", " << cols[c].soff << ", " << (kind == 0 ? u++ : 0u) << ")";
@@ -338,9 +339,9 @@ hipError_t jit_encode_launch(const JitEncKernel* k, const EncodeArgs& a, uint32_
     void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &args, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
     if (a.nutf8) {
         // tile starts: tile sums (a workgroup per tile), then their exclusive
-        // scan over 4096-tile groups (sums, one-workgroup scan of the sums, prefixes)
+        // scan over kEncScanPer-tile groups (sums, one-workgroup scan of the sums, prefixes)
         const uint32_t tiles = (uint32_t)std::min<uint64_t>(a.total_tiles, 0x7FFFFFFFull);
-        const uint32_t groups = (uint32_t)((a.total_tiles + 4095) / 4096);
+        const uint32_t groups = (uint32_t)((a.total_tiles + kEncScanPer - 1) / kEncScanPer);
         // (no utf8 column with a validity buffer: the scan derives the tile
         // totals from the offsets itself, murr_jit_encode.hip sizes_inline)
         hipError_t e = inline_sizes ? hipSuccess

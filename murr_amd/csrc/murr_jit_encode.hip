@@ -569,7 +569,11 @@ template <uint32_t N> DEV void tile_bytes_inline(uint64_t t0, uint64_t hi, uint6
 // kernel over contiguous ranges of SCAN_PER tiles per workgroup: pass 0 sums
 // each range into lookback[T + 1 + g]; pass 1 (after a one-workgroup scan of
 // those sums) rewrites each range as its exclusive prefix.
-constexpr uint32_t SCAN_PER = 4096;
+#ifndef MJE_SCAN_PER
+#define MJE_SCAN_PER 1024
+#endif
+constexpr uint32_t SCAN_PER = MJE_SCAN_PER;
+static_assert(SCAN_PER % 1024 == 0, "whole threads per tile group");
 DEV uint64_t block_excl(uint64_t x, LAS uint64_t* s_t, uint64_t* total) {
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     uint64_t inc = x;
@@ -598,7 +602,7 @@ extern "C" __global__ void __launch_bounds__(1024) murr_jit_encode_scan(mje::Arg
     const uint64_t T = A->total_tiles;
     GAS uint64_t* sums = v + T + 1;
     const uint64_t ngroups = (T + SCAN_PER - 1) / SCAN_PER;
-    if (pass == 2) {  // one workgroup: exclusive scan of the group sums (ngroups <= 1024 * 64)
+    if (pass == 2) {  // one workgroup: exclusive scan of the group sums, 1024 at a time
         uint64_t carry = 0;
         for (uint64_t g0 = 0; g0 < ngroups; g0 += 1024) {
             const uint64_t g = g0 + tid;
