@@ -31,7 +31,8 @@ sys.path.insert(0, ROOT)
 # Load the HIP library before torch so one HIP runtime serves the process.
 import murr_amd  # noqa: E402
 from murr_amd import _abi, synth  # noqa: E402
-from murr_amd.device import Context, DecodeOutputs, DeviceBlock, device_count, encode_batch  # noqa: E402
+from murr_amd.device import Context, DecodeOutputs, DeviceBlock, device_count, encode_batch, parse_opts, \
+    set_default_opts  # noqa: E402
 from murr_amd.schema import DTypeName as D, SegmentSchema  # noqa: E402
 from murr_amd.shard import Group, shard_rows  # noqa: E402
 
@@ -594,7 +595,11 @@ def main():
     ap.add_argument("--pmc-csv", default=None)
     ap.add_argument("--enc-config", default="E", choices=["B", "C", "E"], help="encode mode: column set")
     ap.add_argument("--proj", default=None, help="comma-separated projected columns (default all)")
+    ap.add_argument("--opts", default=None,
+                    help="kernel selection (murr_ctx_set_opts), e.g. shape=16x2,lds=163840,mode=local")
     args = ap.parse_args()
+    if args.opts:
+        set_default_opts(**parse_opts(args.opts))
     if args.rows is None:
         args.rows = {"A": 1000, "B": 100_000, "C": 1_000_000, "D": 1_250_000, "E": 20_000_000}[args.config]
         if args.mode == "encode":

@@ -130,6 +130,49 @@ int  murr_ctx_last_kernel_ms(murr_ctx_t* ctx, float* ms);
 const char* murr_ctx_last_kernel(murr_ctx_t* ctx);
 int  murr_device_count(int* n);
 
+/* Kernel selection of one context, for tests and benchmarks.  All zero (the
+ * state of a new context) = the library's own choice.  Set once; every later
+ * call on the context reads it.  A release build reads no environment
+ * variable on the decode / encode path. */
+typedef struct {
+    uint32_t kernel;        /* decode: 0 auto (layout-specialised, generic kernel if hiprtc
+                               cannot compile the layout), 1 specialised only (a compile
+                               failure is MURR_E_INTERNAL), 2 generic kernel */
+    uint32_t mode;          /* specialised decode: 0 auto, 1 local (workgroups own whole
+                               blocks), 2 split (segments + look-back), 3 local over blocks
+                               cut on their utf8 index whenever every block can be cut */
+    uint32_t shape_nw;      /* tile shape: waves per workgroup (0 = auto) ... */
+    uint32_t shape_r;       /* ... and 64-row chunks per decode wave */
+    uint32_t seg_tiles;     /* split mode: tiles per segment (0 = auto) */
+    uint32_t vrows;         /* cut blocks: rows per virtual block (0 = auto) */
+    uint32_t lds_budget;    /* LDS bytes per workgroup for the tile ring (0 = auto) */
+    uint32_t stage;         /* LDS stage bytes per ring slot (0 = auto) */
+    uint32_t encode_kernel; /* encode: 0 auto, 1 specialised only, 2 generic kernel */
+    uint32_t verbose;       /* 1: one line per decode launch on stderr */
+} murr_opts_t;
+int murr_ctx_set_opts(murr_ctx_t* ctx, const murr_opts_t* opts);
+int murr_ctx_get_opts(murr_ctx_t* ctx, murr_opts_t* opts);
+
+/* What the context's decodes did (counters since creation). */
+typedef struct {
+    uint64_t decodes;        /* decode launches (murr_decode_enqueue*, a retry not counted) */
+    uint64_t split_retries;  /* split-mode launches whose bounded look-back wait expired and
+                                that were re-run in local mode (0 on a healthy device) */
+    uint32_t last_mode;      /* last decode: 0 generic kernel, 1 local, 2 local over cut
+                                blocks, 3 split (after a retry: the retry's mode) */
+    uint32_t last_grid;      /* its workgroups */
+    uint32_t last_shape_nw;  /* its tile shape (specialised kernel) */
+    uint32_t last_shape_r;
+} murr_ctx_stats_t;
+int murr_ctx_stats(murr_ctx_t* ctx, murr_ctx_stats_t* out);
+
+/* The in-memory cache of compiled segment layouts (murr_segment_prepare,
+ * first decode of a layout): least recently used layouts beyond `max_layouts`
+ * (default 64; 0 = leave it) are retired, their code objects unloaded only
+ * after every launch that may use them has finished.  Reports the bound and
+ * the layouts held.  The on-disk cache is not affected. */
+int murr_jit_cache_limit(uint32_t max_layouts, uint32_t* limit, uint32_t* cached);
+
 int murr_dev_alloc(murr_ctx_t* ctx, uint64_t bytes, void** p);
 int murr_dev_free(murr_ctx_t* ctx, void* p);
 int murr_host_alloc(murr_ctx_t* ctx, uint64_t bytes, void** p); /* pinned */

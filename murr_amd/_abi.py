@@ -34,6 +34,17 @@ class Error(C.Structure):
                 ("column", C.c_uint32), ("row", C.c_uint64), ("required", C.c_uint64)]
 
 
+class Opts(C.Structure):
+    """murr_opts_t: kernel selection of one context (tests, benchmarks)."""
+    _fields_ = [(n, C.c_uint32) for n in ("kernel", "mode", "shape_nw", "shape_r", "seg_tiles", "vrows",
+                                          "lds_budget", "stage", "encode_kernel", "verbose")]
+
+
+class CtxStats(C.Structure):
+    _fields_ = [("decodes", C.c_uint64), ("split_retries", C.c_uint64), ("last_mode", C.c_uint32),
+                ("last_grid", C.c_uint32), ("last_shape_nw", C.c_uint32), ("last_shape_r", C.c_uint32)]
+
+
 class Block(C.Structure):
     _fields_ = [("data", C.c_void_p), ("row_off", C.c_void_p), ("n_rows", C.c_uint64),
                 ("data_bytes", C.c_uint64)]
@@ -85,6 +96,10 @@ SIGNATURES = {
     "murr_ctx_last_kernel_ms": (I32, [P, C.POINTER(C.c_float)]),
     "murr_ctx_last_kernel": (C.c_char_p, [P]),
     "murr_device_count": (I32, [C.POINTER(I32)]),
+    "murr_ctx_set_opts": (I32, [P, C.POINTER(Opts)]),
+    "murr_ctx_get_opts": (I32, [P, C.POINTER(Opts)]),
+    "murr_ctx_stats": (I32, [P, C.POINTER(CtxStats)]),
+    "murr_jit_cache_limit": (I32, [U32, C.POINTER(U32), C.POINTER(U32)]),
     "murr_dev_alloc": (I32, [P, U64, PP]),
     "murr_dev_free": (I32, [P, P]),
     "murr_host_alloc": (I32, [P, U64, PP]),

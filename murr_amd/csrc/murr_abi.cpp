@@ -80,6 +80,8 @@ struct murr_ctx {
     double r_est = 0;
     int pending_status = MURR_OK;
     const char* last_kernel = "";  // kernel of the last decode launch
+    murr_opts_t opts{};            // kernel selection (murr_ctx_set_opts)
+    murr_ctx_stats_t stats{};
     // Staging buffers of freed builders, reused by the next ones (a read builds
     // a ReadBatchBuilder per batch, src/io/row/read.rs:69-83; pinned and device
     // allocations cost far more than the batch itself).
@@ -154,6 +156,26 @@ int ensure_hs(murr_ctx* c, uint64_t bytes, murr_error_t* err) {
 }
 
 // Decode the packed device error word into murr_error_t.
+#ifdef MURR_TUNING
+// Tuning builds (make tuning): the MURR_* tuning variables of earlier rounds'
+// tools, read once per context.  Release builds never read them.
+void opts_from_env(murr_opts_t* o) {
+    auto num = [](const char* n, uint32_t* v) {
+        if (const char* e = std::getenv(n)) *v = (uint32_t)std::atoll(e);
+    };
+    if (const char* e = std::getenv("MURR_DECODE_JIT")) o->kernel = std::atoi(e) == 0 ? 2u : 1u;
+    if (const char* e = std::getenv("MURR_ENCODE_JIT")) o->encode_kernel = std::atoi(e) == 0 ? 2u : 1u;
+    if (const char* e = std::getenv("MURR_JIT_MODE")) o->mode = std::string(e) == "local" ? 1u : 2u;
+    if (std::getenv("MURR_JIT_CUT")) o->mode = 3;
+    if (const char* e = std::getenv("MURR_JIT_SHAPE")) std::sscanf(e, "%ux%u", &o->shape_nw, &o->shape_r);
+    num("MURR_JIT_SEGTILES", &o->seg_tiles);
+    num("MURR_JIT_VROWS", &o->vrows);
+    num("MURR_JIT_LDS", &o->lds_budget);
+    num("MURR_JIT_STAGE", &o->stage);
+    if (std::getenv("MURR_DECODE_VERBOSE")) o->verbose = 1;
+}
+#endif
+
 int unpack_err(unsigned long long word, murr_error_t* err) {
     if (!word) return MURR_OK;
     uint64_t key = ~(uint64_t)word;
@@ -419,6 +441,9 @@ int murr_ctx_create(int device, murr_ctx_t** out) {
     // Persistent grid: blocks that are certainly co-resident (one below the
     // occupancy answer: MI355X_MICROARCH.md "Residency"), at least one per CU.
     c->enc_grid_per_cu = std::max(1, std::min(8, encode_blocks_per_cu()) - 1);
+#ifdef MURR_TUNING
+    opts_from_env(&c->opts);  // tuning builds only: once, at creation
+#endif
     HIPC(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     HIPC(hipEventCreate(&c->k0));
     HIPC(hipEventCreate(&c->k1));
@@ -453,6 +478,32 @@ int murr_ctx_last_kernel_ms(murr_ctx_t* c, float* ms) {
 }
 
 const char* murr_ctx_last_kernel(murr_ctx_t* c) { return c ? c->last_kernel : ""; }
+
+int murr_ctx_set_opts(murr_ctx_t* c, const murr_opts_t* o) {
+    if (!c || !o || o->kernel > 2 || o->mode > 3 || o->encode_kernel > 2 || (!o->shape_nw) != (!o->shape_r))
+        return MURR_E_ARGUMENT;
+    c->opts = *o;
+    return MURR_OK;
+}
+
+int murr_ctx_get_opts(murr_ctx_t* c, murr_opts_t* o) {
+    if (!c || !o) return MURR_E_ARGUMENT;
+    *o = c->opts;
+    return MURR_OK;
+}
+
+int murr_jit_cache_limit(uint32_t max_layouts, uint32_t* limit, uint32_t* cached) {
+    const size_t l = jit_layout_limit(max_layouts);
+    if (limit) *limit = (uint32_t)l;
+    if (cached) *cached = (uint32_t)jit_layout_cached();
+    return MURR_OK;
+}
+
+int murr_ctx_stats(murr_ctx_t* c, murr_ctx_stats_t* out) {
+    if (!c || !out) return MURR_E_ARGUMENT;
+    *out = c->stats;
+    return MURR_OK;
+}
 
 int murr_dev_alloc(murr_ctx_t* c, uint64_t bytes, void** p) {
     murr_error_t* err = nullptr;
@@ -591,7 +642,8 @@ int decode_enqueue_jit(murr_ctx* c, const murr_segment_t* seg, const JitLayout* 
                        const std::vector<DecProj>& dp, double est_row, bool force_local = false,
                        const uint64_t* const* uidx = nullptr, uint32_t stride = 0) {
     murr_error_t* err = nullptr;
-    const bool verbose = std::getenv("MURR_DECODE_VERBOSE") != nullptr;
+    const murr_opts_t& O = c->opts;
+    const bool verbose = O.verbose != 0;
     uint32_t nu_layout = 0;
     for (uint32_t i = 0; i < seg->ncols; i++) nu_layout += seg->cols[i].dtype == MURR_UTF8;
     const uint32_t nu = std::max<uint32_t>(nu_layout, 1);
@@ -614,19 +666,15 @@ int decode_enqueue_jit(murr_ctx* c, const murr_segment_t* seg, const JitLayout* 
     else if (lds_for(0, 1.15) <= 40960) { si = 0; slack = 1.15; budget = 40960; }
     else if (lds_for(2, 1.08) <= 40960) { si = 2; budget = 40960; }
     else if (lds_for(1, 1.08) <= 65536) si = 1;
-    if (const char* e = std::getenv("MURR_JIT_SHAPE")) {  // tuning: "NWxR" or "NWxRs3"
-        uint32_t w = 0, r = 0, ns = 2;
-        if (std::sscanf(e, "%ux%us%u", &w, &r, &ns) >= 2)
-            for (uint32_t s = 0; s < kJitShapes; s++)
-                if (jl->shapes[s].nw == w && jl->shapes[s].r == r && jl->shapes[s].nslot == ns) si = s;
-    }
-    if (const char* e = std::getenv("MURR_JIT_LDS")) budget = (uint32_t)std::atoi(e);  // tuning
-    if (const char* e = std::getenv("MURR_JIT_SLACK")) slack = std::atof(e);  // tuning
+    if (O.shape_nw)
+        for (uint32_t s = 0; s < kJitShapes; s++)
+            if (jl->shapes[s].nw == O.shape_nw && jl->shapes[s].r == O.shape_r) si = s;
+    if (O.lds_budget) budget = O.lds_budget;
     const JitShapeK& K = jl->shapes[si];
     const uint32_t smax = std::max<uint32_t>(
         1024, ((budget - std::min(budget, jit_lds_bytes(K.nw, K.r, K.nslot, 0, nu_layout))) / K.nslot) & ~1023u);
     uint32_t stage = (uint32_t)std::min<uint64_t>(round_up((uint64_t)(K.tr * est_row * slack) + 64, 1024), smax);
-    if (const char* e = std::getenv("MURR_JIT_STAGE")) stage = (uint32_t)round_up((uint64_t)std::atof(e), 1024);
+    if (O.stage) stage = (uint32_t)round_up(O.stage, 1024);
     const uint32_t lds = jit_lds_bytes(K.nw, K.r, K.nslot, stage, nu_layout);
 
     // Workgroups per CU: the occupancy answer, never above the LDS bound.
@@ -669,11 +717,11 @@ int decode_enqueue_jit(murr_ctx* c, const murr_segment_t* seg, const JitLayout* 
         const uint64_t rounds = (nonempty + G - 1) / G;
         local = nonempty * 4 >= rounds * G * 3;
         if (!local && cuttable && stride_ok(nu_layout ? stride : 64)) local = cut = true;
-        // tuning: cut whenever possible (whole blocks may leave workgroup slots idle)
-        if (std::getenv("MURR_JIT_CUT") && cuttable && stride_ok(nu_layout ? stride : 64)) local = cut = true;
+        // mode 3: cut whenever possible (whole blocks may leave workgroup slots idle)
+        if (O.mode == 3 && cuttable && stride_ok(nu_layout ? stride : 64)) local = cut = true;
     }
-    if (const char* e = std::getenv("MURR_JIT_MODE")) {  // tuning
-        local = std::string(e) == "local";
+    if (O.mode == 1 || O.mode == 2) {
+        local = O.mode == 1;
         cut = cut && local;
     }
     if (force_local) local = true;
@@ -684,7 +732,7 @@ int decode_enqueue_jit(murr_ctx* c, const murr_segment_t* seg, const JitLayout* 
         const uint64_t S = nu_layout ? std::max<uint32_t>(stride, 1) : K.tr;  // (stride checked when cut)
         uint64_t V = std::max<uint64_t>(K.tr, (total_rows + 8 * G - 1) / (8 * G));
         V = (V + S - 1) / S * S;
-        if (const char* e = std::getenv("MURR_JIT_VROWS")) V = std::max<uint64_t>(S, (uint64_t)std::atoll(e) / S * S);
+        if (O.vrows) V = std::max<uint64_t>(S, (uint64_t)O.vrows / S * S);
         for (uint32_t b = 0; b < nblocks; b++) {
             const uint64_t n = blocks[b].n_rows;
             if (!n) continue;
@@ -702,7 +750,7 @@ int decode_enqueue_jit(murr_ctx* c, const murr_segment_t* seg, const JitLayout* 
     const double tile_in = K.tr * (est_row + 8.0);
     const uint64_t grid_rounds = std::max<uint64_t>(1, (uint64_t)std::ceil(tiles * tile_in / 100663296.0));
     uint64_t seg_tiles = std::max<uint64_t>(1, (tiles + grid_rounds * G_split - 1) / (grid_rounds * G_split));
-    if (const char* e = std::getenv("MURR_JIT_SEGTILES")) seg_tiles = std::max(1, std::atoi(e));  // tuning
+    if (O.seg_tiles) seg_tiles = O.seg_tiles;
     std::vector<JitSeg> jsegs;
     if (!local) {
         for (uint32_t b = 0; b < nblocks; b++) {
@@ -803,6 +851,10 @@ int decode_enqueue_jit(murr_ctx* c, const murr_segment_t* seg, const JitLayout* 
         }
         c->last_kernel = "murr_jit_decode";
     }
+    c->stats.last_mode = cut ? 2u : local ? 1u : 3u;
+    c->stats.last_grid = (uint32_t)grid;
+    c->stats.last_shape_nw = K.nw;
+    c->stats.last_shape_r = K.r;
     HIPC(hipEventRecord(c->k1, c->stream));
     c->timed = true;
     HIPC(hipMemcpyAsync(c->hs + rb, c->ws, z_lb, hipMemcpyDeviceToHost, c->stream));
@@ -905,7 +957,6 @@ int murr_decode_enqueue_ix(murr_ctx_t* c, const murr_segment_t* seg, const uint3
     // (NW-1) * S < 64.  Take the first shape whose ring fits the LDS budget
     // with P >= 3 (else >= 2).
     double budget = 81920.0;  // bytes of LDS per workgroup (2 workgroups per CU)
-    if (const char* e = std::getenv("MURR_DECODE_LDS")) budget = std::atof(e);  // tuning
     static const uint32_t shapes[][2] = {{8, 1}, {4, 2}, {8, 2}, {4, 4}, {4, 1}};
     uint32_t nw = 4, kc = 1, stage = 4096, depth = 2, slots = 4;
     auto plan = [&](uint32_t w, uint32_t k, uint32_t want_p, uint32_t* p_out, uint32_t* s_out, uint32_t* st_out) {
@@ -925,8 +976,7 @@ int murr_decode_enqueue_ix(murr_ctx_t* c, const murr_segment_t* seg, const uint3
         }
         return false;
     };
-    uint32_t want_p = 8;
-    if (const char* e = std::getenv("MURR_DECODE_DEPTH")) want_p = (uint32_t)std::max(2, std::atoi(e));
+    const uint32_t want_p = 8;
     bool found = false;
     for (uint32_t minp : {3u, 2u}) {
         for (const auto& sh : shapes) {
@@ -938,29 +988,27 @@ int murr_decode_enqueue_ix(murr_ctx_t* c, const murr_segment_t* seg, const uint3
         }
         if (found) break;
     }
-    if (const char* e = std::getenv("MURR_DECODE_SHAPE")) {  // tuning: "NWxKC"
-        uint32_t w = 0, k = 0, p, s, st;
-        if (std::sscanf(e, "%ux%u", &w, &k) == 2 && decode_shape_ok(w, k) && plan(w, k, want_p, &p, &s, &st)) {
-            nw = w; kc = k; depth = p; slots = s; stage = st; found = true;
-        }
-    }
     if (!found) {  // very wide rows: the smallest ring; fills past the stage go to HBM
         nw = 4; kc = 1; depth = 2; slots = 4; stage = 16384;
     }
-    // Layout-specialised kernel (murr_jit.cpp), the default.  MURR_DECODE_JIT=0
-    // selects the generic kernel; =1 makes a JIT failure an error; otherwise a
+    // Layout-specialised kernel (murr_jit.cpp), the default.  opts.kernel 2
+    // selects the generic kernel; 1 makes a JIT failure an error; otherwise a
     // layout hiprtc cannot compile falls back to the generic kernel with one
     // message per process.
+    c->stats.decodes++;
     {
-        const char* je = std::getenv("MURR_DECODE_JIT");
-        const int jmode = je ? std::atoi(je) : -1;
+        const int jmode = c->opts.kernel == 2 ? 0 : c->opts.kernel == 1 ? 1 : -1;
         uint64_t max_rows = 0;
         for (uint32_t b = 0; b < nblocks; b++) max_rows = std::max<uint64_t>(max_rows, blocks[b].n_rows);
         if (jmode != 0 && max_rows < 0x7FFFFFFFull) {
             std::string why;
-            const JitLayout* jl = jit_layout(c->device, seg, &why);
-            if (jl) return decode_enqueue_jit(c, seg, jl, proj, nproj, blocks, nblocks, outs, dp, est_row, false, uidx,
-                                              stride);
+            const JitLayout* jl = jit_layout(c->device, seg, &why, true);
+            if (jl) {
+                const int st = decode_enqueue_jit(c, seg, jl, proj, nproj, blocks, nblocks, outs, dp, est_row, false,
+                                                  uidx, stride);
+                jit_layout_unpin(jl);
+                return st;
+            }
             if (jmode == 1) {
                 std::fprintf(stderr, "murr: JIT decode unavailable: %s\n", why.c_str());
                 return MURR_E_INTERNAL;
@@ -982,7 +1030,7 @@ int murr_decode_enqueue_ix(murr_ctx_t* c, const murr_segment_t* seg, const uint3
         tiles += (blocks[b].n_rows + R - 1) / R;
         nonempty += blocks[b].n_rows != 0;
     }
-    const bool verbose = std::getenv("MURR_DECODE_VERBOSE") != nullptr;
+    const bool verbose = c->opts.verbose != 0;
     std::vector<DecOut> dout((uint64_t)nblocks * nproj);
     for (uint64_t i = 0; i < dout.size(); i++)
         dout[i] = DecOut{(uint8_t*)outs[i].values, outs[i].validity, outs[i].offsets, outs[i].values_cap};
@@ -1003,7 +1051,7 @@ int murr_decode_enqueue_ix(murr_ctx_t* c, const murr_segment_t* seg, const uint3
     uint64_t grid = std::min<uint64_t>(std::max<uint64_t>(tiles, 1), (uint64_t)c->cus * bpc);
     // Block-local mode when every workgroup gets whole blocks: no cross-tile
     // prefix protocol at all.  Otherwise tiles round-robin + window prefix.
-    const bool local = nonempty >= grid || std::getenv("MURR_DECODE_LOCAL") != nullptr;
+    const bool local = nonempty >= grid;
     if (local) grid = std::max<uint64_t>(1, std::min<uint64_t>(grid, nonempty));
     const uint64_t d_end_desc = round_up(d_outs + sizeof(DecOut) * dout.size(), 16);
     const uint64_t dend = d_end_desc;
@@ -1053,6 +1101,10 @@ int murr_decode_enqueue_ix(murr_ctx_t* c, const murr_segment_t* seg, const uint3
         HIPC(launch_decode(a, nw, kc, (uint32_t)grid, c->stream));
         c->last_kernel = "decode_kernel";
     }
+    c->stats.last_mode = 0;
+    c->stats.last_grid = (uint32_t)grid;
+    c->stats.last_shape_nw = nw;
+    c->stats.last_shape_r = kc;
     HIPC(hipEventRecord(c->k1, c->stream));
     c->timed = true;
     HIPC(hipMemcpyAsync(c->hs + rb, c->ws, z_lb, hipMemcpyDeviceToHost, c->stream));
@@ -1105,13 +1157,14 @@ int murr_decode_wait(murr_ctx_t* c, murr_error_t* err) {
         // a stream-mode wait timed out (the grid was not co-resident, e.g. a
         // shared GPU): the same decode in local mode, which never waits
         c->retry_local = false;
+        c->stats.split_retries++;
         static bool said = false;
         if (!said) {
             said = true;
             std::fprintf(stderr, "murr: stream-mode decode timed out; re-running in local mode\n");
         }
         std::string why;
-        const JitLayout* jl = jit_layout(c->device, &c->r_seg, &why);
+        const JitLayout* jl = jit_layout(c->device, &c->r_seg, &why, true);
         std::vector<DecProj> dp(c->r_proj.size());
         for (size_t p = 0; p < dp.size(); p++) {
             const murr_column_t& col = c->r_seg.cols[c->r_proj[p]];
@@ -1122,13 +1175,14 @@ int murr_decode_wait(murr_ctx_t* c, murr_error_t* err) {
         const int st = jl ? decode_enqueue_jit(c, &c->r_seg, jl, proj.data(), (uint32_t)proj.size(), blocks.data(),
                                                (uint32_t)blocks.size(), c->outs, dp, c->r_est, true)
                           : MURR_E_INTERNAL;
+        jit_layout_unpin(jl);
         if (st) return set_err(err, st);
         return murr_decode_wait(c, err);
     }
     c->retry_local = false;
     const uint64_t nbp = (uint64_t)c->nblocks * c->nproj;
     const unsigned long long* nulls = (const unsigned long long*)(rb + kErrBytes);
-    if (std::getenv("MURR_DECODE_VERBOSE")) {  // phase stamps of a MURR_ABLATE & 8 build
+    if (c->opts.verbose) {  // phase stamps of a stamped (MJ_STAMPS) tuning build
         const unsigned long long* stp = (const unsigned long long*)(rb + 16);
         if (stp[0] | stp[4]) {
             std::fprintf(stderr, "stamps (Gcycles, sum over waves; murr_jit_kernel.hip / murr_decode.hip Stamps):");
@@ -1245,14 +1299,14 @@ int murr_encode_batch_at(murr_ctx_t* c, const murr_segment_t* seg, const murr_co
     // be compiled: then the generic encode_kernel).
     const JitEncKernel* ek = nullptr;
     {
-        const char* je = std::getenv("MURR_ENCODE_JIT");
-        if (!(je && std::atoi(je) == 0) && seg->ncols) {
+        const uint32_t ek_mode = c->opts.encode_kernel;
+        if (ek_mode != 2 && seg->ncols) {
             std::string why;
             ek = jit_encode_kernel(c->device, seg->bitset_size, seg->capacity, ec.data(), seg->ncols,
                                    jit_encode_stage(n, blob_cap), &why);
-            if (!ek && (std::getenv("MURR_DECODE_VERBOSE") || (je && std::atoi(je) == 1)))
+            if (!ek && (c->opts.verbose || ek_mode == 1))
                 std::fprintf(stderr, "murr: JIT encode unavailable: %s\n", why.c_str());
-            if (!ek && je && std::atoi(je) == 1) return set_err(err, MURR_E_INTERNAL);
+            if (!ek && ek_mode == 1) return set_err(err, MURR_E_INTERNAL);
         }
     }
     HIPC(hipEventRecord(c->k0, c->stream));

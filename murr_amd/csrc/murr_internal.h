@@ -110,7 +110,10 @@ __host__ __device__ inline uint64_t err_key(uint64_t block, uint64_t row, uint32
 constexpr uint32_t kJitShapes = 4;
 // waves x 64-row chunks per decode wave x LDS ring slots (murr_jit_kernel.hip
 // MJ_KERNEL instantiates each; a 3-slot ring measured no faster on B or C;
-// 5x4 and 7x2 measured slower on B than 5x3)
+// 5x4 and 7x2 measured slower on B than 5x3; so did one 1024-thread
+// workgroup per CU with 1920-row tiles (16x2: 1.16 vs 0.74 ms), 13x2 and 9x3
+// at two per CU, although a bare LDS-DMA stream of this byte mix runs fastest
+// at one workgroup per CU with 32 KiB tiles: tools/ubench/lds_mix*.hip)
 constexpr uint32_t kJitShapeTab[kJitShapes][3] = {{5, 2, 2}, {5, 1, 2}, {3, 1, 2}, {5, 3, 2}};
 struct JitShapeK {
     hipFunction_t fn = nullptr, fn_split = nullptr;  // local / split mode kernels
@@ -145,7 +148,13 @@ struct JitArgsHead {               // = mj::Args without its trailing slot[] (mu
     unsigned int* abort_word;      // split mode: a timed-out wait aborts the launch (zeroed)
 };
 static_assert(sizeof(JitArgsHead) == 136, "mj::Args layout");
-const JitLayout* jit_layout(int device, const murr_segment_t* seg, std::string* why);
+// The compiled layout (cached; least recently used beyond 64 are retired).
+// pin: the caller will launch from it and calls jit_layout_unpin after the
+// launch is enqueued; until then no eviction unloads its module.
+const JitLayout* jit_layout(int device, const murr_segment_t* seg, std::string* why, bool pin = false);
+void jit_layout_unpin(const JitLayout* k);
+size_t jit_layout_cached();  // layouts held in memory (tests)
+size_t jit_layout_limit(size_t n);  // set the in-memory bound (n > 0) and return it
 uint32_t jit_lds_bytes(uint32_t nw, uint32_t r, uint32_t nslot, uint32_t stage, uint32_t nutf8);
 hipError_t jit_decode_launch(const JitShapeK& k, bool split, const void* args, size_t bytes, uint32_t grid,
                              uint32_t lds, hipStream_t s);

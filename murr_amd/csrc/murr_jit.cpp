@@ -125,27 +125,60 @@ struct Entry {
     bool ok = false;
     std::string why;
     uint64_t used = 0;
+    int device = 0;
 };
 
 std::mutex g_mu;
 std::map<std::string, std::unique_ptr<Entry>> g_cache;
 uint64_t g_clock = 0;
-constexpr size_t kMaxLayouts = 64;
+size_t kMaxLayouts = 64;  // murr_jit_cache_limit (tests) may lower it
 
-// Evict the least recently used layouts beyond kMaxLayouts (caller holds g_mu).
-void evict() {
+// Evict the least recently used layouts beyond kMaxLayouts, never `keep`
+// (the entry being returned; caller holds g_mu).  A JitLayout pointer handed
+// out earlier may still be in use: a launch enqueued on some stream, or a
+// caller between jit_layout() and its launch.  So an evicted entry's module is
+// not unloaded here: the entry moves to a retired list, and retired modules
+// are unloaded only once the list passes kMaxLayouts, after a device-wide
+// synchronise (every enqueued launch has finished by then) and only for
+// entries not pinned (jit_layout(..., pin = true) until jit_layout_unpin).
+std::vector<std::unique_ptr<Entry>> g_retired;
+std::map<const JitLayout*, int> g_pins;
+
+void evict(const Entry* keep) {
     while (g_cache.size() > kMaxLayouts) {
-        auto victim = g_cache.begin();
+        auto victim = g_cache.end();
         for (auto it = g_cache.begin(); it != g_cache.end(); ++it)
-            if (it->second->used < victim->second->used) victim = it;
-        if (victim->second->mod) (void)hipModuleUnload(victim->second->mod);
+            if (it->second.get() != keep && (victim == g_cache.end() || it->second->used < victim->second->used))
+                victim = it;
+        if (victim == g_cache.end()) return;
+        g_retired.push_back(std::move(victim->second));
         g_cache.erase(victim);
     }
+    if (g_retired.size() <= kMaxLayouts) return;
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    std::vector<std::unique_ptr<Entry>> still;
+    for (auto& e : g_retired) {
+        if (g_pins.count(&e->k)) {
+            still.push_back(std::move(e));
+            continue;
+        }
+        if (e->mod) {
+            (void)hipSetDevice(e->device);
+            (void)hipDeviceSynchronize();
+            (void)hipModuleUnload(e->mod);
+        }
+    }
+    (void)hipSetDevice(cur);
+    g_retired.swap(still);
 }
 
-// tuning: MURR_JIT_DEFS="NAME=VALUE,..." extra #defines (ablation builds of
-// the decode and encode kernels)
+// tuning builds (make tuning) only: MURR_JIT_DEFS="NAME=VALUE,..." extra
+// #defines (ablation variants of the decode and encode kernels)
 void tuning_defs(std::ostringstream& o) {
+#ifndef MURR_TUNING
+    (void)o;
+#else
     if (const char* e = std::getenv("MURR_JIT_DEFS")) {
         std::string d(e);
         size_t pos = 0;
@@ -158,6 +191,7 @@ void tuning_defs(std::ostringstream& o) {
             pos = end + 1;
         }
     }
+#endif
 }
 
 // Prelude: the segment layout (src/io/schema.rs:23-54), nothing of the
@@ -182,10 +216,12 @@ std::string prelude(const murr_segment_t* seg) {
 
 // The kernel source: embedded, or (tuning) the file MURR_JIT_SRC names.
 std::string kernel_source() {
+#ifdef MURR_TUNING
     if (const char* f = std::getenv("MURR_JIT_SRC")) {
         std::vector<char> t;
         if (read_file(f, &t)) return std::string(t.begin(), t.end());
     }
+#endif
     return kJitSrc;
 }
 
@@ -221,14 +257,22 @@ bool compile(Entry& e, const std::string& pre, int device) {
 // decode waves' utf8 totals and the loader's 1 KiB prefetch scratch.
 uint32_t jit_lds_bytes(uint32_t nw, uint32_t r, uint32_t nslot, uint32_t stage, uint32_t nutf8) {
     const uint32_t tr = 64 * (nw - 1) * r;
+#ifdef MURR_TUNING
+    const uint32_t ro = ((tr + 1) * 8 + 16 + 15) & ~15u;  // room for MJ_RO64=1 (whole u64 row offsets)
+#else
     const uint32_t ro = ((tr + 1) * 4 + 16 + 15) & ~15u;
+#endif
     const uint32_t nu = std::max<uint32_t>(nutf8, 1);
     return nslot * (ro + stage + 64) + 128 + 256 + 16 + 8 * nu + ((4 * nu * (nw - 1) + 15) & ~15u) + 1024;
 }
 
-const JitLayout* jit_layout(int device, const murr_segment_t* seg, std::string* why) {
+const JitLayout* jit_layout(int device, const murr_segment_t* seg, std::string* why, bool pin) {
     const std::string pre = prelude(seg);
+#ifdef MURR_TUNING
     const char* srcf = std::getenv("MURR_JIT_SRC");
+#else
+    const char* srcf = nullptr;
+#endif
     const std::string key = std::to_string(device) + "\n" + (srcf ? srcf : "") + "\n" + pre;
     std::lock_guard<std::mutex> lk(g_mu);
     auto it = g_cache.find(key);
@@ -236,16 +280,36 @@ const JitLayout* jit_layout(int device, const murr_segment_t* seg, std::string* 
         auto e = std::make_unique<Entry>();
         e->ok = compile(*e, pre, device);
         e->k.ncols = seg->ncols;
+        e->device = device;
         it = g_cache.emplace(key, std::move(e)).first;
-        evict();
-        it = g_cache.find(key);
     }
-    it->second->used = ++g_clock;
-    if (!it->second->ok) {
-        if (why) *why = it->second->why;
+    Entry* e = it->second.get();
+    e->used = ++g_clock;  // before evict: the new entry is the most recent
+    evict(e);
+    if (!e->ok) {
+        if (why) *why = e->why;
         return nullptr;
     }
-    return &it->second->k;
+    if (pin) g_pins[&e->k]++;  // under the lock: no eviction can unload it before the caller launches
+    return &e->k;
+}
+
+void jit_layout_unpin(const JitLayout* k) {
+    if (!k) return;
+    std::lock_guard<std::mutex> lk(g_mu);
+    auto it = g_pins.find(k);
+    if (it != g_pins.end() && --it->second <= 0) g_pins.erase(it);
+}
+
+size_t jit_layout_cached() {
+    std::lock_guard<std::mutex> lk(g_mu);
+    return g_cache.size();
+}
+
+size_t jit_layout_limit(size_t n) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (n) kMaxLayouts = n;
+    return kMaxLayouts;
 }
 
 hipError_t jit_decode_launch(const JitShapeK& k, bool split, const void* args, size_t bytes, uint32_t grid,

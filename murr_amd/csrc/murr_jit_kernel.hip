@@ -324,12 +324,22 @@ DEV void wait_vmcnt(uint32_t n) {
     }
 }
 
+// Row offsets in the ring slot: their low dwords gathered 64 per LDS-DMA
+// instruction (MJ_RO64 0, the default), or whole u64s, 128 per dwordx4
+// instruction (1: 27 -> 20 loader instructions per 768-row tile, measured
+// neutral on config B; tuning builds only, the host sizes LDS for 4 B per
+// row).  Only the low dwords are read (a tile's span is below 4 GiB).
+#ifndef MJ_RO64
+#define MJ_RO64 0
+#endif
+constexpr uint32_t RO_STRIDE = MJ_RO64 ? 2 : 1;  // dwords per row offset in LDS
+
 // ---- shape ---------------------------------------------------------------------
 template <uint32_t NW_, uint32_t R_, uint32_t NSLOT_>
 struct Shape {
     static constexpr uint32_t NW = NW_, NC = NW_ - 1, R = R_, TR = 64 * (NW_ - 1) * R_;
     // LDS slot: [row offsets, low dwords: (TR+1)*4 + 16][stage + 64 pad]
-    static constexpr uint32_t RO_BYTES = ((TR + 1) * 4 + 16 + 15) & ~15u;
+    static constexpr uint32_t RO_BYTES = ((TR + 1) * (MJ_RO64 ? 8 : 4) + 16 + 15) & ~15u;
     // ring slots: 2 (one tile in flight while one decodes) or 3 (two in flight)
     static constexpr uint32_t NSLOT = NSLOT_;
     static_assert(NSLOT == 2 || NSLOT == 3, "ring of 2 or 3 slots");
@@ -516,8 +526,21 @@ template <uint32_t TR, uint32_t RO_BYTES>
 DEV uint32_t tile_dma(const Tile& T, LAS uint8_t* slot, uint32_t lane) {
     uint32_t n = 0;
     const GAS uint32_t* ro = (const GAS uint32_t*)(T.row_off + T.r0);
-    for (uint32_t q = 0; q * 64 <= T.nr; q++, n++)  // lane 0 is always active: one instruction each
-        if (q * 64 + lane <= T.nr) glds4(ro + 2 * (q * 64 + lane), slot + q * 256);
+    if constexpr (MJ_RO64) {
+        // offsets r0 .. r0 + nr: whole pairs as dwordx4 (lane j of piece q:
+        // offsets 128q + 2j, +1), an odd last one as two dwords (lanes 0, 1),
+        // so nothing past row_off[n_rows] is read
+        const uint32_t cnt = T.nr + 1, pairs = cnt >> 1;
+        for (uint32_t q = 0; q * 64 < pairs; q++, n++)  // lane 0 is always active: one instruction each
+            if (q * 64 + lane < pairs) glds16(ro + 4 * (q * 64 + lane), slot + q * 1024);
+        if (cnt & 1) {
+            if (lane < 2) glds4(ro + 2 * (cnt - 1) + lane, slot + 8 * (cnt - 1));
+            n++;
+        }
+    } else {
+        for (uint32_t q = 0; q * 64 <= T.nr; q++, n++)  // lane 0 is always active: one instruction each
+            if (q * 64 + lane <= T.nr) glds4(ro + 2 * (q * 64 + lane), slot + q * 256);
+    }
     if (T.hbm) return n;
     const GAS uint8_t* g = gp(T.data) + T.abase;
     for (uint32_t q = 0; q * 1024 < T.span; q++, n++)
@@ -939,7 +962,7 @@ DEV void decode_tile(const Src& src, const Tile& T, const LAS uint32_t* ro, LAS 
 #pragma unroll
     for (uint32_t k = 0; k < R; k++) {
         const uint32_t i = rbase + k * 64 + lane;
-        const uint32_t a0 = ro[i], a1 = ro[i + 1];
+        const uint32_t a0 = ro[RO_STRIDE * i], a1 = ro[RO_STRIDE * (i + 1)];
         const uint32_t rl = i < T.nr ? a1 - a0 : 0u;
         W.ra[k] = a0 - abase;
         W.rl[k] = rl;

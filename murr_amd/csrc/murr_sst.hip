@@ -724,13 +724,18 @@ __global__ void __launch_bounds__(1024) scan_add(uint64_t* y, uint64_t n, const 
 
 }  // namespace
 
-// Lanes per tier-0 block: MURR_SST_LANES for sst_count, MURR_SST_DLANES for
-// sst_decode (4, 8, 16, 32 or 64; tuning), defaults kCountLanes / kDecodeLanes.
+// Lanes per tier-0 block: kCountLanes for sst_count, kDecodeLanes for
+// sst_decode (tuning builds: MURR_SST_LANES / MURR_SST_DLANES, 4 to 64).
 constexpr uint32_t kCountLanes = 16, kDecodeLanes = 8;
 uint32_t lanes_env(const char* name, uint32_t dflt) {
+#ifdef MURR_TUNING
     const char* e = std::getenv(name);
     const uint32_t v = e ? (uint32_t)std::atoi(e) : dflt;
     return (v == 4 || v == 8 || v == 16 || v == 32 || v == 64) ? v : dflt;
+#else
+    (void)name;
+    return dflt;
+#endif
 }
 template <uint32_t G>
 hipError_t launch_tier0(bool decode, const SstArgs& a, hipStream_t s) {

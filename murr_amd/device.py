@@ -8,6 +8,7 @@ in HBM (murr_encode_batch).  Buffers are plain device pointers; no torch.
 from __future__ import annotations
 
 import ctypes as C
+import weakref
 from dataclasses import dataclass
 
 import numpy as np
@@ -23,6 +24,39 @@ def device_count() -> int:
     return n.value
 
 
+# murr_opts_t field values by name (murr_codec.h)
+KERNELS = {"auto": 0, "jit": 1, "generic": 2}
+MODES = {"auto": 0, "local": 1, "split": 2, "cut": 3}
+_default_opts: dict = {}
+_live = weakref.WeakSet()
+
+
+def parse_opts(text: str | None) -> dict:
+    """"shape=16x2,lds=163840,mode=local" -> set_opts keywords (bench/tools)."""
+    out = {}
+    for kv in (text or "").split(","):
+        if not kv.strip():
+            continue
+        k, v = kv.split("=", 1)
+        k = k.strip()
+        if k == "shape":
+            nw, r = v.lower().split("x")
+            out["shape"] = (int(nw), int(r))
+        elif k in ("kernel", "encode_kernel", "mode"):
+            out[k] = v
+        else:
+            out[{"lds": "lds_budget"}.get(k, k)] = int(v)
+    return out
+
+
+def set_default_opts(**kw):
+    """Options every live and later Context gets (tests switch kernels with it)."""
+    _default_opts.clear()
+    _default_opts.update(kw)
+    for c in list(_live):
+        c.set_opts(**kw)
+
+
 class Context:
     """murr_ctx_t: one device, one stream, one workspace.  Not thread-safe."""
 
@@ -34,6 +68,29 @@ class Context:
             raise DeviceError(f"murr_ctx_create(device={device}): {_abi.status_str(st)}")
         self.h = h
         self.device = device
+        _live.add(self)
+        if _default_opts:
+            self.set_opts(**_default_opts)
+
+    def set_opts(self, kernel="auto", mode="auto", shape=None, seg_tiles=0, vrows=0, lds_budget=0, stage=0,
+                 encode_kernel="auto", verbose=0):
+        """murr_ctx_set_opts: kernel selection for this context (all defaults =
+        the library's own choice).  kernel / encode_kernel: auto|jit|generic;
+        mode: auto|local|split|cut; shape: (waves, chunks) e.g. (5, 3)."""
+        o = _abi.Opts()
+        o.kernel, o.mode, o.encode_kernel = KERNELS[kernel], MODES[mode], KERNELS[encode_kernel]
+        o.shape_nw, o.shape_r = shape if shape else (0, 0)
+        o.seg_tiles, o.vrows, o.lds_budget, o.stage, o.verbose = seg_tiles, vrows, lds_budget, stage, int(verbose)
+        raise_status(self.L.murr_ctx_set_opts(self.h, C.byref(o)), what="murr_ctx_set_opts")
+
+    def stats(self) -> dict:
+        """murr_ctx_stats: decodes, split_retries, last_mode (0 generic, 1 local,
+        2 local-cut, 3 split), last_grid, last_shape."""
+        s = _abi.CtxStats()
+        raise_status(self.L.murr_ctx_stats(self.h, C.byref(s)), what="murr_ctx_stats")
+        return {"decodes": s.decodes, "split_retries": s.split_retries,
+                "last_mode": ("generic", "local", "cut", "split")[s.last_mode], "last_grid": s.last_grid,
+                "last_shape": (s.last_shape_nw, s.last_shape_r)}
 
     def close(self):
         if self.h:

@@ -7,7 +7,7 @@ import oracle as O
 from golden_util import assert_array_equal, block_from_rows, expected_array, load_cases
 from randgen import ALL, drop_rows, random_columns
 from murr_amd import MurrError, SegmentError, synth
-from murr_amd.device import Context, DeviceBlock, decode_blocks, download_array
+from murr_amd.device import set_default_opts, Context, DeviceBlock, decode_blocks, download_array
 from murr_amd.schema import DTypeName as D, SegmentSchema
 
 pytestmark = pytest.mark.gpu
@@ -25,11 +25,12 @@ KERNEL = {"jit": "murr_jit_decode", "generic": "decode_kernel"}
 
 
 @pytest.fixture(autouse=True, params=["jit", "generic"])
-def kernel_mode(request, monkeypatch):
+def kernel_mode(request):
     """Every decode test runs on both kernels: the run-time specialised one
     (murr_jit_kernel.hip) and the generic one (murr_decode.hip)."""
-    monkeypatch.setenv("MURR_DECODE_JIT", "1" if request.param == "jit" else "0")
-    return request.param
+    set_default_opts(kernel=request.param)
+    yield request.param
+    set_default_opts()
 
 
 def seg_of(dtypes):
@@ -229,15 +230,14 @@ def test_many_blocks_one_launch(ctx, kernel_mode, nblocks):
 @pytest.mark.parametrize("mode,shape,segtiles", [("split", "5x2", 0), ("split", "5x1", 0), ("split", "3x1", 0),
                                                  ("split", "5x3", 0), ("split", "5x2", 1), ("split", "3x1", 2),
                                                  ("local", "5x2", 0), ("local", "3x1", 0), ("local", "5x3", 0)])
-def test_split_blocks_utf8_prefix(ctx, kernel_mode, monkeypatch, mode, shape, segtiles):
+def test_split_blocks_utf8_prefix(ctx, kernel_mode, mode, shape, segtiles):
     # few large blocks: in split mode the JIT kernel cuts them into segments
     # (two passes each) and each segment's utf8 starting offsets come from
     # the decoupled look-back over its predecessors; local mode walks every
     # block in one workgroup (forced here to cover it on few blocks)
-    monkeypatch.setenv("MURR_JIT_MODE", mode)
-    monkeypatch.setenv("MURR_JIT_SHAPE", shape)
-    if segtiles:
-        monkeypatch.setenv("MURR_JIT_SEGTILES", str(segtiles))
+    nw, r = (int(x) for x in shape.split("x"))
+    set_default_opts(kernel=kernel_mode, mode=mode, shape=(nw, r), seg_tiles=segtiles)
+    before = ctx.stats()
     rng = np.random.default_rng(40 + len(mode) + int(shape[0]) + segtiles)
     dtypes = [D.Utf8, D.Int16, D.Utf8, D.Bool, D.Float64]
     oseg = O.Segment([int(d) for d in dtypes])
@@ -251,17 +251,27 @@ def test_split_blocks_utf8_prefix(ctx, kernel_mode, monkeypatch, mode, shape, se
         wants.append(O.decode_block(oseg, proj, data, off))
     got = gpu_decode(ctx, seg_of(dtypes), proj, blocks)
     assert ctx.last_kernel() == KERNEL[kernel_mode]
+    assert_mode(ctx, before, kernel_mode, mode)
     for b in range(len(blocks)):
         for p in range(len(proj)):
             assert_array_equal(got[b][p], wants[b][p], f"block {b} proj {p}")
 
 
-def test_split_many_segments_look_back(ctx, kernel_mode, monkeypatch):
+def assert_mode(ctx, before, kernel_mode, mode):
+    """The decode ran in `mode` (JIT kernel) and no split-mode look-back wait
+    expired (an expired wait re-runs the launch in local mode, which would
+    hide a broken look-back behind correct output)."""
+    st = ctx.stats()
+    assert st["split_retries"] == before["split_retries"], "split-mode look-back timed out and was re-run"
+    if kernel_mode == "jit":
+        assert st["last_mode"] == mode, st
+
+
+def test_split_many_segments_look_back(ctx, kernel_mode):
     # one block cut into more than 512 one-tile segments: look-backs that span
     # several 512-segment windows and several rounds of the grid
-    monkeypatch.setenv("MURR_JIT_MODE", "split")
-    monkeypatch.setenv("MURR_JIT_SHAPE", "3x1")
-    monkeypatch.setenv("MURR_JIT_SEGTILES", "1")
+    set_default_opts(kernel=kernel_mode, mode="split", shape=(3, 1), seg_tiles=1)
+    before = ctx.stats()
     rng = np.random.default_rng(4242)
     dtypes = [D.Utf8, D.Int32, D.Utf8]
     oseg = O.Segment([int(d) for d in dtypes])
@@ -271,6 +281,7 @@ def test_split_many_segments_look_back(ctx, kernel_mode, monkeypatch):
     miss = set(rng.choice(n, size=n // 50, replace=False).tolist())
     _, data, off = oracle_block(dtypes, cols, n, miss)
     got = gpu_decode(ctx, seg_of(dtypes), proj, [(data, off)])[0]
+    assert_mode(ctx, before, kernel_mode, "split")
     want = O.decode_block(oseg, proj, data, off)
     for p in range(len(proj)):
         assert_array_equal(got[p], want[p], f"proj {p}")
@@ -366,11 +377,10 @@ def test_utf8_index_rows_the_decode_rejects_count_zero(ctx):
 
 @pytest.mark.parametrize("seed,n,nblocks,vrows", [(51, 50000, 1, 0), (52, 30000, 3, 512), (53, 9000, 2, 1024),
                                                   (54, 257, 1, 0)])
-def test_cut_blocks_decode_bit_exact(ctx, kernel_mode, monkeypatch, seed, n, nblocks, vrows):
+def test_cut_blocks_decode_bit_exact(ctx, kernel_mode, seed, n, nblocks, vrows):
     # few large blocks with a utf8 index: local mode over virtual blocks, each
     # starting at its index entry; same buffers as the oracle
-    if vrows:
-        monkeypatch.setenv("MURR_JIT_VROWS", str(vrows))
+    set_default_opts(kernel=kernel_mode, vrows=vrows)
     rng = np.random.default_rng(seed)
     dtypes = [D.Utf8, D.Int64, D.Bool, D.Utf8, D.Float32, D.UInt8, D.Utf8]
     oseg = O.Segment([int(d) for d in dtypes])

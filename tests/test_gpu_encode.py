@@ -7,18 +7,19 @@ import oracle as O
 from golden_util import block_from_rows, encode_inputs, load_cases
 from randgen import ALL, random_columns
 from murr_amd import synth
-from murr_amd.device import Context, encode_batch
+from murr_amd.device import set_default_opts, Context, encode_batch
 from murr_amd.schema import DTypeName as D, SegmentSchema
 
 pytestmark = pytest.mark.gpu
 
 
 @pytest.fixture(autouse=True, params=["jit", "generic"])
-def kernel_mode(request, monkeypatch):
+def kernel_mode(request):
     """Every encode test runs on both kernels: run-time specialised
     (murr_jit_encode.hip) and generic (murr_kernels.hip)."""
-    monkeypatch.setenv("MURR_ENCODE_JIT", "1" if request.param == "jit" else "0")
-    return request.param
+    set_default_opts(encode_kernel=request.param)
+    yield request.param
+    set_default_opts()
 CASES = load_cases()
 
 

@@ -7,17 +7,18 @@ import pytest
 import oracle as O
 from golden_util import assert_array_equal
 from murr_amd import synth
-from murr_amd.device import Context, DeviceBlock, decode_blocks, download_array, encode_batch
+from murr_amd.device import set_default_opts, Context, DeviceBlock, decode_blocks, download_array, encode_batch
 from murr_amd.schema import DTypeName as D, SegmentSchema
 
 pytestmark = pytest.mark.gpu
 
 
 @pytest.fixture(autouse=True, params=["jit", "generic"])
-def kernel_mode(request, monkeypatch):
+def kernel_mode(request):
     """Decode through both kernels: run-time specialised and generic."""
-    monkeypatch.setenv("MURR_DECODE_JIT", "1" if request.param == "jit" else "0")
-    return request.param
+    set_default_opts(kernel=request.param)
+    yield request.param
+    set_default_opts()
 
 
 @pytest.fixture(scope="module")

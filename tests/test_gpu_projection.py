@@ -20,9 +20,9 @@ from test_gpu_resident import C_DTYPES, assert_same, batch_c, expected, schema_c
 pytestmark = pytest.mark.gpu
 
 
-def test_new_projection_first_read_costs_no_compile(monkeypatch):
-    monkeypatch.setenv("MURR_DECODE_JIT", "1")  # a JIT failure is an error here
+def test_new_projection_first_read_costs_no_compile():
     ctx = default_context()
+    ctx.set_opts(kernel="jit")  # a JIT failure is an error here
     rt = ResidentTable(schema_c(), ctx)  # compiles the layout (or loads it)
     batch = batch_c(20_000)
     rt.write(batch)
@@ -45,3 +45,4 @@ def test_new_projection_first_read_costs_no_compile(monkeypatch):
         assert_same(got, expected([batch], keys, cols))
         # no compile: within 1 ms of a warm read of every column
         assert first < warm_s + 1e-3, (cols, first, warm_s)
+    ctx.set_opts()

@@ -12,6 +12,8 @@ import numpy as np
 import pyarrow as pa
 import pytest
 
+from murr_amd.device import set_default_opts
+
 from murr_amd import ColumnSchema, DTypeName as D, TableSchema
 from murr_amd.resident import ROW_MISSING, DeviceIndex, ResidentTable
 from murr_amd.row import default_context
@@ -26,9 +28,10 @@ C_DTYPES = [D.Bool, D.Int8, D.Int16, D.Int32, D.Int64, D.UInt8, D.UInt16, D.UInt
 
 
 @pytest.fixture(autouse=True, params=["jit", "generic"])
-def kernel_mode(request, monkeypatch):
-    monkeypatch.setenv("MURR_DECODE_JIT", "1" if request.param == "jit" else "0")
-    return request.param
+def kernel_mode(request):
+    set_default_opts(kernel=request.param)
+    yield request.param
+    set_default_opts()
 
 
 def schema_c():

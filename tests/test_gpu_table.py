@@ -7,6 +7,8 @@ import pyarrow as pa
 import pyarrow.parquet as pq
 import pytest
 
+from murr_amd.device import set_default_opts
+
 from golden_util import GOLDEN
 from murr_amd import ColumnSchema, DTypeName as D, TableSchema
 from murr_amd.row import ReadBatchBuilder
@@ -18,10 +20,11 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.fixture(autouse=True, params=["jit", "generic"])
-def kernel_mode(request, monkeypatch):
+def kernel_mode(request):
     """Decode through both kernels: run-time specialised and generic."""
-    monkeypatch.setenv("MURR_DECODE_JIT", "1" if request.param == "jit" else "0")
-    return request.param
+    set_default_opts(kernel=request.param)
+    yield request.param
+    set_default_opts()
 
 
 def schema_id_score():

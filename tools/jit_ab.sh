@@ -2,6 +2,8 @@
 # A/B of JIT decode variants in one box session: each line of VARIANTS is a
 # MURR_JIT_DEFS value ("-" = none); prints kernel ms per variant, twice.
 set -u
+# MURR_JIT_DEFS is read by the tuning build only
+export MURR_LIB=${MURR_LIB:-murr_amd/libmurr_codec_tuning.so}
 mkdir -p gpurun_out
 for rep in 1 2; do
 for v in ${VARIANTS:--}; do
