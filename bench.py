@@ -28,15 +28,13 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-# Load the HIP library before torch so one HIP runtime serves the process.
-import murr_amd  # noqa: E402
+import murr_amd  # noqa: E402  (the HIP library is loaded in main(), after the rank spawn decision)
 from murr_amd import _abi, synth  # noqa: E402
-from murr_amd.device import Context, DecodeOutputs, DeviceBlock, device_count, encode_batch, parse_opts, \
-    set_default_opts  # noqa: E402
+from murr_amd.device import Context, DecodeOutputs, DecodePlan, DeviceBlock, device_count, encode_batch, \
+    encode_block, parse_opts, set_default_opts  # noqa: E402
 from murr_amd.schema import DTypeName as D, SegmentSchema  # noqa: E402
 from murr_amd.shard import Group, shard_rows  # noqa: E402
 
-murr_amd.lib()
 
 METRIC = "block-decode GiB/s device-resident (Arrow bytes out) at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec); no MFMA on this path
@@ -194,52 +192,124 @@ def L_len(ctx, seg, rows, stride):
     return ctx.L.murr_utf8_index_len(C.byref(seg.c), rows, stride)
 
 
-def run_decode(args, dist, rank, world, local_rank):
+def check_gpus(local_rank, world):
     ndev = device_count()
     if local_rank >= ndev:
         # one GPU per rank: more ranks than GPUs would share a GPU and report a
         # wrong aggregate, so refuse instead of wrapping around
-        raise SystemExit(f"rank {rank} (local {local_rank}) has no GPU of its own: {ndev} visible, "
-                         f"WORLD_SIZE {world}")
+        raise SystemExit(f"local rank {local_rank} has no GPU of its own: {ndev} visible, WORLD_SIZE {world}")
+
+
+def copy_block(ctx, b: DeviceBlock) -> DeviceBlock:
+    """A resident copy of a block (and its index), device to device."""
+    data, off = ctx.alloc(b.data_bytes + 16), ctx.alloc(8 * (b.n_rows + 1))
+    data.copy_from(b.data, b.data_bytes)
+    off.copy_from(b.row_off, 8 * (b.n_rows + 1))
+    ux = None
+    if b.uidx is not None:
+        ux = ctx.alloc(b.uidx.nbytes)
+        ux.copy_from(b.uidx, b.uidx.nbytes)
+    return DeviceBlock(data, off, b.n_rows, b.data_bytes, ux, b.stride)
+
+
+def config_d_table(ctx, rows: int, start: int, chunk: int = 2_000_000):
+    """Config D's shard: the config-C schema with keys "key{i}", rows
+    [start, start + rows), written into a ResidentTable (device encode, key
+    index, utf8 index kept by every write)."""
+    import pyarrow as pa
+    from murr_amd import ColumnSchema, TableSchema
+    from murr_amd.resident import ResidentTable
+    cols_s = {"key": ColumnSchema(D.Utf8, False)}
+    cols_s.update({f"c{i}": ColumnSchema(c["dtype"]) for i, c in enumerate(synth.config_c(1))})
+    rt = ResidentTable(TableSchema("key", cols_s), ctx)
+    names = [c for c in cols_s if c != "key"]
+    for s0 in range(start, start + rows, chunk):
+        m = min(chunk, start + rows - s0)
+        cols = synth.config_c(m, start=s0)
+        keys = pa.array([f"key{i}" for i in range(s0, s0 + m)], pa.string())
+        rt.write(pa.RecordBatch.from_arrays([keys] + [synth.to_arrow(c) for c in cols], names=["key"] + names))
+    return rt, names
+
+
+def verify_arrays(ctx, seg, proj, outs, b, host_blob, host_off, want=None):
+    """Decoded block b (device) against the oracle's decode of its host bytes,
+    bit for bit (the comparator of tests/golden_util.assert_array_equal).
+    Returns a list of mismatch descriptions (empty = identical)."""
+    from murr_amd.device import download_array
+    if want is None:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle as O
+        want = O.decode_block(O.Segment([int(c.dtype) for c in seg.columns]), proj, host_blob, host_off)
+    n = host_off.size - 1
+    bad = []
+    for p, ci in enumerate(proj):
+        e = want[p]
+        g = download_array(ctx, outs.array(b, p), int(seg.columns[ci].dtype), n)
+        nb = (n + 7) // 8
+        if g["null_count"] != e["null_count"]:
+            bad.append(f"block {b} col {p}: null_count")
+        elif e["validity"] is not None and bytes(g["validity"][:nb]) != e["validity"]:
+            bad.append(f"block {b} col {p}: validity")
+        dt = e["dtype"]
+        if dt == 0:
+            if not np.array_equal(np.asarray(g["offsets"][: n + 1], np.int32), e["offsets"]):
+                bad.append(f"block {b} col {p}: offsets")
+            elif bytes(g["values"][: int(e["offsets"][-1])]) != e["values"]:
+                bad.append(f"block {b} col {p}: utf8 data")
+        elif dt == 1:
+            if bytes(g["values"][:nb]) != e["values"]:
+                bad.append(f"block {b} col {p}: bool bits")
+        elif bytes(g["values"][: len(e["values"])]) != e["values"]:
+            bad.append(f"block {b} col {p}: values")
+    return bad, want
+
+
+def run_decode(args, dist, rank, world, local_rank):
+    check_gpus(local_rank, world)
     ctx = Context(local_rank)
     rows, K = args.rows, args.blocks
     start, _ = shard_rows(rank, world, rows * world)  # weak scaling: `rows` per rank
-    cols = make_columns(args.config, rows, start=start)
-    dtypes = [c["dtype"] for c in cols]
-    seg = SegmentSchema([(f"c{i}", d) for i, d in enumerate(dtypes)])
-    proj = list(range(len(cols))) if args.proj is None else [int(x) for x in args.proj.split(",")]
-    # One block's row blobs, produced by the device encoder, then K resident copies.
-    dblob, doff, blen = encode_batch(ctx, seg, synth.upload_columns(ctx, cols), rows)
-    host_blob = dblob.download(blen)
-    host_off = doff.download((rows + 1) * 8).view(np.uint64).copy()
-    del dblob, doff
-    blocks = [DeviceBlock.upload(ctx, host_blob, host_off) for _ in range(K)]
-    # each block's utf8 index, written with the block (murr_utf8_index; not timed,
-    # like the encode): one large block decodes on the whole GPU in one pass
-    ix_bytes = 0
-    if args.uidx_stride:
-        for b in blocks:
-            b.index_utf8(ctx, seg, args.uidx_stride)
-        ix_bytes = 8 * int(L_len(ctx, seg, rows, args.uidx_stride)) if blocks[0].uidx is not None else 0
-        ctx.sync()
-    outs = DecodeOutputs(ctx, seg, proj, blocks)
-    cb = (_abi.Block * K)()
-    for i, b in enumerate(blocks):
-        cb[i].data, cb[i].row_off, cb[i].n_rows = b.data.ptr, b.row_off.ptr, b.n_rows
-        cb[i].data_bytes = b.data_bytes
-    pj = (C.c_uint32 * len(proj))(*proj)
-    err = _abi.Error()
-    L = ctx.L
-    ux = (C.c_void_p * K)(*[b.uidx.ptr if b.uidx is not None else None for b in blocks]) if ix_bytes else None
-
-    def step():
-        if ux is not None:
-            st = L.murr_decode_blocks_ix(ctx.h, C.byref(seg.c), pj, len(proj), cb, K, ux, args.uidx_stride,
-                                         outs.arrays, C.byref(err))
+    rt = None
+    t_build = time.perf_counter()
+    if args.config == "D":
+        # config D: this rank's key-range shard as a resident table; one step =
+        # ResidentTable.scan_device, the whole shard in one launch cut on the
+        # table's own utf8 index (kept by every write)
+        K = 1
+        rt, names = config_d_table(ctx, rows, start)
+        seg = rt.segment
+        proj = list(range(len(seg.columns))) if args.proj is None else [int(x) for x in args.proj.split(",")]
+        blocks = [rt.block()]
+        ix_stride = blocks[0].stride
+    else:
+        cols = make_columns(args.config, rows, start=start)
+        seg = SegmentSchema([(f"c{i}", c["dtype"]) for i, c in enumerate(cols)])
+        proj = list(range(len(cols))) if args.proj is None else [int(x) for x in args.proj.split(",")]
+        dcols = synth.upload_columns(ctx, cols)
+        if args.uidx_stride:
+            # the block and its utf8 index, written together (murr_encode_batch_ix)
+            b0 = encode_block(ctx, seg, dcols, rows, args.uidx_stride)
         else:
-            st = L.murr_decode_blocks(ctx.h, C.byref(seg.c), pj, len(proj), cb, K, outs.arrays, C.byref(err))
-        if st:
-            raise RuntimeError(f"decode failed: {_abi.status_str(st)} row {err.row} col {err.column}")
+            dblob, doff, blen = encode_batch(ctx, seg, dcols, rows)
+            b0 = DeviceBlock(dblob, doff, rows, blen)
+        del dcols
+        blocks = [b0] + [copy_block(ctx, b0) for _ in range(K - 1)]  # K resident blocks
+        ix_stride = b0.stride
+    ctx.sync()
+    build_s = time.perf_counter() - t_build
+    host_blob = blocks[0].data.download(blocks[0].data_bytes)
+    host_off = blocks[0].row_off.download((rows + 1) * 8).view(np.uint64).copy()
+    ix_bytes = 8 * int(L_len(ctx, seg, rows, ix_stride)) if blocks[0].uidx is not None else 0
+    outs = DecodeOutputs(ctx, seg, proj, blocks)
+    if rt is not None:
+        names = [seg.columns[c].name for c in proj]
+
+        def step():
+            rt.scan_device(names, outs)  # the product call (its prepared plan after the first)
+    else:
+        # the launch prepared once (murr_decode_plan); a step = murr_decode_run
+        plan = DecodePlan(ctx, seg, proj, blocks, outs)
+        step = plan.run
 
     for _ in range(args.warmup):
         step()
@@ -254,6 +324,7 @@ def run_decode(args, dist, rank, world, local_rank):
     barrier(dist)
     elapsed = time.perf_counter() - t0
     elapsed = max_over_ranks(dist, elapsed)
+    stats = ctx.stats()
 
     a0 = [outs.array(0, p) for p in range(len(proj))]
     out_block = arrow_out_bytes(seg, proj, rows, [a.null_count for a in a0],
@@ -265,6 +336,28 @@ def run_decode(args, dist, rank, world, local_rank):
     k_avg_ms = float(np.mean(kms))
     achieved = (in_block + out_block) * K / (k_avg_ms * 1e-3) / 1e9
     traffic = pmc_traffic(args.pmc_csv)
+
+    # after the timed region: the timed launch's output, checked against the
+    # oracle (first and last block); a mismatch fails the run
+    checked = sorted({0, K - 1})
+    bad, want = [], None
+    for b in checked:
+        bb, want = verify_arrays(ctx, seg, proj, outs, b, host_blob, host_off, want)
+        bad += bb
+    if bad:
+        raise SystemExit("bench: decoded output differs from the oracle: " + "; ".join(bad[:8]))
+    # the same launch without the utf8 index (untimed variant, for DESIGN.md)
+    no_index_ms = None
+    if ix_bytes:
+        bare = [DeviceBlock(b.data, b.row_off, b.n_rows, b.data_bytes) for b in blocks]
+        p2 = DecodePlan(ctx, seg, proj, bare, outs)
+        nk = []
+        for _ in range(5):
+            p2.run()
+            nk.append(ctx.last_kernel_ms())
+        no_index_ms = round(float(np.mean(nk[1:])), 5)
+        p2.close()
+        step()  # leave the indexed output in place
     line = {
         "metric": METRIC, "value": round(value, 3), "unit": "GiB/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup,
@@ -272,17 +365,22 @@ def run_decode(args, dist, rank, world, local_rank):
         "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
         "config": {"workload": {"B": "configs[1] read_block shape: 100k-row FLOAT32+UTF8 blocks",
                                 "C": "configs[2] schema: 16-col mixed nullable blocks",
-                                "D": "configs[3] shard: 16-col mixed nullable, key-range shard per GPU"
-                                }.get(args.config, args.config),
+                                "D": "configs[3] shard: 16-col mixed nullable, key-range shard per GPU, "
+                                     "ResidentTable.scan"}.get(args.config, args.config),
                    "rows_per_block": rows, "blocks_per_step": K, "columns": len(proj),
-                   "utf8_index_stride": args.uidx_stride if ix_bytes else None,
+                   "utf8_index_stride": ix_stride if ix_bytes else None,
                    "bytes_in_per_step": in_block * K, "bytes_out_per_step": out_step,
-                   "parallelism": f"{world} key-range shard(s), no collective"},
+                   "parallelism": f"{world} key-range shard(s), no collective",
+                   "launch": {"mode": stats["last_mode"], "grid": stats["last_grid"],
+                              "shape": "%dx%d" % stats["last_shape"], "split_retries": stats["split_retries"]},
+                   "setup_s": round(build_s, 2)},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic, "kernel": ctx.last_kernel(),
                      "kernel_ms_avg": round(k_avg_ms, 5),
                      "algorithmic_bytes_per_launch": (in_block + out_block) * K},
+        "verified": f"blocks {checked} of the timed launch bit-exact vs the oracle",
+        "no_index_ms": no_index_ms,
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -293,7 +391,34 @@ def run_decode(args, dist, rank, world, local_rank):
                                                                   min(5.0, args.cpu_seconds), threads)
     if rank == 0:
         print(json.dumps(line), flush=True)
+    if rt is None:
+        plan.close()
+    del rt
     ctx.close()
+
+
+def run_harness(args, dist, rank, world, local_rank):
+    """Self-test of the multi-rank harness (spawner, barriers, max/sum over
+    ranks, the JSON line) without a GPU: the "step" copies a host buffer.
+    Never a measurement: data = "harness self-test"."""
+    buf = np.zeros(1 << 20, np.uint8)
+    dst = np.empty_like(buf)
+    for _ in range(args.warmup):
+        np.copyto(dst, buf)
+    barrier(dist)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        np.copyto(dst, buf)
+    barrier(dist)
+    elapsed = max_over_ranks(dist, time.perf_counter() - t0)
+    total = sum_over_ranks(dist, float(buf.nbytes * args.steps))
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": round(total / elapsed / GIB, 3), "unit": "GiB/s",
+                          "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                          "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
+                          "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "harness self-test",
+                          "config": {"workload": "host memcpy (harness test only)",
+                                     "parallelism": f"{world} rank(s)"}}), flush=True)
 
 
 def run_host(args):
@@ -573,6 +698,65 @@ def sst_cpu_baseline(stored, target_s):
                       f"oracle/libmurr_oracle.so oc_sst_decode_all, {dt:.1f} s"}
 
 
+def visible_gpus():
+    """GPUs this process may use, counted without initialising HIP (the rank
+    processes do all GPU work): KFD topology nodes with a GPU target, narrowed
+    by HIP_/ROCR_/CUDA_VISIBLE_DEVICES.  None when it cannot tell."""
+    base = "/sys/class/kfd/kfd/topology/nodes"
+    try:
+        n = 0
+        for node in os.listdir(base):
+            with open(os.path.join(base, node, "properties")) as f:
+                props = dict(ln.split() for ln in f if len(ln.split()) == 2)
+            n += int(props.get("gfx_target_version", "0")) != 0
+    except (OSError, ValueError):
+        return None
+    for var in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            n = min(n, len([x for x in v.split(",") if x.strip()]))
+    return n
+
+
+def spawn_ranks(args) -> int:
+    """`--gpus N` without WORLD_SIZE: start N rank processes of this script,
+    one per GPU (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 /
+    MASTER_PORT set, as torch.distributed.run would), wait for them and return
+    the first failing exit code.  This process touches no GPU.  Rank 0 prints
+    the JSON line."""
+    import signal
+    import socket
+    import subprocess
+    n = args.gpus
+    if args.mode != "harness":
+        have = visible_gpus()
+        if have is not None and have < n:
+            print(f"bench: --gpus {n} but only {have} GPU(s) visible", file=sys.stderr)
+            return 2
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    pending = list(procs)
+    while pending:
+        for pr in list(pending):
+            code = pr.poll()
+            if code is None:
+                continue
+            pending.remove(pr)
+            if code and not rc:
+                rc = code
+                for other in pending:  # the others would wait at a barrier for it
+                    other.send_signal(signal.SIGTERM)
+        time.sleep(0.05)
+    return rc
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -581,7 +765,8 @@ def main():
     ap.add_argument("--config", default="B", choices=["A", "B", "C", "D", "E"])
     ap.add_argument("--rows", type=int, default=None, help="rows per block")
     ap.add_argument("--blocks", type=int, default=None, help="blocks per launch")
-    ap.add_argument("--mode", default="decode", choices=["decode", "host", "encode", "resident", "sst"])
+    ap.add_argument("--mode", default="decode", choices=["decode", "host", "encode", "resident", "sst", "harness"],
+                    help="harness: CPU self-test of the multi-rank harness (no GPU, not a measurement)")
     ap.add_argument("--sst-compression", default="snappy", choices=["none", "snappy", "lz4"],
                     help="sst mode: stored block compression")
     ap.add_argument("--keys", type=int, default=1000, help="resident mode: keys per read")
@@ -598,6 +783,10 @@ def main():
     ap.add_argument("--opts", default=None,
                     help="kernel selection (murr_ctx_set_opts), e.g. shape=16x2,lds=163840,mode=local")
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args))
+    if args.mode != "harness":
+        murr_amd.lib()  # raises if the HIP library is not built (no CPU fallback)
     if args.opts:
         set_default_opts(**parse_opts(args.opts))
     if args.rows is None:
@@ -619,7 +808,7 @@ def main():
     dist, rank, world, local_rank = dist_init(args)
     if world != args.gpus and rank == 0:
         print(f"note: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
-    run_decode(args, dist, rank, world, local_rank)
+    (run_harness if args.mode == "harness" else run_decode)(args, dist, rank, world, local_rank)
     dist.close()
 
 

@@ -163,6 +163,8 @@ typedef struct {
     uint32_t last_grid;      /* its workgroups */
     uint32_t last_shape_nw;  /* its tile shape (specialised kernel) */
     uint32_t last_shape_r;
+    uint64_t readback_fallbacks;  /* prepared runs whose epilogue read-back flag never came
+                                     (counts then copied back the ordinary way; 0 normally) */
 } murr_ctx_stats_t;
 int murr_ctx_stats(murr_ctx_t* ctx, murr_ctx_stats_t* out);
 
@@ -248,6 +250,24 @@ int murr_decode_enqueue(murr_ctx_t* ctx, const murr_segment_t* seg,
                         murr_array_t* outs);
 int murr_decode_wait(murr_ctx_t* ctx, murr_error_t* err);
 
+/* ---- prepared decode ---------------------------------------------------------
+ * A batch read repeated over the same blocks and output buffers (a resident
+ * table scanned again, a benchmark loop) prepared once: the launch shape,
+ * descriptors and kernel arguments are computed and uploaded by
+ * murr_decode_plan; each murr_decode_run zeroes the counters, launches, waits
+ * and fills the arrays' counts exactly as murr_decode_blocks_ix would.  The
+ * blocks' bytes and the output buffers may change between runs, their
+ * addresses and sizes may not; `outs` is written by every run.  Free every
+ * plan before its context. */
+typedef struct murr_plan murr_plan_t;
+int murr_decode_plan(murr_ctx_t* ctx, const murr_segment_t* seg,
+                     const uint32_t* proj, uint32_t nproj,
+                     const murr_block_t* blocks, uint32_t nblocks,
+                     const uint64_t* const* uidx, uint32_t stride,
+                     murr_array_t* outs, murr_plan_t** out);
+int murr_decode_run(murr_plan_t* plan, murr_error_t* err);   /* synchronous */
+void murr_plan_free(murr_plan_t* plan);
+
 /* ---- utf8 index of a block (optional) --------------------------------------
  * For every utf8 column of the layout (column order), the string bytes of the
  * rows before row j * stride, j = 0 .. ceil(n_rows / stride): the offsets the
@@ -260,6 +280,14 @@ int murr_decode_wait(murr_ctx_t* ctx, murr_error_t* err);
 uint64_t murr_utf8_index_len(const murr_segment_t* seg, uint64_t n_rows, uint32_t stride);
 int murr_utf8_index(murr_ctx_t* ctx, const murr_segment_t* seg, const murr_block_t* block,
                     uint32_t stride, uint64_t* out /* device, murr_utf8_index_len entries */);  /* enqueue */
+/* Extend an index after rows were appended to a block (MemoryStore::write
+ * appends, src/io/store/memory.rs:47-60): `block` now holds n_rows rows, `out`
+ * holds the index of its first `from` rows (murr_utf8_index_len(seg, from,
+ * stride) entries, the last being their total) and has room for
+ * murr_utf8_index_len(seg, n_rows, stride).  Reads only rows from .. n_rows.
+ * from = 0 builds the whole index (= murr_utf8_index).  Enqueued. */
+int murr_utf8_index_update(murr_ctx_t* ctx, const murr_segment_t* seg, const murr_block_t* block,
+                           uint64_t from, uint32_t stride, uint64_t* out);
 /* murr_decode_enqueue / murr_decode_blocks with an index per block (uidx[b]
  * null: block b has none; uidx null: no block has one).  Same outputs. */
 int murr_decode_enqueue_ix(murr_ctx_t* ctx, const murr_segment_t* seg,
@@ -311,6 +339,16 @@ int murr_encode_batch_at(murr_ctx_t* ctx, const murr_segment_t* seg,
                          const murr_col_in_t* cols, uint64_t n_rows,
                          uint8_t* out_blob, uint64_t blob_cap, uint64_t* out_row_off,
                          uint64_t row_base, uint64_t* blob_len, murr_error_t* err);
+
+/* murr_encode_batch that also writes the new block's utf8 index (uidx:
+ * murr_utf8_index_len(seg, n_rows, stride) entries; unused when the layout
+ * has no utf8 column), so a written block can be decoded by the whole GPU in
+ * one pass (Table::write, src/io/table/mod.rs:54-112, is where a block
+ * becomes known).  Synchronous, like murr_encode_batch. */
+int murr_encode_batch_ix(murr_ctx_t* ctx, const murr_segment_t* seg,
+                         const murr_col_in_t* cols, uint64_t n_rows,
+                         uint8_t* out_blob, uint64_t blob_cap, uint64_t* out_row_off,
+                         uint32_t stride, uint64_t* uidx, uint64_t* blob_len, murr_error_t* err);
 
 /* ---- host-memory path (pinned staging + hipMemcpyAsync both ways) -------- */
 

@@ -42,7 +42,8 @@ class Opts(C.Structure):
 
 class CtxStats(C.Structure):
     _fields_ = [("decodes", C.c_uint64), ("split_retries", C.c_uint64), ("last_mode", C.c_uint32),
-                ("last_grid", C.c_uint32), ("last_shape_nw", C.c_uint32), ("last_shape_r", C.c_uint32)]
+                ("last_grid", C.c_uint32), ("last_shape_nw", C.c_uint32), ("last_shape_r", C.c_uint32),
+                ("readback_fallbacks", C.c_uint64)]
 
 
 class Block(C.Structure):
@@ -121,9 +122,16 @@ SIGNATURES = {
     "murr_decode_enqueue_ix": (I32, [P, C.POINTER(Segment), C.POINTER(U32), U32, C.POINTER(Block), U32,
                                      C.POINTER(C.c_void_p), U32, C.POINTER(Array)]),
     "murr_utf8_index_len": (U64, [C.POINTER(Segment), U64, U32]),
+    "murr_decode_plan": (I32, [P, C.POINTER(Segment), C.POINTER(U32), U32, C.POINTER(Block), U32,
+                               C.POINTER(C.c_void_p), U32, C.POINTER(Array), PP]),
+    "murr_decode_run": (I32, [P, C.POINTER(Error)]),
+    "murr_plan_free": (None, [P]),
     "murr_sst_decode": (I32, [P, C.POINTER(SstBlock), U32, C.POINTER(SstResult), C.POINTER(Error)]),
     "murr_sst_result_free": (None, [P, C.POINTER(SstResult)]),
     "murr_utf8_index": (I32, [P, C.POINTER(Segment), C.POINTER(Block), U32, P]),
+    "murr_utf8_index_update": (I32, [P, C.POINTER(Segment), C.POINTER(Block), U64, U32, P]),
+    "murr_encode_batch_ix": (I32, [P, C.POINTER(Segment), C.POINTER(ColIn), U64, P, U64, P, U32, P,
+                                   C.POINTER(U64), C.POINTER(Error)]),
     "murr_encode_bound": (U64, [C.POINTER(Segment), U64, C.POINTER(U64)]),
     "murr_encode_batch": (I32, [P, C.POINTER(Segment), C.POINTER(ColIn), U64, P, U64, P,
                                 C.POINTER(U64), C.POINTER(Error)]),

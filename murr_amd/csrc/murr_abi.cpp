@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -629,6 +630,31 @@ int pending_set(murr_ctx* c, murr_array_t* outs, const murr_block_t* blocks, uin
 // A utf8 index stride: a power of two in [64, 2^30].
 bool stride_ok(uint64_t s) { return s >= 64 && s <= (1ull << 30) && (s & (s - 1)) == 0; }
 
+// A prepared launch of the specialised decode (murr_decode_plan): its own
+// device workspace holding the descriptors (uploaded once), the kernel
+// arguments per projection round, and a pinned readback buffer.  A run zeroes
+// the counters, launches, reads back the counts: no host-side preparation and
+// no descriptor upload per launch.
+struct JitReplay {
+    uint8_t* dws = nullptr;        // device workspace: [counter set 0 | descriptors | sink]
+    uint8_t* zb2 = nullptr;        // counter set 1 (runs alternate; each launch zeroes the other set)
+    uint8_t* hrb = nullptr;        // pinned readback (z_lb bytes) + done flag
+    uint8_t* hrb_dev = nullptr;    // its device address
+    uint64_t zbytes = 0, z_lb = 0;
+    uint64_t runs = 0;
+    std::vector<std::vector<uint8_t>> kargs[2];  // per counter set: per projection round
+    JitShapeK K{};
+    bool split = false, emit = false;
+    uint32_t grid = 0, lds = 0, mode = 0;
+    std::vector<int32_t*> empty_offsets;  // utf8 offsets of empty blocks: [0] = 0 per run
+    void release() {
+        if (dws) (void)hipFree(dws);
+        if (zb2) (void)hipFree(zb2);
+        if (hrb) (void)hipHostFree(hrb);
+        dws = zb2 = hrb = nullptr;
+    }
+};
+
 // The layout-specialised decode (murr_jit_kernel.hip).  Tile shape from the
 // mean row size.  Local mode (a workgroup owns whole blocks) when the blocks
 // fill the co-resident grid; or, when every block can be cut (it has a utf8
@@ -640,7 +666,7 @@ bool stride_ok(uint64_t s) { return s >= 64 && s <= (1ull << 30) && (s & (s - 1)
 int decode_enqueue_jit(murr_ctx* c, const murr_segment_t* seg, const JitLayout* jl, const uint32_t* proj,
                        uint32_t nproj, const murr_block_t* blocks, uint32_t nblocks, murr_array_t* outs,
                        const std::vector<DecProj>& dp, double est_row, bool force_local = false,
-                       const uint64_t* const* uidx = nullptr, uint32_t stride = 0) {
+                       const uint64_t* const* uidx = nullptr, uint32_t stride = 0, JitReplay* rep = nullptr) {
     murr_error_t* err = nullptr;
     const murr_opts_t& O = c->opts;
     const bool verbose = O.verbose != 0;
@@ -787,8 +813,22 @@ int decode_enqueue_jit(murr_ctx* c, const murr_segment_t* seg, const JitLayout* 
     const uint64_t d_projc = round_up(d_slots + 2 * (uint64_t)npad * rounds, 16);
     const uint64_t d_sink = round_up(d_projc + 2 * (uint64_t)nproj, 256);
     const uint64_t dend = d_sink + 1024;
-    int st = ensure_ws(c, dend, err);
-    if (st) return st;
+    int st = MURR_OK;
+    uint8_t* ws = nullptr;
+    if (rep) {
+        HIPC(hipMalloc(&rep->dws, dend));
+        HIPC(hipMalloc(&rep->zb2, zbytes));
+        HIPC(hipMemsetAsync(rep->zb2, 0, zbytes, c->stream));
+        // read-back + done flag, written by the kernel's epilogue: coherent
+        // (fine-grained) pinned memory the device writes over PCIe
+        HIPC(hipHostMalloc(&rep->hrb, round_up(z_flags, 64) + 64, hipHostMallocMapped | hipHostMallocCoherent));
+        HIPC(hipHostGetDevicePointer((void**)&rep->hrb_dev, rep->hrb, 0));
+        ws = rep->dws;
+    } else {
+        st = ensure_ws(c, dend, err);
+        if (st) return st;
+        ws = c->ws;
+    }
     const uint64_t z_lb = z_flags;  // readback: error word, stamps, nulls, lens
     const uint64_t hz = zbytes <= 65536 ? zbytes : 0;
     const uint64_t hdesc = d_sink - zbytes, rb = round_up(hz + hdesc, 64);
@@ -805,26 +845,29 @@ int decode_enqueue_jit(murr_ctx* c, const murr_segment_t* seg, const JitLayout* 
     std::memcpy(hd + (d_slots - zbytes), slots.data(), 2 * slots.size());
     for (uint32_t p = 0; p < nproj; p++) ((uint16_t*)(hd + (d_projc - zbytes)))[p] = (uint16_t)proj[p];
 
-    if (!hz) HIPC(hipMemsetAsync(c->ws, 0, zbytes, c->stream));
-    HIPC(hipMemcpyAsync(c->ws + zbytes - hz, c->hs, hz + hdesc, hipMemcpyHostToDevice, c->stream));
+    if (!hz) HIPC(hipMemsetAsync(ws, 0, zbytes, c->stream));
+    HIPC(hipMemcpyAsync(ws + zbytes - hz, c->hs, hz + hdesc, hipMemcpyHostToDevice, c->stream));
+    if (rep) HIPC(hipStreamSynchronize(c->stream));  // c->hs is reused by the next call
     // Empty blocks: utf8 offsets = [0] (StringBuilder starts with offset 0).
     for (uint32_t b = 0; b < nblocks; b++)
         if (blocks[b].n_rows == 0)
             for (uint32_t p = 0; p < nproj; p++)
-                if (dp[p].is_utf8 && outs[(uint64_t)b * nproj + p].offsets)
-                    HIPC(hipMemsetAsync(outs[(uint64_t)b * nproj + p].offsets, 0, 4, c->stream));
+                if (dp[p].is_utf8 && outs[(uint64_t)b * nproj + p].offsets) {
+                    if (rep) rep->empty_offsets.push_back(outs[(uint64_t)b * nproj + p].offsets);
+                    else HIPC(hipMemsetAsync(outs[(uint64_t)b * nproj + p].offsets, 0, 4, c->stream));
+                }
 
     std::vector<uint8_t> karg(round_up(sizeof(JitArgsHead) + 2 * (uint64_t)npad, 8), 0);
     JitArgsHead h{};
-    h.blocks = (const DecBlock*)(c->ws + d_blocks);
-    h.outs = (const DecOut*)(c->ws + d_outs);
+    h.blocks = (const DecBlock*)(ws + d_blocks);
+    h.outs = (const DecOut*)(ws + d_outs);
     h.order = nullptr;
-    h.segs = (const JitSeg*)(c->ws + d_segs);
-    h.projcols = (const uint16_t*)(c->ws + d_projc);
-    h.nulls = (unsigned long long*)(c->ws + z_nulls);
-    h.lens = (unsigned long long*)(c->ws + z_lens);
-    h.err = (unsigned long long*)(c->ws + z_err);
-    h.sink = c->ws + d_sink;
+    h.segs = (const JitSeg*)(ws + d_segs);
+    h.projcols = (const uint16_t*)(ws + d_projc);
+    h.nulls = (unsigned long long*)(ws + z_nulls);
+    h.lens = (unsigned long long*)(ws + z_lens);
+    h.err = (unsigned long long*)(ws + z_err);
+    h.sink = ws + d_sink;
     h.nseg = nseg;
     h.emit = emit;
     h.nblocks = nblocks;
@@ -838,19 +881,54 @@ int decode_enqueue_jit(murr_ctx* c, const murr_segment_t* seg, const JitLayout* 
                      K.nw, K.r, K.nslot, cut ? "local-cut" : local ? "local" : "split", (unsigned long long)grid, bpc, bpc_safe,
                      (unsigned long long)(local ? lsegs.size() : nonempty),
                      (unsigned long long)tiles, (unsigned long long)nseg, (unsigned long long)seg_tiles, K.tr, stage, lds, rounds);
-    HIPC(hipEventRecord(c->k0, c->stream));
+    if (rep) {
+        rep->zbytes = zbytes;
+        rep->z_lb = z_lb;
+        rep->K = K;
+        rep->split = !local;
+        rep->emit = emit;
+        rep->grid = (uint32_t)grid;
+        rep->lds = lds;
+        rep->mode = cut ? 2u : local ? 1u : 3u;
+    } else {
+        HIPC(hipEventRecord(c->k0, c->stream));
+    }
     if (tiles) {
         for (uint32_t r = 0; r < rounds; r++) {
-            h.slot_tab = (const uint16_t*)(c->ws + d_slots + 2 * (uint64_t)npad * r);
-            h.abort_word = local || !emit ? nullptr : (unsigned int*)(c->ws + 8);  // read back beside the error word
-            h.flags = (unsigned long long*)(c->ws + z_flags + flag_bytes * r);
+            h.slot_tab = (const uint16_t*)(ws + d_slots + 2 * (uint64_t)npad * r);
+            h.abort_word = local || !emit ? nullptr : (unsigned int*)(ws + 8);  // read back beside the error word
+            h.flags = (unsigned long long*)(ws + z_flags + flag_bytes * r);
             h.report = r == 0;
             std::memcpy(karg.data(), &h, sizeof h);
             std::memcpy(karg.data() + sizeof h, slots.data() + (uint64_t)npad * r, 2 * (uint64_t)npad);
-            HIPC(jit_decode_launch(K, !local, karg.data(), karg.size(), (uint32_t)grid, lds, c->stream));
+            if (rep) {
+                // counter set 0 (in ws) zeroes set 1 after the last round, and
+                // the other way round; rounds before the last zero nothing
+                for (int set = 0; set < 2; set++) {
+                    JitArgsHead hs = h;
+                    uint8_t* zb = set ? rep->zb2 : ws;
+                    hs.nulls = (unsigned long long*)(zb + z_nulls);
+                    hs.lens = (unsigned long long*)(zb + z_lens);
+                    hs.err = (unsigned long long*)(zb + z_err);
+                    hs.flags = (unsigned long long*)(zb + z_flags + flag_bytes * r);
+                    hs.abort_word = h.abort_word ? (unsigned int*)(zb + 8) : nullptr;
+                    hs.zero_next = r + 1 == rounds ? (unsigned int*)(set ? ws : rep->zb2) : nullptr;
+                    hs.zero_words = (uint32_t)(zbytes / 4);
+                    // the last round's epilogue hands the counters to the host
+                    hs.ticket = (unsigned int*)(zb + 12);
+                    hs.rb_words = (uint32_t)(z_lb / 8);
+                    hs.rb_host = r + 1 == rounds ? (unsigned long long*)rep->hrb_dev : nullptr;
+                    std::vector<uint8_t> ka = karg;
+                    std::memcpy(ka.data(), &hs, sizeof hs);
+                    rep->kargs[set].push_back(ka);
+                }
+            } else {
+                HIPC(jit_decode_launch(K, !local, karg.data(), karg.size(), (uint32_t)grid, lds, c->stream));
+            }
         }
-        c->last_kernel = "murr_jit_decode";
+        if (!rep) c->last_kernel = "murr_jit_decode";
     }
+    if (rep) return MURR_OK;
     c->stats.last_mode = cut ? 2u : local ? 1u : 3u;
     c->stats.last_grid = (uint32_t)grid;
     c->stats.last_shape_nw = K.nw;
@@ -901,9 +979,13 @@ int murr_decode_enqueue(murr_ctx_t* c, const murr_segment_t* seg, const uint32_t
     return murr_decode_enqueue_ix(c, seg, proj, nproj, blocks, nblocks, nullptr, 0, outs);
 }
 
-int murr_decode_enqueue_ix(murr_ctx_t* c, const murr_segment_t* seg, const uint32_t* proj,
-                           uint32_t nproj, const murr_block_t* blocks, uint32_t nblocks,
-                           const uint64_t* const* uidx, uint32_t stride, murr_array_t* outs) {
+namespace {
+// Argument checks of a decode (the reference's errors first: zero columns is
+// ArrowError, an unknown column SegmentError) and its per-projection
+// descriptors and mean row size.
+int decode_prep(murr_ctx* c, const murr_segment_t* seg, const uint32_t* proj, uint32_t nproj,
+                const murr_block_t* blocks, uint32_t nblocks, const uint64_t* const* uidx, uint32_t stride,
+                const murr_array_t* outs, std::vector<DecProj>& dp, double& est_row) {
     murr_error_t* err = nullptr;
     if (!c || !valid_segment(seg) || (nblocks && (!blocks || !outs)) || (nproj && !proj) ||
         c->pending)
@@ -915,7 +997,7 @@ int murr_decode_enqueue_ix(murr_ctx_t* c, const murr_segment_t* seg, const uint3
         if (proj[p] >= seg->ncols) return MURR_E_BAD_COLUMN;
     HIPC(hipSetDevice(c->device));
 
-    std::vector<DecProj> dp(nproj);
+    dp.assign(nproj, DecProj{});
     uint32_t nutf8 = 0;
     for (uint32_t p = 0; p < nproj; p++) {
         const murr_column_t& col = seg->cols[proj[p]];
@@ -947,9 +1029,25 @@ int murr_decode_enqueue_ix(murr_ctx_t* c, const murr_segment_t* seg, const uint3
         hint_bytes += blocks[b].data_bytes;
         hint_rows += blocks[b].n_rows;
     }
-    double est_row = (double)seg->bitset_size + seg->capacity;
+    est_row = (double)seg->bitset_size + seg->capacity;
     for (uint32_t i = 0; i < seg->ncols; i++) est_row += seg->cols[i].dtype == MURR_UTF8 ? 20.0 : 0.0;
     if (hinted && hint_rows) est_row = (double)hint_bytes / (double)hint_rows;
+    return MURR_OK;
+}
+}  // namespace
+
+int murr_decode_enqueue_ix(murr_ctx_t* c, const murr_segment_t* seg, const uint32_t* proj,
+                           uint32_t nproj, const murr_block_t* blocks, uint32_t nblocks,
+                           const uint64_t* const* uidx, uint32_t stride, murr_array_t* outs) {
+    murr_error_t* err = nullptr;
+    std::vector<DecProj> dp;
+    double est_row = 0;
+    {
+        const int pst = decode_prep(c, seg, proj, nproj, blocks, nblocks, uidx, stride, outs, dp, est_row);
+        if (pst) return pst;
+    }
+    uint32_t nutf8 = 0;
+    for (const DecProj& d : dp) nutf8 += d.is_utf8;
     // Per workgroup (NW waves: NW-1 consumers + 1 loader) a ring of S slots of
     // one fill each (F = 64 * KC * (NW-1) rows), P fills in flight:
     // (P-1) * E <= 63 (the loader's vmcnt field), S = P + 2, and the look-back
@@ -1121,8 +1219,14 @@ uint64_t murr_utf8_index_len(const murr_segment_t* seg, uint64_t n_rows, uint32_
 
 int murr_utf8_index(murr_ctx_t* c, const murr_segment_t* seg, const murr_block_t* block, uint32_t stride,
                     uint64_t* out) {
+    return murr_utf8_index_update(c, seg, block, 0, stride, out);
+}
+
+int murr_utf8_index_update(murr_ctx_t* c, const murr_segment_t* seg, const murr_block_t* block, uint64_t from,
+                           uint32_t stride, uint64_t* out) {
     murr_error_t* err = nullptr;
-    if (!c || !valid_segment(seg) || !block || !stride_ok(stride) || c->pending) return MURR_E_ARGUMENT;
+    if (!c || !valid_segment(seg) || !block || !stride_ok(stride) || c->pending || from > block->n_rows)
+        return MURR_E_ARGUMENT;
     Utf8IndexArgs a{};
     for (uint32_t i = 0; i < seg->ncols; i++) {
         if (seg->cols[i].dtype != MURR_UTF8) continue;
@@ -1134,15 +1238,27 @@ int murr_utf8_index(murr_ctx_t* c, const murr_segment_t* seg, const murr_block_t
     if (!a.nu) return MURR_OK;  // no utf8 column: nothing to index
     if (!out || (block->n_rows && (!block->data || !block->row_off))) return MURR_E_ARGUMENT;
     HIPC(hipSetDevice(c->device));
+    const uint64_t nwin = utf8_index_windows(from, block->n_rows, stride);
+    const int st = ensure_ws(c, 8 * std::max<uint64_t>(nwin, 1) * a.nu, err);
+    if (st) return st;
     a.data = block->data;
     a.row_off = block->row_off;
     a.out = out;
+    a.part = (uint64_t*)c->ws;
+    a.from = from;
     a.n = block->n_rows;
     a.stride = stride;
     a.bs = seg->bitset_size;
     HIPC(launch_utf8_index(a, c->stream));
     return MURR_OK;
 }
+
+}  // extern "C"
+namespace {
+int finish_counts(murr_ctx* c, const uint8_t* rb, murr_array_t* outs, uint32_t nblocks, uint32_t nproj,
+                  const uint64_t* n_rows, const uint32_t* dtypes, murr_error_t* err);
+}  // namespace
+extern "C" {
 
 int murr_decode_wait(murr_ctx_t* c, murr_error_t* err) {
     if (!c || !c->pending) return set_err(err, MURR_E_ARGUMENT);
@@ -1180,7 +1296,17 @@ int murr_decode_wait(murr_ctx_t* c, murr_error_t* err) {
         return murr_decode_wait(c, err);
     }
     c->retry_local = false;
-    const uint64_t nbp = (uint64_t)c->nblocks * c->nproj;
+    return finish_counts(c, rb, c->outs, c->nblocks, c->nproj, c->n_rows.data(), c->dtypes.data(), err);
+}
+
+namespace {
+// The read-back counters of a finished decode -> the arrays' null counts and
+// data lengths, and the first error.
+int finish_counts(murr_ctx* c, const uint8_t* rb, murr_array_t* outs, uint32_t nblocks, uint32_t nproj,
+                  const uint64_t* n_rows, const uint32_t* dtypes, murr_error_t* err) {
+    unsigned long long word;
+    std::memcpy(&word, rb, 8);
+    const uint64_t nbp = (uint64_t)nblocks * nproj;
     const unsigned long long* nulls = (const unsigned long long*)(rb + kErrBytes);
     if (c->opts.verbose) {  // phase stamps of a stamped (MJ_STAMPS) tuning build
         const unsigned long long* stp = (const unsigned long long*)(rb + 16);
@@ -1191,22 +1317,164 @@ int murr_decode_wait(murr_ctx_t* c, murr_error_t* err) {
         }
     }
     const unsigned long long* lens = nulls + nbp;
-    for (uint32_t b = 0; b < c->nblocks; b++) {
-        for (uint32_t p = 0; p < c->nproj; p++) {
-            murr_array_t& o = c->outs[(uint64_t)b * c->nproj + p];
-            const uint64_t n = c->n_rows[b];
-            const uint32_t d = c->dtypes[p];
-            o.null_count = nulls[(uint64_t)b * c->nproj + p];
-            o.data_len = d == MURR_UTF8 ? lens[(uint64_t)b * c->nproj + p]
+    for (uint32_t b = 0; b < nblocks; b++) {
+        for (uint32_t p = 0; p < nproj; p++) {
+            murr_array_t& o = outs[(uint64_t)b * nproj + p];
+            const uint64_t n = n_rows[b];
+            const uint32_t d = dtypes[p];
+            o.null_count = nulls[(uint64_t)b * nproj + p];
+            o.data_len = d == MURR_UTF8 ? lens[(uint64_t)b * nproj + p]
                          : d == MURR_BOOL ? (n + 7) / 8 : n * (uint64_t)dtype_size(d);
         }
     }
     if (err) std::memset(err, 0, sizeof *err);
     int st = unpack_err(word, err);
-    if (st == MURR_E_CAPACITY && err)
-        err->required = c->outs[(uint64_t)err->block * c->nproj + err->column].data_len;
+    if (st == MURR_E_CAPACITY && err) err->required = outs[(uint64_t)err->block * nproj + err->column].data_len;
     return st;
 }
+}  // namespace
+
+// ---- prepared decode (murr_decode_plan) -----------------------------------------
+
+struct murr_plan {
+    murr_ctx* c = nullptr;
+    std::vector<murr_column_t> cols;
+    murr_segment_t seg{};
+    std::vector<uint32_t> proj;
+    std::vector<murr_block_t> blocks;
+    std::vector<const uint64_t*> uidx;
+    uint32_t stride = 0;
+    murr_array_t* outs = nullptr;
+    std::vector<DecProj> dp;
+    std::vector<uint64_t> n_rows;
+    std::vector<uint32_t> dtypes;
+    double est_row = 0;
+    const JitLayout* jl = nullptr;  // pinned while the plan lives
+    bool replay = false;
+    JitReplay r;
+};
+
+extern "C" {
+
+int murr_decode_plan(murr_ctx_t* c, const murr_segment_t* seg, const uint32_t* proj, uint32_t nproj,
+                     const murr_block_t* blocks, uint32_t nblocks, const uint64_t* const* uidx, uint32_t stride,
+                     murr_array_t* outs, murr_plan_t** out) {
+    if (!out) return MURR_E_ARGUMENT;
+    *out = nullptr;
+    std::vector<DecProj> dp;
+    double est_row = 0;
+    const int pst = decode_prep(c, seg, proj, nproj, blocks, nblocks, uidx, stride, outs, dp, est_row);
+    if (pst) return pst;
+    std::unique_ptr<murr_plan> P(new (std::nothrow) murr_plan());
+    if (!P) return MURR_E_INTERNAL;
+    P->c = c;
+    P->cols.assign(seg->cols, seg->cols + seg->ncols);
+    P->seg = *seg;
+    P->seg.cols = P->cols.data();
+    P->proj.assign(proj, proj + nproj);
+    P->blocks.assign(blocks, blocks + nblocks);
+    if (uidx) P->uidx.assign(uidx, uidx + nblocks);
+    P->stride = stride;
+    P->outs = outs;
+    P->dp = dp;
+    P->est_row = est_row;
+    for (uint32_t b = 0; b < nblocks; b++) P->n_rows.push_back(blocks[b].n_rows);
+    for (const DecProj& d : dp) P->dtypes.push_back(d.dtype);
+    uint64_t max_rows = 0;
+    for (uint32_t b = 0; b < nblocks; b++) max_rows = std::max<uint64_t>(max_rows, blocks[b].n_rows);
+    if (c->opts.kernel != 2 && max_rows < 0x7FFFFFFFull && seg->ncols) {
+        std::string why;
+        P->jl = jit_layout(c->device, &P->seg, &why, true);
+        if (P->jl) {
+            const int st = decode_enqueue_jit(c, &P->seg, P->jl, P->proj.data(), nproj, P->blocks.data(), nblocks,
+                                              outs, P->dp, est_row, false, uidx ? P->uidx.data() : nullptr, stride,
+                                              &P->r);
+            if (st) {
+                P->r.release();
+                jit_layout_unpin(P->jl);
+                return st;
+            }
+            P->replay = true;
+        } else if (c->opts.kernel == 1) {
+            return MURR_E_INTERNAL;
+        }
+    }
+    *out = P.release();
+    return MURR_OK;
+}
+
+int murr_decode_run(murr_plan_t* P, murr_error_t* err) {
+    if (!P) return set_err(err, MURR_E_ARGUMENT);
+    murr_ctx* c = P->c;
+    if (c->pending) return set_err(err, MURR_E_ARGUMENT);
+    const uint32_t nblocks = (uint32_t)P->blocks.size(), nproj = (uint32_t)P->proj.size();
+    if (!P->replay)
+        return murr_decode_blocks_ix(c, &P->seg, P->proj.data(), nproj, P->blocks.data(), nblocks,
+                                     P->uidx.empty() ? nullptr : P->uidx.data(), P->stride, P->outs, err);
+    JitReplay& R = P->r;
+    HIPC(hipSetDevice(c->device));
+    c->stats.decodes++;
+    // counter sets alternate: this run counts into `set`, which the previous
+    // run zeroed (both were zeroed when the plan was made)
+    const int set = (int)(R.runs++ & 1);
+    for (int32_t* o : R.empty_offsets) HIPC(hipMemsetAsync(o, 0, 4, c->stream));
+    volatile uint64_t* done = (volatile uint64_t*)(R.hrb + R.z_lb);
+    *done = 0;
+    std::atomic_thread_fence(std::memory_order_seq_cst);
+    HIPC(hipEventRecord(c->k0, c->stream));
+    for (const auto& ka : R.kargs[set])
+        HIPC(jit_decode_launch(R.K, R.split, ka.data(), ka.size(), R.grid, R.lds, c->stream));
+    HIPC(hipEventRecord(c->k1, c->stream));
+    // The last workgroup's epilogue writes the counters here and sets `done`:
+    // no read-back copy, no stream synchronisation.  Should the stream go idle
+    // without the flag (it cannot, short of a device fault), read the
+    // counters back the ordinary way.
+    bool flagged = false;
+    if (!R.kargs[set].empty()) {
+        for (uint64_t spin = 1;; spin++) {
+            if (*done) { flagged = true; break; }
+            if ((spin & 4095) == 0 && hipStreamQuery(c->stream) == hipSuccess) {
+                flagged = *done != 0;
+                break;
+            }
+            __builtin_ia32_pause();
+        }
+    }
+    std::atomic_thread_fence(std::memory_order_acquire);
+    if (!flagged) {
+        if (!R.kargs[set].empty()) c->stats.readback_fallbacks++;
+        HIPC(hipMemcpyAsync(R.hrb, set ? R.zb2 : R.dws, R.z_lb, hipMemcpyDeviceToHost, c->stream));
+        HIPC(hipStreamSynchronize(c->stream));
+    }
+    c->timed = true;
+    if (!R.kargs[0].empty()) c->last_kernel = "murr_jit_decode";
+    c->stats.last_mode = R.mode;
+    c->stats.last_grid = R.grid;
+    c->stats.last_shape_nw = R.K.nw;
+    c->stats.last_shape_r = R.K.r;
+    uint32_t aborted = 0;
+    std::memcpy(&aborted, R.hrb + 8, 4);
+    if (R.split && R.emit && aborted) {
+        // a split-mode look-back wait expired: the same decode in local mode
+        c->stats.split_retries++;
+        const int st = decode_enqueue_jit(c, &P->seg, P->jl, P->proj.data(), nproj, P->blocks.data(), nblocks,
+                                          P->outs, P->dp, P->est_row, true);
+        if (st) return set_err(err, st);
+        return murr_decode_wait(c, err);
+    }
+    return finish_counts(c, R.hrb, P->outs, nblocks, nproj, P->n_rows.data(), P->dtypes.data(), err);
+}
+
+void murr_plan_free(murr_plan_t* P) {
+    if (!P) return;
+    if (P->c) (void)hipSetDevice(P->c->device);
+    if (P->r.dws) (void)hipStreamSynchronize(P->c->stream);
+    P->r.release();
+    jit_layout_unpin(P->jl);
+    delete P;
+}
+
+}  // extern "C"
 
 int murr_decode_blocks(murr_ctx_t* c, const murr_segment_t* seg, const uint32_t* proj,
                        uint32_t nproj, const murr_block_t* blocks, uint32_t nblocks,
@@ -1240,6 +1508,19 @@ int murr_encode_batch(murr_ctx_t* c, const murr_segment_t* seg, const murr_col_i
                       uint64_t n, uint8_t* out_blob, uint64_t blob_cap, uint64_t* out_row_off,
                       uint64_t* blob_len, murr_error_t* err) {
     return murr_encode_batch_at(c, seg, cols, n, out_blob, blob_cap, out_row_off, 0, blob_len, err);
+}
+
+int murr_encode_batch_ix(murr_ctx_t* c, const murr_segment_t* seg, const murr_col_in_t* cols, uint64_t n,
+                         uint8_t* out_blob, uint64_t blob_cap, uint64_t* out_row_off, uint32_t stride,
+                         uint64_t* uidx, uint64_t* blob_len, murr_error_t* err) {
+    if (!stride_ok(stride) || (murr_utf8_index_len(seg, n, stride) && !uidx)) return set_err(err, MURR_E_ARGUMENT);
+    const int st = murr_encode_batch_at(c, seg, cols, n, out_blob, blob_cap, out_row_off, 0, blob_len, err);
+    if (st) return st;
+    const murr_block_t blk{out_blob, out_row_off, n, blob_len ? *blob_len : 0};
+    const int ist = murr_utf8_index_update(c, seg, &blk, 0, stride, uidx);
+    if (ist) return set_err(err, ist);
+    HIPC(hipStreamSynchronize(c->stream));
+    return MURR_OK;
 }
 
 int murr_encode_batch_at(murr_ctx_t* c, const murr_segment_t* seg, const murr_col_in_t* cols,

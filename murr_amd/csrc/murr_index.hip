@@ -405,10 +405,14 @@ __device__ __forceinline__ uint32_t ld32u(const uint8_t* p) {
     return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
 }
 
-// One workgroup per stride of rows: the stride's string bytes per column.
+// One workgroup per stride window: window k (from floor(from / stride)) is
+// the rows [max(k * stride, from), min((k + 1) * stride, n)); its string bytes
+// per column go to part[k - k0].
 __global__ void __launch_bounds__(256) uidx_sums(Utf8IndexArgs A) {
     __shared__ uint64_t part[4];
-    const uint64_t r0 = (uint64_t)blockIdx.x * A.stride, r1 = r0 + A.stride < A.n ? r0 + A.stride : A.n;
+    const uint64_t k = A.from / A.stride + blockIdx.x;
+    const uint64_t w0 = k * A.stride, r0 = w0 > A.from ? w0 : A.from;
+    const uint64_t r1 = w0 + A.stride < A.n ? w0 + A.stride : A.n;
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     for (uint32_t u = 0; u < A.nu; u++) {
         const uint32_t c = A.col[u], fo = A.fo[u];
@@ -429,22 +433,28 @@ __global__ void __launch_bounds__(256) uidx_sums(Utf8IndexArgs A) {
         for (int m = 32; m >= 1; m >>= 1) sum += (uint64_t)__shfl_xor((unsigned long long)sum, m, 64);
         if (lane == 0) part[wave] = sum;
         __syncthreads();
-        if (threadIdx.x == 0) gp(A.out)[(uint64_t)blockIdx.x * A.nu + u] = part[0] + part[1] + part[2] + part[3];
+        if (threadIdx.x == 0) gp(A.part)[(uint64_t)blockIdx.x * A.nu + u] = part[0] + part[1] + part[2] + part[3];
         __syncthreads();
     }
 }
 
-// One workgroup: the strides' sums -> exclusive prefixes in place, plus the
-// block total at entry nstrides.
-__global__ void __launch_bounds__(1024) uidx_scan(uint64_t* out, uint64_t nstrides, uint32_t nu) {
+// One workgroup: entries k0 + 1 .. k0 + nwin = the total before `from` (the
+// index's old total, entry ceil(from / stride), read before any entry is
+// written) plus the inclusive prefix of the window sums; entry 0 = 0 for a
+// fresh index.  The last of them is the new total.
+__global__ void __launch_bounds__(1024) uidx_scan(uint64_t* out, const uint64_t* part, uint64_t nwin, uint32_t nu,
+                                                  uint64_t k0, uint64_t from, uint64_t stride) {
     __shared__ uint64_t wsum[16];
-    __shared__ uint64_t carry_s;
+    __shared__ uint64_t base_s;
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     for (uint32_t u = 0; u < nu; u++) {
-        uint64_t carry = 0;
-        for (uint64_t base = 0; base < nstrides; base += 1024) {
+        if (threadIdx.x == 0) base_s = from ? gp(out)[((from + stride - 1) / stride) * nu + u] : 0;
+        __syncthreads();
+        uint64_t carry = base_s;
+        if (from == 0 && threadIdx.x == 0) gp(out)[u] = 0;
+        for (uint64_t base = 0; base < nwin; base += 1024) {
             const uint64_t j = base + threadIdx.x;
-            const uint64_t v = j < nstrides ? gp(out)[j * nu + u] : 0;
+            const uint64_t v = j < nwin ? gp(part)[j * nu + u] : 0;
             uint64_t inc = v;
             for (int d = 1; d < 64; d <<= 1) {
                 const uint64_t o = (uint64_t)__shfl_up((unsigned long long)inc, d, 64);
@@ -457,22 +467,25 @@ __global__ void __launch_bounds__(1024) uidx_scan(uint64_t* out, uint64_t nstrid
                 before += w < wave ? wsum[w] : 0;
                 total += wsum[w];
             }
-            if (j < nstrides) gp(out)[j * nu + u] = carry + before + inc - v;
+            if (j < nwin) gp(out)[(k0 + 1 + j) * nu + u] = carry + before + inc;
             carry += total;
             __syncthreads();
         }
-        if (threadIdx.x == 0) carry_s = carry;
-        __syncthreads();
-        if (threadIdx.x == 0) gp(out)[nstrides * nu + u] = carry_s;
-        __syncthreads();
+        __syncthreads();  // every thread has its base before thread 0 reads the next column's
     }
 }
 }  // namespace
 
+uint64_t utf8_index_windows(uint64_t from, uint64_t n, uint64_t stride) {
+    return n > from ? (n + stride - 1) / stride - from / stride : 0;
+}
+
 hipError_t launch_utf8_index(const Utf8IndexArgs& a, hipStream_t s) {
-    const uint64_t nstrides = (a.n + a.stride - 1) / a.stride;
-    if (nstrides) hipLaunchKernelGGL(uidx_sums, dim3((uint32_t)nstrides), dim3(256), 0, s, a);
-    hipLaunchKernelGGL(uidx_scan, dim3(1), dim3(1024), 0, s, a.out, nstrides, a.nu);
+    const uint64_t nwin = utf8_index_windows(a.from, a.n, a.stride);
+    if (nwin) hipLaunchKernelGGL(uidx_sums, dim3((uint32_t)nwin), dim3(256), 0, s, a);
+    if (nwin || a.from == 0)
+        hipLaunchKernelGGL(uidx_scan, dim3(1), dim3(1024), 0, s, a.out, (const uint64_t*)a.part, nwin, a.nu,
+                           a.from / a.stride, a.from, a.stride);
     return hipGetLastError();
 }
 

@@ -146,8 +146,12 @@ struct JitArgsHead {               // = mj::Args without its trailing slot[] (mu
     uint32_t emit;                 // split mode: a second pass writes utf8 cells
     uint32_t ulog;                 // log2 of the utf8 index stride
     unsigned int* abort_word;      // split mode: a timed-out wait aborts the launch (zeroed)
+    unsigned int* zero_next;       // prepared launches: the other counter set, zeroed by this launch
+    uint32_t zero_words, rb_words;
+    unsigned int* ticket;          // prepared launches: workgroups finished (in the counter set)
+    unsigned long long* rb_host;   // prepared launches: pinned read-back + done flag (last round only)
 };
-static_assert(sizeof(JitArgsHead) == 136, "mj::Args layout");
+static_assert(sizeof(JitArgsHead) == 168, "mj::Args layout");
 // The compiled layout (cached; least recently used beyond 64 are retired).
 // pin: the caller will launch from it and calls jit_layout_unpin after the
 // launch is enqueued; until then no eviction unloads its module.
@@ -223,12 +227,16 @@ struct Utf8IndexArgs {
     const uint8_t* data;
     const uint64_t* row_off;
     uint64_t* out;                 // [(n + stride - 1) / stride + 1][nu]
+    uint64_t* part;                // scratch: [windows][nu] window sums
+    uint64_t from;                 // rows before `from` are indexed already (their entries, and the
+                                   // total at entry ceil(from / stride), are in out)
     uint64_t n, stride;
     uint32_t bs, nu;
     uint32_t col[kMaxUidxCols];    // segment column index of utf8 column u
     uint32_t fo[kMaxUidxCols];     // its slot's row offset (bitset_size + offset)
 };
 hipError_t launch_utf8_index(const Utf8IndexArgs& a, hipStream_t s);
+uint64_t utf8_index_windows(uint64_t from, uint64_t n, uint64_t stride);  // part[] entries per column
 
 // Device key index + row gather (murr_index.hip).
 constexpr uint32_t kMissing = 0xFFFFFFFFu;

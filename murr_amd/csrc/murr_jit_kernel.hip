@@ -108,6 +108,10 @@ struct Args {
     uint32_t emit;                // split mode: some utf8 column is projected (second pass)
     uint32_t ulog;                // log2 of the utf8 index stride
     unsigned int* abort_word;     // split mode: set when a wait timed out (every wait then gives up)
+    unsigned int* zero_next;      // prepared launches: the other counter set, zeroed for the next run
+    uint32_t zero_words, rb_words;  // ... its dwords; counter words the epilogue copies to rb_host
+    unsigned int* ticket;         // prepared launches: workgroups finished (in the counter set)
+    unsigned long long* rb_host;  // prepared launches: pinned host read-back ([rb_words] + done flag)
     uint16_t slot[(NCOLS + 1) & ~1u];  // output position of column c, 0xFFFF = not decoded
 };
 constexpr uint16_t kNone = 0xFFFF;
@@ -1168,7 +1172,9 @@ DEV void decode_tile(const Src& src, const Tile& T, const LAS uint32_t* ro, LAS 
             const uint64_t base = tile_pre[U] + before[U];                                              \
             if (T.first && wave == 0 && lane == 0) gp(o.offsets)[0] = 0;                                \
             if (T.last && wave == 0 && lane == 0)                                                       \
-                gp(args()->lens)[(uint64_t)T.b * args()->nproj + P] = tile_pre[U] + tot[U];            \
+                __hip_atomic_store(gp(args()->lens) + (uint64_t)T.b * args()->nproj + P,             \
+                                   (unsigned long long)(tile_pre[U] + tot[U]), __ATOMIC_RELAXED,        \
+                                   __HIP_MEMORY_SCOPE_AGENT); /* write-through: read by the epilogue */ \
             GAS int32_t* obf = gp(o.offsets) + T.r0 + 1;                                                \
             _Pragma("unroll") for (uint32_t k = 0; k < R; k++) {                                        \
                 const uint32_t i = rbase + k * 64 + lane;                                               \
@@ -1198,6 +1204,51 @@ DEV void decode_tile(const Src& src, const Tile& T, const LAS uint32_t* ro, LAS 
 #undef MJ_SLOT
 }
 
+// ---- read-back epilogue (prepared launches) ---------------------------------------
+// The counters (error word, null counts, utf8 byte totals) are written only by
+// agent-scope atomics and write-through stores, so once every workgroup has
+// drained them the last one to finish can hand them to the host: each decode
+// wave waits for its own memory operations, the workgroup's last decode wave
+// (an LDS count) takes a ticket, and the workgroup holding the last ticket
+// copies the counters into pinned host memory and then sets the done flag the
+// host polls.  Replaces the read-back copy and the stream synchronisation of
+// a run (MI355X_MICROARCH.md, inter-workgroup visibility: one agent-scope add
+// per storing workgroup after its waits; the last adder reads).  Relaxed
+// atomics throughout: everything handed over is already coherent (atomics,
+// write-through stores), and a release / acquire here would write back and
+// invalidate the L2 at the end of every workgroup.
+template <uint32_t NC> DEV void epilogue(LAS uint8_t* ctl, uint32_t lane) {
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // this wave's stores and atomics landed
+    uint32_t last = 0;
+    if (lane == 0)
+        last = __hip_atomic_fetch_add((LAS uint32_t*)ctl + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == NC - 1;
+    if (!__builtin_amdgcn_readfirstlane(last)) return;
+    uint32_t t = 0;
+    if (lane == 0)
+        t = __hip_atomic_fetch_add(gp(args()->ticket), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (__builtin_amdgcn_readfirstlane(t) != gridDim.x - 1) return;
+    const uint32_t words = args()->rb_words;
+    const GAS unsigned long long* __restrict__ src = (const GAS unsigned long long*)args()->err;
+    GAS unsigned long long* __restrict__ dst = gp(args()->rb_host);
+    for (uint32_t base = 0; base < words; base += 64 * 8) {
+        unsigned long long v[8];
+#pragma unroll
+        for (uint32_t k = 0; k < 8; k++) {
+            const uint32_t i = base + 64 * k + lane;
+            v[k] = i < words ? __hip_atomic_load(src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < 8; k++) {
+            const uint32_t i = base + 64 * k + lane;
+            if (i < words) dst[i] = v[k];
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __threadfence_system();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane == 0) __hip_atomic_store(dst + words, 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // ---- kernel body ---------------------------------------------------------------------
 // MODE 0: local, 1: split (separate kernels: the split path's look-back
 // registers would otherwise cost the local kernel occupancy).
@@ -1215,7 +1266,14 @@ DEV void kernel_body() {
     LAS uint8_t* infos = spans + SH::SPAN_B;
     LAS uint8_t* ctl = infos + SH::INFO_B;
     LAS uint8_t* pf = ctl + SH::CNT_B + 8 * NU + ((4 * NU * NC + 15) & ~15u);
-    if (threadIdx.x < 2) ((LAS uint32_t*)ctl)[threadIdx.x] = 0;
+    if (threadIdx.x < 3) ((LAS uint32_t*)ctl)[threadIdx.x] = 0;
+    // A prepared launch (murr_decode_run) alternates two counter sets: this
+    // launch counts into one and zeroes the other for the next run, so a run
+    // needs no memset of its own.
+    if (blockIdx.x == 0 && args()->zero_next) {
+        GAS unsigned int* z = gp(args()->zero_next);
+        for (uint32_t i = threadIdx.x; i < args()->zero_words; i += blockDim.x) z[i] = 0u;
+    }
 
     if (wave == NC) {
         // ---- loader: NSLOT - 1 tiles in flight.  At iteration i (after
@@ -1362,6 +1420,7 @@ DEV void kernel_body() {
     if (lane == 0)
         __hip_atomic_fetch_add((GAS unsigned long long*)args()->err + 2 + 9, (unsigned long long)(__builtin_amdgcn_s_memtime() - ct0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #endif
+    if (args()->rb_host) epilogue<NC>(ctl, lane);
 }
 
 }  // namespace mj

@@ -83,6 +83,12 @@ class Context:
         o.seg_tiles, o.vrows, o.lds_budget, o.stage, o.verbose = seg_tiles, vrows, lds_budget, stage, int(verbose)
         raise_status(self.L.murr_ctx_set_opts(self.h, C.byref(o)), what="murr_ctx_set_opts")
 
+    def opts_key(self) -> tuple:
+        """The context's current murr_opts_t as a tuple (plan cache keys)."""
+        o = _abi.Opts()
+        raise_status(self.L.murr_ctx_get_opts(self.h, C.byref(o)), what="murr_ctx_get_opts")
+        return tuple(getattr(o, f) for f, _ in o._fields_)
+
     def stats(self) -> dict:
         """murr_ctx_stats: decodes, split_retries, last_mode (0 generic, 1 local,
         2 local-cut, 3 split), last_grid, last_shape."""
@@ -90,7 +96,7 @@ class Context:
         raise_status(self.L.murr_ctx_stats(self.h, C.byref(s)), what="murr_ctx_stats")
         return {"decodes": s.decodes, "split_retries": s.split_retries,
                 "last_mode": ("generic", "local", "cut", "split")[s.last_mode], "last_grid": s.last_grid,
-                "last_shape": (s.last_shape_nw, s.last_shape_r)}
+                "last_shape": (s.last_shape_nw, s.last_shape_r), "readback_fallbacks": s.readback_fallbacks}
 
     def close(self):
         if self.h:
@@ -270,6 +276,53 @@ def decode_blocks(ctx: Context, segment: SegmentSchema, proj, blocks, outs: Deco
     return outs
 
 
+class DecodePlan:
+    """murr_decode_plan: one decode over fixed blocks and output buffers,
+    prepared once (shape, descriptors, kernel arguments uploaded); run()
+    repeats it with one launch and one small read-back (murr_decode_run).
+    The blocks and `outs` must stay alive and in place while the plan lives."""
+
+    def __init__(self, ctx: Context, segment: SegmentSchema, proj, blocks, outs: "DecodeOutputs | None" = None):
+        self.ctx, self.segment, self.proj, self.blocks = ctx, segment, list(proj), list(blocks)
+        self.outs = outs or DecodeOutputs(ctx, segment, self.proj, self.blocks)
+        k = max(len(self.blocks), 1)
+        self._cb = (_abi.Block * k)()
+        for i, blk in enumerate(self.blocks):
+            self._cb[i].data, self._cb[i].row_off = blk.data.ptr, blk.row_off.ptr
+            self._cb[i].n_rows, self._cb[i].data_bytes = blk.n_rows, blk.data_bytes
+        self._pj = (C.c_uint32 * max(len(self.proj), 1))(*self.proj)
+        ix = [b.uidx for b in self.blocks]
+        self._ux, stride = None, 0
+        if any(u is not None for u in ix):
+            strides = {b.stride for b in self.blocks if b.uidx is not None}
+            if len(strides) != 1:
+                raise ValueError("blocks of one decode share one utf8 index stride")
+            stride = strides.pop()
+            self._ux = (C.c_void_p * k)(*[u.ptr if u is not None else None for u in ix])
+        h = C.c_void_p()
+        st = ctx.L.murr_decode_plan(ctx.h, C.byref(segment.c), self._pj, len(self.proj), self._cb, len(self.blocks),
+                                    self._ux, stride, self.outs.arrays, C.byref(h))
+        raise_status(st, what="murr_decode_plan")
+        self.h = h.value
+        self._err = _abi.Error()
+
+    def run(self) -> "DecodeOutputs":
+        st = self.ctx.L.murr_decode_run(self.h, C.byref(self._err))
+        raise_status(st, self._err, "murr_decode_run")
+        return self.outs
+
+    def close(self):
+        if getattr(self, "h", None) and self.ctx.h:
+            self.ctx.L.murr_plan_free(self.h)
+        self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 def download_array(ctx: Context, a, dtype: int, n: int) -> dict:
     """Copy one decoded Arrow array (murr_array_t) back to host buffers."""
     def d2h(ptr, nbytes):
@@ -292,12 +345,24 @@ def download_array(ctx: Context, a, dtype: int, n: int) -> dict:
     return res
 
 
-def encode_batch(ctx: Context, segment: SegmentSchema, cols, n: int, blob_cap: int | None = None):
-    """murr_encode_batch over device-resident Arrow columns.
+def encode_block(ctx: Context, segment: SegmentSchema, cols, n: int, stride: int = 512) -> "DeviceBlock":
+    """murr_encode_batch_ix: Arrow columns (device) -> a decode block with its
+    utf8 index (a layout without utf8 columns gets none)."""
+    cin, ub = _col_in(cols)
+    blob_cap = int(ctx.L.murr_encode_bound(C.byref(segment.c), n, ub))
+    blob = ctx.alloc(max(blob_cap, 16))
+    row_off = ctx.alloc((n + 1) * 8)
+    nix = int(ctx.L.murr_utf8_index_len(C.byref(segment.c), n, stride))
+    uidx = ctx.alloc(8 * nix) if nix else None
+    blen = C.c_uint64()
+    err = _abi.Error()
+    st = ctx.L.murr_encode_batch_ix(ctx.h, C.byref(segment.c), cin, n, blob.ptr, blob_cap, row_off.ptr, stride,
+                                    uidx.ptr if uidx is not None else None, C.byref(blen), C.byref(err))
+    raise_status(st, err, "murr_encode_batch_ix")
+    return DeviceBlock(blob, row_off, n, blen.value, uidx, stride if uidx is not None else 0)
 
-    cols: per segment column dict {values: DeviceBuffer, validity: DeviceBuffer|None,
-    offsets: DeviceBuffer|None, offset: int, utf8_bytes: int}.
-    Returns (blob DeviceBuffer, row_off DeviceBuffer, blob_len)."""
+
+def _col_in(cols):
     cin = (_abi.ColIn * max(len(cols), 1))()
     ub = (C.c_uint64 * max(len(cols), 1))()
     for i, c in enumerate(cols):
@@ -306,6 +371,16 @@ def encode_batch(ctx: Context, segment: SegmentSchema, cols, n: int, blob_cap: i
         cin[i].offsets = c["offsets"].ptr if c.get("offsets") is not None else None
         cin[i].offset = int(c.get("offset", 0))
         ub[i] = int(c.get("utf8_bytes", 0))
+    return cin, ub
+
+
+def encode_batch(ctx: Context, segment: SegmentSchema, cols, n: int, blob_cap: int | None = None):
+    """murr_encode_batch over device-resident Arrow columns.
+
+    cols: per segment column dict {values: DeviceBuffer, validity: DeviceBuffer|None,
+    offsets: DeviceBuffer|None, offset: int, utf8_bytes: int}.
+    Returns (blob DeviceBuffer, row_off DeviceBuffer, blob_len)."""
+    cin, ub = _col_in(cols)
     if blob_cap is None:
         blob_cap = int(ctx.L.murr_encode_bound(C.byref(segment.c), n, ub))
     blob = ctx.alloc(max(blob_cap, 16))

@@ -25,7 +25,7 @@ import numpy as np
 import pyarrow as pa
 
 from . import _abi
-from .device import Context, DecodeOutputs, DeviceBlock, decode_blocks, download_array
+from .device import Context, DecodeOutputs, DecodePlan, DeviceBlock, decode_blocks, download_array
 from .errors import SegmentError, raise_status
 from .row import host_array_to_arrow
 from .schema import DTypeName, TableSchema
@@ -155,6 +155,10 @@ def _key_array(keys) -> pa.Array:
 # Gathers whose worst case (keys x longest row) is above this size first look
 # the rows up and size the block exactly (one 8-byte read-back), then copy.
 TWO_PHASE_BYTES = 64 << 20
+# utf8 index stride of the resident arena (murr_utf8_index_update): every
+# UIDX_STRIDE rows, each utf8 column's string bytes so far (0.016 B per row
+# and column), so a whole-table scan decodes on the whole GPU in one pass.
+UIDX_STRIDE = 512
 
 
 class ResidentTable:
@@ -174,6 +178,9 @@ class ResidentTable:
         self.n = 0
         self.max_row = 0
         self._reader = None    # murr_reader_t: scratch of the one-call host read
+        self.uidx = None       # utf8 index of the arena (UIDX_STRIDE), kept with every write
+        self.uidx_cap = 0      # entries
+        self._scan_plan = None  # (key, DecodePlan) of the last scan_device
 
     def __del__(self):
         try:
@@ -236,9 +243,29 @@ class ResidentTable:
             self.index = DeviceIndex(self.ctx, keys)
         else:
             self.index.append(keys)
+        n_old = self.n
         self.used += blen.value
         self.n += m
         self.max_row = max(self.max_row, int(sizes.max()))
+        self._index_tail(n_old)
+
+    def _index_tail(self, n_old: int):
+        """Extend the arena's utf8 index over rows n_old .. n (the written
+        block's index, kept as the table grows: only the new rows are read)."""
+        L, seg = self.ctx.L, self.segment
+        need = int(L.murr_utf8_index_len(C.byref(seg.c), self.n, UIDX_STRIDE))
+        if need == 0:
+            return
+        if need > self.uidx_cap:
+            cap = max(need, 2 * self.uidx_cap, 64)
+            buf = self.ctx.alloc(8 * cap)
+            if self.uidx is not None and n_old:
+                buf.copy_from(self.uidx, 8 * int(L.murr_utf8_index_len(C.byref(seg.c), n_old, UIDX_STRIDE)))
+                self.uidx.free()
+            self.uidx, self.uidx_cap = buf, cap
+        blk = _abi.Block(self.arena.ptr, self.row_off.ptr, self.n, self.used)
+        raise_status(L.murr_utf8_index_update(self.ctx.h, C.byref(seg.c), C.byref(blk), n_old, UIDX_STRIDE,
+                                              self.uidx.ptr), what="murr_utf8_index_update")
 
     def load_sst(self, entries):
         """Rehydrate an empty table from SST entries decoded on the device
@@ -262,6 +289,7 @@ class ResidentTable:
         self.row_off, self.off_cap = entries.value_offsets, n + 1
         self.used, self.n = entries.value_bytes, n
         self.max_row = int(lens.max())
+        self._index_tail(0)
 
     def gather(self, keys):
         """Lookup + gather on the device: a DeviceBlock of the rows of `keys` in
@@ -293,6 +321,47 @@ class ResidentTable:
         st = L.murr_index_gather_copy(self.ctx.h, rows.ptr, nq, self.arena.ptr, self.row_off.ptr, offs.ptr, data.ptr)
         raise_status(st, what="murr_index_gather_copy")
         return DeviceBlock(data, offs, nq, max(nb, 16)), (qd, qo, rows)
+
+    def block(self) -> DeviceBlock:
+        """The whole arena as one decode block, with its utf8 index."""
+        return DeviceBlock(self.arena, self.row_off, self.n, self.used, self.uidx,
+                           UIDX_STRIDE if self.uidx is not None else 0)
+
+    def scan_device(self, columns, outs: DecodeOutputs | None = None) -> DecodeOutputs:
+        """Every row of the table, decoded on the device in one launch over the
+        whole arena (cut on its utf8 index, so every CU takes part): Arrow
+        buffers in HBM.  `outs` (from an earlier scan of the same columns and
+        row count) is reused.  The bulk read of SURVEY.md §8(e) mode 1: a GPU
+        decodes its whole shard."""
+        req = self._resolve(columns)
+        if self.n == 0:
+            raise SegmentError("resident table is empty")
+        proj = [c.index for c in req]
+        state = (tuple(proj), self.arena.ptr, self.row_off.ptr, self.uidx.ptr if self.uidx is not None else 0,
+                 self.n, self.used, self.ctx.opts_key())
+        plan = self._scan_plan
+        if plan is None or plan[0] != state or (outs is not None and outs is not plan[1].outs):
+            # prepared once per (columns, table state, outputs): a repeated
+            # scan is one launch and one small read-back (murr_decode_run).
+            # Without `outs` the plan's own outputs are reused (valid until
+            # the next scan).
+            if plan is not None:
+                plan[1].close()
+            blk = self.block()
+            p = DecodePlan(self.ctx, self.segment, proj, [blk],
+                           outs or DecodeOutputs(self.ctx, self.segment, proj, [blk]))
+            self._scan_plan = plan = (state, p)
+        return plan[1].run()
+
+    def scan(self, columns) -> pa.RecordBatch:
+        """scan_device, brought to the host as a RecordBatch (rows in write
+        order; a key written twice appears twice, as in the arena)."""
+        req = self._resolve(columns)
+        if self.n == 0:
+            return host_batch(req, [_null_dict(c.dtype, 0) for c in req])
+        outs = self.scan_device(columns)
+        return host_batch(req, [download_array(self.ctx, outs.array(0, p), int(c.dtype), self.n)
+                                for p, c in enumerate(req)])
 
     def _resolve(self, columns):
         req = []

@@ -223,3 +223,32 @@ def test_route_batch_and_owned_check():
     other = (owners["k7"] + 1) % 3
     with pytest.raises(ValueError, match="belong to other shards"):
         check_owned(pa.array(["k7"]), other, 3)
+
+
+def _bench(*argv, timeout=180):
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    p = subprocess.run([sys.executable, os.path.join(root, "bench.py"), *argv], capture_output=True, text=True,
+                       timeout=timeout, env=env)
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    return p.returncode, (json.loads(lines[-1]) if lines else None), p.stderr
+
+
+def test_bench_spawns_its_own_ranks():
+    # `bench.py --gpus N` without torchrun starts N rank processes itself; the
+    # harness self-test mode runs the same spawner / barrier / max-sum / JSON
+    # path with a host copy as the step (no GPU here)
+    rc, line, err = _bench("--mode", "harness", "--gpus", "2", "--steps", "3", "--warmup", "1")
+    assert rc == 0, err[-2000:]
+    assert line["n_gpus"] == 2 and line["data"] == "harness self-test"
+    assert line["scaling"] == "weak" and line["value"] > 0
+
+
+def test_bench_refuses_ranks_without_gpus():
+    # a decode run with more ranks than GPUs exits non-zero instead of sharing
+    rc, line, err = _bench("--gpus", "2", "--steps", "1", "--warmup", "0", "--no-cpu")
+    assert rc != 0 and line is None

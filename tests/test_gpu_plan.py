@@ -1,0 +1,114 @@
+"""Prepared decodes (murr_decode_plan / murr_decode_run): a run gives the
+same buffers and counts as murr_decode_blocks_ix on the same inputs, picks
+up changed block bytes (same addresses and sizes) on the next run, and covers
+every launch form: whole blocks, blocks cut on their utf8 index, split mode,
+duplicate projections (several rounds), empty blocks, both kernels."""
+import numpy as np
+import pytest
+
+import oracle as O
+from golden_util import assert_array_equal
+from randgen import random_columns
+from murr_amd import SegmentError, synth
+from murr_amd.device import Context, DecodeOutputs, DecodePlan, DeviceBlock, download_array, set_default_opts
+from murr_amd.schema import DTypeName as D, SegmentSchema
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    c = Context(0)
+    yield c
+    c.close()
+
+
+@pytest.fixture(autouse=True, params=["jit", "generic"])
+def kernel_mode(request):
+    set_default_opts(kernel=request.param)
+    yield request.param
+    set_default_opts()
+
+
+def make(rng, dtypes, n, nulls=0.1):
+    cols = random_columns(rng, dtypes, n, null_p=nulls, max_str=14) if n else random_columns(rng, dtypes, 0)
+    oseg = O.Segment([int(d) for d in dtypes])
+    data, off = O.encode_batch(oseg, synth.oracle_cols(cols), n)
+    return oseg, data, off
+
+
+def check(ctx, seg, oseg, proj, hosts, outs, tag):
+    for b, (data, off) in enumerate(hosts):
+        n = off.size - 1
+        want = O.decode_block(oseg, proj, data, off)
+        for p, ci in enumerate(proj):
+            got = download_array(ctx, outs.array(b, p), int(seg.columns[ci].dtype), n)
+            assert_array_equal(got, want[p], f"{tag} block {b} proj {p}")
+
+
+@pytest.mark.parametrize("form", ["whole", "cut", "split", "dup"])
+def test_plan_runs_match_the_oracle(ctx, kernel_mode, form):
+    rng = np.random.default_rng(hash(form) % 1000)
+    dtypes = [D.Utf8, D.Float32, D.Bool, D.Utf8, D.Int64]
+    seg = SegmentSchema([(f"c{i}", d) for i, d in enumerate(dtypes)])
+    sizes = {"whole": [700, 0, 300, 64, 1], "cut": [40000, 9000], "split": [30000, 513], "dup": [2000, 0, 77]}[form]
+    proj = [3, 0, 1, 2, 4, 0] if form == "dup" else [4, 3, 2, 1, 0]
+    hosts, blocks = [], []
+    for n in sizes:
+        oseg, data, off = make(rng, dtypes, n)
+        hosts.append((data, off))
+        blk = DeviceBlock.upload(ctx, data, off)
+        if form == "cut":
+            blk.index_utf8(ctx, seg, 512)
+        blocks.append(blk)
+    if form in ("split", "whole"):
+        ctx.set_opts(kernel=kernel_mode, mode="split" if form == "split" else "local")
+    try:
+        plan = DecodePlan(ctx, seg, proj, blocks)
+        for rnd in range(2):
+            plan.run()
+            check(ctx, seg, oseg, proj, hosts, plan.outs, f"{form} run {rnd}")
+        st = ctx.stats()
+        assert st["split_retries"] == 0 and st["readback_fallbacks"] == 0, st
+        if kernel_mode == "jit":
+            assert st["last_mode"] == {"whole": "local", "cut": "cut", "split": "split", "dup": "split"}[form], st
+        plan.close()
+    finally:
+        ctx.set_opts(kernel=kernel_mode)
+
+
+def test_plan_rereads_changed_bytes(ctx, kernel_mode):
+    # same sizes, new contents: the next run decodes the new bytes
+    rng = np.random.default_rng(3)
+    dtypes = [D.Int32, D.Utf8]
+    seg = SegmentSchema([("a", D.Int32), ("b", D.Utf8)])
+    oseg, d1, off = make(rng, dtypes, 5000, nulls=0.0)
+    blk = DeviceBlock.upload(ctx, d1, off)
+    plan = DecodePlan(ctx, seg, [1, 0], [blk])
+    plan.run()
+    check(ctx, seg, oseg, [1, 0], [(d1, off)], plan.outs, "first")
+    d2 = d1.copy()
+    # flip int32 payload bytes of every row (the row layout, hence the sizes, is unchanged)
+    starts = off[:-1].astype(np.int64)
+    d2[starts + 1] ^= 0x5A
+    blk.data.copy_from(DeviceBlock.upload(ctx, d2, off).data, d2.size)
+    plan.run()
+    check(ctx, seg, oseg, [1, 0], [(d2, off)], plan.outs, "second")
+    plan.close()
+
+
+def test_plan_reports_errors_each_run(ctx, kernel_mode):
+    dtypes = [D.Utf8]
+    seg = SegmentSchema([("s", D.Utf8)])
+    rng = np.random.default_rng(4)
+    oseg, data, off = make(rng, dtypes, 3000, nulls=0.0)
+    data = data.copy()
+    r = int(np.argmax(np.diff(off.astype(np.int64)) > 5))
+    a = int(off[r])
+    data[a + 1 + int.from_bytes(data[a + 1:a + 5].tobytes(), "little") + 4] = 0xFF
+    blk = DeviceBlock.upload(ctx, data, off)
+    plan = DecodePlan(ctx, seg, [0], [blk])
+    for _ in range(2):
+        with pytest.raises(SegmentError, match=f"row {r},"):
+            plan.run()
+    plan.close()

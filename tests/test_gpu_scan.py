@@ -1,0 +1,126 @@
+"""The utf8 index as a product artifact, and whole-table scans.
+
+* murr_encode_batch_ix writes a block's index with the block; its entries are
+  the oracle decode's own utf8 offsets at every stride.
+* ResidentTable.write keeps the arena's index as it grows (appends of odd
+  sizes: only the new rows are indexed, murr_utf8_index_update), and so does
+  load_sst.
+* ResidentTable.scan decodes the whole arena in one launch cut on that index
+  (config D's "each GPU decodes its whole shard"), bit-exact against the
+  oracle's decode of the same blob -- at 1.25 M config-C rows too.
+"""
+import ctypes as C
+
+import numpy as np
+import pyarrow as pa
+import pytest
+
+import oracle as O
+from golden_util import assert_array_equal
+from randgen import random_columns
+from murr_amd import synth
+from murr_amd.device import Context, DecodeOutputs, download_array, encode_block, set_default_opts
+from murr_amd.resident import UIDX_STRIDE, ResidentTable
+from murr_amd.schema import DTypeName as D, SegmentSchema
+
+from test_gpu_resident import C_DTYPES, batch_c, schema_c
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    c = Context(0)
+    yield c
+    c.close()
+
+
+def index_of(oseg, dtypes, data, off, n, stride):
+    uc = [i for i, d in enumerate(dtypes) if d == D.Utf8]
+    want = O.decode_block(oseg, uc, data, off)
+    js = list(range(0, n, stride)) + [n]
+    return np.array([[int(want[u]["offsets"][j]) for u in range(len(uc))] for j in js], np.uint64)
+
+
+@pytest.mark.parametrize("n,stride", [(1, 64), (1000, 64), (4099, 512), (30000, 256)])
+def test_encode_block_writes_the_index(ctx, n, stride):
+    rng = np.random.default_rng(n)
+    dtypes = [D.Utf8, D.Int16, D.Utf8, D.Bool]
+    cols = random_columns(rng, dtypes, n, null_p=0.2, max_str=20)
+    seg = SegmentSchema([(f"c{i}", d) for i, d in enumerate(dtypes)])
+    blk = encode_block(ctx, seg, synth.upload_columns(ctx, cols), n, stride)
+    oseg = O.Segment([int(d) for d in dtypes])
+    data, off = O.encode_batch(oseg, synth.oracle_cols(cols), n)
+    assert blk.data.download(blk.data_bytes).tobytes() == data.tobytes()
+    got = blk.uidx.download().view(np.uint64).reshape(-1, 2)
+    assert np.array_equal(got, index_of(oseg, dtypes, data, off, n, stride))
+
+
+def test_encode_block_without_utf8_has_no_index(ctx):
+    seg = SegmentSchema([("a", D.Float32), ("b", D.Int64)])
+    cols = synth.config_e(100, ncols=1) + [synth.column(D.Int64, np.arange(100))]
+    blk = encode_block(ctx, seg, synth.upload_columns(ctx, cols), 100)
+    assert blk.uidx is None and blk.n_rows == 100
+
+
+def arena(rt):
+    data = rt.arena.download(rt.used)
+    off = rt.row_off.download(8 * (rt.n + 1)).view(np.uint64).copy()
+    return data, off
+
+
+@pytest.mark.parametrize("kernel", ["jit", "generic"])
+def test_resident_appends_keep_the_index_and_scan(ctx, kernel):
+    set_default_opts(kernel=kernel)
+    try:
+        rt = ResidentTable(schema_c(), ctx)
+        sizes = [1000, 777, 1, 513, 4099, 512, 3]
+        start = 0
+        for k, m in enumerate(sizes):
+            rt.write(batch_c(m, start=start, seed=40 + k))
+            start += m
+            data, off = arena(rt)
+            oseg = O.Segment([int(d) for d in C_DTYPES])
+            want_ix = index_of(oseg, C_DTYPES, data, off, rt.n, UIDX_STRIDE)
+            got_ix = rt.uidx.download(8 * want_ix.size).view(np.uint64).reshape(want_ix.shape)
+            assert np.array_equal(got_ix, want_ix), f"after append {k}"
+        names = [f"c{i}" for i in range(len(C_DTYPES))]
+        proj = [12, 0, 11, 3, 12]
+        outs = rt.scan_device([names[i] for i in proj])
+        st = ctx.stats()
+        if kernel == "jit":
+            assert st["last_mode"] == "cut", st
+        want = O.decode_block(oseg, proj, data, off)
+        for p, ci in enumerate(proj):
+            assert_array_equal(download_array(ctx, outs.array(0, p), int(C_DTYPES[ci]), rt.n), want[p], f"proj {p}")
+        # the host form: the written rows in write order
+        whole = pa.Table.from_batches([batch_c(m, start=sum(sizes[:k]), seed=40 + k)
+                                       for k, m in enumerate(sizes)]).combine_chunks()
+        got = rt.scan(["c12", "c0", "c4"])
+        for name, col in zip(["c12", "c0", "c4"], got.columns):
+            assert col.equals(whole.column(name).combine_chunks()), name
+    finally:
+        set_default_opts()
+
+
+def test_scan_device_bit_exact_config_d_shard(ctx):
+    # config D's per-GPU work: one 1.25 M-row shard of the config-C schema,
+    # decoded whole in one launch over the arena cut on its index
+    n = 1_250_000
+    rt = ResidentTable(schema_c(), ctx)
+    rt.write(batch_c(n))
+    names = [f"c{i}" for i in range(len(C_DTYPES))]
+    outs = rt.scan_device(names)
+    assert ctx.last_kernel() == "murr_jit_decode"
+    st = ctx.stats()
+    assert st["last_mode"] == "cut" and st["split_retries"] == 0, st
+    data, off = arena(rt)
+    oseg = O.Segment([int(d) for d in C_DTYPES])
+    want = O.decode_block(oseg, list(range(len(C_DTYPES))), data, off)
+    for p, d in enumerate(C_DTYPES):
+        assert_array_equal(download_array(ctx, outs.array(0, p), int(d), n), want[p], f"col {p}")
+    # the outputs are reused across scans of the same shard
+    again = rt.scan_device(names, outs)
+    assert again is outs
+    for p in (0, 11, 12):
+        assert_array_equal(download_array(ctx, outs.array(0, p), int(C_DTYPES[p]), n), want[p], f"again {p}")
