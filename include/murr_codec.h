@@ -428,6 +428,14 @@ void murr_index_free(murr_index_t* idx);
 int murr_index_append(murr_ctx_t* ctx, murr_index_t* idx, const uint8_t* key_data,
                       const int32_t* key_offsets, uint64_t key_offset, uint64_t n,
                       murr_error_t* err);
+/* Resolve equal keys by sequence number instead of row: afterwards each key
+ * maps to its row with the highest seqs[row] (equal sequence numbers: the
+ * later row).  seqs: device array of idx.n entries.  For indexes over SST
+ * entries (ResidentTable.load_sst), where RocksDB stores a key's versions
+ * newest first (InternalKeyComparator: user key ascending, sequence number
+ * descending) and overlapping files repeat keys in any order; the version
+ * with the highest sequence number is the one a read returns.  Synchronous. */
+int murr_index_prefer_seq(murr_ctx_t* ctx, murr_index_t* idx, const uint64_t* seqs, murr_error_t* err);
 /* Rows indexed (n at build) and hash-table slots. */
 int murr_index_info(const murr_index_t* idx, uint64_t* n, uint64_t* slots);
 

@@ -156,6 +156,7 @@ SIGNATURES = {
     "murr_index_free": (None, [P]),
     "murr_index_append": (I32, [P, P, P, P, U64, U64, C.POINTER(Error)]),
     "murr_index_info": (I32, [P, C.POINTER(U64), C.POINTER(U64)]),
+    "murr_index_prefer_seq": (I32, [P, P, P, C.POINTER(Error)]),
     "murr_index_lookup": (I32, [P, P, P, P, U64, P]),
     "murr_index_gather": (I32, [P, P, P, P, U64, P, P, P, U64, P, P, P]),
     "murr_index_gather_copy": (I32, [P, P, U64, P, P, P, P]),

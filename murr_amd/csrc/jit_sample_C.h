@@ -1,4 +1,4 @@
-// Sample prelude (config C: 16 mixed columns, bs 2) for `make jitcheck`.
+// Sample prelude (config C: 16 mixed nullable columns) for make jitcheck
 #define MJ_BS 2
 #define MJ_FIX 73
 #define MJ_NCOLS 16

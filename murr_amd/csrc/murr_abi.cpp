@@ -9,6 +9,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <map>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -83,6 +84,10 @@ struct murr_ctx {
     const char* last_kernel = "";  // kernel of the last decode launch
     murr_opts_t opts{};            // kernel selection (murr_ctx_set_opts)
     murr_ctx_stats_t stats{};
+#ifdef MURR_TUNING
+    uint64_t tl_off = 0;  // stamped builds, verbose: per-workgroup timeline in ws (0 = none)
+    uint64_t tl_n = 0;
+#endif
     // Staging buffers of freed builders, reused by the next ones (a read builds
     // a ReadBatchBuilder per batch, src/io/row/read.rs:69-83; pinned and device
     // allocations cost far more than the batch itself).
@@ -174,6 +179,46 @@ void opts_from_env(murr_opts_t* o) {
     num("MURR_JIT_LDS", &o->lds_budget);
     num("MURR_JIT_STAGE", &o->stage);
     if (std::getenv("MURR_DECODE_VERBOSE")) o->verbose = 1;
+}
+#endif
+
+#ifdef MURR_TUNING
+// Per-workgroup timeline of an MJ_TIMELINE JIT launch, in microseconds
+// from the first workgroup's start: percentiles of the start, of the wait for
+// the first tile, of the end; tiles per workgroup; the end by tile count and
+// by XCD.
+void print_timeline(murr_ctx* c) {
+    std::vector<uint64_t> t(4 * c->tl_n);
+    if (hipMemcpy(t.data(), c->ws + c->tl_off, 8 * t.size(), hipMemcpyDeviceToHost) != hipSuccess) return;
+    uint64_t t0 = ~0ull;
+    for (uint64_t g = 0; g < c->tl_n; g++)
+        if (t[4 * g]) t0 = std::min(t0, t[4 * g]);
+    std::vector<double> st, b0, en, dur;
+    std::map<uint32_t, std::pair<double, int>> by_tiles, by_xcc;
+    for (uint64_t g = 0; g < c->tl_n; g++) {
+        if (!t[4 * g]) continue;
+        const double s0 = (t[4 * g] - t0) * 0.01, s1 = (t[4 * g + 1] - t0) * 0.01, s2 = (t[4 * g + 2] - t0) * 0.01;
+        st.push_back(s0), b0.push_back(s1 - s0), en.push_back(s2), dur.push_back(s2 - s0);
+        const uint32_t tiles = (uint32_t)(t[4 * g + 3] & 0xFFFF), xcc = (uint32_t)(t[4 * g + 3] >> 48) & 0xF;
+        auto& a = by_tiles[tiles];
+        a.first = std::max(a.first, s2), a.second++;
+        auto& x = by_xcc[xcc];
+        x.first = std::max(x.first, s2), x.second++;
+    }
+    auto pct = [](std::vector<double> v, const char* name) {
+        std::sort(v.begin(), v.end());
+        if (v.empty()) return;
+        auto q = [&](double f) { return v[(size_t)std::min<double>(v.size() - 1, f * (v.size() - 1))]; };
+        std::fprintf(stderr, "  %-10s p0 %7.2f p10 %7.2f p50 %7.2f p90 %7.2f p99 %7.2f max %7.2f us\n", name, q(0), q(0.1),
+                     q(0.5), q(0.9), q(0.99), q(1));
+    };
+    std::fprintf(stderr, "timeline (%zu workgroups):\n", st.size());
+    pct(st, "start");
+    pct(b0, "first tile");
+    pct(dur, "duration");
+    pct(en, "end");
+    for (auto& kv : by_tiles) std::fprintf(stderr, "  tiles %u: %d workgroups, last end %.2f us\n", kv.first, kv.second.second, kv.second.first);
+    for (auto& kv : by_xcc) std::fprintf(stderr, "  xcc %u: %d workgroups, last end %.2f us\n", kv.first, kv.second.second, kv.second.first);
 }
 #endif
 
@@ -279,6 +324,31 @@ int murr_index_append(murr_ctx_t* c, murr_index_t* x, const uint8_t* key_data, c
     if (word) return set_err(err, MURR_E_INTERNAL);
     x->n = total;
     x->key_bytes += bytes;
+    return MURR_OK;
+}
+
+int murr_index_prefer_seq(murr_ctx_t* c, murr_index_t* x, const uint64_t* seqs, murr_error_t* err) {
+    if (!c || !x || x->device != c->device || c->pending || (x->n && !seqs)) return set_err(err, MURR_E_ARGUMENT);
+    if (!x->n) return MURR_OK;
+    HIPC(hipSetDevice(c->device));
+    const uint64_t slots = x->mask + 1;
+    unsigned long long* tmp = nullptr;  // best seq, then winning row + 1, per slot
+    HIPC(hipMalloc(&tmp, 16 * slots));
+    std::unique_ptr<unsigned long long, hipError_t (*)(void*)> hold(tmp, hipFree);
+    HIPC(hipMemsetAsync(tmp, 0, 16 * slots, c->stream));
+    IndexArgs a{};
+    a.key_data = x->key_data;
+    a.key_off = x->key_off;
+    a.slots = x->slots;
+    a.loc = x->loc;
+    a.mask = x->mask;
+    a.n = x->n;
+    a.err = x->err;
+    HIPC(launch_index_seq(a, seqs, tmp, tmp + slots, c->stream));
+    unsigned long long word = 0;
+    HIPC(hipMemcpyAsync(&word, x->err, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPC(hipStreamSynchronize(c->stream));
+    if (word) return set_err(err, MURR_E_INTERNAL);
     return MURR_OK;
 }
 
@@ -812,7 +882,12 @@ int decode_enqueue_jit(murr_ctx* c, const murr_segment_t* seg, const JitLayout* 
     const uint64_t d_slots = round_up(d_segs + sizeof(JitSeg) * segs_out.size(), 16);
     const uint64_t d_projc = round_up(d_slots + 2 * (uint64_t)npad * rounds, 16);
     const uint64_t d_sink = round_up(d_projc + 2 * (uint64_t)nproj, 256);
-    const uint64_t dend = d_sink + 1024;
+#ifdef MURR_TUNING
+    const uint64_t tl_bytes = 32 * grid;  // a stamped build's timeline (MJ_TIMELINE writes it to the sink)
+#else
+    const uint64_t tl_bytes = 0;
+#endif
+    const uint64_t dend = d_sink + std::max<uint64_t>(1024, tl_bytes);
     int st = MURR_OK;
     uint8_t* ws = nullptr;
     if (rep) {
@@ -881,6 +956,11 @@ int decode_enqueue_jit(murr_ctx* c, const murr_segment_t* seg, const JitLayout* 
                      K.nw, K.r, K.nslot, cut ? "local-cut" : local ? "local" : "split", (unsigned long long)grid, bpc, bpc_safe,
                      (unsigned long long)(local ? lsegs.size() : nonempty),
                      (unsigned long long)tiles, (unsigned long long)nseg, (unsigned long long)seg_tiles, K.tr, stage, lds, rounds);
+#ifdef MURR_TUNING
+    c->tl_off = rep ? 0 : d_sink;
+    c->tl_n = grid;
+    if (tl_bytes) HIPC(hipMemsetAsync(ws + d_sink, 0, tl_bytes, c->stream));
+#endif
     if (rep) {
         rep->zbytes = zbytes;
         rep->z_lb = z_lb;
@@ -1264,6 +1344,9 @@ int murr_decode_wait(murr_ctx_t* c, murr_error_t* err) {
     if (!c || !c->pending) return set_err(err, MURR_E_ARGUMENT);
     c->pending = false;
     HIPC(hipStreamSynchronize(c->stream));
+#ifdef MURR_TUNING
+    if (c->opts.verbose && c->tl_off) print_timeline(c);
+#endif
     const uint8_t* rb = c->hs + c->rb_off;
     unsigned long long word;
     std::memcpy(&word, rb, 8);

@@ -142,6 +142,54 @@ __global__ void __launch_bounds__(256) index_insert(IndexArgs A) {
     report(A.err, err_key(0, i, 0, kStInternal));  // table full: cannot happen at load <= 1/2
 }
 
+// Slot holding stored key i (inserted already): index_probe's walk over the
+// index's own key copy.
+__device__ __forceinline__ uint64_t slot_of(const IndexArgs& A, uint64_t i) {
+    const GAS int32_t* ko = gp(A.key_off);
+    const int32_t k0 = ko[i];
+    const uint32_t len = (uint32_t)(ko[i + 1] - k0);
+    const GAS uint8_t* key = gp(A.key_data) + k0;
+    KeyChunk kc;
+    const uint64_t h = key_hash(key, len, &kc);
+    const GAS uint64_t* slots = gp(A.slots);
+    const GAS uint64_t* loc = gp(A.loc);
+    uint64_t s = h & A.mask;
+    for (uint64_t probe = 0; probe <= A.mask; probe++, s = (s + 1) & A.mask) {
+        const uint64_t e = slots[s], l = loc[s];
+        if (e == kEmpty) break;
+        if ((e >> 32) == (h >> 32) && (uint32_t)l == len && key_eq(gp(A.key_data) + (uint32_t)(l >> 32), kc, key, len))
+            return s;
+    }
+    return kEmpty;
+}
+
+// Equal keys resolved by sequence number instead of row (SST entries: RocksDB
+// keeps a user key's versions newest first, and overlapping files repeat
+// keys in any order; the version with the highest sequence number is the
+// live one, DBImpl's read path).  Phase 0, per row: best[slot] = max seq;
+// phase 1, per row holding that seq: win[slot] = max row + 1 (equal seqs:
+// the later row); phase 2, per slot: install the winner.
+__global__ void __launch_bounds__(256) index_seq(IndexArgs A, const uint64_t* seqs, unsigned long long* best,
+                                                 unsigned long long* win, uint32_t phase) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (phase == 2) {
+        if (i > A.mask) return;
+        const uint64_t w = gp(win)[i];
+        if (w) gp(A.slots)[i] = (gp(A.slots)[i] & 0xFFFFFFFF00000000ull) | (w - 1);
+        return;
+    }
+    if (i >= A.n) return;
+    const uint64_t s = slot_of(A, i);
+    if (s == kEmpty) {
+        report(A.err, err_key(0, i, 0, kStInternal));
+        return;
+    }
+    const uint64_t q = gp(seqs)[i];
+    if (phase == 0) __hip_atomic_fetch_max(gp(best) + s, (unsigned long long)q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else if (q == gp(best)[s])
+        __hip_atomic_fetch_max(gp(win) + s, (unsigned long long)(i + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // Row of query i, or kMissing.
 __device__ __forceinline__ uint32_t probe_one(const IndexArgs& A, uint64_t i) {
     const GAS int32_t* qo = gp(A.q_off);
@@ -339,6 +387,16 @@ hipError_t launch_index_insert(const IndexArgs& a, hipStream_t s) {
 hipError_t launch_index_probe(const IndexArgs& a, hipStream_t s) {
     if (!a.nq) return hipSuccess;
     hipLaunchKernelGGL(index_probe, dim3((uint32_t)((a.nq + 255) / 256)), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_index_seq(const IndexArgs& a, const uint64_t* seqs, unsigned long long* best,
+                            unsigned long long* win, hipStream_t s) {
+    if (!a.n) return hipSuccess;
+    for (uint32_t ph = 0; ph < 3; ph++) {
+        const uint64_t n = ph == 2 ? a.mask + 1 : a.n;
+        hipLaunchKernelGGL(index_seq, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, a, seqs, best, win, ph);
+    }
     return hipGetLastError();
 }
 

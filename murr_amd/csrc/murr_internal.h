@@ -23,7 +23,8 @@ constexpr uint32_t kStage = 32768;
 // Default decode stage (bytes of row blobs per tile held in LDS).
 constexpr uint32_t kDecStage = 36864;
 // Workspace head: the error word, then phase-stamp slots of tuning builds
-// (err[2 .. 2 + kStampSlots)), then the per-(block, column) counters.
+// (err[2 .. 2 + kStampSlots)), then the per-(block, column) counters.  The
+// last stamp slot, err[17], is the JIT kernel's virtual-block queue.
 constexpr uint32_t kStampSlots = 16;
 constexpr uint64_t kErrBytes = 8 * (2 + kStampSlots);
 // Projected columns per decode call (10 bits in the packed error key).
@@ -263,6 +264,8 @@ struct IndexArgs {
 };
 hipError_t launch_index_insert(const IndexArgs& a, hipStream_t s);
 hipError_t launch_index_probe(const IndexArgs& a, hipStream_t s);
+hipError_t launch_index_seq(const IndexArgs& a, const uint64_t* seqs, unsigned long long* best,
+                            unsigned long long* win, hipStream_t s);
 uint64_t gather_scan_groups(uint64_t nq);
 hipError_t launch_gather(const IndexArgs& a, hipStream_t s);
 hipError_t launch_gather_scan(const IndexArgs& a, hipStream_t s);  // probe + sizes + scan, no copy

@@ -17,6 +17,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -258,7 +259,9 @@ bool compile(Entry& e, const std::string& pre, int device) {
 uint32_t jit_lds_bytes(uint32_t nw, uint32_t r, uint32_t nslot, uint32_t stage, uint32_t nutf8) {
     const uint32_t tr = 64 * (nw - 1) * r;
 #ifdef MURR_TUNING
-    const uint32_t ro = ((tr + 1) * 8 + 16 + 15) & ~15u;  // room for MJ_RO64=1 (whole u64 row offsets)
+    const char* defs = std::getenv("MURR_JIT_DEFS");
+    const uint32_t rw = defs && std::strstr(defs, "MJ_RO64=1") ? 8 : 4;  // MJ_RO64=1: whole u64 row offsets
+    const uint32_t ro = ((tr + 1) * rw + 16 + 15) & ~15u;
 #else
     const uint32_t ro = ((tr + 1) * 4 + 16 + 15) & ~15u;
 #endif

@@ -115,6 +115,7 @@ struct Args {
     uint16_t slot[(NCOLS + 1) & ~1u];  // output position of column c, 0xFFFF = not decoded
 };
 constexpr uint16_t kNone = 0xFFFF;
+constexpr uint32_t kQueueWord = 17;  // err[17]: local mode's virtual-block queue (the last stamp slot)
 
 enum : uint32_t { kStUtf8 = 1, kStOverflow = 4, kStMalformed = 5, kStCapacity = 6, kStInternal = 10 };
 // Phase stamps of tuning builds (MURR_JIT_DEFS=MJ_STAMPS): shader cycles
@@ -409,6 +410,27 @@ DEV Cur cur_seg(uint32_t k) {
     return cur_make(ok, k, ok ? sgpr(sp->b) : 0u, ok ? sgpr(sp->first) : 0u, 1, rb, re, rb);
 }
 template <uint32_t MODE> DEV Cur cur_first() { return MODE == 0 ? cur_local(blockIdx.x) : cur_seg(blockIdx.x); }
+// Tuning (MJ_QUEUE=1): local mode hands out the virtual blocks after each
+// workgroup's first from a queue (a counter beside the error word, zeroed
+// with it), so a workgroup that runs fast takes more of them.  Measured
+// slower: one agent-scope counter serves about one claim per 10 ns, so the
+// D shard's first tiles waited 13 us (512-row virtual blocks, 0.086 -> 0.097
+// ms) and 52 us (128-row ones, 0.167 ms); C gained 1-2 %, B neutral.  The
+// static deal (workgroup g takes g, g + G, ...) stays.
+#ifndef MJ_QUEUE
+#define MJ_QUEUE 0
+#endif
+DEV uint32_t claim_vblock(uint32_t k_static) {
+#if MJ_QUEUE
+    (void)k_static;
+    uint32_t k = 0;
+    if (lane_id() == 0)
+        k = __hip_atomic_fetch_add((GAS uint32_t*)(args()->err + kQueueWord), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return gridDim.x + sgpr(k);
+#else
+    return k_static;
+#endif
+}
 // The next tile: local mode walks the block, then the next block of the
 // order; split mode walks the segment, then walks it again (second pass,
 // when there are utf8 cells to write), then takes segment k + G.
@@ -419,7 +441,7 @@ template <uint32_t TR> DEV Cur cur_next(const Cur& c) {
         n.r0 = c.r0 + TR;
         return n;
     }
-    if (c.phase == 0) return cur_local(c.k + gridDim.x);
+    if (c.phase == 0) return cur_local(claim_vblock(c.k + gridDim.x));
     if (c.phase == 1 && args()->emit) {
         Cur n = c;
         n.phase = 2;
@@ -1359,10 +1381,20 @@ DEV void kernel_body() {
 #ifdef MJ_STAMPS
     const uint64_t ct0 = __builtin_amdgcn_s_memtime();
 #endif
+#ifdef MJ_TIMELINE
+    const uint64_t tl0 = __builtin_amdgcn_s_memrealtime();
+    uint32_t tl_tiles = 0;
+#endif
     lds_barrier();  // B_0
+#ifdef MJ_TIMELINE
+    const uint64_t tl_b0 = __builtin_amdgcn_s_memrealtime();
+#endif
     for (uint32_t it = 0;; it++) {
         const LAS uint8_t* info = infos + (it & 7) * 32;
         if (!tile_valid(info)) break;
+#ifdef MJ_TIMELINE
+        tl_tiles++;
+#endif
         LAS uint8_t* slot = lds + (it % NSLOT) * SLOT;
         const Tile T = tile_read(spans + (it & 7) * 16, info, stage);
         const LAS uint32_t* ro = (const LAS uint32_t*)slot;
@@ -1419,6 +1451,16 @@ DEV void kernel_body() {
 #ifdef MJ_STAMPS
     if (lane == 0)
         __hip_atomic_fetch_add((GAS unsigned long long*)args()->err + 2 + 9, (unsigned long long)(__builtin_amdgcn_s_memtime() - ct0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
+#ifdef MJ_TIMELINE
+    // timeline (MURR_JIT_DEFS=MJ_TIMELINE=1, tuning builds) (100 MHz realtime): decode wave 0's start, first tile, end,
+    // tiles, and where the workgroup ran (HW_ID, XCC_ID)
+    if (wave == 0 && lane < 4) {
+        const uint64_t hw = ((uint64_t)__builtin_amdgcn_s_getreg(20 | (15 << 11)) << 32) | __builtin_amdgcn_s_getreg(4 | (31 << 11));
+        const uint64_t tl_end = __builtin_amdgcn_s_memrealtime();
+        const uint64_t v = lane == 0 ? tl0 : lane == 1 ? tl_b0 : lane == 2 ? tl_end : ((uint64_t)tl_tiles | (hw << 16));
+        ((GAS uint64_t*)args()->sink)[(uint64_t)blockIdx.x * 4 + lane] = v;
+    }
 #endif
     if (args()->rb_host) epilogue<NC>(ctl, lane);
 }

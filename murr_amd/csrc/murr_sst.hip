@@ -485,6 +485,11 @@ __device__ __forceinline__ bool winflate_lz4(const uint8_t* c, uint32_t p, uint3
     return o == ulen;
 }
 
+// A claimed uncompressed length no stream of n bytes can reach is malformed
+// before anything is sized from it: LZ4 expands at most 255 x (one length
+// byte per 255 bytes of match), Snappy about 21 x (a 3-byte copy of 64).
+__device__ __forceinline__ bool expansion_ok(uint64_t ulen, uint64_t n) { return ulen <= 256 * n + 64; }
+
 // Stage + inflate a block into L.raw: 1 ok, 0 malformed, 2 larger than the
 // slot (big_len = its uncompressed size).  The block is L.raw[r0, r0 + ulen).
 template <uint32_t G, class Lds>
@@ -501,7 +506,7 @@ __device__ __forceinline__ int wave_inflate(const SstBlock& blk, Lds& L, uint32_
     if (blk.size > Lds::kComp) {  // sized from the length prefix, read from HBM
         const uint8_t* p = blk.data;
         uint32_t v = 0;
-        if (!varint32(p, blk.data + blk.size, v)) return 0;
+        if (!varint32(p, blk.data + blk.size, v) || !expansion_ok(v, blk.size)) return 0;
         big_len = v;
         return 2;
     }
@@ -511,7 +516,7 @@ __device__ __forceinline__ int wave_inflate(const SstBlock& blk, Lds& L, uint32_
     // the varint32 length prefix (Snappy's own, RocksDB's for LZ4)
     uint32_t v = 0;
     const uint32_t hl = n ? wvarint(L.comp, c0, c0 + n, v) : 0;
-    if (!hl) return 0;
+    if (!hl || !expansion_ok(v, n)) return 0;
     big_len = v;
     if (v > Lds::kRaw) return 2;
     ulen = v;

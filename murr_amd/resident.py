@@ -272,8 +272,11 @@ class ResidentTable:
         (murr_amd.sst.decode): the values are the table's row blobs and become
         the arena as they lie, the user keys go into the device index.  The
         entries must be live rows (value type kTypeValue, as in a compacted
-        bottommost file); a key seen twice maps to its later entry, as with
-        write().  Nothing but the value lengths and types crosses to the host."""
+        bottommost file).  A key seen more than once maps to its entry with
+        the highest sequence number (RocksDB keeps a key's versions newest
+        first within a file, and overlapping files repeat keys in any order;
+        murr_index_prefer_seq).  Nothing but the value lengths and types
+        crosses to the host."""
         if self.n:
             raise SegmentError("load_sst rehydrates an empty resident table")
         n = entries.n
@@ -285,6 +288,9 @@ class ResidentTable:
             raise SegmentError(f"entry {i} has value type {int(types[i])}: only live values (type 1) rehydrate")
         lens = np.diff(entries.value_offsets.download(8 * (n + 1)).view(np.uint64))
         self.index = DeviceIndex(self.ctx, device_keys=(entries.keys, entries.key_offsets, n))
+        err = _abi.Error()
+        raise_status(self.ctx.L.murr_index_prefer_seq(self.ctx.h, self.index.h, entries.seqs.ptr, C.byref(err)),
+                     err, "murr_index_prefer_seq")
         self.arena, self.arena_cap = entries.values, entries.value_bytes + 16
         self.row_off, self.off_cap = entries.value_offsets, n + 1
         self.used, self.n = entries.value_bytes, n

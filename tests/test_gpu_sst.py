@@ -53,6 +53,24 @@ def test_blocks_bit_exact(comp, restart, hash_index):
     check([(G.compress(b, comp), comp) for b in blocks])
 
 
+def snappy_wrap(raw: bytes) -> bytes:
+    """A Snappy stream of `raw` with a literal of length field 0xFFFFFFFF
+    spliced in after the header (tag 0xFC: four length bytes).  The Snappy
+    library computes len + 1 in 32 bits and reads an empty literal
+    (tests/test_sst.py pins that against pyarrow's codec), so the block
+    decodes as `raw` on the device too."""
+    good = G.snappy(raw)
+    hdr = G.varint32(len(raw))
+    assert good.startswith(hdr)
+    return hdr + b"\xfc\xff\xff\xff\xff" + good[len(hdr):]
+
+
+def test_snappy_wrapped_literal_length_as_the_library():
+    rng = np.random.default_rng(5)
+    blocks = G.blocks_of(G.random_entries(rng, 300), restart_interval=8)
+    check([(snappy_wrap(b) if i % 2 else G.snappy(b), G.SNAPPY) for i, b in enumerate(blocks)])
+
+
 def test_mixed_compression_and_block_sizes():
     rng = np.random.default_rng(11)
     entries = G.random_entries(rng, 4000, max_key=60, max_val=2000, dup_p=0.1)
@@ -110,7 +128,8 @@ def test_many_blocks_scan_carry():
     assert np.all(e.seqs.download(8 * nb).view(np.uint64) == 5)
 
 
-@pytest.mark.parametrize("bad", ["truncated_snappy", "lz4_cut", "unknown_type", "footer", "varint", "shared"])
+@pytest.mark.parametrize("bad", ["truncated_snappy", "huge_len", "lz4_cut", "unknown_type", "footer", "varint",
+                                 "shared"])
 def test_first_corrupt_block_is_named(bad):
     rng = np.random.default_rng(3)
     blocks = G.blocks_of(G.random_entries(rng, 600), restart_interval=8)
@@ -119,6 +138,11 @@ def test_first_corrupt_block_is_named(bad):
     raw = blocks[9]
     if bad == "truncated_snappy":
         broken = (G.snappy(raw)[:-3], G.SNAPPY)
+    elif bad == "huge_len":
+        # a length prefix of ~4 GiB no stream of this size can inflate to:
+        # malformed before anything is allocated from it
+        good = G.snappy(raw)
+        broken = (G.varint32(0xFFFFFFF0) + good[len(G.varint32(len(raw))):], G.SNAPPY)
     elif bad == "lz4_cut":
         broken = (G.lz4(raw)[:-1], G.LZ4)
     elif bad == "unknown_type":
@@ -168,3 +192,38 @@ def test_rehydrate_rejects_tombstones():
     t = ResidentTable(schema_c())
     with pytest.raises(SegmentError, match="entry 1"):
         t.load_sst(sst.decode_host(t.ctx, [(blk, 0)]))
+
+
+def _versions(batch, seq0):
+    """(user key, seq, type, row blob) of every row of `batch`, as a table's
+    write would store them."""
+    src = ResidentTable(schema_c())
+    src.write(batch)
+    arena = src.arena.download(src.used).tobytes()
+    offs = src.row_off.download(8 * (src.n + 1)).view(np.uint64)
+    keys = batch.column(0).to_pylist()
+    return [(keys[i].encode(), seq0 + i, G.TYPE_VALUE, arena[offs[i]:offs[i + 1]]) for i in range(len(keys))]
+
+
+@pytest.mark.parametrize("layout", ["one_file", "newer_file_first", "newer_file_last"])
+def test_rehydrate_duplicate_keys_take_the_highest_seq(layout):
+    # keys 2500..2999 exist in two versions: the newer (higher seq) must win,
+    # wherever it sits -- first of its key in one file (RocksDB's order: user
+    # key ascending, seq descending), or in a second file listed before or
+    # after the first
+    old, new = batch_c(3000, seed=1), batch_c(1000, start=2500, seed=2)
+    v_old, v_new = _versions(old, 100), _versions(new, 10_000)
+    order = lambda es: sorted(es, key=lambda e: (e[0], -e[1]))  # noqa: E731
+    if layout == "one_file":
+        files = [order(v_old + v_new)]
+    elif layout == "newer_file_first":
+        files = [order(v_new), order(v_old)]
+    else:
+        files = [order(v_old), order(v_new)]
+    stored = [(G.snappy(b), G.SNAPPY) for f in files for b in G.blocks_of(f)]
+    t = ResidentTable(schema_c())
+    t.load_sst(sst.decode_host(t.ctx, stored))
+    rng = np.random.default_rng(9)
+    q = [f"key{i}" for i in rng.integers(2400, 3600, size=1500)] + ["key2500", "key2999", "key0"]
+    cols = [f"c{i}" for i in range(16)]
+    assert_same(t.read(q, cols), expected([old, new], q, cols))

@@ -40,6 +40,18 @@ def test_snappy_corrupt_is_an_error():
         O.snappy_decompress(b"\xff\xff\xff\xff\xff\xff")
 
 
+def test_snappy_literal_of_2_pow_32_reads_as_snappy_does():
+    # a 4-byte literal length of 0xFFFFFFFF spliced after the header: the
+    # Snappy library (pyarrow's, the codec RocksDB links) computes len + 1 in
+    # 32 bits and reads an empty literal, so the stream still decodes; the
+    # restatement (and the device inflaters, tests/test_gpu_sst.py) do the same
+    data = b"hello hello hello hello"
+    good = pa.Codec("snappy").compress(data, asbytes=True)
+    bad = good[:1] + b"\xfc\xff\xff\xff\xff" + good[1:]
+    assert pa.Codec("snappy").decompress(bad, decompressed_size=len(data), asbytes=True) == data
+    assert O.snappy_decompress(bad) == data
+
+
 @pytest.mark.parametrize("data", [b"", b"a", b"abcd" * 3, b"hello hello hello hello", bytes(range(256)) * 40,
                                   b"x" * 100000, b"ab" * 7000])
 def test_lz4_matches_pyarrow(data):
