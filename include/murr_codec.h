@@ -436,6 +436,37 @@ int murr_index_append(murr_ctx_t* ctx, murr_index_t* idx, const uint8_t* key_dat
  * descending) and overlapping files repeat keys in any order; the version
  * with the highest sequence number is the one a read returns.  Synchronous. */
 int murr_index_prefer_seq(murr_ctx_t* ctx, murr_index_t* idx, const uint64_t* seqs, murr_error_t* err);
+/* One read over a table sharded by key across GPUs (SURVEY.md §8(e) mode 2),
+ * without a collective and with no host synchronisation: the caller's nq
+ * query keys sit on the home GPU grouped by owner shard (shard s owns grouped
+ * positions [shards[s-1].q_end, shards[s].q_end)), src[i] = the grouped
+ * position of caller query i.  Each shard looks its keys up on its own
+ * context's stream, all shards at once (reading the keys from home memory,
+ * writing rows[p] there); the home stream waits on those lookups (events, not
+ * the host), then writes the caller-order block: out_row_off (nq + 1) and the
+ * rows' blobs copied straight from each shard's arena (peer reads over xGMI)
+ * -- row i is the row of key i, a miss an empty row (the positional contract
+ * of RocksDBStore::read, src/io/store/rocksdb/mod.rs:368-399).  out_data
+ * NULL: sizes and offsets only (*needed = the block's bytes), then
+ * murr_multi_gather_copy.  Offsets are clamped to out_cap; *needed (optional
+ * with out_data) gets the true total.  A shard with no index (nothing written)
+ * misses every key.  At most 16 shards.  Asynchronous on the home stream. */
+typedef struct {
+    murr_ctx_t* ctx;             /* the shard's context (its GPU and stream) */
+    const murr_index_t* index;   /* its key index (NULL: empty shard) */
+    const uint8_t* arena;        /* its row blobs */
+    const uint64_t* row_off;     /* and their offsets */
+    uint64_t q_end;              /* end of its grouped query range */
+} murr_shard_read_t;
+int murr_multi_gather(murr_ctx_t* home, const murr_shard_read_t* shards, uint32_t nshards,
+                      const uint8_t* q_data, const int32_t* q_offsets, const uint32_t* src, uint64_t nq,
+                      uint32_t* rows, uint64_t* out_row_off, uint8_t* out_data, uint64_t out_cap,
+                      uint64_t* needed, murr_error_t* err);
+/* The copy of a murr_multi_gather whose out_data was NULL, into out_data
+ * (>= *needed bytes, 16-B aligned).  Asynchronous on the home stream. */
+int murr_multi_gather_copy(murr_ctx_t* home, const murr_shard_read_t* shards, uint32_t nshards,
+                           const uint32_t* src, uint64_t nq, const uint32_t* rows,
+                           const uint64_t* out_row_off, uint8_t* out_data, murr_error_t* err);
 /* Rows indexed (n at build) and hash-table slots. */
 int murr_index_info(const murr_index_t* idx, uint64_t* n, uint64_t* slots);
 

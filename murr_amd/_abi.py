@@ -61,6 +61,11 @@ class ColIn(C.Structure):
                 ("offset", C.c_uint64)]
 
 
+class ShardRead(C.Structure):
+    _fields_ = [("ctx", C.c_void_p), ("index", C.c_void_p), ("arena", C.c_void_p), ("row_off", C.c_void_p),
+                ("q_end", C.c_uint64)]
+
+
 class SstBlock(C.Structure):
     _fields_ = [("data", C.c_void_p), ("size", C.c_uint64), ("compression", C.c_uint32), ("_pad", C.c_uint32)]
 
@@ -157,6 +162,8 @@ SIGNATURES = {
     "murr_index_append": (I32, [P, P, P, P, U64, U64, C.POINTER(Error)]),
     "murr_index_info": (I32, [P, C.POINTER(U64), C.POINTER(U64)]),
     "murr_index_prefer_seq": (I32, [P, P, P, C.POINTER(Error)]),
+    "murr_multi_gather": (I32, [P, C.POINTER(ShardRead), U32, P, P, P, U64, P, P, P, U64, P, C.POINTER(Error)]),
+    "murr_multi_gather_copy": (I32, [P, C.POINTER(ShardRead), U32, P, U64, P, P, P, C.POINTER(Error)]),
     "murr_index_lookup": (I32, [P, P, P, P, U64, P]),
     "murr_index_gather": (I32, [P, P, P, P, U64, P, P, P, U64, P, P, P]),
     "murr_index_gather_copy": (I32, [P, P, U64, P, P, P, P]),

@@ -10,6 +10,8 @@
 #include <algorithm>
 #include <atomic>
 #include <map>
+#include <mutex>
+#include <set>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -100,6 +102,7 @@ struct murr_ctx {
     std::vector<hipEvent_t> event_pool;
     uint64_t* aux = nullptr;  // device scratch of the gather scan (group sums)
     uint64_t aux_cap = 0;     // entries
+    hipEvent_t xev = nullptr; // multi-GPU reads: this stream's work, awaited by the home stream
 };
 
 // Device key index (murr_index.hip): the keys' own copy and the slot table.
@@ -360,6 +363,18 @@ int murr_index_info(const murr_index_t* x, uint64_t* n, uint64_t* slots) {
 }
 
 namespace {
+// Device scratch of the gather scans (group sums, rows): at least `need` u64.
+int ensure_aux(murr_ctx* c, uint64_t need, murr_error_t* err) {
+    if (need <= c->aux_cap) return MURR_OK;
+    if (c->aux) HIPC(hipFree(c->aux));
+    c->aux = nullptr;
+    c->aux_cap = 0;
+    const uint64_t cap = std::max<uint64_t>(need, 1 << 16);
+    HIPC(hipMalloc(&c->aux, 8 * cap));
+    c->aux_cap = cap;
+    return MURR_OK;
+}
+
 IndexArgs index_args(const murr_index_t* x, const uint8_t* q_data, const int32_t* q_offsets, uint64_t nq) {
     IndexArgs a{};
     a.key_data = x->key_data;
@@ -402,14 +417,7 @@ int murr_index_gather(murr_ctx_t* c, const murr_index_t* x, const uint8_t* q_dat
     // scratch: the scan's group sums, then the rows when the caller wants none
     const uint64_t groups = gather_scan_groups(nq);
     const uint64_t need = groups + 1 + (rows ? 0 : (nq + 1) / 2);
-    if (need > c->aux_cap) {
-        if (c->aux) HIPC(hipFree(c->aux));
-        c->aux = nullptr;
-        c->aux_cap = 0;
-        const uint64_t cap = std::max<uint64_t>(need, 1 << 16);
-        HIPC(hipMalloc(&c->aux, 8 * cap));
-        c->aux_cap = cap;
-    }
+    if (const int st = ensure_aux(c, need, err)) return st;
     IndexArgs a = index_args(x, q_data, q_offsets, nq);
     a.rows = rows ? rows : (uint32_t*)(c->aux + groups + 1);
     a.blob = blob;
@@ -425,6 +433,118 @@ int murr_index_gather(murr_ctx_t* c, const murr_index_t* x, const uint8_t* q_dat
     } else {
         HIPC(launch_gather(a, c->stream));  // probe included
     }
+    return MURR_OK;
+}
+
+namespace {
+// Peer access dev -> peer (kernels on dev dereference peer's memory over
+// xGMI), enabled once per pair.
+int enable_peer(int dev, int peer, murr_error_t* err) {
+    if (dev == peer) return MURR_OK;
+    static std::mutex mu;
+    static std::set<std::pair<int, int>> done;
+    std::lock_guard<std::mutex> g(mu);
+    if (done.count({dev, peer})) return MURR_OK;
+    HIPC(hipSetDevice(dev));
+    const hipError_t e = hipDeviceEnablePeerAccess(peer, 0);
+    if (e == hipErrorPeerAccessAlreadyEnabled) (void)hipGetLastError();
+    else if (e != hipSuccess) return hip_fail(err, e);
+    done.insert({dev, peer});
+    return MURR_OK;
+}
+
+int multi_tab(murr_ctx_t* home, const murr_shard_read_t* shards, uint32_t nshards, uint64_t nq, MultiTab* t,
+              murr_error_t* err) {
+    if (!home || !shards || !nshards || nshards > kMaxShards || home->pending) return set_err(err, MURR_E_ARGUMENT);
+    t->n = nshards;
+    uint64_t prev = 0;
+    for (uint32_t s = 0; s < nshards; s++) {
+        const murr_shard_read_t& sh = shards[s];
+        if (!sh.ctx || sh.q_end < prev || sh.q_end > nq || sh.ctx->pending ||
+            (sh.index && (sh.index->device != sh.ctx->device || (sh.index->n && (!sh.arena || !sh.row_off)))))
+            return set_err(err, MURR_E_ARGUMENT);
+        t->arena[s] = sh.arena;
+        t->row_off[s] = sh.row_off;
+        t->q_end[s] = sh.q_end;
+        prev = sh.q_end;
+    }
+    if (prev != nq) return set_err(err, MURR_E_ARGUMENT);
+    return MURR_OK;
+}
+}  // namespace
+
+int murr_multi_gather(murr_ctx_t* home, const murr_shard_read_t* shards, uint32_t nshards, const uint8_t* q_data,
+                      const int32_t* q_offsets, const uint32_t* src, uint64_t nq, uint32_t* rows,
+                      uint64_t* out_row_off, uint8_t* out_data, uint64_t out_cap, uint64_t* needed,
+                      murr_error_t* err) {
+    MultiTab t{};
+    int st = multi_tab(home, shards, nshards, nq, &t, err);
+    if (st) return st;
+    if (!out_row_off || (nq && (!q_data || !q_offsets || !src || !rows)) || (!out_data && !needed) ||
+        nq >= kMissing || ((uintptr_t)out_data & 15))
+        return set_err(err, MURR_E_ARGUMENT);
+    // 1. every shard looks up its queries on its own stream (all concurrently);
+    //    the home stream waits for each shard's lookup, never the host
+    uint64_t q0 = 0;
+    for (uint32_t s = 0; s < nshards; s++) {
+        const murr_shard_read_t& sh = shards[s];
+        const uint64_t n = sh.q_end - q0;
+        murr_ctx* sc = sh.ctx;
+        if (n && sh.index && sh.index->n) {
+            if ((st = enable_peer(sc->device, home->device, err))) return st;
+            HIPC(hipSetDevice(sc->device));
+            IndexArgs a = index_args(sh.index, q_data, q_offsets + q0, n);
+            a.rows = rows + q0;
+            HIPC(launch_index_probe(a, sc->stream));
+            if (sc != home) {
+                if (!sc->xev) HIPC(hipEventCreateWithFlags(&sc->xev, hipEventDisableTiming));
+                HIPC(hipEventRecord(sc->xev, sc->stream));
+                HIPC(hipSetDevice(home->device));
+                HIPC(hipStreamWaitEvent(home->stream, sc->xev, 0));
+            }
+        } else if (n) {  // nothing written to this shard yet: every key is missing
+            HIPC(hipSetDevice(home->device));
+            HIPC(hipMemsetAsync(rows + q0, 0xFF, 4 * n, home->stream));
+        }
+        q0 = sh.q_end;
+    }
+    // 2. on home: sizes in caller order, their scan, the rows copied from the
+    //    shards' arenas (peer reads)
+    for (uint32_t s = 0; s < nshards; s++)
+        if ((st = enable_peer(home->device, shards[s].ctx->device, err))) return st;
+    HIPC(hipSetDevice(home->device));
+    if ((st = ensure_aux(home, gather_scan_groups(nq) + 1, err))) return st;
+    IndexArgs a{};
+    a.nq = nq;
+    a.src = src;
+    a.rows = rows;
+    a.sizes = out_row_off;
+    a.out = out_data;
+    a.out_cap = out_data ? out_cap : ~0ull;
+    a.needed = needed;
+    a.scratch = home->aux;
+    if (nq) HIPC(launch_multi_gather(a, t, out_data != nullptr, home->stream));
+    else HIPC(hipMemsetAsync(out_row_off, 0, 8, home->stream));
+    if (!nq && needed) HIPC(hipMemsetAsync(needed, 0, 8, home->stream));
+    return MURR_OK;
+}
+
+int murr_multi_gather_copy(murr_ctx_t* home, const murr_shard_read_t* shards, uint32_t nshards, const uint32_t* src,
+                           uint64_t nq, const uint32_t* rows, const uint64_t* out_row_off, uint8_t* out_data,
+                           murr_error_t* err) {
+    MultiTab t{};
+    int st = multi_tab(home, shards, nshards, nq, &t, err);
+    if (st) return st;
+    if (nq && (!src || !rows || !out_row_off || !out_data || ((uintptr_t)out_data & 15)))
+        return set_err(err, MURR_E_ARGUMENT);
+    HIPC(hipSetDevice(home->device));
+    IndexArgs a{};
+    a.nq = nq;
+    a.src = src;
+    a.rows = const_cast<uint32_t*>(rows);
+    a.sizes = const_cast<uint64_t*>(out_row_off);
+    a.out = out_data;
+    HIPC(launch_multi_copy(a, t, home->stream));
     return MURR_OK;
 }
 
@@ -531,6 +651,7 @@ void murr_ctx_destroy(murr_ctx_t* c) {
     if (c->hs) (void)hipHostFree(c->hs);
     for (const auto& b : c->pool) (void)(b.pinned ? hipHostFree(b.p) : hipFree(b.p));
     for (hipEvent_t e : c->event_pool) (void)hipEventDestroy(e);
+    if (c->xev) (void)hipEventDestroy(c->xev);
     if (c->k0) (void)hipEventDestroy(c->k0);
     if (c->k1) (void)hipEventDestroy(c->k1);
     if (c->stream) (void)hipStreamDestroy(c->stream);

@@ -333,18 +333,10 @@ __global__ void __launch_bounds__(kScanThreads) gather_probe_scan(IndexArgs A) {
 // with v_alignbyte.  Interior blocks are one 16-B store, the row's first and
 // last blocks byte stores.  One row per wave (the first version) spent most of
 // its time creating waves: ~100-B rows gave a wave one load and one store.
+// Lane j of kCopyLanes copies the row at blob[s0 ..) to out[d0, d1).
 template <uint32_t kCopyLanes>
-__global__ void __launch_bounds__(256) gather_copy(IndexArgs A) {
-    const uint64_t i = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / kCopyLanes;
-    const uint32_t j = threadIdx.x % kCopyLanes;
-    if (i >= A.nq) return;
-    const uint32_t row = gp(A.rows)[i];
-    if (row == kMissing) return;
-    const uint64_t d0 = gp(A.sizes)[i], d1 = gp(A.sizes)[i + 1];
-    if (d1 <= d0) return;
-    const uint64_t s0 = gp(A.row_off)[row];
-    const GAS uint8_t* blob = gp(A.blob);
-    GAS uint8_t* out = gp(A.out);
+__device__ __forceinline__ void copy_row(const GAS uint8_t* blob, uint64_t s0, GAS uint8_t* out, uint64_t d0,
+                                         uint64_t d1, uint32_t j) {
     const uint64_t first = d0 & ~(uint64_t)15;
     for (uint64_t D = first + 16 * (uint64_t)j; D < d1; D += 16 * kCopyLanes) {
         const uint64_t lo = D > d0 ? D : d0, hi = D + 16 < d1 ? D + 16 : d1;
@@ -374,6 +366,53 @@ __global__ void __launch_bounds__(256) gather_copy(IndexArgs A) {
             }
         }
     }
+}
+
+template <uint32_t kCopyLanes>
+__global__ void __launch_bounds__(256) gather_copy(IndexArgs A) {
+    const uint64_t i = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / kCopyLanes;
+    const uint32_t j = threadIdx.x % kCopyLanes;
+    if (i >= A.nq) return;
+    const uint32_t row = gp(A.rows)[i];
+    if (row == kMissing) return;
+    const uint64_t d0 = gp(A.sizes)[i], d1 = gp(A.sizes)[i + 1];
+    if (d1 <= d0) return;
+    copy_row<kCopyLanes>(gp(A.blob), gp(A.row_off)[row], gp(A.out), d0, d1, j);
+}
+
+// ---- one read over a table sharded across GPUs (murr_multi_gather) ----------------
+// The caller's queries are grouped by owner shard (shard s holds grouped
+// positions [q_end[s - 1], q_end[s])); src[i] = grouped position of caller
+// query i; rows[p] = the row shard s's lookup found for grouped position p.
+// Each query's row is read straight from its shard's arena (peer memory over
+// xGMI when the shard lives on another GPU).
+__device__ __forceinline__ uint32_t multi_shard(const MultiTab& T, uint64_t p) {
+    uint32_t s = 0;
+    while (s + 1 < T.n && p >= T.q_end[s]) s++;
+    return s;
+}
+
+__global__ void __launch_bounds__(256) multi_sizes(IndexArgs A, MultiTab T) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= A.nq) return;
+    const uint64_t p = gp(A.src)[i];
+    const uint32_t row = gp(A.rows)[p];
+    const uint32_t s = multi_shard(T, p);
+    gp(A.sizes)[i] = row == kMissing ? 0 : gp(T.row_off[s])[row + 1] - gp(T.row_off[s])[row];
+}
+
+template <uint32_t kCopyLanes>
+__global__ void __launch_bounds__(256) multi_copy(IndexArgs A, MultiTab T) {
+    const uint64_t i = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / kCopyLanes;
+    const uint32_t j = threadIdx.x % kCopyLanes;
+    if (i >= A.nq) return;
+    const uint64_t p = gp(A.src)[i];
+    const uint32_t row = gp(A.rows)[p];
+    if (row == kMissing) return;
+    const uint64_t d0 = gp(A.sizes)[i], d1 = gp(A.sizes)[i + 1];
+    if (d1 <= d0) return;
+    const uint32_t s = multi_shard(T, p);
+    copy_row<kCopyLanes>(gp(T.arena[s]), gp(T.row_off[s])[row], gp(A.out), d0, d1, j);
 }
 
 }  // namespace
@@ -427,6 +466,34 @@ hipError_t launch_gather_copy(const IndexArgs& a, hipStream_t s) {
         const dim3 grid((uint32_t)((a.nq + rows_per_wg - 1) / rows_per_wg));
         hipLaunchKernelGGL(gather_copy<8>, grid, dim3(256), 0, s, a);
     }
+    return hipGetLastError();
+}
+
+// Sizes of the caller-order block (each query's row in its shard) and their
+// scan into A.sizes; then, when A.out is set, the rows copied.
+hipError_t launch_multi_gather(const IndexArgs& a, const MultiTab& t, bool copy, hipStream_t s) {
+    if (!a.nq) return hipSuccess;
+    hipLaunchKernelGGL(multi_sizes, dim3((uint32_t)((a.nq + 255) / 256)), dim3(256), 0, s, a, t);
+    const uint64_t groups = gather_scan_groups(a.nq);
+    if (groups <= 1) {
+        hipLaunchKernelGGL(gather_scan, dim3(1), dim3(kScanThreads), 0, s, a, 1u);
+    } else {
+        hipLaunchKernelGGL(gather_scan, dim3((uint32_t)groups), dim3(kScanThreads), 0, s, a, 0u);
+        hipLaunchKernelGGL(gather_scan, dim3(1), dim3(kScanThreads), 0, s, a, 2u);
+        hipLaunchKernelGGL(gather_scan, dim3((uint32_t)groups), dim3(kScanThreads), 0, s, a, 1u);
+    }
+    if (copy) {
+        constexpr uint32_t rows_per_wg = 256 / 8;
+        hipLaunchKernelGGL(multi_copy<8>, dim3((uint32_t)((a.nq + rows_per_wg - 1) / rows_per_wg)), dim3(256), 0, s,
+                           a, t);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_multi_copy(const IndexArgs& a, const MultiTab& t, hipStream_t s) {
+    if (!a.nq) return hipSuccess;
+    constexpr uint32_t rows_per_wg = 256 / 8;
+    hipLaunchKernelGGL(multi_copy<8>, dim3((uint32_t)((a.nq + rows_per_wg - 1) / rows_per_wg)), dim3(256), 0, s, a, t);
     return hipGetLastError();
 }
 

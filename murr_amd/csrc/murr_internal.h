@@ -261,7 +261,19 @@ struct IndexArgs {
     uint64_t out_cap;
     uint64_t* needed;           //   out (optional): unclamped block bytes
     uint64_t* scratch;          //   scan group sums
+    const uint32_t* src;        // multi-shard gather: caller query -> grouped position
 };
+// Shards of a multi-GPU read (murr_multi_gather): arenas, row offsets and the
+// end of each shard's grouped query range.
+constexpr uint32_t kMaxShards = 16;
+struct MultiTab {
+    uint32_t n;
+    const uint8_t* arena[kMaxShards];
+    const uint64_t* row_off[kMaxShards];
+    uint64_t q_end[kMaxShards];
+};
+hipError_t launch_multi_gather(const IndexArgs& a, const MultiTab& t, bool copy, hipStream_t s);
+hipError_t launch_multi_copy(const IndexArgs& a, const MultiTab& t, hipStream_t s);
 hipError_t launch_index_insert(const IndexArgs& a, hipStream_t s);
 hipError_t launch_index_probe(const IndexArgs& a, hipStream_t s);
 hipError_t launch_index_seq(const IndexArgs& a, const uint64_t* seqs, unsigned long long* best,

@@ -5,30 +5,35 @@ Rows are owned by key: shard_of(key) (fmix64 of FNV-1a, murr_shard_of) picks
 the GPU, and each GPU holds its shard as a ResidentTable (blob arena + device
 key index).  Table::read (src/io/table/mod.rs:114-129) over the whole table:
 
-1. the caller's keys are routed to their owner shards on the host;
-2. every shard looks its keys up and gathers their row blobs on its own GPU
-   (murr_index_gather; a miss is an empty row);
-3. the gathered blocks are copied to the home GPU, back to back (peer copies
-   over xGMI, murr_memcpy_peer -- point to point, no collective);
-4. one gather on the home GPU puts the rows in caller order
-   (murr_index_gather_copy: row i of the read is the gathered row of key i;
-   the positional contract of the reference store,
+1. the caller's keys are routed to their owner shards on the host and
+   uploaded to the home GPU once, grouped by owner;
+2. every shard looks its keys up on its own GPU and stream, all at once
+   (reading the keys from home memory and writing their rows there, peer
+   access over xGMI);
+3. the home stream waits on those lookups (events, not the host) and builds
+   the caller-order block: each key's row blob is copied straight from its
+   shard's arena (murr_multi_gather: row i of the read is the row of key i, a
+   miss an empty row -- the positional contract of the reference store,
    src/io/store/rocksdb/mod.rs:368-399);
-5. one decode there (murr_decode_blocks) gives the Arrow batch.
+4. one decode there (murr_decode_blocks) gives the Arrow batch; its wait is
+   the read's one host synchronisation.
 
-Only row blobs cross GPUs, once each, and no GPU waits on another except for
-its own peer copy.  Writes route every row to its owner (route_batch), so a
+Only row blobs cross GPUs, once each, no collective runs, and no host round
+trip sits between the shards' lookups and the decode.  Writes route every row to its owner (route_batch), so a
 key written again lands on the shard that holds it and the later write wins
 (src/io/store/memory.rs:47-60).
 """
 from __future__ import annotations
 
+import ctypes as C
+
 import numpy as np
 import pyarrow as pa
 
+from . import _abi
 from .device import DecodeOutputs, DeviceBlock, decode_blocks, download_array
 from .errors import raise_status
-from .resident import ResidentTable, _null_dict, host_batch
+from .resident import TWO_PHASE_BYTES, ResidentTable, _null_dict, host_batch
 from .schema import TableSchema
 from .shard import route_batch, shard_of
 
@@ -62,58 +67,65 @@ class MultiDeviceTable:
         return host_batch(req, hs)
 
     def read_host(self, keys, columns):
+        """The read's columns as host arrays (murr_multi_gather + one decode on
+        home).  The host routes the keys and uploads them once, grouped by
+        owner; everything after is enqueued on the GPUs' streams with
+        stream-to-stream waits, and the host waits once, for the decode."""
         req = self.shards[0]._resolve(columns)
         nq = len(keys)
-        owner = shard_of(keys, self.nshards)
         home = self.home
         L = home.L
-        # 2. per shard: gathered block of its keys (caller order within the shard)
-        parts = []  # (shard, positions, data buffer, host offsets)
-        for s, shard in enumerate(self.shards):
-            pos = np.flatnonzero(owner == s)
-            if pos.size == 0 or shard.index is None:
-                continue
-            blk, keep = shard.gather([keys[i] for i in pos])
-            offs = blk.row_off.download(8 * (pos.size + 1)).view(np.uint64).copy()
-            parts.append((s, pos, blk, offs, keep))
-        if not parts:
+        if nq == 0 or all(sh.index is None for sh in self.shards):
             return req, [_null_dict(c.dtype, nq) for c in req]
-        # 3. peer copies to home, back to back (16-B aligned bases)
-        bases, total = [], 0
-        for _, pos, _, offs, _ in parts:
-            bases.append(total)
-            total += (int(offs[-1]) + 15) & ~15
-        arena = home.alloc(max(total, 16) + 16)
-        for (s, pos, blk, offs, _), base in zip(parts, bases):
-            nb = int(offs[-1])
-            src_ctx = self.contexts[s]
-            raise_status(L.murr_memcpy_peer(home.h, arena.ptr + base, blk.data.ptr, src_ctx.device, nb),
-                         what="murr_memcpy_peer")
-        # 4. caller-order gather on home: row i = gathered row of key i
-        row_start = np.zeros(nq + 1, np.uint64)
-        sizes = np.zeros(nq, np.uint64)
-        rows = np.zeros(nq, np.uint32)
-        cat_off, nrows = [], 0
-        for (s, pos, blk, offs, _), base in zip(parts, bases):
-            cat_off.append(offs[:-1] + np.uint64(base))
-            sizes[pos] = np.diff(offs)
-            rows[pos] = np.arange(nrows, nrows + pos.size, dtype=np.uint32)
-            nrows += pos.size
-        owned = np.zeros(nq, bool)
-        for _, pos, _, _, _ in parts:
-            owned[pos] = True
-        rows[~owned] = 0xFFFFFFFF  # a shard with nothing written yet: the key is missing
-        cat = np.concatenate(cat_off + [np.zeros(1, np.uint64)])
-        np.cumsum(sizes, out=row_start[1:])
-        d_rows, d_cat, d_out_off = home.upload(rows), home.upload(cat), home.upload(row_start)
-        nb = int(row_start[-1])
-        data = home.alloc(max(nb, 16) + 16)
-        if nq:
-            raise_status(L.murr_index_gather_copy(home.h, d_rows.ptr, nq, arena.ptr, d_cat.ptr, d_out_off.ptr,
-                                                  data.ptr), what="murr_index_gather_copy")
-        # 5. one decode on home
-        blk = DeviceBlock(data, d_out_off, nq, max(nb, 16))
+        # 1. route: grouped position of every caller query, shard ranges
+        kb = pa.array([k.encode() if isinstance(k, str) else bytes(k) for k in keys], pa.binary())
+        owner = shard_of(kb, self.nshards)
+        order = np.argsort(owner, kind="stable")
+        src = np.empty(nq, np.uint32)
+        src[order] = np.arange(nq, dtype=np.uint32)
+        q_end = np.cumsum(np.bincount(owner, minlength=self.nshards)).astype(np.uint64)
+        grouped = kb.take(pa.array(order))
+        goff = np.frombuffer(grouped.buffers()[1], np.int32)[grouped.offset: grouped.offset + nq + 1]
+        gdat = grouped.buffers()[2]
+        gdat = np.frombuffer(gdat, np.uint8) if gdat is not None else np.zeros(0, np.uint8)
+        # one upload: [offsets (nq + 1) i32 | src (nq) u32 | key bytes]
+        o_src = (4 * (nq + 1) + 15) & ~15
+        o_dat = (o_src + 4 * nq + 15) & ~15
+        kbytes = gdat[int(goff[0]): int(goff[-1])]
+        packed = np.zeros(o_dat + kbytes.size + 16, np.uint8)
+        packed[: 4 * (nq + 1)] = (goff - goff[0]).astype(np.int32).view(np.uint8)
+        packed[o_src: o_src + 4 * nq] = src.view(np.uint8)
+        packed[o_dat: o_dat + kbytes.size] = kbytes
+        qbuf = home.upload(packed)
+        # 2. lookups on every shard's stream, caller-order block on home
+        tab = (_abi.ShardRead * self.nshards)()
+        for s_, sh in enumerate(self.shards):
+            tab[s_].ctx = self.contexts[s_].h
+            tab[s_].index = sh.index.h if sh.index is not None else None
+            tab[s_].arena = sh.arena.ptr if sh.index is not None else None
+            tab[s_].row_off = sh.row_off.ptr if sh.index is not None else None
+            tab[s_].q_end = int(q_end[s_])
+        rows = home.alloc(4 * nq)
+        out_off = home.alloc(8 * (nq + 1))
+        needed = home.alloc(8)
+        bound = max(16, nq * max(sh.max_row for sh in self.shards if sh.index is not None))
+        two_phase = bound > TWO_PHASE_BYTES
+        data = None if two_phase else home.alloc(bound + 16)
+        err = _abi.Error()
+        raise_status(L.murr_multi_gather(home.h, tab, self.nshards, qbuf.ptr + o_dat, qbuf.ptr, qbuf.ptr + o_src, nq,
+                                         rows.ptr, out_off.ptr, data.ptr if data else None, bound, needed.ptr,
+                                         C.byref(err)), err, "murr_multi_gather")
+        if two_phase:  # the block's size first (one more wait), then its copy
+            nb = int(needed.download(8).view(np.uint64)[0])
+            data = home.alloc(max(nb, 16) + 16)
+            raise_status(L.murr_multi_gather_copy(home.h, tab, self.nshards, qbuf.ptr + o_src, nq, rows.ptr,
+                                                  out_off.ptr, data.ptr, C.byref(err)), err, "murr_multi_gather_copy")
+            bound = max(nb, 16)
+        # 3. one decode on home (its wait is the read's host synchronisation)
+        blk = DeviceBlock(data, out_off, nq, min(bound, max(16, int(sum(sh.used for sh in self.shards)
+                                                                     / max(1, sum(sh.n for sh in self.shards)) * nq))))
         proj = [c.index for c in req]
         outs = DecodeOutputs(home, self.segment, proj, [blk])
         decode_blocks(home, self.segment, proj, [blk], outs)
+        self._keep = (qbuf, rows, needed)
         return req, [download_array(home, outs.array(0, p), int(c.dtype), nq) for p, c in enumerate(req)]

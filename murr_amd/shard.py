@@ -222,7 +222,14 @@ class ShardedResidentTable:
     """One key-range shard of a table per rank (one process per GPU), each a
     ResidentTable in that GPU's HBM.  `read` is Table::read over the whole
     table: every rank passes the same keys and gets the same caller-order
-    batch."""
+    batch.
+
+    Not the default multi-GPU read: every rank looks up every key and the
+    ranks byte-sum their host results over the process group (merge_reads),
+    which suits a job whose ranks all want the same batch (a data-parallel
+    reader on gloo or RCCL).  A server that owns all of a node's GPUs reads
+    through MultiDeviceTable (murr_multi_gather: lookups on each GPU at once,
+    one caller-order block on the home GPU, no collective)."""
 
     def __init__(self, table, group: "Group", ctx=None, name: str = "shard"):
         from .resident import ResidentTable
