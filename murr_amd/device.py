@@ -374,17 +374,24 @@ def _col_in(cols):
     return cin, ub
 
 
-def encode_batch(ctx: Context, segment: SegmentSchema, cols, n: int, blob_cap: int | None = None):
+def encode_batch(ctx: Context, segment: SegmentSchema, cols, n: int, blob_cap: int | None = None, out=None):
     """murr_encode_batch over device-resident Arrow columns.
 
     cols: per segment column dict {values: DeviceBuffer, validity: DeviceBuffer|None,
     offsets: DeviceBuffer|None, offset: int, utf8_bytes: int}.
+    out: optional (blob, row_off) DeviceBuffers to write into (a repeated
+    encode of the same shape reuses them instead of allocating each call).
     Returns (blob DeviceBuffer, row_off DeviceBuffer, blob_len)."""
     cin, ub = _col_in(cols)
     if blob_cap is None:
         blob_cap = int(ctx.L.murr_encode_bound(C.byref(segment.c), n, ub))
-    blob = ctx.alloc(max(blob_cap, 16))
-    row_off = ctx.alloc((n + 1) * 8)
+    if out is not None:
+        blob, row_off = out
+        if blob.nbytes < max(blob_cap, 16) or row_off.nbytes < (n + 1) * 8:
+            raise ValueError("encode_batch: out buffers smaller than the encode bound")
+    else:
+        blob = ctx.alloc(max(blob_cap, 16))
+        row_off = ctx.alloc((n + 1) * 8)
     blen = C.c_uint64()
     err = _abi.Error()
     st = ctx.L.murr_encode_batch(ctx.h, C.byref(segment.c), cin, n, blob.ptr, blob_cap, row_off.ptr,
