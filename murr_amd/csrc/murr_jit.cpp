@@ -426,6 +426,10 @@ hipError_t jit_encode_launch(const JitEncKernel* k, const EncodeArgs& a, uint32_
         if (e == hipSuccess) e = hipModuleLaunchKernel(k->fn_scan, groups, 1, 1, 1024, 1, 1, 0, s, nullptr, scfg);
         if (e != hipSuccess) return e;
         grid = tiles;  // no co-resident grid needed: a workgroup per tile
+#ifdef MURR_TUNING
+        if (const char* g = std::getenv("MURR_ENC_GRID"))  // workgroups per CU of a persistent grid (A/B)
+            grid = std::min<uint32_t>(tiles, (uint32_t)std::atoi(g) * (uint32_t)(a.total_tiles ? 256 : 1));
+#endif
     }
     return hipModuleLaunchKernel(k->fn, grid, 1, 1, 256, 1, 1, 0, s, nullptr, cfg);
 }

@@ -104,6 +104,11 @@ DEV bool valid(const Col& c, uint64_t e) {
 // reach past the bitmap's bytes (nbytes = ceil((offset + n) / 8)) takes the
 // per-lane byte load.
 DEV bool bit_of_wave(const uint8_t* bm, uint64_t ew, uint32_t lane, uint64_t nbytes) {
+    // a bitmap that does not start on a dword: its bits counted from the dword below
+    const uint32_t mis = (uint32_t)((uintptr_t)bm & 3u);
+    bm -= mis;
+    ew += 8 * mis;
+    nbytes += mis;
     const uint64_t d = ew >> 5;
     if ((d + 3) * 4 <= nbytes) {
         const CAS uint32_t* p = (const CAS uint32_t*)bm + d;
@@ -120,6 +125,38 @@ DEV bool valid_wave(const Col& c, uint64_t ew, uint32_t lane, uint64_t nbytes) {
     if (!c.validity) return true;
     return bit_of_wave(c.validity, ew, lane, nbytes);
 }
+
+// Column kinds at compile time (0 utf8, 9 bool, else width) and each bool
+// column's ordinal among the bool columns.
+constexpr uint32_t kKind[NCOLS ? NCOLS : 1] = {
+#define MJE_K(C, KIND, SOFF, U) KIND,
+    MJE_COLS(MJE_K)
+#undef MJE_K
+};
+constexpr uint32_t bool_ord(uint32_t c) {
+    uint32_t n = 0;
+    for (uint32_t j = 0; j < c; j++) n += kKind[j] == 9;
+    return n;
+}
+constexpr uint32_t NBOOL = bool_ord(NCOLS);
+
+// Every bitmap word a wave needs, in one vector load.  Lane j < NCOLS takes
+// column j's validity bitmap, lane NCOLS + k the k-th bool column's values;
+// each loads the three dwords covering the wave's 64 bits and realigns them
+// to a 64-bit window (wlo, whi), and column C's window is then two
+// v_readlane's.  This replaced three scalar loads per bitmap whose uses sat
+// in separate branches, so a wave waited for each column's bitmaps in turn
+// (validity reads were a third of config C's encode).  A lane
+// whose window would pass the bitmap's bytes (the batch's last rows) marks
+// its bitmap for the per-lane byte path (`slow`).
+#ifndef MJE_VBITS
+#define MJE_VBITS 1
+#endif
+constexpr bool VBITS = MJE_VBITS && NCOLS + NBOOL <= 64;
+struct Bits {
+    uint32_t wlo, whi;  // lane j: the window of bitmap j
+    uint64_t slow;      // bitmaps read per lane instead
+};
 
 // The fixed part of one row as dwords, byte placement at compile time.
 struct Row {
@@ -199,9 +236,56 @@ struct RowBuild {
     uint32_t pre[NUTF8 ? NUTF8 : 1][PF];  // its first PF aligned dwords
 };
 
+DEV Bits load_bits(uint64_t rw, uint32_t lane) {
+    Bits b{0u, 0u, 0ull};
+    if constexpr (VBITS) {
+        // lane j's bitmap and element offset, picked from the columns'
+        // descriptors (scalar loads, cached) -- no vector load before the
+        // bitmap load, and nothing at all when no column has a bitmap
+        const uint8_t* bm = nullptr;
+        uint64_t eoff = 0;
+        bool any = false;
+#define MJE_BM(C, KIND, SOFF, U)                                                          \
+        {                                                                                 \
+            const Col c = ldcol(C);                                                       \
+            any = any || c.validity || KIND == 9;                                         \
+            if (lane == C) { bm = c.validity; eoff = c.offset; }                          \
+            if (KIND == 9 && lane == NCOLS + bool_ord(C)) { bm = c.values; eoff = c.offset; } \
+        }
+        MJE_COLS(MJE_BM)
+#undef MJE_BM
+        if (!any) return b;
+        const uint32_t mis = (uint32_t)((uintptr_t)bm & 3u);
+        const uint64_t ew = eoff + rw + 8 * mis;
+        const uint64_t nbytes = (eoff + args()->n_rows + 7) / 8 + mis;
+        const uint64_t d = ew >> 5;
+        const bool fast = bm && (d + 3) * 4 <= nbytes;
+        uint32_t x0 = 0, x1 = 0, x2 = 0;
+        if (fast) {
+            const GAS uint32_t* p = (const GAS uint32_t*)(bm - mis) + d;
+            x0 = p[0];
+            x1 = p[1];
+            x2 = p[2];
+        }
+        const uint32_t sh = (uint32_t)ew & 31u;
+        const uint64_t lo = ((uint64_t)x1 << 32) | x0;
+        const uint64_t w = sh ? (lo >> sh) | ((uint64_t)x2 << (64 - sh)) : lo;
+        b.wlo = (uint32_t)w;
+        b.whi = (uint32_t)(w >> 32);
+        b.slow = __ballot(bm && !fast);
+    }
+    return b;
+}
+// Bit `lane` of bitmap j's window (j compile-time).
+template <uint32_t J> DEV bool bits_at(const Bits& b, uint32_t lane) {
+    const uint64_t w = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(b.whi, J) << 32) |
+                       (uint32_t)__builtin_amdgcn_readlane(b.wlo, J);
+    return (w >> lane) & 1;
+}
+
 // rw: the wave's first row (uniform); row = rw + lane for the active lanes
 template <uint32_t C, uint32_t KIND, uint32_t SOFF, uint32_t U>
-DEV void build_col(RowBuild& B, uint64_t row, uint64_t rw, uint32_t lane) {
+DEV void build_col(RowBuild& B, uint64_t row, uint64_t rw, uint32_t lane, const Bits& bits) {
     const Col c = ldcol(C);
     const uint64_t e = c.offset + row;
     // the wave's first element and the bitmaps' byte length (used only with a
@@ -211,7 +295,14 @@ DEV void build_col(RowBuild& B, uint64_t row, uint64_t rw, uint32_t lane) {
                ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)((c.offset + rw) >> 32)) << 32);
     };
     auto bm_bytes = [&]() { return (c.offset + args()->n_rows + 7) >> 3; };
-    const bool v = c.validity ? bit_of_wave(c.validity, wave_ew(), lane, bm_bytes()) : true;
+    bool v = true;
+    if (c.validity) {
+        if constexpr (VBITS) {
+            v = (bits.slow >> C) & 1 ? bit_of_wave(c.validity, wave_ew(), lane, bm_bytes()) : bits_at<C>(bits, lane);
+        } else {
+            v = bit_of_wave(c.validity, wave_ew(), lane, bm_bytes());
+        }
+    }
     B.vmask[C / 32] |= (uint32_t)v << (C % 32);
     constexpr uint32_t OFF = BS + SOFF;
     // Every load below is unconditional (in bounds for any row < n_rows) and
@@ -234,7 +325,13 @@ DEV void build_col(RowBuild& B, uint64_t row, uint64_t rw, uint32_t lane) {
 #pragma unroll
         for (uint32_t i = 0; i < PF; i++) B.pre[U][i] = i < nd ? w[i] : 0u;
     } else if constexpr (KIND == 9) {  // bool: b as u8 (bool_.rs:111-117)
-        const uint32_t b = bit_of_wave(c.values, wave_ew(), lane, bm_bytes());
+        uint32_t b;
+        if constexpr (VBITS) {
+            constexpr uint32_t J = NCOLS + bool_ord(C);
+            b = (bits.slow >> J) & 1 ? bit_of_wave(c.values, wave_ew(), lane, bm_bytes()) : bits_at<J>(bits, lane);
+        } else {
+            b = bit_of_wave(c.values, wave_ew(), lane, bm_bytes());
+        }
         put8<OFF>(B.r, v ? b : 0u);
     } else if constexpr (KIND == 8) {
         const GAS uint32_t* p = (const GAS uint32_t*)(gp(c.values) + e * 8);
@@ -348,10 +445,17 @@ struct Emit {
 // Utf8 payload of column C into the emitter: u32 len, then the string in
 // 4-byte chunks realigned from the aligned dwords that cover it (dwords past
 // the string are never loaded; they read as 0).
+#ifndef MJE_ABL_NOSTR  // ablation (tuning): string bytes not copied
+#define MJE_ABL_NOSTR 0
+#endif
+#ifndef MJE_ABL_NOOUT  // ablation (tuning): the stage is not written out
+#define MJE_ABL_NOOUT 0
+#endif
 template <uint32_t C, uint32_t U> DEV void emit_payload(const RowBuild& B, Emit& E) {
     if (!((B.vmask[C / 32] >> (C % 32)) & 1)) return;
     const uint32_t n = B.ulen[U];
     E.put(n, 4);
+    if (MJE_ABL_NOSTR) return;
     const Col c = ldcol(C);
     const uintptr_t sa_ptr = (uintptr_t)(gp(c.values) + B.ustart[U]);
     const uint32_t sa = (uint32_t)(sa_ptr & 3);
@@ -404,7 +508,8 @@ extern "C" __global__ void __launch_bounds__(256) MJE_WPE_ATTR murr_jit_encode(m
 #pragma unroll
         for (uint32_t k = 0; k < sizeof(B.vmask) / 4; k++) B.vmask[k] = 0;
         B.pos = FIXED;
-#define MJE_DO_COL(C, KIND, SOFF, U) build_col<C, KIND, SOFF, U>(B, row, r0 + 64 * wave, lane);
+        const Bits bits = load_bits(r0 + 64 * wave, lane);
+#define MJE_DO_COL(C, KIND, SOFF, U) build_col<C, KIND, SOFF, U>(B, row, r0 + 64 * wave, lane, bits);
         MJE_COLS(MJE_DO_COL)
 #undef MJE_DO_COL
         put_bitset(B);
@@ -474,7 +579,7 @@ extern "C" __global__ void __launch_bounds__(256) MJE_WPE_ATTR murr_jit_encode(m
                 }
             }
             __syncthreads();
-            write_out((const LAS uint8_t*)stage, gp(A->out), tstart, span, tid);
+            if (!MJE_ABL_NOOUT) write_out((const LAS uint8_t*)stage, gp(A->out), tstart, span, tid);
             __syncthreads();
         } else if (active) {
             // a tile over the stage: bytes straight to HBM (cold)

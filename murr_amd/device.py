@@ -54,7 +54,8 @@ def set_default_opts(**kw):
     _default_opts.clear()
     _default_opts.update(kw)
     for c in list(_live):
-        c.set_opts(**kw)
+        if c.h:  # (a closed context may linger in the set until collected)
+            c.set_opts(**kw)
 
 
 class Context:
