@@ -78,6 +78,9 @@ DEV void report(unsigned long long* err, uint64_t key) {
                            __HIP_MEMORY_SCOPE_AGENT);
 }
 DEV uint32_t umin(uint32_t a, uint32_t b) { return a < b ? a : b; }
+DEV uint64_t sgpr64(uint64_t v) {
+    return ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32) | __builtin_amdgcn_readfirstlane((uint32_t)v);
+}
 template <class T> DEV GAS T* gp(T* p) { return (GAS T*)p; }
 template <class T> DEV const GAS T* gp(const T* p) { return (const GAS T*)p; }
 
@@ -234,6 +237,8 @@ struct RowBuild {
     uint32_t ulen[NUTF8 ? NUTF8 : 1];
     uint64_t ustart[NUTF8 ? NUTF8 : 1];  // Arrow data offset of the string
     uint32_t pre[NUTF8 ? NUTF8 : 1][PF];  // its first PF aligned dwords
+    int32_t s0[NUTF8 ? NUTF8 : 1], s1[NUTF8 ? NUTF8 : 1];  // its Arrow offsets
+    uint32_t x[NCOLS ? NCOLS : 1], xh[NCOLS ? NCOLS : 1];  // fixed-width values as loaded (xh: high dword of 8-byte ones)
 };
 
 DEV Bits load_bits(uint64_t rw, uint32_t lane) {
@@ -283,70 +288,100 @@ template <uint32_t J> DEV bool bits_at(const Bits& b, uint32_t lane) {
     return (w >> lane) & 1;
 }
 
-// rw: the wave's first row (uniform); row = rw + lane for the active lanes
-template <uint32_t C, uint32_t KIND, uint32_t SOFF, uint32_t U>
-DEV void build_col(RowBuild& B, uint64_t row, uint64_t rw, uint32_t lane, const Bits& bits) {
-    const Col c = ldcol(C);
-    const uint64_t e = c.offset + row;
-    // the wave's first element and the bitmaps' byte length (used only with a
-    // validity buffer or for bool values)
-    auto wave_ew = [&]() {
-        return (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(c.offset + rw)) |
-               ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)((c.offset + rw) >> 32)) << 32);
-    };
-    auto bm_bytes = [&]() { return (c.offset + args()->n_rows + 7) >> 3; };
-    bool v = true;
-    if (c.validity) {
-        if constexpr (VBITS) {
-            v = (bits.slow >> C) & 1 ? bit_of_wave(c.validity, wave_ew(), lane, bm_bytes()) : bits_at<C>(bits, lane);
+// One row is built in four phases, each over every column, so that a wave's
+// loads are all in flight before it waits for any of them: the utf8 offsets;
+// the bitmap windows (load_bits); every fixed-width value; then, once the
+// offsets and the bitmaps are in, each string's first dwords; and last the row
+// assembly.  Every load is unconditional (in bounds for any row < n_rows)
+// and masked by the validity bit afterwards: a load guarded by the bit would
+// wait for the validity load, one more round trip per column.
+
+// The validity of column C's cell in this lane's row.
+template <uint32_t C>
+DEV bool valid_of(const Col& c, uint64_t rw, uint32_t lane, const Bits& bits) {
+    if (!c.validity) return true;
+    if constexpr (VBITS) {
+        if (!((bits.slow >> C) & 1)) return bits_at<C>(bits, lane);
+    }
+    return bit_of_wave(c.validity, sgpr64(c.offset + rw), lane, (c.offset + args()->n_rows + 7) >> 3);
+}
+
+template <uint32_t C, uint32_t KIND, uint32_t SOFF, uint32_t U> DEV void ld_offs(RowBuild& B, uint64_t row) {
+    if constexpr (KIND == 0) {
+        const Col c = ldcol(C);
+        const uint64_t e = c.offset + row;
+        B.s0[U] = gp(c.offsets)[e];
+        B.s1[U] = gp(c.offsets)[e + 1];
+    }
+}
+
+template <uint32_t C, uint32_t KIND, uint32_t SOFF, uint32_t U> DEV void ld_fixed(RowBuild& B, uint64_t row) {
+    if constexpr (KIND != 0 && KIND != 9) {
+        const Col c = ldcol(C);
+        const uint64_t e = c.offset + row;
+        if constexpr (KIND == 8) {
+            const GAS uint32_t* p = (const GAS uint32_t*)(gp(c.values) + e * 8);
+            B.x[C] = p[0];
+            B.xh[C] = p[1];
+        } else if constexpr (KIND == 4) {
+            B.x[C] = ((const GAS uint32_t*)gp(c.values))[e];
+        } else if constexpr (KIND == 2) {
+            B.x[C] = ((const GAS uint16_t*)gp(c.values))[e];
         } else {
-            v = bit_of_wave(c.validity, wave_ew(), lane, bm_bytes());
+            B.x[C] = gp(c.values)[e];
         }
     }
-    B.vmask[C / 32] |= (uint32_t)v << (C % 32);
-    constexpr uint32_t OFF = BS + SOFF;
-    // Every load below is unconditional (in bounds for any row < n_rows) and
-    // masked by the validity bit afterwards: a load guarded by the bit would
-    // wait for the validity load, one more round trip per column.
-    if constexpr (KIND == 0) {  // utf8: slot = payload offset relative to the static region
-        const int32_t s0 = gp(c.offsets)[e], s1 = gp(c.offsets)[e + 1];
-        const uint32_t len = v ? (uint32_t)(s1 - s0) : 0u;
-        const uint64_t a = v ? (uint64_t)(int64_t)s0 : 0u;
-        put32<OFF>(B.r, v ? B.pos - BS : 0u);
-        B.ulen[U] = v ? len : 0u;
+}
+
+// A string's first aligned dwords, so their latency overlaps the row assembly
+// and the tile scan (an aligned dword never crosses a page: bytes around the
+// string are safe to load and masked later).
+template <uint32_t C, uint32_t KIND, uint32_t SOFF, uint32_t U>
+DEV void ld_str(RowBuild& B, uint64_t rw, uint32_t lane, const Bits& bits) {
+    if constexpr (KIND == 0) {
+        const Col c = ldcol(C);
+        const bool v = valid_of<C>(c, rw, lane, bits);
+        const uint32_t len = v ? (uint32_t)(B.s1[U] - B.s0[U]) : 0u;
+        const uint64_t a = v ? (uint64_t)(int64_t)B.s0[U] : 0u;
+        B.ulen[U] = len;
         B.ustart[U] = a;
-        if (v) B.pos += 4 + len;
-        // the string's first aligned dwords now, so their latency overlaps the
-        // rest of the row and the tile scan (an aligned dword never crosses a
-        // page: bytes around the string are safe to load and masked later)
         const uintptr_t sp = (uintptr_t)(gp(c.values) + a);
         const GAS uint32_t* w = (const GAS uint32_t*)(sp & ~(uintptr_t)3);
         const uint32_t nd = v ? (len + (uint32_t)(sp & 3) + 3) / 4 : 0u;
 #pragma unroll
         for (uint32_t i = 0; i < PF; i++) B.pre[U][i] = i < nd ? w[i] : 0u;
+    }
+}
+
+// rw: the wave's first row (uniform)
+template <uint32_t C, uint32_t KIND, uint32_t SOFF, uint32_t U>
+DEV void put_col(RowBuild& B, uint64_t rw, uint32_t lane, const Bits& bits) {
+    const Col c = ldcol(C);
+    const bool v = valid_of<C>(c, rw, lane, bits);
+    B.vmask[C / 32] |= (uint32_t)v << (C % 32);
+    constexpr uint32_t OFF = BS + SOFF;
+    if constexpr (KIND == 0) {  // utf8: slot = payload offset relative to the static region
+        put32<OFF>(B.r, v ? B.pos - BS : 0u);
+        if (v) B.pos += 4 + B.ulen[U];
     } else if constexpr (KIND == 9) {  // bool: b as u8 (bool_.rs:111-117)
-        uint32_t b;
+        uint32_t b = 0;
         if constexpr (VBITS) {
             constexpr uint32_t J = NCOLS + bool_ord(C);
-            b = (bits.slow >> J) & 1 ? bit_of_wave(c.values, wave_ew(), lane, bm_bytes()) : bits_at<J>(bits, lane);
+            b = (bits.slow >> J) & 1 ? bit_of_wave(c.values, sgpr64(c.offset + rw), lane, (c.offset + args()->n_rows + 7) >> 3)
+                                    : bits_at<J>(bits, lane);
         } else {
-            b = bit_of_wave(c.values, wave_ew(), lane, bm_bytes());
+            b = bit_of_wave(c.values, sgpr64(c.offset + rw), lane, (c.offset + args()->n_rows + 7) >> 3);
         }
         put8<OFF>(B.r, v ? b : 0u);
     } else if constexpr (KIND == 8) {
-        const GAS uint32_t* p = (const GAS uint32_t*)(gp(c.values) + e * 8);
-        const uint32_t lo = p[0], hi = p[1];
-        put32<OFF>(B.r, v ? lo : 0u);
-        put32<OFF + 4>(B.r, v ? hi : 0u);
+        put32<OFF>(B.r, v ? B.x[C] : 0u);
+        put32<OFF + 4>(B.r, v ? B.xh[C] : 0u);
     } else if constexpr (KIND == 4) {
-        const uint32_t x = ((const GAS uint32_t*)gp(c.values))[e];
-        put32<OFF>(B.r, v ? x : 0u);
+        put32<OFF>(B.r, v ? B.x[C] : 0u);
     } else if constexpr (KIND == 2) {
-        const uint32_t x = ((const GAS uint16_t*)gp(c.values))[e];
-        put16<OFF>(B.r, v ? x : 0u);
+        put16<OFF>(B.r, v ? B.x[C] : 0u);
     } else {
-        const uint32_t x = gp(c.values)[e];
-        put8<OFF>(B.r, v ? x : 0u);
+        put8<OFF>(B.r, v ? B.x[C] : 0u);
     }
 }
 
@@ -508,10 +543,20 @@ extern "C" __global__ void __launch_bounds__(256) MJE_WPE_ATTR murr_jit_encode(m
 #pragma unroll
         for (uint32_t k = 0; k < sizeof(B.vmask) / 4; k++) B.vmask[k] = 0;
         B.pos = FIXED;
-        const Bits bits = load_bits(r0 + 64 * wave, lane);
-#define MJE_DO_COL(C, KIND, SOFF, U) build_col<C, KIND, SOFF, U>(B, row, r0 + 64 * wave, lane, bits);
-        MJE_COLS(MJE_DO_COL)
-#undef MJE_DO_COL
+        const uint64_t rw = r0 + 64 * wave;
+#define MJE_DO_OFFS(C, KIND, SOFF, U) ld_offs<C, KIND, SOFF, U>(B, row);
+        MJE_COLS(MJE_DO_OFFS)
+#undef MJE_DO_OFFS
+        const Bits bits = load_bits(rw, lane);
+#define MJE_DO_FIXED(C, KIND, SOFF, U) ld_fixed<C, KIND, SOFF, U>(B, row);
+        MJE_COLS(MJE_DO_FIXED)
+#undef MJE_DO_FIXED
+#define MJE_DO_STR(C, KIND, SOFF, U) ld_str<C, KIND, SOFF, U>(B, rw, lane, bits);
+        MJE_COLS(MJE_DO_STR)
+#undef MJE_DO_STR
+#define MJE_DO_PUT(C, KIND, SOFF, U) put_col<C, KIND, SOFF, U>(B, rw, lane, bits);
+        MJE_COLS(MJE_DO_PUT)
+#undef MJE_DO_PUT
         put_bitset(B);
         const uint32_t size = active ? B.pos : 0u;
 
