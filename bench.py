@@ -70,6 +70,16 @@ def make_columns(config: str, rows: int, start: int):
     raise SystemExit(f"unknown config {config}")
 
 
+def parse_proj(text, ncols):
+    """--proj: comma-separated columns, "rev" (every column, reversed), or
+    None (every column in order: the whole-table projection)."""
+    if text is None:
+        return list(range(ncols))
+    if text == "rev":
+        return list(reversed(range(ncols)))
+    return [int(x) for x in text.split(",")]
+
+
 def arrow_out_bytes(seg, proj, n, null_counts, utf8_lens):
     """SURVEY.md §8(d) bytes_out: values + offsets + string bytes + validity of
     columns that have nulls."""
@@ -87,11 +97,13 @@ def arrow_out_bytes(seg, proj, n, null_counts, utf8_lens):
     return tot
 
 
-def pmc_traffic(paths):
+def pmc_traffic(paths, kernel=None):
     """HBM bytes per decode launch from rocprofv3 --pmc CSVs (comma-separated;
     FETCH_SIZE and WRITE_SIZE come from separate passes).  MI355X_MICROARCH.md
     §HBM: FETCH_SIZE counts half the bytes of wide streaming reads on gfx950,
-    so it is doubled; WRITE_SIZE is exact for 16-B stores; both in KiB."""
+    so it is doubled; WRITE_SIZE is exact for 16-B stores; both in KiB.
+    kernel: only dispatches of that kernel (the timed launch's; the untimed
+    no-index variant runs another one)."""
     if not paths:
         return None
     import csv
@@ -102,7 +114,8 @@ def pmc_traffic(paths):
         per = {}
         with open(path) as f:
             for r in csv.DictReader(f):
-                if "decode" not in r.get("Kernel_Name", ""):
+                name = r.get("Kernel_Name", "")
+                if "decode" not in name or (kernel and name.split("(")[0].strip() != kernel):
                     continue
                 key = (r.get("Counter_Name"), r.get("Dispatch_Id"))
                 per[key] = per.get(key, 0.0) + float(r.get("Counter_Value", 0))
@@ -278,13 +291,13 @@ def run_decode(args, dist, rank, world, local_rank):
         K = 1
         rt, names = config_d_table(ctx, rows, start)
         seg = rt.segment
-        proj = list(range(len(seg.columns))) if args.proj is None else [int(x) for x in args.proj.split(",")]
+        proj = parse_proj(args.proj, len(seg.columns))
         blocks = [rt.block()]
         ix_stride = blocks[0].stride
     else:
         cols = make_columns(args.config, rows, start=start)
         seg = SegmentSchema([(f"c{i}", c["dtype"]) for i, c in enumerate(cols)])
-        proj = list(range(len(cols))) if args.proj is None else [int(x) for x in args.proj.split(",")]
+        proj = parse_proj(args.proj, len(cols))
         dcols = synth.upload_columns(ctx, cols)
         if args.uidx_stride:
             # the block and its utf8 index, written together (murr_encode_batch_ix)
@@ -335,7 +348,10 @@ def run_decode(args, dist, rank, world, local_rank):
     value = total_out / elapsed / GIB
     k_avg_ms = float(np.mean(kms))
     achieved = (in_block + out_block) * K / (k_avg_ms * 1e-3) / 1e9
-    traffic = pmc_traffic(args.pmc_csv)
+    shape = "%dx%d" % tuple(stats["last_shape"])
+    timed_kernel = ("decode_kernel" if stats["last_mode"] == "generic" else
+                    "murr_jit_decode_%s%s" % ("split_" if stats["last_mode"] == "split" else "", shape))
+    traffic = pmc_traffic(args.pmc_csv, timed_kernel)
 
     # after the timed region: the timed launch's output, checked against the
     # oracle (first and last block); a mismatch fails the run
@@ -781,7 +797,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--pmc-csv", default=None)
     ap.add_argument("--enc-config", default="E", choices=["B", "C", "E"], help="encode mode: column set")
-    ap.add_argument("--proj", default=None, help="comma-separated projected columns (default all)")
+    ap.add_argument("--proj", default=None, help="comma-separated projected columns, or rev (default all, in order)")
     ap.add_argument("--opts", default=None,
                     help="kernel selection (murr_ctx_set_opts), e.g. shape=16x2,lds=163840,mode=local")
     args = ap.parse_args()

@@ -227,7 +227,7 @@ DEV void write_out(const LAS uint8_t* buf, GAS uint8_t* out, uint64_t g0, uint64
 // One row's fixed part and payload sizes.  `pos` = payload append position
 // (write.rs:44-52), starting at bs + cap.
 #ifndef MJE_PF
-#define MJE_PF 3
+#define MJE_PF 5
 #endif
 constexpr uint32_t PF = MJE_PF;  // aligned dwords of each string loaded with the row (the rest later)
 struct RowBuild {

@@ -169,3 +169,28 @@ def test_wide_schema_encode(ctx, kernel_mode):
     wblob, woff = O.encode_batch(O.Segment([int(d) for d in dtypes]), synth.oracle_cols(cols), n)
     assert np.array_equal(off, woff)
     assert blob.tobytes() == wblob.tobytes()
+
+
+@pytest.mark.parametrize("shift", [1, 2, 3])
+def test_bitmaps_not_on_a_dword(ctx, shift):
+    # validity and bool bitmaps at device addresses that are not 4-byte
+    # aligned (any C caller may pass such a pointer): the wave's bitmap
+    # windows are read from the dword below and shifted by the misalignment
+    from types import SimpleNamespace
+    rng = np.random.default_rng(90 + shift)
+    dtypes = [D.Bool, D.Int32, D.Utf8, D.Bool, D.Float64, D.Int8]
+    n = 3000 + shift
+    cols = random_columns(rng, dtypes, n, null_p=0.3)
+    dcols = synth.upload_columns(ctx, cols)
+    keep = []
+    for c, d in zip(cols, dcols):
+        for key in ("validity",) + (("values",) if c["dtype"] == D.Bool else ()):
+            if c[key] is None:
+                continue
+            buf = ctx.upload(np.concatenate([np.full(shift, 0xA5, np.uint8), c[key]]))
+            keep.append(buf)
+            d[key] = SimpleNamespace(ptr=buf.ptr + shift)
+    blob, row_off, blen = encode_batch(ctx, seg_of(dtypes), dcols, n)
+    wblob, woff = O.encode_batch(O.Segment([int(d) for d in dtypes]), synth.oracle_cols(cols), n)
+    assert np.array_equal(row_off.download((n + 1) * 8).view(np.uint64), woff)
+    assert blob.download(blen).tobytes() == wblob.tobytes()
