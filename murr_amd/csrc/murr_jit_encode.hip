@@ -445,6 +445,32 @@ DEV void put_payload(const RowBuild& B, LAS uint32_t* stw, uint32_t rb, uint32_t
 #ifndef MJE_STREAM
 #define MJE_STREAM 1
 #endif
+// Bytes [lo, hi) of dword v to stage bytes a + lo .. a + hi (a dword-aligned):
+// the partial dwords a row shares with its neighbours are written bytewise,
+// so the stage needs no zeroing pass before the rows are merged into it.
+// Short rows (a fixed part under 32 bytes, e.g. config B's 9) zero the
+// stage and OR-merge the shared edge dwords instead: with two edges per ~18
+// bytes the byte writes cost more than the zeroing pass (B 0.212 vs 0.226 ms;
+// C 1.07 vs 1.11 and E 0.353 vs 0.359 ms the other way round).
+#ifndef MJE_ZERO
+#define MJE_ZERO (MJE_BS + MJE_CAP < 32)
+#endif
+DEV void put_bytes(LAS uint32_t* stw, uint32_t d, uint32_t v, uint32_t lo, uint32_t hi) {
+    if (MJE_ZERO) {
+        const uint32_t m = (hi >= 4 ? ~0u : (1u << (8 * hi)) - 1u) & (~0u << (8 * lo));
+        __hip_atomic_fetch_or(stw + d, v & m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        return;
+    }
+    if (lo == 0 && hi >= 4) {
+        stw[d] = v;
+        return;
+    }
+    LAS uint8_t* b = (LAS uint8_t*)(stw + d);
+#pragma unroll
+    for (uint32_t j = 0; j < 4; j++)
+        if (j >= lo && j < hi) b[j] = (uint8_t)(v >> (8 * j));
+}
+
 struct Emit {
     LAS uint32_t* stw;
     uint32_t d, d0, sh;  // next stage dword, the row's first dword, its byte offset in it
@@ -458,7 +484,7 @@ struct Emit {
         nb = sh;  // the first dword's leading bytes are the previous row's (zero here)
     }
     DEV void emit(uint32_t w) {
-        if (d == d0 && sh) __hip_atomic_fetch_or(stw + d, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (d == d0 && sh) put_bytes(stw, d, w, sh, 4);  // the first dword's leading bytes are the previous row's
         else stw[d] = w;
         d++;
     }
@@ -473,7 +499,7 @@ struct Emit {
         }
     }
     DEV void finish() {
-        if (nb) __hip_atomic_fetch_or(stw + d, (uint32_t)acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (nb) put_bytes(stw, d, (uint32_t)acc, d == d0 ? sh : 0u, nb);
     }
 };
 
@@ -591,9 +617,12 @@ extern "C" __global__ void __launch_bounds__(256) MJE_WPE_ATTR murr_jit_encode(m
             continue;  // uniform
         }
         if (span <= STAGE) {
-            // zero the stage, merge the rows, write it out
-            for (uint32_t k = tid; k < (uint32_t)((span + 7) >> 2) + 1; k += TILE) stw[k] = 0;
-            __syncthreads();
+            // merge the rows (every byte of the span is some row's: no zeroing
+            // in stream mode), write it out
+            if (!MJE_STREAM || MJE_ZERO) {  // (tuning: the OR-merge path)
+                for (uint32_t k = tid; k < (uint32_t)((span + 7) >> 2) + 1; k += TILE) stw[k] = 0;
+                __syncthreads();
+            }
 #if MJE_STREAM
             if (active && NUTF8) {
                 Emit E;
@@ -614,7 +643,11 @@ extern "C" __global__ void __launch_bounds__(256) MJE_WPE_ATTR murr_jit_encode(m
                     const uint32_t v = sh ? __builtin_amdgcn_alignbyte(cur, prev, 4 - sh) : cur;
                     // dwords wholly inside the fixed part are this row's alone
                     if (k >= 1 && 4 * k + 4 <= FIXED + sh) stw[d0 + k] = v;
-                    else if (v) __hip_atomic_fetch_or(stw + d0 + k, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    else if (MJE_STREAM && !NUTF8) {  // an edge shared with a neighbour: this row's bytes only
+                        if (FIXED + sh > 4 * k) put_bytes(stw, d0 + k, v, k ? 0u : sh, FIXED + sh - 4 * k);
+                    } else if (v) {
+                        __hip_atomic_fetch_or(stw + d0 + k, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    }
                 }
                 if (NUTF8) {
                     uint32_t p = FIXED;
