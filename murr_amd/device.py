@@ -83,6 +83,7 @@ class Context:
         o.shape_nw, o.shape_r = shape if shape else (0, 0)
         o.seg_tiles, o.vrows, o.lds_budget, o.stage, o.verbose = seg_tiles, vrows, lds_budget, stage, int(verbose)
         raise_status(self.L.murr_ctx_set_opts(self.h, C.byref(o)), what="murr_ctx_set_opts")
+        self.opts_gen = getattr(self, "opts_gen", 0) + 1  # plan caches key on it (no library call per read)
 
     def opts_key(self) -> tuple:
         """The context's current murr_opts_t as a tuple (plan cache keys)."""

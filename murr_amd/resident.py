@@ -339,14 +339,16 @@ class ResidentTable:
         buffers in HBM.  `outs` (from an earlier scan of the same columns and
         row count) is reused.  The bulk read of SURVEY.md §8(e) mode 1: a GPU
         decodes its whole shard."""
-        req = self._resolve(columns)
         if self.n == 0:
+            self._resolve(columns)  # (an unknown column is reported first)
             raise SegmentError("resident table is empty")
-        proj = [c.index for c in req]
-        state = (tuple(proj), self.arena.ptr, self.row_off.ptr, self.uidx.ptr if self.uidx is not None else 0,
-                 self.n, self.used, self.ctx.opts_key())
+        # the plan's key: columns, table state, the context's options (a
+        # repeated scan costs a tuple compare here and one library call)
+        state = (tuple(columns), self.arena.ptr, self.row_off.ptr, self.uidx.ptr if self.uidx is not None else 0,
+                 self.n, self.used, getattr(self.ctx, "opts_gen", 0))
         plan = self._scan_plan
         if plan is None or plan[0] != state or (outs is not None and outs is not plan[1].outs):
+            proj = [c.index for c in self._resolve(columns)]
             # prepared once per (columns, table state, outputs): a repeated
             # scan is one launch and one small read-back (murr_decode_run).
             # Without `outs` the plan's own outputs are reused (valid until

@@ -24,7 +24,7 @@ def last_json(path):
 
 names = {"bench": "bench.json", "decode_C": "decode_C.json", "decode_D1": "decode_D1.json",
          "host_B": "host_B.json", "encode_E": "encode_E.json", "decode_C_noindex": "decode_C_noindex.json",
-         "decode_D": "decode_D.json", "decode_D1_noindex": "decode_D1_noindex.json",
+         "decode_D10M": "decode_D10M.json", "decode_D1_noindex": "decode_D1_noindex.json",
          "decode_B_generic": "decode_B_generic.json", "host_C": "host_C.json", "encode_B": "encode_B.json",
          "encode_C": "encode_C.json", "resident_1000": "resident_1000.json",
          "resident_read_plain": "resident_read_plain.json", "resident_read_block": "resident_read_block.json",

@@ -31,7 +31,7 @@ if [ -z "${QUICK:-}" ]; then
   run host_B 300 python3 bench.py --mode host --config B --steps 10 --warmup 2
   run encode_E 300 python3 bench.py --mode encode --steps 10 --warmup 2
   run decode_C_noindex 300 python3 bench.py --config C --blocks 10 --steps 10 --warmup 2 --no-cpu --uidx-stride 0
-  run decode_D 300 python3 bench.py --config D --rows 100000 --blocks 125 --steps 10 --warmup 2 --no-cpu
+  run decode_D10M 300 python3 bench.py --config D --rows 10000000 --steps 10 --warmup 2 --no-cpu
   run decode_D1_noindex 300 python3 bench.py --config D --steps 10 --warmup 2 --no-cpu --uidx-stride 0
   run decode_B_generic 300 python3 bench.py --steps 10 --warmup 2 --no-cpu --opts kernel=generic
   run host_C 300 python3 bench.py --mode host --config C --rows 1000 --steps 50 --warmup 5
