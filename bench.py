@@ -126,6 +126,55 @@ def pmc_traffic(paths, kernel=None):
     return round((2.0 * sum(fetch) / len(fetch) + sum(write) / len(write)) * 1024.0)
 
 
+def measure_traffic(args, kernel):
+    """roofline.traffic of this very configuration, measured: the bench
+    re-runs itself (2 steps) under `rocprofv3 --pmc FETCH_SIZE`, then under
+    `--pmc WRITE_SIZE` (one counter per pass, never with a trace domain), as
+    child processes after the timed region, and pmc_traffic reads the
+    timed kernel's dispatches.  None when rocprofv3 is absent or a pass fails
+    (each pass is bounded to 150 s and killed with its process group)."""
+    import shutil
+    import signal
+    import subprocess
+    import tempfile
+    prof = shutil.which("rocprofv3")
+    if not prof:
+        return None
+    keep = [a for a in sys.argv[1:]]
+    drop = {"--steps", "--warmup", "--gpus"}
+    argv, skip = [], False
+    for a in keep:
+        if skip:
+            skip = False
+            continue
+        if a in drop:
+            skip = True
+            continue
+        if a.split("=")[0] in drop or a in ("--no-cpu", "--no-traffic"):
+            continue
+        argv.append(a)
+    paths = []
+    with tempfile.TemporaryDirectory(prefix="murr_pmc_") as d:
+        for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+            cmd = [prof, "--pmc", ctr, "--output-format", "csv", "-d", d, "-o", ctr.lower(), "--",
+                   sys.executable, os.path.abspath(__file__), *argv, "--steps", "2", "--warmup", "1",
+                   "--no-cpu", "--no-traffic"]
+            env = {k: v for k, v in os.environ.items() if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE")}
+            pr = subprocess.Popen(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, env=env,
+                                  start_new_session=True)
+            try:
+                rc = pr.wait(timeout=150)
+            except subprocess.TimeoutExpired:
+                os.killpg(pr.pid, signal.SIGKILL)
+                pr.wait()
+                return None
+            path = os.path.join(d, f"{ctr.lower()}_counter_collection.csv")
+            if rc != 0 or not os.path.exists(path):
+                return None
+            paths.append(path)
+        return pmc_traffic(",".join(paths), kernel)
+
+
 def cpu_model() -> str:
     """The host CPU's model name (lscpu model next to every
     CPU number), from /proc/cpuinfo."""
@@ -320,22 +369,42 @@ def run_decode(args, dist, rank, world, local_rank):
         def step():
             rt.scan_device(names, outs)  # the product call (its prepared plan after the first)
     else:
-        # the launch prepared once (murr_decode_plan); a step = murr_decode_run
-        plan = DecodePlan(ctx, seg, proj, blocks, outs)
-        step = plan.run
+        # the launch prepared once (murr_decode_plan), twice over two output
+        # sets: step s runs plan s % 2, launched (murr_decode_run_async)
+        # before step s - 1 is waited for, so the host's launch and read-back
+        # work overlaps the previous step's kernel, as a serving loop would;
+        # on the GPU the steps run one after the other (one stream)
+        plans = [DecodePlan(ctx, seg, proj, blocks, outs),
+                 DecodePlan(ctx, seg, proj, blocks, DecodeOutputs(ctx, seg, proj, blocks))]
 
-    for _ in range(args.warmup):
-        step()
+    def run_steps(n):
+        ms = []
+        if rt is not None or args.sync_steps:
+            run = step if rt is not None else plans[0].run
+            for _ in range(n):
+                run()
+                ms.append(ctx.last_kernel_ms())
+            return ms
+        if n:
+            plans[0].run_async()
+        for s in range(n):
+            if s + 1 < n:
+                plans[(s + 1) % 2].run_async()
+            plans[s % 2].wait()
+            ms.append(ctx.last_kernel_ms())
+        return ms
+
+    run_steps(args.warmup)
     barrier(dist)
     ctx.sync()
-    kms = []
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-        kms.append(ctx.last_kernel_ms())
+    kms = run_steps(args.steps)
     ctx.sync()
     barrier(dist)
     elapsed = time.perf_counter() - t0
+    if rt is None:
+        last = 0 if args.sync_steps else (args.steps - 1) % 2
+        outs = plans[last].outs  # the last timed step's output (checked below)
     elapsed = max_over_ranks(dist, elapsed)
     stats = ctx.stats()
 
@@ -352,6 +421,8 @@ def run_decode(args, dist, rank, world, local_rank):
     timed_kernel = ("decode_kernel" if stats["last_mode"] == "generic" else
                     "murr_jit_decode_%s%s" % ("split_" if stats["last_mode"] == "split" else "", shape))
     traffic = pmc_traffic(args.pmc_csv, timed_kernel)
+    if traffic is None and not args.pmc_csv and not args.no_traffic and world == 1 and rank == 0:
+        traffic = measure_traffic(args, timed_kernel)
 
     # after the timed region: the timed launch's output, checked against the
     # oracle (first and last block); a mismatch fails the run
@@ -373,7 +444,8 @@ def run_decode(args, dist, rank, world, local_rank):
             nk.append(ctx.last_kernel_ms())
         no_index_ms = round(float(np.mean(nk[1:])), 5)
         p2.close()
-        step()  # leave the indexed output in place
+        # leave the indexed output in place
+        (step if rt is not None else plans[last].run)()
     line = {
         "metric": METRIC, "value": round(value, 3), "unit": "GiB/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup,
@@ -408,7 +480,8 @@ def run_decode(args, dist, rank, world, local_rank):
     if rank == 0:
         print(json.dumps(line), flush=True)
     if rt is None:
-        plan.close()
+        for pl in plans:
+            pl.close()
     del rt
     ctx.close()
 
@@ -796,6 +869,10 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--pmc-csv", default=None)
+    ap.add_argument("--sync-steps", action="store_true",
+                    help="one plan, each step waited for before the next is launched (A/B of the pipelined loop)")
+    ap.add_argument("--no-traffic", action="store_true",
+                    help="skip the two rocprofv3 --pmc child passes that fill roofline.traffic (N=1)")
     ap.add_argument("--enc-config", default="E", choices=["B", "C", "E"], help="encode mode: column set")
     ap.add_argument("--proj", default=None, help="comma-separated projected columns, or rev (default all, in order)")
     ap.add_argument("--opts", default=None,

@@ -266,6 +266,14 @@ int murr_decode_plan(murr_ctx_t* ctx, const murr_segment_t* seg,
                      const uint64_t* const* uidx, uint32_t stride,
                      murr_array_t* outs, murr_plan_t** out);
 int murr_decode_run(murr_plan_t* plan, murr_error_t* err);   /* synchronous */
+/* murr_decode_run in two halves: _async launches the run on the context's
+ * stream and returns; _wait waits for it and fills the arrays' counts.  One
+ * run of a plan in flight at a time; runs of different plans on one context
+ * queue in stream order, so a caller alternating two plans (two output sets)
+ * launches the next run while the host finishes the previous one.  The
+ * context's last kernel time (murr_ctx_last_kernel_ms) is the waited run's. */
+int murr_decode_run_async(murr_plan_t* plan);
+int murr_decode_run_wait(murr_plan_t* plan, murr_error_t* err);
 void murr_plan_free(murr_plan_t* plan);
 
 /* ---- utf8 index of a block (optional) --------------------------------------

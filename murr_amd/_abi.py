@@ -130,6 +130,8 @@ SIGNATURES = {
     "murr_decode_plan": (I32, [P, C.POINTER(Segment), C.POINTER(U32), U32, C.POINTER(Block), U32,
                                C.POINTER(C.c_void_p), U32, C.POINTER(Array), PP]),
     "murr_decode_run": (I32, [P, C.POINTER(Error)]),
+    "murr_decode_run_async": (I32, [P]),
+    "murr_decode_run_wait": (I32, [P, C.POINTER(Error)]),
     "murr_plan_free": (None, [P]),
     "murr_sst_decode": (I32, [P, C.POINTER(SstBlock), U32, C.POINTER(SstResult), C.POINTER(Error)]),
     "murr_sst_result_free": (None, [P, C.POINTER(SstResult)]),

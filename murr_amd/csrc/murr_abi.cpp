@@ -63,6 +63,7 @@ struct murr_ctx {
     int enc_grid_per_cu = 1;
     hipStream_t stream = nullptr;
     hipEvent_t k0 = nullptr, k1 = nullptr;
+    hipEvent_t lk0 = nullptr, lk1 = nullptr;  // a prepared run's events, when it was the last timed op
     bool timed = false;
     uint8_t* ws = nullptr;  // device workspace
     uint64_t ws_cap = 0;
@@ -664,8 +665,9 @@ int murr_ctx_last_kernel_ms(murr_ctx_t* c, float* ms) {
     murr_error_t* err = nullptr;
     if (!c || !ms) return MURR_E_ARGUMENT;
     if (!c->timed) { *ms = 0.f; return MURR_OK; }
-    HIPC(hipEventSynchronize(c->k1));
-    HIPC(hipEventElapsedTime(ms, c->k0, c->k1));
+    hipEvent_t e0 = c->lk0 ? c->lk0 : c->k0, e1 = c->lk1 ? c->lk1 : c->k1;
+    HIPC(hipEventSynchronize(e1));
+    HIPC(hipEventElapsedTime(ms, e0, e1));
     return MURR_OK;
 }
 
@@ -838,11 +840,17 @@ struct JitReplay {
     bool split = false, emit = false;
     uint32_t grid = 0, lds = 0, mode = 0;
     std::vector<int32_t*> empty_offsets;  // utf8 offsets of empty blocks: [0] = 0 per run
+    hipEvent_t e0 = nullptr, e1 = nullptr;  // the run's kernel time
+    bool inflight = false;                  // murr_decode_run_async issued, murr_decode_run_wait not yet
+    int set = 0;                            // the in-flight run's counter set
     void release() {
         if (dws) (void)hipFree(dws);
         if (zb2) (void)hipFree(zb2);
         if (hrb) (void)hipHostFree(hrb);
+        if (e0) (void)hipEventDestroy(e0);
+        if (e1) (void)hipEventDestroy(e1);
         dws = zb2 = hrb = nullptr;
+        e0 = e1 = nullptr;
     }
 };
 
@@ -1136,6 +1144,7 @@ int decode_enqueue_jit(murr_ctx* c, const murr_segment_t* seg, const JitLayout* 
     c->stats.last_shape_r = K.r;
     HIPC(hipEventRecord(c->k1, c->stream));
     c->timed = true;
+    c->lk0 = c->lk1 = nullptr;
     HIPC(hipMemcpyAsync(c->hs + rb, c->ws, z_lb, hipMemcpyDeviceToHost, c->stream));
     c->retry_local = !local && emit && tiles;
     if (c->retry_local) {
@@ -1406,6 +1415,7 @@ int murr_decode_enqueue_ix(murr_ctx_t* c, const murr_segment_t* seg, const uint3
     c->stats.last_shape_r = kc;
     HIPC(hipEventRecord(c->k1, c->stream));
     c->timed = true;
+    c->lk0 = c->lk1 = nullptr;
     HIPC(hipMemcpyAsync(c->hs + rb, c->ws, z_lb, hipMemcpyDeviceToHost, c->stream));
 
     return pending_set(c, outs, blocks, nblocks, nproj, dp, rb);
@@ -1556,6 +1566,9 @@ struct murr_plan {
     const JitLayout* jl = nullptr;  // pinned while the plan lives
     bool replay = false;
     JitReplay r;
+    bool sync_pending = false;  // (no replay) murr_decode_run_async ran the decode; wait returns its status
+    int sync_status = 0;
+    murr_error_t sync_err{};
 };
 
 extern "C" {
@@ -1599,6 +1612,11 @@ int murr_decode_plan(murr_ctx_t* c, const murr_segment_t* seg, const uint32_t* p
                 return st;
             }
             P->replay = true;
+            if (hipEventCreate(&P->r.e0) != hipSuccess || hipEventCreate(&P->r.e1) != hipSuccess) {
+                P->r.release();
+                jit_layout_unpin(P->jl);
+                return MURR_E_HIP;
+            }
         } else if (c->opts.kernel == 1) {
             return MURR_E_INTERNAL;
         }
@@ -1607,14 +1625,20 @@ int murr_decode_plan(murr_ctx_t* c, const murr_segment_t* seg, const uint32_t* p
     return MURR_OK;
 }
 
-int murr_decode_run(murr_plan_t* P, murr_error_t* err) {
-    if (!P) return set_err(err, MURR_E_ARGUMENT);
+int murr_decode_run_async(murr_plan_t* P) {
+    if (!P) return MURR_E_ARGUMENT;
     murr_ctx* c = P->c;
-    if (c->pending) return set_err(err, MURR_E_ARGUMENT);
+    if (c->pending || P->r.inflight || P->sync_pending) return MURR_E_ARGUMENT;
     const uint32_t nblocks = (uint32_t)P->blocks.size(), nproj = (uint32_t)P->proj.size();
-    if (!P->replay)
-        return murr_decode_blocks_ix(c, &P->seg, P->proj.data(), nproj, P->blocks.data(), nblocks,
-                                     P->uidx.empty() ? nullptr : P->uidx.data(), P->stride, P->outs, err);
+    if (!P->replay) {  // (generic kernel) the ordinary decode, done now; wait reports it
+        P->sync_err = murr_error_t{};
+        P->sync_status = murr_decode_blocks_ix(c, &P->seg, P->proj.data(), nproj, P->blocks.data(), nblocks,
+                                               P->uidx.empty() ? nullptr : P->uidx.data(), P->stride, P->outs,
+                                               &P->sync_err);
+        P->sync_pending = true;
+        return MURR_OK;
+    }
+    murr_error_t* err = nullptr;
     JitReplay& R = P->r;
     HIPC(hipSetDevice(c->device));
     c->stats.decodes++;
@@ -1625,19 +1649,39 @@ int murr_decode_run(murr_plan_t* P, murr_error_t* err) {
     volatile uint64_t* done = (volatile uint64_t*)(R.hrb + R.z_lb);
     *done = 0;
     std::atomic_thread_fence(std::memory_order_seq_cst);
-    HIPC(hipEventRecord(c->k0, c->stream));
+    HIPC(hipEventRecord(R.e0, c->stream));
     for (const auto& ka : R.kargs[set])
         HIPC(jit_decode_launch(R.K, R.split, ka.data(), ka.size(), R.grid, R.lds, c->stream));
-    HIPC(hipEventRecord(c->k1, c->stream));
+    HIPC(hipEventRecord(R.e1, c->stream));
+    R.set = set;
+    R.inflight = true;
+    return MURR_OK;
+}
+
+int murr_decode_run_wait(murr_plan_t* P, murr_error_t* err) {
+    if (!P) return set_err(err, MURR_E_ARGUMENT);
+    murr_ctx* c = P->c;
+    if (P->sync_pending) {
+        P->sync_pending = false;
+        if (err) *err = P->sync_err;
+        return P->sync_status;
+    }
+    JitReplay& R = P->r;
+    if (!R.inflight) return set_err(err, MURR_E_ARGUMENT);
+    R.inflight = false;
+    const int set = R.set;
+    const uint32_t nblocks = (uint32_t)P->blocks.size(), nproj = (uint32_t)P->proj.size();
+    HIPC(hipSetDevice(c->device));
     // The last workgroup's epilogue writes the counters here and sets `done`:
-    // no read-back copy, no stream synchronisation.  Should the stream go idle
+    // no read-back copy, no stream synchronisation.  Should the run end
     // without the flag (it cannot, short of a device fault), read the
     // counters back the ordinary way.
+    volatile uint64_t* done = (volatile uint64_t*)(R.hrb + R.z_lb);
     bool flagged = false;
     if (!R.kargs[set].empty()) {
         for (uint64_t spin = 1;; spin++) {
             if (*done) { flagged = true; break; }
-            if ((spin & 4095) == 0 && hipStreamQuery(c->stream) == hipSuccess) {
+            if ((spin & 4095) == 0 && hipEventQuery(R.e1) == hipSuccess) {
                 flagged = *done != 0;
                 break;
             }
@@ -1651,6 +1695,8 @@ int murr_decode_run(murr_plan_t* P, murr_error_t* err) {
         HIPC(hipStreamSynchronize(c->stream));
     }
     c->timed = true;
+    c->lk0 = R.e0;
+    c->lk1 = R.e1;
     if (!R.kargs[0].empty()) c->last_kernel = "murr_jit_decode";
     c->stats.last_mode = R.mode;
     c->stats.last_grid = R.grid;
@@ -1669,10 +1715,20 @@ int murr_decode_run(murr_plan_t* P, murr_error_t* err) {
     return finish_counts(c, R.hrb, P->outs, nblocks, nproj, P->n_rows.data(), P->dtypes.data(), err);
 }
 
+int murr_decode_run(murr_plan_t* P, murr_error_t* err) {
+    const int st = murr_decode_run_async(P);
+    if (st) return set_err(err, st);
+    return murr_decode_run_wait(P, err);
+}
+
 void murr_plan_free(murr_plan_t* P) {
     if (!P) return;
     if (P->c) (void)hipSetDevice(P->c->device);
     if (P->r.dws) (void)hipStreamSynchronize(P->c->stream);
+    if (P->c && P->r.e0 && P->c->lk0 == P->r.e0) {  // its events were the context's last timing
+        P->c->lk0 = P->c->lk1 = nullptr;
+        P->c->timed = false;
+    }
     P->r.release();
     jit_layout_unpin(P->jl);
     delete P;
@@ -1811,6 +1867,7 @@ int murr_encode_batch_at(murr_ctx_t* c, const murr_segment_t* seg, const murr_co
     }
     HIPC(hipEventRecord(c->k1, c->stream));
     c->timed = true;
+    c->lk0 = c->lk1 = nullptr;
     HIPC(hipMemcpyAsync(c->hs + rb, c->ws, 8, hipMemcpyDeviceToHost, c->stream));
     HIPC(hipMemcpyAsync(c->hs + rb + 8, out_row_off + n, 8, hipMemcpyDeviceToHost, c->stream));
     HIPC(hipStreamSynchronize(c->stream));
@@ -2384,6 +2441,7 @@ int murr_sst_decode(murr_ctx_t* c, const murr_sst_block_t* blocks, uint32_t nblo
         if (raw) SSTC(launch_sst_big_decode(a, c->stream));
         SSTC(hipEventRecord(c->k1, c->stream));
         c->timed = true;
+    c->lk0 = c->lk1 = nullptr;
         c->last_kernel = "sst_decode";
     }
     SSTC(hipStreamSynchronize(c->stream));

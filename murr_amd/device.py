@@ -313,6 +313,15 @@ class DecodePlan:
         raise_status(st, self._err, "murr_decode_run")
         return self.outs
 
+    def run_async(self):
+        """Launch a run and return (murr_decode_run_async); wait() finishes it."""
+        raise_status(self.ctx.L.murr_decode_run_async(self.h), what="murr_decode_run_async")
+
+    def wait(self) -> "DecodeOutputs":
+        st = self.ctx.L.murr_decode_run_wait(self.h, C.byref(self._err))
+        raise_status(st, self._err, "murr_decode_run_wait")
+        return self.outs
+
     def close(self):
         if getattr(self, "h", None) and self.ctx.h:
             self.ctx.L.murr_plan_free(self.h)
