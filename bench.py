@@ -362,36 +362,38 @@ def run_decode(args, dist, rank, world, local_rank):
     host_blob = blocks[0].data.download(blocks[0].data_bytes)
     host_off = blocks[0].row_off.download((rows + 1) * 8).view(np.uint64).copy()
     ix_bytes = 8 * int(L_len(ctx, seg, rows, ix_stride)) if blocks[0].uidx is not None else 0
-    outs = DecodeOutputs(ctx, seg, proj, blocks)
+    # Two output sets: step s decodes into set s % 2 and is launched
+    # (murr_decode_run_async) before step s - 1 is waited for, so the host's
+    # launch and read-back work overlaps the previous step's kernel, as a
+    # serving loop would; on the GPU the steps run one after the other (one
+    # stream).  --sync-steps: one set, each step waited for (the A/B).
+    out_sets = [DecodeOutputs(ctx, seg, proj, blocks), DecodeOutputs(ctx, seg, proj, blocks)]
     if rt is not None:
         names = [seg.columns[c].name for c in proj]
 
-        def step():
-            rt.scan_device(names, outs)  # the product call (its prepared plan after the first)
+        def launch(i):  # the product call (its prepared plan after the first)
+            return rt.scan_device_async(names, out_sets[i])
     else:
-        # the launch prepared once (murr_decode_plan), twice over two output
-        # sets: step s runs plan s % 2, launched (murr_decode_run_async)
-        # before step s - 1 is waited for, so the host's launch and read-back
-        # work overlaps the previous step's kernel, as a serving loop would;
-        # on the GPU the steps run one after the other (one stream)
-        plans = [DecodePlan(ctx, seg, proj, blocks, outs),
-                 DecodePlan(ctx, seg, proj, blocks, DecodeOutputs(ctx, seg, proj, blocks))]
+        # the launch prepared once per output set (murr_decode_plan)
+        plans = [DecodePlan(ctx, seg, proj, blocks, o) for o in out_sets]
+
+        def launch(i):
+            plans[i].run_async()
+            return plans[i]
 
     def run_steps(n):
         ms = []
-        if rt is not None or args.sync_steps:
-            run = step if rt is not None else plans[0].run
+        if args.sync_steps:
             for _ in range(n):
-                run()
+                launch(0).wait()
                 ms.append(ctx.last_kernel_ms())
             return ms
-        if n:
-            plans[0].run_async()
+        h = launch(0) if n else None
         for s in range(n):
-            if s + 1 < n:
-                plans[(s + 1) % 2].run_async()
-            plans[s % 2].wait()
+            hn = launch((s + 1) % 2) if s + 1 < n else None
+            h.wait()
             ms.append(ctx.last_kernel_ms())
+            h = hn
         return ms
 
     run_steps(args.warmup)
@@ -402,9 +404,8 @@ def run_decode(args, dist, rank, world, local_rank):
     ctx.sync()
     barrier(dist)
     elapsed = time.perf_counter() - t0
-    if rt is None:
-        last = 0 if args.sync_steps else (args.steps - 1) % 2
-        outs = plans[last].outs  # the last timed step's output (checked below)
+    last = 0 if args.sync_steps else (args.steps - 1) % 2
+    outs = out_sets[last]  # the last timed step's output (checked below)
     elapsed = max_over_ranks(dist, elapsed)
     stats = ctx.stats()
 
@@ -445,7 +446,7 @@ def run_decode(args, dist, rank, world, local_rank):
         no_index_ms = round(float(np.mean(nk[1:])), 5)
         p2.close()
         # leave the indexed output in place
-        (step if rt is not None else plans[last].run)()
+        launch(last).wait()
     line = {
         "metric": METRIC, "value": round(value, 3), "unit": "GiB/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup,

@@ -180,7 +180,7 @@ class ResidentTable:
         self._reader = None    # murr_reader_t: scratch of the one-call host read
         self.uidx = None       # utf8 index of the arena (UIDX_STRIDE), kept with every write
         self.uidx_cap = 0      # entries
-        self._scan_plan = None  # (key, DecodePlan) of the last scan_device
+        self._scan_plans = {}  # id(outs) (None: the plan's own outputs) -> (key, DecodePlan) of scan_device
 
     def __del__(self):
         try:
@@ -339,6 +339,13 @@ class ResidentTable:
         buffers in HBM.  `outs` (from an earlier scan of the same columns and
         row count) is reused.  The bulk read of SURVEY.md §8(e) mode 1: a GPU
         decodes its whole shard."""
+        return self.scan_device_async(columns, outs).wait()
+
+    def scan_device_async(self, columns, outs: DecodeOutputs | None = None) -> DecodePlan:
+        """scan_device's launch only (murr_decode_run_async): returns the
+        prepared plan, whose wait() finishes the scan and returns its outputs.
+        A caller alternating two `outs` launches the next scan before waiting
+        for the previous one; each `outs` keeps its own prepared plan."""
         if self.n == 0:
             self._resolve(columns)  # (an unknown column is reported first)
             raise SegmentError("resident table is empty")
@@ -346,7 +353,8 @@ class ResidentTable:
         # repeated scan costs a tuple compare here and one library call)
         state = (tuple(columns), self.arena.ptr, self.row_off.ptr, self.uidx.ptr if self.uidx is not None else 0,
                  self.n, self.used, getattr(self.ctx, "opts_gen", 0))
-        plan = self._scan_plan
+        slot = id(outs) if outs is not None else None
+        plan = self._scan_plans.get(slot)
         if plan is None or plan[0] != state or (outs is not None and outs is not plan[1].outs):
             proj = [c.index for c in self._resolve(columns)]
             # prepared once per (columns, table state, outputs): a repeated
@@ -355,11 +363,17 @@ class ResidentTable:
             # the next scan).
             if plan is not None:
                 plan[1].close()
+            if len(self._scan_plans) >= 4:  # a few output sets at most
+                for k in list(self._scan_plans):
+                    if k != slot:
+                        self._scan_plans.pop(k)[1].close()
+                        break
             blk = self.block()
             p = DecodePlan(self.ctx, self.segment, proj, [blk],
                            outs or DecodeOutputs(self.ctx, self.segment, proj, [blk]))
-            self._scan_plan = plan = (state, p)
-        return plan[1].run()
+            self._scan_plans[slot] = plan = (state, p)
+        plan[1].run_async()
+        return plan[1]
 
     def scan(self, columns) -> pa.RecordBatch:
         """scan_device, brought to the host as a RecordBatch (rows in write
