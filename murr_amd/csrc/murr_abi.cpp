@@ -1176,7 +1176,7 @@ int murr_segment_prepare(murr_ctx_t* c, const murr_segment_t* seg) {
         ec[i] = EncCol{nullptr, nullptr, nullptr, 0, col.dtype, col.index, col.offset, col.size};
     }
     if (seg->ncols &&
-        !jit_encode_kernel(c->device, seg->bitset_size, seg->capacity, ec.data(), seg->ncols, 32768, &why)) {
+        !jit_encode_kernel(c->device, seg->bitset_size, seg->capacity, ec.data(), seg->ncols, 32768, 256, &why)) {
         std::fprintf(stderr, "murr: JIT encode unavailable: %s\n", why.c_str());
         return MURR_E_INTERNAL;
     }
@@ -1807,7 +1807,23 @@ int murr_encode_batch_at(murr_ctx_t* c, const murr_segment_t* seg, const murr_co
         return MURR_E_CAPACITY;
     }
     if (n && !out_blob) return set_err(err, MURR_E_ARGUMENT);
-    const uint64_t tiles = (n + kTile - 1) / kTile;
+    // Run-time specialised encode kernel unless the context asks for the
+    // generic one (or it cannot be compiled: then the generic encode_kernel).
+    const JitEncKernel* ek = nullptr;
+    {
+        const uint32_t ek_mode = c->opts.encode_kernel;
+        if (ek_mode != 2 && seg->ncols) {
+            std::string why;
+            const uint32_t tile = jit_encode_tile(n, blob_cap);
+            ek = jit_encode_kernel(c->device, seg->bitset_size, seg->capacity, ec.data(), seg->ncols,
+                                   jit_encode_stage(n, blob_cap, tile), tile, &why);
+            if (!ek && (c->opts.verbose || ek_mode == 1))
+                std::fprintf(stderr, "murr: JIT encode unavailable: %s\n", why.c_str());
+            if (!ek && ek_mode == 1) return set_err(err, MURR_E_INTERNAL);
+        }
+    }
+    const uint32_t tile = ek ? ek->tile : kTile;
+    const uint64_t tiles = (n + tile - 1) / tile;
     // utf8 layouts: tile totals / starts, then the group sums (JIT scan)
     const uint64_t z_lb = 16,
                    zbytes = round_up(z_lb + 8 * (nutf8 ? tiles + 1 + (tiles + kEncScanPer - 1) / kEncScanPer : 0), 16);
@@ -1836,20 +1852,6 @@ int murr_encode_batch_at(murr_ctx_t* c, const murr_segment_t* seg, const murr_co
     a.nutf8 = nutf8;
     a.bs = seg->bitset_size;
     a.cap = seg->capacity;
-    // Run-time specialised encode kernel unless MURR_ENCODE_JIT=0 (or it cannot
-    // be compiled: then the generic encode_kernel).
-    const JitEncKernel* ek = nullptr;
-    {
-        const uint32_t ek_mode = c->opts.encode_kernel;
-        if (ek_mode != 2 && seg->ncols) {
-            std::string why;
-            ek = jit_encode_kernel(c->device, seg->bitset_size, seg->capacity, ec.data(), seg->ncols,
-                                   jit_encode_stage(n, blob_cap), &why);
-            if (!ek && (c->opts.verbose || ek_mode == 1))
-                std::fprintf(stderr, "murr: JIT encode unavailable: %s\n", why.c_str());
-            if (!ek && ek_mode == 1) return set_err(err, MURR_E_INTERNAL);
-        }
-    }
     HIPC(hipEventRecord(c->k0, c->stream));
     if (tiles) {
         // persistent grid, co-resident (the utf8 window prefix waits on tiles t-G+1 .. t-1)

@@ -167,13 +167,16 @@ hipError_t jit_decode_launch(const JitShapeK& k, bool split, const void* args, s
 // Run-time specialised encode kernel (murr_jit.cpp, murr_jit_encode.hip).
 struct JitEncKernel {
     hipFunction_t fn, fn_sizes, fn_scan;  // encode; tile sizes and their scan (utf8 layouts)
-    int bpc;  // resident workgroups per CU
+    int bpc;        // resident workgroups per CU
+    uint32_t tile;  // rows per tile = threads per workgroup (jit_encode_tile)
 };
 struct EncCol;
 // stage: LDS bytes of a tile's blobs (jit_encode_stage), a compile-time size.
-uint32_t jit_encode_stage(uint64_t n_rows, uint64_t blob_cap);
+uint32_t jit_encode_stage(uint64_t n_rows, uint64_t blob_cap, uint32_t tile);
+// tile: rows per encode tile (jit_encode_tile: 256).
+uint32_t jit_encode_tile(uint64_t n_rows, uint64_t blob_cap);
 const JitEncKernel* jit_encode_kernel(int device, uint32_t bs, uint32_t cap, const EncCol* cols, uint32_t ncols,
-                                      uint32_t stage, std::string* why);
+                                      uint32_t stage, uint32_t tile, std::string* why);
 struct EncodeArgs;
 // inline_sizes: no utf8 column has a validity buffer (the scan computes the
 // tile totals; no sizes pass).

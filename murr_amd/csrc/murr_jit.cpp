@@ -335,12 +335,14 @@ struct EncEntry {
 };
 std::map<std::string, std::unique_ptr<EncEntry>> g_enc;
 
-std::string enc_prelude(uint32_t bs, uint32_t cap, const EncCol* cols, uint32_t ncols, uint32_t stage) {
+std::string enc_prelude(uint32_t bs, uint32_t cap, const EncCol* cols, uint32_t ncols, uint32_t stage,
+                        uint32_t tile) {
     std::ostringstream o;
     uint32_t nutf8 = 0;
     for (uint32_t c = 0; c < ncols; c++) nutf8 += cols[c].dtype == MURR_UTF8;
     o << "#define MJE_BS " << bs << "\n#define MJE_CAP " << cap << "\n#define MJE_NCOLS " << ncols
-      << "\n#define MJE_NUTF8 " << nutf8 << "\n#define MJE_STAGE " << stage << "\n#define MJE_SCAN_PER " << kEncScanPer
+      << "\n#define MJE_NUTF8 " << nutf8 << "\n#define MJE_STAGE " << stage << "\n#define MJE_TILE " << tile
+      << "\n#define MJE_SCAN_PER " << kEncScanPer
       << "\n#define MJE_COLS(X)";
     for (uint32_t c = 0, u = 0; c < ncols; c++) {
         const uint32_t kind = cols[c].dtype == MURR_UTF8 ? 0u : cols[c].dtype == MURR_BOOL ? 9u : cols[c].width;
@@ -358,15 +360,31 @@ std::string enc_prelude(uint32_t bs, uint32_t cap, const EncCol* cols, uint32_t 
 // of headroom.  Small stages let eight workgroups share a CU; a tile over its
 // stage is written straight to HBM (correct, slower).  Three variants per
 // layout at most (each one compile, cached).
-uint32_t jit_encode_stage(uint64_t n_rows, uint64_t blob_cap) {
+uint32_t jit_encode_stage(uint64_t n_rows, uint64_t blob_cap, uint32_t tile) {
     const uint64_t mean = n_rows ? (blob_cap + n_rows - 1) / n_rows : 128;
-    const uint64_t want = 256 * mean * 5 / 4 + 64;
+    const uint64_t want = tile * mean * 5 / 4 + 64;
     return want <= 8192 ? 8192u : want <= 16384 ? 16384u : 32768u;
 }
 
+// Rows per encode tile (= threads per workgroup): 256 for every layout.
+// Measured (profiles/r03/probes/enc_tile_ab.txt): 128-row tiles for wide rows
+// (twice the workgroups per CU, half the rows between barriers) took config
+// C from 1.07 to 1.59 ms; 512 rows 3.7 ms; B and E within 3 % at 128 / 512.
+uint32_t jit_encode_tile(uint64_t n_rows, uint64_t blob_cap) {
+    (void)n_rows;
+    (void)blob_cap;
+#ifdef MURR_TUNING
+    if (const char* e = std::getenv("MURR_ENC_TILE")) {  // A/B
+        const int t = std::atoi(e);
+        if (t == 64 || t == 128 || t == 256 || t == 512) return (uint32_t)t;
+    }
+#endif
+    return 256u;
+}
+
 const JitEncKernel* jit_encode_kernel(int device, uint32_t bs, uint32_t cap, const EncCol* cols, uint32_t ncols,
-                                      uint32_t stage, std::string* why) {
-    const std::string pre = enc_prelude(bs, cap, cols, ncols, stage);
+                                      uint32_t stage, uint32_t tile, std::string* why) {
+    const std::string pre = enc_prelude(bs, cap, cols, ncols, stage, tile);
     const std::string key = std::to_string(device) + "\n" + pre;
     std::lock_guard<std::mutex> lk(g_mu);
     auto it = g_enc.find(key);
@@ -383,9 +401,10 @@ const JitEncKernel* jit_encode_kernel(int device, uint32_t bs, uint32_t cap, con
             if (he == hipSuccess) he = hipModuleGetFunction(&e->k.fn_scan, e->mod, "murr_jit_encode_scan");
             int bpc = 0;
             if (he == hipSuccess &&
-                (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, e->k.fn, 256, 0) != hipSuccess || bpc < 1))
+                (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, e->k.fn, tile, 0) != hipSuccess || bpc < 1))
                 bpc = 1;
             e->k.bpc = bpc;
+            e->k.tile = tile;
             if (he != hipSuccess) e->why = std::string("module load: ") + hipGetErrorString(he);
             e->ok = he == hipSuccess;
             (void)hipSetDevice(cur);
@@ -412,7 +431,7 @@ hipError_t jit_encode_launch(const JitEncKernel* k, const EncodeArgs& a, uint32_
         // (no utf8 column with a validity buffer: the scan derives the tile
         // totals from the offsets itself, murr_jit_encode.hip sizes_inline)
         hipError_t e = inline_sizes ? hipSuccess
-                                    : hipModuleLaunchKernel(k->fn_sizes, tiles, 1, 1, 256, 1, 1, 0, s, nullptr, cfg);
+                                    : hipModuleLaunchKernel(k->fn_sizes, tiles, 1, 1, k->tile, 1, 1, 0, s, nullptr, cfg);
         struct {
             EncodeArgs a;
             uint32_t pass;
@@ -436,7 +455,7 @@ hipError_t jit_encode_launch(const JitEncKernel* k, const EncodeArgs& a, uint32_
     if (const char* g = std::getenv("MURR_ENC_GRID"))  // workgroups per CU of a persistent grid (A/B)
         if (std::atoi(g)) grid = (uint32_t)std::min<uint64_t>(a.total_tiles, (uint64_t)std::atoi(g) * 256);
 #endif
-    return hipModuleLaunchKernel(k->fn, grid, 1, 1, 256, 1, 1, 0, s, nullptr, cfg);
+    return hipModuleLaunchKernel(k->fn, grid, 1, 1, k->tile, 1, 1, 0, s, nullptr, cfg);
 }
 
 }  // namespace murr

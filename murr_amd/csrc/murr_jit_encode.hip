@@ -61,7 +61,10 @@ struct Args {  // = murr::EncodeArgs
     uint64_t row_base;       // row_off values are row_base + offset in out
 };
 
-constexpr uint32_t TILE = 256, BS = MJE_BS, CAP = MJE_CAP, NCOLS = MJE_NCOLS, NUTF8 = MJE_NUTF8,
+#ifndef MJE_TILE
+#define MJE_TILE 256
+#endif
+constexpr uint32_t TILE = MJE_TILE, NWAVE = MJE_TILE / 64, BS = MJE_BS, CAP = MJE_CAP, NCOLS = MJE_NCOLS, NUTF8 = MJE_NUTF8,
                    STAGE = MJE_STAGE;
 constexpr uint32_t FIXED = BS + CAP;
 constexpr uint32_t NR = (FIXED + 3) / 4;  // dwords of the fixed part
@@ -545,7 +548,7 @@ template <uint32_t C, uint32_t U> DEV void emit_payload(const RowBuild& B, Emit&
 #else
 #define MJE_WPE_ATTR
 #endif
-extern "C" __global__ void __launch_bounds__(256) MJE_WPE_ATTR murr_jit_encode(mje::Args) {
+extern "C" __global__ void __launch_bounds__(MJE_TILE) MJE_WPE_ATTR murr_jit_encode(mje::Args) {
     using namespace mje;
     __shared__ __attribute__((aligned(16))) uint32_t stage[STAGE / 4 + 8];
     __shared__ uint64_t s_w[8];
@@ -598,7 +601,7 @@ extern "C" __global__ void __launch_bounds__(256) MJE_WPE_ATTR murr_jit_encode(m
             __syncthreads();
             uint64_t before = 0, agg = 0;
 #pragma unroll
-            for (uint32_t w = 0; w < 4; w++) {
+            for (uint32_t w = 0; w < NWAVE; w++) {
                 const uint64_t v = s_w[w];
                 before += w < wave ? v : 0u;
                 agg += v;
@@ -682,9 +685,9 @@ extern "C" __global__ void __launch_bounds__(256) MJE_WPE_ATTR murr_jit_encode(m
 
 // Row sizes of each tile: bs + cap + sum over non-null utf8 of (4 + len),
 // summed into lookback[t] (the Arrow validity and offsets only).
-extern "C" __global__ void __launch_bounds__(256) murr_jit_encode_sizes(mje::Args) {
+extern "C" __global__ void __launch_bounds__(MJE_TILE) murr_jit_encode_sizes(mje::Args) {
     using namespace mje;
-    __shared__ uint64_t s_w[4];
+    __shared__ uint64_t s_w[NWAVE];
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const CAS Args* A = args();
     const uint64_t n_rows = A->n_rows, total_tiles = A->total_tiles;
@@ -707,7 +710,12 @@ extern "C" __global__ void __launch_bounds__(256) murr_jit_encode_sizes(mje::Arg
         for (int m = 32; m >= 1; m >>= 1) size += (uint64_t)__shfl_xor((unsigned long long)size, m, 64);
         if (lane == 0) s_w[wave] = size;
         __syncthreads();
-        if (tid == 0) gp(A->lookback)[t] = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+        if (tid == 0) {
+            uint64_t tot = 0;
+#pragma unroll
+            for (uint32_t w = 0; w < NWAVE; w++) tot += s_w[w];
+            gp(A->lookback)[t] = tot;
+        }
         __syncthreads();
     }
 }
