@@ -140,6 +140,10 @@ def measure_traffic(args, kernel):
     prof = shutil.which("rocprofv3")
     if not prof:
         return None
+    # never nested: a bench already running under rocprofv3 (its tool library
+    # preloaded, ROCPROF_* set) leaves the counters to that profiler
+    if "rocprof" in os.environ.get("LD_PRELOAD", "") or any(k.startswith("ROCPROF") for k in os.environ):
+        return None
     keep = [a for a in sys.argv[1:]]
     drop = {"--steps", "--warmup", "--gpus"}
     argv, skip = [], False

@@ -16,15 +16,15 @@ run() {  # run <name> <timeout> <cmd...>
   [ $rc -eq 0 ] || exit $rc
 }
 # the driver's exact command (bench.py --gpus 1 --steps 20 --warmup 5), traced
-run trace 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out/trace -o decode -- python3 bench.py --gpus 1 --steps 20 --warmup 5
-run fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $out/pmc -o fetch -- python3 bench.py --steps 3 --warmup 1 --no-cpu
-run write 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $out/pmc -o write -- python3 bench.py --steps 3 --warmup 1 --no-cpu
+run trace 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out/trace -o decode -- python3 bench.py --gpus 1 --steps 20 --warmup 5 --no-traffic
+run fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $out/pmc -o fetch -- python3 bench.py --steps 3 --warmup 1 --no-cpu --no-traffic
+run write 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $out/pmc -o write -- python3 bench.py --steps 3 --warmup 1 --no-cpu --no-traffic
 run bench 400 python3 bench.py --gpus 1 --steps 20 --warmup 5 --pmc-csv "$out/pmc/fetch_counter_collection.csv,$out/pmc/write_counter_collection.csv"
 # wide-schema decode (configs C / D one-shard) with their own traffic passes
 for cfg in "C:--config C --blocks 10" "D1:--config D"; do
   n=${cfg%%:*}; a=${cfg#*:}
-  run fetch_$n 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $out/pmc -o fetch_$n -- python3 bench.py $a --steps 3 --warmup 1 --no-cpu
-  run write_$n 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $out/pmc -o write_$n -- python3 bench.py $a --steps 3 --warmup 1 --no-cpu
+  run fetch_$n 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $out/pmc -o fetch_$n -- python3 bench.py $a --steps 3 --warmup 1 --no-cpu --no-traffic
+  run write_$n 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $out/pmc -o write_$n -- python3 bench.py $a --steps 3 --warmup 1 --no-cpu --no-traffic
   run decode_$n 300 python3 bench.py $a --steps 10 --warmup 2 --no-cpu --pmc-csv "$out/pmc/fetch_${n}_counter_collection.csv,$out/pmc/write_${n}_counter_collection.csv"
 done
 if [ -z "${QUICK:-}" ]; then
