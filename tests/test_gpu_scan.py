@@ -124,3 +124,25 @@ def test_scan_device_bit_exact_config_d_shard(ctx):
     assert again is outs
     for p in (0, 11, 12):
         assert_array_equal(download_array(ctx, outs.array(0, p), int(C_DTYPES[p]), n), want[p], f"again {p}")
+
+
+def test_scan_device_async_alternating_outputs(ctx):
+    # two output sets, the next scan launched before the previous is waited
+    # for (bench.py's timed loop for config D): each keeps its own prepared
+    # plan and both hold the oracle's arrays
+    n = 200_000
+    rt = ResidentTable(schema_c(), ctx)
+    rt.write(batch_c(n))
+    names = [f"c{i}" for i in range(len(C_DTYPES))]
+    first = rt.scan_device(names)
+    sets = [DecodeOutputs(ctx, rt.segment, list(range(len(C_DTYPES))), [rt.block()]) for _ in range(2)]
+    h = rt.scan_device_async(names, sets[0])
+    for s in range(4):
+        hn = rt.scan_device_async(names, sets[(s + 1) % 2]) if s < 3 else None
+        assert h.wait() is sets[s % 2]
+        h = hn
+    data, off = arena(rt)
+    want = O.decode_block(O.Segment([int(d) for d in C_DTYPES]), list(range(len(C_DTYPES))), data, off)
+    for outs in sets + [first]:
+        for p in (0, 3, 11, 12, 15):
+            assert_array_equal(download_array(ctx, outs.array(0, p), int(C_DTYPES[p]), n), want[p], f"col {p}")
