@@ -229,8 +229,14 @@ DEV void write_out(const LAS uint8_t* buf, GAS uint8_t* out, uint64_t g0, uint64
 
 // One row's fixed part and payload sizes.  `pos` = payload append position
 // (write.rs:44-52), starting at bs + cap.
+// Strings of up to 4 * MJE_PF - 4 bytes are loaded whole with the row, among
+// the other columns' loads: 9 dwords for wide rows (a fixed part of 32 bytes
+// or more) with one or two utf8 columns (config C 1.04-1.08 -> 1.01-1.04 ms,
+// E unchanged), else 5 (config B's 9-byte rows 0.212 -> 0.222 ms at 9; past
+// two utf8 columns 4 more dwords each would cost occupancy);
+// profiles/r03/probes/enc_pf_ab.txt.
 #ifndef MJE_PF
-#define MJE_PF 5
+#define MJE_PF (MJE_BS + MJE_CAP >= 32 && MJE_NUTF8 <= 2 ? 9 : 5)
 #endif
 constexpr uint32_t PF = MJE_PF;  // aligned dwords of each string loaded with the row (the rest later)
 struct RowBuild {
