@@ -334,7 +334,12 @@ def run_decode(args, dist, rank, world, local_rank):
     check_gpus(local_rank, world)
     ctx = Context(local_rank)
     rows, K = args.rows, args.blocks
-    start, _ = shard_rows(rank, world, rows * world)  # weak scaling: `rows` per rank
+    if args.table_rows:
+        # configs[3] as written: ONE table of --table-rows rows split by key
+        # range over the ranks (strong scaling: rank r decodes its range)
+        start, rows = shard_rows(rank, world, args.table_rows)
+    else:
+        start, _ = shard_rows(rank, world, rows * world)  # weak scaling: `rows` per rank
     rt = None
     t_build = time.perf_counter()
     if args.config == "D":
@@ -455,12 +460,16 @@ def run_decode(args, dist, rank, world, local_rank):
         "metric": METRIC, "value": round(value, 3), "unit": "GiB/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
+        "scaling": "strong" if args.table_rows else "weak", "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic",
         "config": {"workload": {"B": "configs[1] read_block shape: 100k-row FLOAT32+UTF8 blocks",
                                 "C": "configs[2] schema: 16-col mixed nullable blocks",
                                 "D": "configs[3] shard: 16-col mixed nullable, key-range shard per GPU, "
                                      "ResidentTable.scan"}.get(args.config, args.config),
                    "rows_per_block": rows, "blocks_per_step": K, "columns": len(proj),
+                   "table_rows": args.table_rows or None,
+                   "rows_per_rank": [shard_rows(r, world, args.table_rows)[1] for r in range(world)]
+                   if args.table_rows else [rows] * world,
                    "utf8_index_stride": ix_stride if ix_bytes else None,
                    "bytes_in_per_step": in_block * K, "bytes_out_per_step": out_step,
                    "parallelism": f"{world} key-range shard(s), no collective",
@@ -495,7 +504,10 @@ def run_harness(args, dist, rank, world, local_rank):
     """Self-test of the multi-rank harness (spawner, barriers, max/sum over
     ranks, the JSON line) without a GPU: the "step" copies a host buffer.
     Never a measurement: data = "harness self-test"."""
-    buf = np.zeros(1 << 20, np.uint8)
+    rows = None
+    if args.table_rows:  # the row split of configs[3] as written (strong scaling)
+        _, rows = shard_rows(rank, world, args.table_rows)
+    buf = np.zeros(max(rows or 0, 1 << 20) if rows is None else max(rows, 1), np.uint8)
     dst = np.empty_like(buf)
     for _ in range(args.warmup):
         np.copyto(dst, buf)
@@ -506,47 +518,145 @@ def run_harness(args, dist, rank, world, local_rank):
     barrier(dist)
     elapsed = max_over_ranks(dist, time.perf_counter() - t0)
     total = sum_over_ranks(dist, float(buf.nbytes * args.steps))
+    rows_all = sum_over_ranks(dist, float(rows or 0))
     if rank == 0:
         print(json.dumps({"metric": METRIC, "value": round(total / elapsed / GIB, 3), "unit": "GiB/s",
                           "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
                           "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
-                          "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "harness self-test",
+                          "scaling": "strong" if args.table_rows else "weak", "vs_baseline": None, "dtype": "u8",
+                          "data": "harness self-test",
                           "config": {"workload": "host memcpy (harness test only)",
+                                     "table_rows": args.table_rows or None,
+                                     "rows_per_rank": [shard_rows(r, world, args.table_rows)[1] for r in range(world)]
+                                     if args.table_rows else None,
+                                     "rows_summed_over_ranks": int(rows_all) if args.table_rows else None,
                                      "parallelism": f"{world} rank(s)"}}), flush=True)
 
 
+def host_arrow_bytes(outs, nproj):
+    """Arrow bytes of one batch's host arrays (SURVEY.md §8(d) bytes_out)."""
+    tot = 0
+    for p in range(nproj):
+        h = outs[p]
+        tot += h.values_len + (4 * (h.length + 1) if h.offsets else 0) + ((h.length + 7) // 8 if h.validity else 0)
+    return tot
+
+
 def run_host(args):
-    """PCIe-inclusive rate: pinned staging -> H2D -> decode -> D2H."""
-    from murr_amd.row import ReadBatchBuilder
+    """PCIe-inclusive rate (north_star: host memory in, host memory out), two ways:
+      stream   murr_hstream (ReadBatchBuilder batches back to back, pipelined
+               over --depth slots: H2D of batch i+1 || decode of i || D2H of
+               i-1), --blocks K batches after --warmup, from a ring of
+               --host-ring distinct blocks held in pinned memory (a block
+               cache allocated with murr_host_alloc) and, as a second line,
+               from pageable memory (one host memcpy into pinned staging per
+               batch);
+      builder  the serial one-batch path (murr_builder_*: H2D, decode, D2H on
+               one stream), the round-3 number.
+    Every block's arrays are checked against the oracle for the first and the
+    last batch of each run."""
+    from murr_amd.row import HostBuffer, HostStream, ReadBatchBuilder, host_array_buffers
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
     ctx = Context(0)
     rows = args.rows
-    cols = make_columns(args.config, rows, 0)
-    seg = SegmentSchema([(f"c{i}", c["dtype"]) for i, c in enumerate(cols)])
-    dblob, doff, blen = encode_batch(ctx, seg, synth.upload_columns(ctx, cols), rows)
-    blob = dblob.download(blen).tobytes()
-    off = doff.download((rows + 1) * 8).view(np.uint64)
-    res = []
-    b = ReadBatchBuilder(seg, seg.columns, rows, ctx)
-    for it in range(args.warmup + args.steps):
+    ring = max(1, min(args.host_ring, args.blocks))
+    blocks = []
+    for r in range(ring):
+        cols = make_columns(args.config, rows, r * rows)
+        seg = SegmentSchema([(f"c{i}", c["dtype"]) for i, c in enumerate(cols)])
+        dblob, doff, blen = encode_batch(ctx, seg, synth.upload_columns(ctx, cols), rows)
+        blocks.append((dblob.download(blen), doff.download((rows + 1) * 8).view(np.uint64).copy()))
+        del dblob, doff
+    proj = list(range(len(seg.columns)))
+    oseg = O.Segment([int(c.dtype) for c in seg.columns])
+    want = {r: O.decode_block(oseg, proj, blocks[r][0], blocks[r][1]) for r in {0, (args.blocks - 1) % ring}}
+    # the pinned block cache: every ring block copied once into murr_host_alloc memory
+    pinned = []
+    for blob, off in blocks:
+        hb, ho = HostBuffer(blob.size + 16, ctx), HostBuffer(off.nbytes, ctx)
+        hb.array[: blob.size] = blob
+        ho.array[:] = off.view(np.uint8)
+        pinned.append((hb, ho, ho.array.view(np.uint64)))
+
+    def check(outs, r):
+        for p in range(len(proj)):
+            g, e = host_array_buffers(outs[p]), want[r][p]
+            ok = g["null_count"] == e["null_count"] and (e["validity"] is None or g["validity"] == e["validity"])
+            if e["dtype"] == 0:
+                ok = ok and np.array_equal(g["offsets"], e["offsets"]) and g["values"] == e["values"]
+            else:
+                ok = ok and g["values"][: len(e["values"])] == e["values"]
+            if not ok:
+                raise SystemExit(f"bench host: batch of ring block {r} col {p} differs from the oracle")
+
+    def stream_run(use_pinned):
+        hs = HostStream(seg, proj, depth=args.depth, ctx=ctx)
+        total = args.warmup + args.blocks
+        out_bytes, t0, done = 0, None, 0
+
+        def submit(i):
+            r = i % ring
+            if use_pinned:
+                hb, _, off = pinned[r]
+                hs.submit(hb.array, off, pinned=True)
+            else:
+                hs.submit(blocks[r][0], blocks[r][1])
+
+        nxt = 0
+        while nxt < min(args.depth, total):
+            submit(nxt)
+            nxt += 1
+        while done < total:
+            if done == args.warmup:
+                st0 = hs.stats()
+                t0 = time.perf_counter()
+            outs = hs.next()
+            i = done
+            done += 1
+            if i >= args.warmup:
+                out_bytes += host_arrow_bytes(outs, len(proj))
+                if i == args.warmup or i == total - 1:
+                    check(outs, i % ring)
+            if nxt < total:
+                submit(nxt)
+                nxt += 1
+        el = time.perf_counter() - t0
+        st1 = hs.stats()
+        hs.close()
+        d = {k: st1[k] - st0[k] for k in st1}
+        nb = d["batches"]
+        return {"GiB_s_host_to_host": round(out_bytes / el / GIB, 3),
+                "ms_per_batch": round(el / args.blocks * 1e3, 4),
+                "arrow_bytes_out_per_batch": out_bytes // args.blocks,
+                "h2d_GB_s": round(d["h2d_bytes"] / (d["h2d_ms"] * 1e-3) / 1e9, 2) if d["h2d_ms"] else None,
+                "d2h_GB_s": round(d["d2h_bytes"] / (d["d2h_ms"] * 1e-3) / 1e9, 2) if d["d2h_ms"] else None,
+                "h2d_ms_per_batch": round(d["h2d_ms"] / nb, 4), "kernel_ms_per_batch": round(d["kernel_ms"] / nb, 4),
+                "d2h_ms_per_batch": round(d["d2h_ms"] / nb, 4),
+                "h2d_bytes_per_batch": d["h2d_bytes"] // nb, "d2h_bytes_per_batch": d["d2h_bytes"] // nb}
+
+    res = {"pinned_source": stream_run(True), "pageable_source": stream_run(False)}
+    # the serial builder path (round 3's number): one batch at a time, rows added one by one
+    blob, off = blocks[0]
+    tm = []
+    for it in range(max(2, min(args.warmup, 3)) + min(args.steps, 20)):
         b = ReadBatchBuilder(seg, seg.columns, rows, ctx)
-        L = ctx.L
-        # bulk append: all rows in one call (the store's pinned slices)
         ptrs = (C.c_void_p * rows)()
         lens = (C.c_uint64 * rows)()
-        base = C.cast(C.c_char_p(blob), C.c_void_p).value
-        for i in range(rows):
-            ptrs[i] = base + int(off[i])
-            lens[i] = int(off[i + 1] - off[i])
-        L.murr_builder_add_rows(b.h, ptrs, lens, rows)
-        rb = b.build()
-        if it >= args.warmup:
-            res.append(b.last_timing())
-    out_bytes = sum(sum(buf.size for buf in col.buffers() if buf is not None) for col in rb.columns)
-    tm = {k: float(np.median([r[k] for r in res])) for k in res[0]}
-    print(json.dumps({"mode": "host", "config": args.config, "rows": rows, "arrow_bytes_out": out_bytes,
-                      "blob_bytes_in": len(blob), "median_ms": tm,
-                      "GiB_s_pcie_inclusive": round(out_bytes / (tm["total_ms"] * 1e-3) / GIB, 3),
-                      "GiB_s_kernel_only": round(out_bytes / (tm["kernel_ms"] * 1e-3) / GIB, 3)}))
+        base = blob.ctypes.data
+        ptrs[:] = (base + off[:-1].astype(np.int64)).tolist()
+        lens[:] = np.diff(off).tolist()
+        ctx.L.murr_builder_add_rows(b.h, ptrs, lens, rows)
+        outs = b._build_host()
+        if it >= 2:
+            tm.append(b.last_timing())
+    obytes = host_arrow_bytes(outs, len(proj))
+    med = {k: float(np.median([t[k] for t in tm])) for k in tm[0]}
+    res["builder_serial"] = {"median_ms": med, "GiB_s_pcie_inclusive": round(obytes / (med["total_ms"] * 1e-3) / GIB, 3)}
+    print(json.dumps({"mode": "host", "config": args.config, "rows_per_batch": rows, "batches": args.blocks,
+                      "warmup": args.warmup, "depth": args.depth, "ring_blocks": ring,
+                      "blob_bytes_per_batch": int(blocks[0][0].size), "verified": "first and last timed batch of "
+                      "each streaming run bit-exact vs the oracle", **res}))
 
 
 def run_encode(args):
@@ -866,6 +976,11 @@ def main():
     ap.add_argument("--sst-compression", default="snappy", choices=["none", "snappy", "lz4"],
                     help="sst mode: stored block compression")
     ap.add_argument("--keys", type=int, default=1000, help="resident mode: keys per read")
+    ap.add_argument("--table-rows", type=int, default=0,
+                    help="config D: one table of this many rows split by key range over the ranks "
+                         "(configs[3] as written, strong scaling); default: --rows per rank (weak)")
+    ap.add_argument("--depth", type=int, default=3, help="host mode: pipeline slots (murr_hstream)")
+    ap.add_argument("--host-ring", type=int, default=16, help="host mode: distinct source blocks in the pinned ring")
     ap.add_argument("--ipc", action="store_true", help="resident mode: also time the Arrow IPC message path")
     ap.add_argument("--uidx-stride", type=int, default=512,
                     help="decode mode: utf8 index stride of each block (0 = no index)")
@@ -897,6 +1012,8 @@ def main():
             args.rows = 1_000_000
     if args.blocks is None:
         args.blocks = {"A": 1, "B": 1000, "C": 1, "D": 1, "E": 1}[args.config]
+        if args.mode == "host":
+            args.blocks = 200
     if args.mode == "host":
         return run_host(args)
     if args.mode == "encode":

@@ -149,6 +149,10 @@ typedef struct {
     uint32_t stage;         /* LDS stage bytes per ring slot (0 = auto) */
     uint32_t encode_kernel; /* encode: 0 auto, 1 specialised only, 2 generic kernel */
     uint32_t verbose;       /* 1: one line per decode launch on stderr */
+    uint32_t grid;          /* local mode: workgroups per launch (0 = auto: the co-resident
+                               grid, each workgroup walking several (virtual) blocks);
+                               0xFFFFFFFF = one workgroup per (virtual) block, handed to the
+                               CUs by the hardware as workgroups finish */
 } murr_opts_t;
 int murr_ctx_set_opts(murr_ctx_t* ctx, const murr_opts_t* opts);
 int murr_ctx_get_opts(murr_ctx_t* ctx, murr_opts_t* opts);
@@ -271,7 +275,9 @@ int murr_decode_run(murr_plan_t* plan, murr_error_t* err);   /* synchronous */
  * run of a plan in flight at a time; runs of different plans on one context
  * queue in stream order, so a caller alternating two plans (two output sets)
  * launches the next run while the host finishes the previous one.  The
- * context's last kernel time (murr_ctx_last_kernel_ms) is the waited run's. */
+ * context's last kernel time (murr_ctx_last_kernel_ms) is the waited run's.
+ * When _wait returns, the run's kernel has ended: its outputs are visible to
+ * the host, to other streams and to peer GPUs, not only in stream order. */
 int murr_decode_run_async(murr_plan_t* plan);
 int murr_decode_run_wait(murr_plan_t* plan, murr_error_t* err);
 void murr_plan_free(murr_plan_t* plan);
@@ -392,6 +398,47 @@ int murr_builder_build(murr_builder_t* b, murr_host_array_t* outs /* nproj */,
 int murr_builder_last_timing(murr_builder_t* b, double* total_ms, float* h2d_ms,
                              float* kernel_ms, float* d2h_ms);
 void murr_builder_free(murr_builder_t* b);
+
+/* ---- streaming host decode ---------------------------------------------------
+ * Batch reads back to back, host memory in and host memory out: the row blobs
+ * a store hands over (the RocksDB block cache, src/io/store/rocksdb/mod.rs:
+ * 259-266) go to the device, are decoded, and the Arrow buffers come back for
+ * the egress (Flight DoGet, src/api/flight/mod.rs:85-87) -- pipelined, so the
+ * H2D of batch i+1, the decode of batch i and the D2H of batch i-1 run at once.
+ * `depth` (2..8) slots, each with its own stream, pinned staging, device
+ * buffers and pinned outputs, all reused from batch to batch (nothing is
+ * allocated per batch once the slots have grown to the batch size).
+ *
+ * murr_hstream_submit enqueues one batch (a host block: rows back to back at
+ * data, row i = data[row_off[i] .. row_off[i+1]), an empty row a missing key)
+ * and returns at once; murr_hstream_next waits for the oldest submitted batch
+ * and points `outs` (nproj arrays) at its decoded buffers, valid until its slot
+ * is submitted again (`depth` submits later).  At most `depth` batches may be
+ * submitted and not yet returned (else MURR_E_ARGUMENT).  With
+ * MURR_HSTREAM_PINNED the caller's data / row_off are pinned (murr_host_alloc or
+ * hipHostRegister) and are copied to the device straight from there; they must
+ * then stay unchanged until next() returns the batch.  Without it they are
+ * copied into the slot's pinned staging first (one host memcpy) and may be
+ * reused as soon as submit returns.  Errors of a batch (malformed rows, invalid
+ * UTF-8, ...) are reported by the next() that returns it, as
+ * ReadBatchBuilder::build (src/io/row/read.rs:100-109) would. */
+typedef struct murr_hstream murr_hstream_t;
+#define MURR_HSTREAM_PINNED 1u
+int murr_hstream_new(murr_ctx_t* ctx, const murr_segment_t* seg, const uint32_t* proj,
+                     uint32_t nproj, uint32_t depth, murr_hstream_t** out);
+int murr_hstream_submit(murr_hstream_t* s, const uint8_t* data, const uint64_t* row_off,
+                        uint64_t n_rows, uint32_t flags, murr_error_t* err);
+int murr_hstream_next(murr_hstream_t* s, murr_host_array_t* outs /* nproj */, murr_error_t* err);
+/* Totals since creation: batches returned, device milliseconds of the H2D
+ * copies, the decode kernels and the D2H copies (HIP events on the slots'
+ * streams), and the bytes each copy direction moved. */
+typedef struct {
+    uint64_t batches;
+    double h2d_ms, kernel_ms, d2h_ms;
+    uint64_t h2d_bytes, d2h_bytes;
+} murr_hstream_stats_t;
+int murr_hstream_stats(murr_hstream_t* s, murr_hstream_stats_t* out);
+void murr_hstream_free(murr_hstream_t* s);
 
 /* Host-memory encode: H2D of the Arrow buffers, murr_encode_batch, D2H of the
  * blobs.  Host input columns use the same murr_col_in_t (host pointers) plus

@@ -10,7 +10,8 @@ import re
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
-# MURR_LIB: load another build of the same library (the ablation build, tools/)
+# MURR_LIB: load another build of the same library (the tuning build of
+# tools/); announced on stderr whenever it is set, so no run swaps it in silently
 LIB_PATH = os.environ.get("MURR_LIB") or os.path.join(HERE, "libmurr_codec.so")
 HEADER = os.path.join(ROOT, "include", "murr_codec.h")
 
@@ -37,7 +38,7 @@ class Error(C.Structure):
 class Opts(C.Structure):
     """murr_opts_t: kernel selection of one context (tests, benchmarks)."""
     _fields_ = [(n, C.c_uint32) for n in ("kernel", "mode", "shape_nw", "shape_r", "seg_tiles", "vrows",
-                                          "lds_budget", "stage", "encode_kernel", "verbose")]
+                                          "lds_budget", "stage", "encode_kernel", "verbose", "grid")]
 
 
 class CtxStats(C.Structure):
@@ -80,6 +81,11 @@ class HostArray(C.Structure):
     _fields_ = [("values", C.c_void_p), ("validity", C.c_void_p), ("offsets", C.c_void_p),
                 ("length", C.c_uint64), ("null_count", C.c_uint64), ("values_len", C.c_uint64),
                 ("dtype", C.c_uint32), ("_pad", C.c_uint32)]
+
+
+class HStreamStats(C.Structure):
+    _fields_ = [("batches", C.c_uint64), ("h2d_ms", C.c_double), ("kernel_ms", C.c_double), ("d2h_ms", C.c_double),
+                ("h2d_bytes", C.c_uint64), ("d2h_bytes", C.c_uint64)]
 
 
 class HostColIn(C.Structure):
@@ -152,6 +158,11 @@ SIGNATURES = {
     "murr_builder_last_timing": (I32, [P, C.POINTER(C.c_double), C.POINTER(C.c_float),
                                        C.POINTER(C.c_float), C.POINTER(C.c_float)]),
     "murr_builder_free": (None, [P]),
+    "murr_hstream_new": (I32, [P, C.POINTER(Segment), C.POINTER(U32), U32, U32, PP]),
+    "murr_hstream_submit": (I32, [P, P, P, U64, U32, C.POINTER(Error)]),
+    "murr_hstream_next": (I32, [P, C.POINTER(HostArray), C.POINTER(Error)]),
+    "murr_hstream_stats": (I32, [P, C.POINTER(HStreamStats)]),
+    "murr_hstream_free": (None, [P]),
     "murr_reader_new": (I32, [P, C.POINTER(Segment), PP]),
     "murr_reader_read": (I32, [P, P, P, P, U64, U64, P, P, U64, U64, C.POINTER(U32), U32,
                                C.POINTER(HostArray), C.POINTER(Error)]),
@@ -197,6 +208,10 @@ def lib():
         if not os.path.exists(LIB_PATH):
             raise ImportError(f"libmurr_codec.so not built at {LIB_PATH}; run "
                               "`python -c 'import __graft_entry__ as g; g.build()'`")
+        if os.environ.get("MURR_LIB"):
+            import sys
+            print(f"murr_amd: MURR_LIB set, loading {LIB_PATH} instead of the in-tree release library",
+                  file=sys.stderr)
         L = C.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
             fn = getattr(L, name)

@@ -104,6 +104,7 @@ struct murr_ctx {
     uint64_t* aux = nullptr;  // device scratch of the gather scan (group sums)
     uint64_t aux_cap = 0;     // entries
     hipEvent_t xev = nullptr; // multi-GPU reads: this stream's work, awaited by the home stream
+    hipEvent_t hev = nullptr; // multi-GPU reads (as home): the work queued before a read, awaited by the shards
 };
 
 // Device key index (murr_index.hip): the keys' own copy and the slot table.
@@ -484,6 +485,11 @@ int murr_multi_gather(murr_ctx_t* home, const murr_shard_read_t* shards, uint32_
     if (!out_row_off || (nq && (!q_data || !q_offsets || !src || !rows)) || (!out_data && !needed) ||
         nq >= kMissing || ((uintptr_t)out_data & 15))
         return set_err(err, MURR_E_ARGUMENT);
+    // 0. the lookups read q_data / q_offsets / src and write `rows`, all in
+    //    home memory: a shard stream other than home's first waits for what
+    //    the caller queued on the home stream before this call (the call is
+    //    ordered on the home stream, as the header promises)
+    bool home_marked = false;
     // 1. every shard looks up its queries on its own stream (all concurrently);
     //    the home stream waits for each shard's lookup, never the host
     uint64_t q0 = 0;
@@ -493,7 +499,14 @@ int murr_multi_gather(murr_ctx_t* home, const murr_shard_read_t* shards, uint32_
         murr_ctx* sc = sh.ctx;
         if (n && sh.index && sh.index->n) {
             if ((st = enable_peer(sc->device, home->device, err))) return st;
+            if (sc != home && !home_marked) {
+                HIPC(hipSetDevice(home->device));
+                if (!home->hev) HIPC(hipEventCreateWithFlags(&home->hev, hipEventDisableTiming));
+                HIPC(hipEventRecord(home->hev, home->stream));
+                home_marked = true;
+            }
             HIPC(hipSetDevice(sc->device));
+            if (sc != home) HIPC(hipStreamWaitEvent(sc->stream, home->hev, 0));
             IndexArgs a = index_args(sh.index, q_data, q_offsets + q0, n);
             a.rows = rows + q0;
             HIPC(launch_index_probe(a, sc->stream));
@@ -653,6 +666,7 @@ void murr_ctx_destroy(murr_ctx_t* c) {
     for (const auto& b : c->pool) (void)(b.pinned ? hipHostFree(b.p) : hipFree(b.p));
     for (hipEvent_t e : c->event_pool) (void)hipEventDestroy(e);
     if (c->xev) (void)hipEventDestroy(c->xev);
+    if (c->hev) (void)hipEventDestroy(c->hev);
     if (c->k0) (void)hipEventDestroy(c->k0);
     if (c->k1) (void)hipEventDestroy(c->k1);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -985,7 +999,13 @@ int decode_enqueue_jit(murr_ctx* c, const murr_segment_t* seg, const JitLayout* 
         }
     }
     const uint64_t nseg = jsegs.size();
-    const uint64_t grid = std::max<uint64_t>(1, local ? std::min<uint64_t>(G, lsegs.size()) : std::min<uint64_t>(G_split, nseg));
+    // Local mode: the co-resident grid walks the (virtual) blocks g, g + G, ...;
+    // opts.grid ~0 launches one workgroup per (virtual) block instead, so the
+    // hardware hands the next one to whichever CU frees a slot first.
+    uint64_t grid_local = std::min<uint64_t>(G, lsegs.size());
+    if (O.grid == 0xFFFFFFFFu) grid_local = lsegs.size();
+    else if (O.grid) grid_local = std::min<uint64_t>(O.grid, lsegs.size());
+    const uint64_t grid = std::max<uint64_t>(1, local ? grid_local : std::min<uint64_t>(G_split, nseg));
     bool emit = false;
     for (uint32_t p = 0; p < nproj; p++) emit |= dp[p].is_utf8;
 
@@ -1689,6 +1709,13 @@ int murr_decode_run_wait(murr_plan_t* P, murr_error_t* err) {
         }
     }
     std::atomic_thread_fence(std::memory_order_acquire);
+    // The flag says every workgroup has stored its outputs, but those stores
+    // are ordered only within c->stream until the kernel ends (the epilogue's
+    // atomics are relaxed): wait for the kernel's end, so the outputs are
+    // visible to the host, other streams and peer GPUs when this returns.
+    // The kernel is in its last workgroup's epilogue by now; a next run queued
+    // behind it keeps the GPU busy meanwhile.
+    if (flagged) HIPC(hipEventSynchronize(R.e1));
     if (!flagged) {
         if (!R.kargs[set].empty()) c->stats.readback_fallbacks++;
         HIPC(hipMemcpyAsync(R.hrb, set ? R.zb2 : R.dws, R.z_lb, hipMemcpyDeviceToHost, c->stream));
@@ -2192,6 +2219,223 @@ void murr_builder_free(murr_builder_t* b) {
         else (void)hipEventDestroy(e);
     }
     delete b;
+}
+
+}  // extern "C"
+
+// ---- streaming host decode (murr_hstream_*) ----------------------------------
+// Batch reads back to back, host in, host out.  Each slot owns a context (its
+// own stream and decode workspace) and grow-only buffers; a batch is one
+// in-order chain on its slot's stream -- H2D of the blobs and row offsets,
+// the decode, one D2H of the slot's whole (bounded) output region -- so the
+// chains of consecutive batches overlap on the copy engines and the CUs, and
+// the only host wait is next()'s, on the oldest batch.
+
+struct HSlot {
+    murr_ctx* c = nullptr;
+    uint8_t* hin = nullptr;  // pinned staging: blobs | row offsets (unpinned sources)
+    uint64_t hin_cap = 0;
+    uint8_t* din = nullptr;  // device input: blobs | row offsets
+    uint64_t din_cap = 0;
+    HostOut out;
+    uint64_t n = 0, h2d_bytes = 0, d2h_bytes = 0;
+    hipEvent_t e0 = nullptr, e1 = nullptr, e2 = nullptr, e3 = nullptr;
+    int submit_status = MURR_OK;  // an enqueue that failed: next() reports it
+    murr_error_t submit_err{};
+};
+
+struct murr_hstream {
+    murr_ctx* owner = nullptr;
+    std::vector<murr_column_t> cols;
+    murr_segment_t seg{};
+    std::vector<uint32_t> proj;
+    std::vector<HSlot> slots;
+    uint64_t head = 0, tail = 0;  // batches submitted / returned
+    murr_hstream_stats_t stats{};
+};
+
+namespace {
+
+// Enqueue batch `s` on its slot's stream (everything after the staging copy is
+// asynchronous).  The output region is laid out as decode_to_host's, its utf8
+// parts bounded by the blob bytes past the rows' fixed parts.
+int hstream_enqueue(murr_hstream* h, HSlot& s, const uint8_t* data, const uint64_t* row_off, uint64_t n,
+                    bool pinned, murr_error_t* err) {
+    murr_ctx* c = s.c;
+    HIPC(hipSetDevice(c->device));
+    const uint64_t b0 = n ? row_off[0] : 0, b1 = n ? row_off[n] : 0;
+    if (b1 < b0) return set_err(err, MURR_E_ARGUMENT);
+    const uint64_t bytes = b1 - b0, head = b0 & 15;
+    const uint64_t dbytes = round_up(head + bytes + 16, 64), obytes = (n + 1) * 8;
+    if (!grow_dev(c, &s.din, &s.din_cap, dbytes + obytes)) return set_err(err, MURR_E_HIP);
+    const uint8_t* src_data = data + (b0 - head);
+    const uint64_t* src_off = row_off;
+    if (!pinned) {
+        // one host copy into the slot's pinned staging (the caller may reuse
+        // its buffers as soon as submit returns)
+        if (!grow_pinned(c, &s.hin, &s.hin_cap, dbytes + obytes, 0)) return set_err(err, MURR_E_HIP);
+        if (head + bytes) std::memcpy(s.hin, src_data, head + bytes);
+        std::memcpy(s.hin + dbytes, row_off, obytes);
+        src_data = s.hin;
+        src_off = (const uint64_t*)(s.hin + dbytes);
+    }
+    uint64_t* doff = (uint64_t*)(s.din + dbytes);
+    HIPC(hipEventRecord(s.e0, c->stream));
+    if (head + bytes) HIPC(hipMemcpyAsync(s.din, src_data, head + bytes, hipMemcpyHostToDevice, c->stream));
+    HIPC(hipMemcpyAsync(doff, src_off, obytes, hipMemcpyHostToDevice, c->stream));
+    HIPC(hipEventRecord(s.e1, c->stream));
+    s.h2d_bytes = head + bytes + obytes;
+    // row i of the block is data[row_off[i]..]: the block's data pointer sits
+    // row_off[0] & ~15 bytes before the staged bytes (16-B aligned)
+    murr_block_t blk{s.din - (b0 - head), doff, n, b1};
+    // the blob bytes bound any one utf8 column's string bytes
+    const uint64_t utf8_cap = std::max<uint64_t>(bytes, 8);
+    const uint32_t np = (uint32_t)h->proj.size();
+    const uint64_t bm = murr_bitmap_bytes(n);
+    HostOut& o = s.out;
+    o.off.assign((size_t)np * 3, 0);
+    uint64_t off = 0;
+    for (uint32_t p = 0; p < np; p++) {
+        const murr_column_t& col = h->seg.cols[h->proj[p]];
+        const uint64_t vb = col.dtype == MURR_UTF8 ? utf8_cap : col.dtype == MURR_BOOL ? bm : n * col.size;
+        o.off[3 * p] = off;
+        off = round_up(off + std::max<uint64_t>(vb, 8), 64);
+        o.off[3 * p + 1] = off;
+        off = round_up(off + std::max<uint64_t>(bm, 8), 64);
+        o.off[3 * p + 2] = off;
+        if (col.dtype == MURR_UTF8) off = round_up(off + (n + 1) * 4, 64);
+    }
+    const uint64_t total_out = std::max<uint64_t>(off, 64);
+    if (!grow_dev(c, &o.dout, &o.dout_cap, total_out) || !grow_pinned(c, &o.hout, &o.hout_cap, total_out, 0))
+        return set_err(err, MURR_E_HIP);
+    o.arr.assign(np, murr_array_t{});
+    for (uint32_t p = 0; p < np; p++) {
+        murr_array_t& a = o.arr[p];
+        a.values = o.dout + o.off[3 * p];
+        a.validity = o.dout + o.off[3 * p + 1];
+        a.offsets = h->seg.cols[h->proj[p]].dtype == MURR_UTF8 ? (int32_t*)(o.dout + o.off[3 * p + 2]) : nullptr;
+        a.values_cap = utf8_cap;
+    }
+    const int st = murr_decode_enqueue(c, &h->seg, h->proj.data(), np, &blk, 1, o.arr.data());
+    if (st) return set_err(err, st, st == MURR_E_HIP ? (int)hipGetLastError() : 0);
+    HIPC(hipEventRecord(s.e2, c->stream));
+    HIPC(hipMemcpyAsync(o.hout, o.dout, total_out, hipMemcpyDeviceToHost, c->stream));
+    HIPC(hipEventRecord(s.e3, c->stream));
+    s.d2h_bytes = total_out;
+    s.n = n;
+    return MURR_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int murr_hstream_new(murr_ctx_t* c, const murr_segment_t* seg, const uint32_t* proj, uint32_t nproj,
+                     uint32_t depth, murr_hstream_t** out) {
+    if (!c || !out || !valid_segment(seg) || (nproj && !proj) || depth < 2 || depth > 8) return MURR_E_ARGUMENT;
+    *out = nullptr;
+    if (nproj == 0) return MURR_E_ARROW;  // RecordBatch::try_new, read.rs:106-108
+    if (nproj > kMaxProj) return MURR_E_ARGUMENT;
+    for (uint32_t p = 0; p < nproj; p++)
+        if (proj[p] >= seg->ncols) return MURR_E_BAD_COLUMN;
+    murr_hstream* h = new (std::nothrow) murr_hstream();
+    if (!h) return MURR_E_INTERNAL;
+    h->owner = c;
+    h->cols.assign(seg->cols, seg->cols + seg->ncols);
+    h->seg = *seg;
+    h->seg.cols = h->cols.data();
+    h->proj.assign(proj, proj + nproj);
+    h->slots.resize(depth);
+    for (HSlot& s : h->slots) {
+        int st = murr_ctx_create(c->device, &s.c);
+        if (!st) st = murr_ctx_set_opts(s.c, &c->opts);
+        for (hipEvent_t* e : {&s.e0, &s.e1, &s.e2, &s.e3})
+            if (!st && hipEventCreate(e) != hipSuccess) st = MURR_E_HIP;
+        if (st) {
+            murr_hstream_free(h);
+            return st;
+        }
+    }
+    *out = h;
+    return MURR_OK;
+}
+
+int murr_hstream_submit(murr_hstream_t* h, const uint8_t* data, const uint64_t* row_off, uint64_t n_rows,
+                        uint32_t flags, murr_error_t* err) {
+    if (!h || !row_off || (n_rows && !data) || h->head - h->tail >= h->slots.size())
+        return set_err(err, MURR_E_ARGUMENT);
+    HSlot& s = h->slots[h->head % h->slots.size()];
+    s.submit_err = murr_error_t{};
+    s.submit_status = hstream_enqueue(h, s, data, row_off, n_rows, (flags & MURR_HSTREAM_PINNED) != 0, &s.submit_err);
+    if (s.submit_status && s.c->pending) {  // (an enqueue failure after the launch: drain it)
+        murr_error_t e2{};
+        (void)murr_decode_wait(s.c, &e2);
+    }
+    h->head++;
+    return MURR_OK;
+}
+
+int murr_hstream_next(murr_hstream_t* h, murr_host_array_t* outs, murr_error_t* err) {
+    if (!h || !outs || h->tail == h->head) return set_err(err, MURR_E_ARGUMENT);
+    HSlot& s = h->slots[h->tail % h->slots.size()];
+    h->tail++;
+    if (s.submit_status) {
+        if (err) *err = s.submit_err;
+        return s.submit_status;
+    }
+    murr_ctx* c = s.c;
+    // the decode's counters come back behind the D2H on the same stream:
+    // this one synchronisation covers the whole chain
+    int st = murr_decode_wait(c, err);
+    if (st) return st;
+    float ms = 0;
+    if (hipEventElapsedTime(&ms, s.e0, s.e1) == hipSuccess) h->stats.h2d_ms += ms;
+    if (murr_ctx_last_kernel_ms(c, &ms) == MURR_OK) h->stats.kernel_ms += ms;
+    if (hipEventElapsedTime(&ms, s.e2, s.e3) == hipSuccess) h->stats.d2h_ms += ms;
+    h->stats.h2d_bytes += s.h2d_bytes;
+    h->stats.d2h_bytes += s.d2h_bytes;
+    h->stats.batches++;
+    const HostOut& o = s.out;
+    for (uint32_t p = 0; p < h->proj.size(); p++) {
+        const murr_array_t& a = o.arr[p];
+        murr_host_array_t& ha = outs[p];
+        ha.values = o.hout + o.off[3 * p];
+        ha.validity = a.null_count ? o.hout + o.off[3 * p + 1] : nullptr;
+        ha.offsets = a.offsets ? (const int32_t*)(o.hout + o.off[3 * p + 2]) : nullptr;
+        ha.length = s.n;
+        ha.null_count = a.null_count;
+        ha.values_len = a.data_len;
+        ha.dtype = h->seg.cols[h->proj[p]].dtype;
+        ha._pad = 0;
+    }
+    return MURR_OK;
+}
+
+int murr_hstream_stats(murr_hstream_t* h, murr_hstream_stats_t* out) {
+    if (!h || !out) return MURR_E_ARGUMENT;
+    *out = h->stats;
+    return MURR_OK;
+}
+
+void murr_hstream_free(murr_hstream_t* h) {
+    if (!h) return;
+    for (HSlot& s : h->slots) {
+        if (!s.c) continue;
+        (void)hipSetDevice(s.c->device);
+        if (s.c->pending) {
+            murr_error_t e{};
+            (void)murr_decode_wait(s.c, &e);
+        }
+        (void)hipStreamSynchronize(s.c->stream);
+        pool_give(s.c, true, s.hin, s.hin_cap);
+        pool_give(s.c, false, s.din, s.din_cap);
+        pool_give(s.c, true, s.out.hout, s.out.hout_cap);
+        pool_give(s.c, false, s.out.dout, s.out.dout_cap);
+        for (hipEvent_t e : {s.e0, s.e1, s.e2, s.e3})
+            if (e) (void)hipEventDestroy(e);
+        murr_ctx_destroy(s.c);  // (frees the pooled buffers too)
+    }
+    delete h;
 }
 
 }  // extern "C"

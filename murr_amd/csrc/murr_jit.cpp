@@ -89,8 +89,14 @@ bool compile_code(const std::string& src, const char* name, std::vector<char>* c
     const std::string dir = cache_dir();
     std::string file;
     if (!dir.empty()) {
+        // key: the source, the options and the compiler (hiprtc's version: a
+        // code object from another ROCm release is never reused)
+        int vmaj = 0, vmin = 0;
+        if (hiprtcVersion(&vmaj, &vmin) != HIPRTC_SUCCESS) vmaj = vmin = -1;
+        const std::string salt = std::string(opts[0]) + opts[1] + opts[2] + " hiprtc " + std::to_string(vmaj) + "." +
+                                 std::to_string(vmin) + " " + std::to_string(HIP_VERSION);
         char hex[32];
-        std::snprintf(hex, sizeof hex, "%016llx", (unsigned long long)fnv64(src, fnv64(std::string(opts[0]) + opts[1] + opts[2])));
+        std::snprintf(hex, sizeof hex, "%016llx", (unsigned long long)fnv64(src, fnv64(salt)));
         file = std::string(name) + "-" + hex + ".co";
         if (read_file(dir + "/" + file, code)) return true;
     }

@@ -74,14 +74,16 @@ class Context:
             self.set_opts(**_default_opts)
 
     def set_opts(self, kernel="auto", mode="auto", shape=None, seg_tiles=0, vrows=0, lds_budget=0, stage=0,
-                 encode_kernel="auto", verbose=0):
+                 encode_kernel="auto", verbose=0, grid=0):
         """murr_ctx_set_opts: kernel selection for this context (all defaults =
         the library's own choice).  kernel / encode_kernel: auto|jit|generic;
-        mode: auto|local|split|cut; shape: (waves, chunks) e.g. (5, 3)."""
+        mode: auto|local|split|cut; shape: (waves, chunks) e.g. (5, 3);
+        grid: local-mode workgroups (0 auto, -1 one per virtual block)."""
         o = _abi.Opts()
         o.kernel, o.mode, o.encode_kernel = KERNELS[kernel], MODES[mode], KERNELS[encode_kernel]
         o.shape_nw, o.shape_r = shape if shape else (0, 0)
         o.seg_tiles, o.vrows, o.lds_budget, o.stage, o.verbose = seg_tiles, vrows, lds_budget, stage, int(verbose)
+        o.grid = grid & 0xFFFFFFFF
         raise_status(self.L.murr_ctx_set_opts(self.h, C.byref(o)), what="murr_ctx_set_opts")
         self.opts_gen = getattr(self, "opts_gen", 0) + 1  # plan caches key on it (no library call per read)
 
@@ -315,15 +317,37 @@ class DecodePlan:
 
     def run_async(self):
         """Launch a run and return (murr_decode_run_async); wait() finishes it."""
+        if not self.h:
+            raise ValueError("DecodePlan is closed")
         raise_status(self.ctx.L.murr_decode_run_async(self.h), what="murr_decode_run_async")
+        self._inflight, self._drained = True, None
 
     def wait(self) -> "DecodeOutputs":
+        if not self.h:
+            # closed with a run in flight (a plan cache evicted it): close()
+            # finished that run; hand over its result once
+            d, self._drained = getattr(self, "_drained", None), None
+            if d is None:
+                raise ValueError("DecodePlan is closed and has no run to wait for")
+            if isinstance(d, BaseException):
+                raise d
+            return d
+        self._inflight = False
         st = self.ctx.L.murr_decode_run_wait(self.h, C.byref(self._err))
         raise_status(st, self._err, "murr_decode_run_wait")
         return self.outs
 
+    @property
+    def inflight(self) -> bool:
+        return bool(getattr(self, "_inflight", False))
+
     def close(self):
         if getattr(self, "h", None) and self.ctx.h:
+            if self.inflight:  # never free a plan under its own running launch
+                try:
+                    self._drained = self.wait()
+                except Exception as e:  # kept for the caller's wait()
+                    self._drained = e
             self.ctx.L.murr_plan_free(self.h)
         self.h = None
 

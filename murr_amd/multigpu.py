@@ -122,8 +122,11 @@ class MultiDeviceTable:
                                                   out_off.ptr, data.ptr, C.byref(err)), err, "murr_multi_gather_copy")
             bound = max(nb, 16)
         # 3. one decode on home (its wait is the read's host synchronisation)
-        blk = DeviceBlock(data, out_off, nq, min(bound, max(16, int(sum(sh.used for sh in self.shards)
-                                                                     / max(1, sum(sh.n for sh in self.shards)) * nq))))
+        # data_bytes sizes every utf8 values buffer of the decode: a safe upper
+        # bound of the gathered bytes (nq x the longest row, at most
+        # TWO_PHASE_BYTES here; the exact size on the two-phase path), never a
+        # mean-row estimate a read of long rows could outgrow
+        blk = DeviceBlock(data, out_off, nq, bound)
         proj = [c.index for c in req]
         outs = DecodeOutputs(home, self.segment, proj, [blk])
         decode_blocks(home, self.segment, proj, [blk], outs)

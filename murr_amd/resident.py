@@ -363,11 +363,14 @@ class ResidentTable:
             # the next scan).
             if plan is not None:
                 plan[1].close()
-            if len(self._scan_plans) >= 4:  # a few output sets at most
-                for k in list(self._scan_plans):
-                    if k != slot:
-                        self._scan_plans.pop(k)[1].close()
-                        break
+            if len(self._scan_plans) >= 4:  # a few output sets at most: evict
+                # one, preferring a plan with no run in flight (closing an
+                # in-flight plan finishes its run first; its wait() still
+                # returns that run's outputs)
+                cand = [k for k in self._scan_plans if k != slot]
+                idle = [k for k in cand if not self._scan_plans[k][1].inflight]
+                if cand:
+                    self._scan_plans.pop((idle or cand)[0])[1].close()
             blk = self.block()
             p = DecodePlan(self.ctx, self.segment, proj, [blk],
                            outs or DecodeOutputs(self.ctx, self.segment, proj, [blk]))

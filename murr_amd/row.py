@@ -144,3 +144,107 @@ def host_array_buffers(h) -> dict:
     if h.dtype == int(DTypeName.Utf8):
         out["offsets"] = np.frombuffer(C.string_at(h.offsets, (n + 1) * 4), dtype=np.int32).copy()
     return out
+
+
+class HostStream:
+    """Batch reads back to back, host memory in and out (murr_hstream_*): the
+    H2D of batch i+1, the decode of batch i and the D2H of batch i-1 overlap
+    on `depth` slots, each with its own stream and reused buffers.
+
+    submit(data, row_off) enqueues one host block (numpy uint8 blob bytes,
+    uint64 row offsets; an empty row is a missing key) and returns at once;
+    next() waits for the oldest submitted block and returns its decoded arrays
+    as murr_host_array_t (valid until `depth` more submits) -- or, with
+    arrow=True, as a RecordBatch (copied out).  `pinned=True` tells the
+    library the buffers are pinned (HostBuffer / murr_host_alloc): they are
+    copied to the device straight from there and must stay unchanged until
+    next() returns that block."""
+
+    def __init__(self, segment: SegmentSchema, columns, depth: int = 3, ctx=None):
+        self.segment = segment
+        self.columns = list(columns)
+        self.ctx = ctx or default_context()
+        self.L = self.ctx.L
+        proj = [c.index if isinstance(c, SegmentColumnSchema) else int(c) for c in self.columns]
+        self._proj = (C.c_uint32 * max(len(proj), 1))(*proj)
+        self._nproj = len(proj)
+        h = C.c_void_p()
+        raise_status(self.L.murr_hstream_new(self.ctx.h, C.byref(segment.c), self._proj, self._nproj, int(depth),
+                                             C.byref(h)), what="murr_hstream_new")
+        self.h = h
+        self.depth = depth
+        self._keep = {}  # submit sequence -> caller buffers kept alive until returned
+        self._seq = self._done = 0
+        self._err = _abi.Error()
+
+    def submit(self, data, row_off, pinned: bool = False):
+        row_off = np.ascontiguousarray(row_off, dtype=np.uint64)
+        n = row_off.size - 1
+        if n < 0:
+            raise ValueError("row_off needs n_rows + 1 entries")
+        dptr = data.ctypes.data if hasattr(data, "ctypes") else int(data)
+        err = _abi.Error()
+        raise_status(self.L.murr_hstream_submit(self.h, dptr, row_off.ctypes.data, n, 1 if pinned else 0,
+                                                C.byref(err)), err, "murr_hstream_submit")
+        self._keep[self._seq] = (data, row_off) if pinned else None
+        self._seq += 1
+
+    def next(self, arrow: bool = False):
+        outs = (_abi.HostArray * self._nproj)()
+        st = self.L.murr_hstream_next(self.h, outs, C.byref(self._err))
+        self._keep.pop(self._done, None)
+        self._done += 1
+        raise_status(st, self._err, "murr_hstream_next")
+        if not arrow:
+            return outs
+        arrays, fields = [], []
+        for p, col in enumerate(self.columns):
+            seg_col = col if isinstance(col, SegmentColumnSchema) else self.segment.columns[int(col)]
+            arrays.append(host_array_to_arrow(outs[p]))
+            fields.append(pa.field(seg_col.name, seg_col.dtype.arrow_dtype(), True))
+        return pa.RecordBatch.from_arrays(arrays, schema=pa.schema(fields))
+
+    @property
+    def pending(self) -> int:
+        return self._seq - self._done
+
+    def stats(self) -> dict:
+        s = _abi.HStreamStats()
+        raise_status(self.L.murr_hstream_stats(self.h, C.byref(s)), what="murr_hstream_stats")
+        return {f: getattr(s, f) for f, _ in s._fields_}
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.murr_hstream_free(self.h)
+            self.h = None
+        self._keep.clear()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class HostBuffer:
+    """Pinned host memory of the library (murr_host_alloc) as a numpy uint8
+    array: the form of a block cache whose blocks the GPU copies directly."""
+
+    def __init__(self, nbytes: int, ctx=None):
+        self.ctx = ctx or default_context()
+        p = C.c_void_p()
+        raise_status(self.ctx.L.murr_host_alloc(self.ctx.h, max(int(nbytes), 1), C.byref(p)), what="murr_host_alloc")
+        self.ptr = p.value
+        self.nbytes = int(nbytes)
+        self.array = np.ctypeslib.as_array((C.c_uint8 * max(self.nbytes, 1)).from_address(self.ptr))[: self.nbytes]
+
+    def close(self):
+        if self.ptr and self.ctx.h:
+            self.ctx.L.murr_host_free(self.ctx.h, self.ptr)
+        self.ptr = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -252,3 +252,15 @@ def test_bench_refuses_ranks_without_gpus():
     # a decode run with more ranks than GPUs exits non-zero instead of sharing
     rc, line, err = _bench("--gpus", "2", "--steps", "1", "--warmup", "0", "--no-cpu")
     assert rc != 0 and line is None
+
+
+def test_bench_table_split_over_ranks():
+    # configs[3] as written: ONE table of --table-rows rows split by key range
+    # over the ranks (strong scaling), through the spawner in harness mode
+    rc, line, err = _bench("--mode", "harness", "--config", "D", "--table-rows", "10000001", "--gpus", "2",
+                           "--steps", "2", "--warmup", "1")
+    assert rc == 0, err[-2000:]
+    cfg = line["config"]
+    assert line["scaling"] == "strong" and line["n_gpus"] == 2
+    assert cfg["table_rows"] == 10000001 and cfg["rows_per_rank"] == [5000001, 5000000]
+    assert cfg["rows_summed_over_ranks"] == 10000001

@@ -40,3 +40,23 @@ def test_eight_shards_read(table8, monkeypatch, two_phase, nq):
         q[:3] = ["absent", "key29999", "key29999"]
     cols = ["c11", "c0", "c12", "c5"]
     assert_same(t.read(q, cols), expected(batches, q, cols))
+
+
+def test_longest_rows_of_skewed_table():
+    """A read of only the longest rows of a table whose row sizes are skewed
+    (a few 4 KiB strings among short rows): the decode's utf8 buffers must be
+    sized for the gathered bytes, not for the table's mean row."""
+    import pyarrow as pa
+    ndev = device_count()
+    t = MultiDeviceTable(schema_c(), [Context(i % ndev) for i in range(4)])
+    b = batch_c(3000, seed=11)
+    s = b.column("c12").to_pylist()
+    long_keys = []
+    for i in range(0, 3000, 97):
+        s[i] = chr(ord("a") + i % 26) * 4096
+        long_keys.append(f"key{i}")
+    b = pa.RecordBatch.from_arrays([*b.columns[:13], pa.array(s, pa.string()), *b.columns[14:]],
+                                   names=b.schema.names)
+    t.write(b)
+    for q in (long_keys[:1], long_keys, long_keys + ["absent", "key5"]):
+        assert_same(t.read(q, ["c12", "c11", "c3"]), expected([b], q, ["c12", "c11", "c3"]))

@@ -146,3 +146,24 @@ def test_scan_device_async_alternating_outputs(ctx):
     for outs in sets + [first]:
         for p in (0, 3, 11, 12, 15):
             assert_array_equal(download_array(ctx, outs.array(0, p), int(C_DTYPES[p]), n), want[p], f"col {p}")
+
+
+def test_scan_plan_eviction_with_runs_in_flight(ctx):
+    # five output sets scanned without waiting: the plan cache holds four, so
+    # one plan is evicted while its run is in flight.  Eviction finishes that
+    # run first; every handle's wait() still returns its own, correct outputs
+    # (a freed plan under a running launch)
+    n = 20_000
+    rt = ResidentTable(schema_c(), ctx)
+    rt.write(batch_c(n, seed=7))
+    names = [f"c{i}" for i in range(len(C_DTYPES))]
+    sets = [DecodeOutputs(ctx, rt.segment, list(range(len(C_DTYPES))), [rt.block()]) for _ in range(5)]
+    hs = [rt.scan_device_async(names, s) for s in sets]
+    data, off = arena(rt)
+    want = O.decode_block(O.Segment([int(d) for d in C_DTYPES]), list(range(len(C_DTYPES))), data, off)
+    for h, outs in zip(hs, sets):
+        assert h.wait() is outs
+        for p in (0, 11, 12):
+            assert_array_equal(download_array(ctx, outs.array(0, p), int(C_DTYPES[p]), n), want[p], f"col {p}")
+    with pytest.raises(ValueError):
+        hs[0].wait()  # its one result was handed over already

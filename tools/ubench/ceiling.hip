@@ -1,0 +1,194 @@
+// HBM ceiling probe (round 4): what this box's HBM streams at for pure reads,
+// pure writes, 1:1 copies and the decode's 2:1 read:write mix, over buffers
+// far larger than the 256 MiB Infinity Cache, at several grid shapes and
+// loads-in-flight depths.  Two loop structures:
+//   gs     grid-stride: lane i of the launch touches i, i + T, i + 2T, ...
+//   chunk  a workgroup streams its own contiguous chunk (U 16-B accesses per
+//          lane in flight, 4 KiB per wave-instruction group)
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 ceiling.hip -o ceiling
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+
+#define CK(x)                                                                              \
+    do {                                                                                   \
+        hipError_t e_ = (x);                                                               \
+        if (e_ != hipSuccess) {                                                            \
+            std::fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+            std::exit(1);                                                                  \
+        }                                                                                  \
+    } while (0)
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+template <int U, bool NT>
+__device__ __forceinline__ u32x4 ld(const u32x4* p) {
+    if constexpr (NT) return __builtin_nontemporal_load(p);
+    else return *p;
+}
+template <bool NT>
+__device__ __forceinline__ void st(u32x4* p, u32x4 v) {
+    if constexpr (NT) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+
+// read-only, grid-stride; the xor keeps the loads alive
+template <int U, bool NT>
+__global__ void rd_gs(const u32x4* __restrict__ in, size_t n, u32x4* sink) {
+    const size_t T = (size_t)gridDim.x * blockDim.x;
+    u32x4 acc = {0, 0, 0, 0};
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += T * U) {
+        u32x4 v[U];
+#pragma unroll
+        for (int k = 0; k < U; k++) v[k] = i + k * T < n ? ld<U, NT>(in + i + k * T) : u32x4{0, 0, 0, 0};
+#pragma unroll
+        for (int k = 0; k < U; k++) acc ^= v[k];
+    }
+    if (acc.x == 0x9E3779B9u && acc.y == 1u) sink[threadIdx.x] = acc;
+}
+template <int U, bool NT>
+__global__ void wr_gs(u32x4* __restrict__ out, size_t n) {
+    const size_t T = (size_t)gridDim.x * blockDim.x;
+    const u32x4 v = {threadIdx.x, blockIdx.x, 1u, 2u};
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += T * U) {
+#pragma unroll
+        for (int k = 0; k < U; k++)
+            if (i + k * T < n) st<NT>(out + i + k * T, v);
+    }
+}
+template <int U, bool NT>
+__global__ void cp_gs(const u32x4* __restrict__ in, u32x4* __restrict__ out, size_t n) {
+    const size_t T = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += T * U) {
+        u32x4 v[U];
+#pragma unroll
+        for (int k = 0; k < U; k++)
+            if (i + k * T < n) v[k] = ld<U, false>(in + i + k * T);
+#pragma unroll
+        for (int k = 0; k < U; k++)
+            if (i + k * T < n) st<NT>(out + i + k * T, v[k]);
+    }
+}
+// a workgroup per contiguous chunk of `per` elements
+template <int U, bool NT>
+__global__ void cp_chunk(const u32x4* __restrict__ in, u32x4* __restrict__ out, size_t n, size_t per) {
+    const size_t b0 = blockIdx.x * per, b1 = b0 + per < n ? b0 + per : n;
+    const size_t B = blockDim.x;
+    for (size_t i = b0 + threadIdx.x; i < b1; i += B * U) {
+        u32x4 v[U];
+#pragma unroll
+        for (int k = 0; k < U; k++)
+            if (i + k * B < b1) v[k] = ld<U, false>(in + i + k * B);
+#pragma unroll
+        for (int k = 0; k < U; k++)
+            if (i + k * B < b1) st<NT>(out + i + k * B, v[k]);
+    }
+}
+template <int U>
+__global__ void rd_chunk(const u32x4* __restrict__ in, size_t n, size_t per, u32x4* sink) {
+    const size_t b0 = blockIdx.x * per, b1 = b0 + per < n ? b0 + per : n;
+    const size_t B = blockDim.x;
+    u32x4 acc = {0, 0, 0, 0};
+    for (size_t i = b0 + threadIdx.x; i < b1; i += B * U) {
+        u32x4 v[U];
+#pragma unroll
+        for (int k = 0; k < U; k++) v[k] = i + k * B < b1 ? in[i + k * B] : u32x4{0, 0, 0, 0};
+#pragma unroll
+        for (int k = 0; k < U; k++) acc ^= v[k];
+    }
+    if (acc.x == 0x9E3779B9u && acc.y == 1u) sink[threadIdx.x] = acc;
+}
+// 2:1 mix: two read streams, one write stream of the same element count
+template <int U>
+__global__ void mix_gs(const u32x4* __restrict__ a, const u32x4* __restrict__ b, u32x4* __restrict__ out, size_t n) {
+    const size_t T = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += T * U) {
+        u32x4 v[U], w[U];
+#pragma unroll
+        for (int k = 0; k < U; k++)
+            if (i + k * T < n) { v[k] = a[i + k * T]; w[k] = b[i + k * T]; }
+#pragma unroll
+        for (int k = 0; k < U; k++)
+            if (i + k * T < n) out[i + k * T] = v[k] ^ w[k];
+    }
+}
+
+int main(int argc, char** argv) {
+    const size_t bytes = (argc > 1 ? std::atoll(argv[1]) : 2048) << 20;  // MiB per buffer
+    const size_t n = bytes / 16;
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    int cus = 0;
+    CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+    u32x4 *a, *b, *o, *sink;
+    CK(hipMalloc(&a, bytes));
+    CK(hipMalloc(&b, bytes));
+    CK(hipMalloc(&o, bytes));
+    CK(hipMalloc(&sink, 1 << 16));
+    CK(hipMemset(a, 1, bytes));
+    CK(hipMemset(b, 2, bytes));
+    CK(hipMemset(o, 3, bytes));
+    CK(hipDeviceSynchronize());
+    auto timeit = [&](auto launch) {
+        float best = 1e9, sum = 0;
+        for (int rep = 0; rep < 14; rep++) {
+            CK(hipEventRecord(e0));
+            launch();
+            CK(hipEventRecord(e1));
+            CK(hipEventSynchronize(e1));
+            float ms;
+            CK(hipEventElapsedTime(&ms, e0, e1));
+            if (rep >= 4) { best = ms < best ? ms : best; sum += ms; }
+        }
+        return std::make_pair(sum / 10, best);
+    };
+    auto show = [&](const char* what, unsigned g, unsigned t, std::pair<float, float> ms, double moved) {
+        std::printf("%-22s grid %6u x %4u: avg %.4f ms %6.0f GB/s (frac %.3f)  best %6.0f GB/s (frac %.3f)\n", what, g, t,
+                    ms.first, moved / ms.first / 1e6, moved / ms.first / 8e9, moved / ms.second / 1e6,
+                    moved / ms.second / 8e9);
+        std::fflush(stdout);
+    };
+    std::printf("buffers %zu MiB, %d CUs\n", bytes >> 20, cus);
+    for (unsigned wpc : {4u, 8u, 16u, 32u}) {
+        const unsigned g = cus * wpc;
+        show("read  gs U4", g, 256, timeit([&] { rd_gs<4, false><<<g, 256>>>(a, n, sink); }), 16.0 * n);
+        show("read  gs U8", g, 256, timeit([&] { rd_gs<8, false><<<g, 256>>>(a, n, sink); }), 16.0 * n);
+        show("read  gs U4 nt", g, 256, timeit([&] { rd_gs<4, true><<<g, 256>>>(a, n, sink); }), 16.0 * n);
+        show("write gs U4", g, 256, timeit([&] { wr_gs<4, false><<<g, 256>>>(o, n); }), 16.0 * n);
+        show("write gs U4 nt", g, 256, timeit([&] { wr_gs<4, true><<<g, 256>>>(o, n); }), 16.0 * n);
+        show("copy  gs U4", g, 256, timeit([&] { cp_gs<4, false><<<g, 256>>>(a, o, n); }), 32.0 * n);
+        show("copy  gs U8", g, 256, timeit([&] { cp_gs<8, false><<<g, 256>>>(a, o, n); }), 32.0 * n);
+        show("copy  gs U4 nt-st", g, 256, timeit([&] { cp_gs<4, true><<<g, 256>>>(a, o, n); }), 32.0 * n);
+        show("mix21 gs U2", g, 256, timeit([&] { mix_gs<2><<<g, 256>>>(a, b, o, n); }), 48.0 * n);
+        show("mix21 gs U4", g, 256, timeit([&] { mix_gs<4><<<g, 256>>>(a, b, o, n); }), 48.0 * n);
+    }
+    for (size_t chunk_kib : {64ull, 256ull, 1024ull}) {
+        const size_t per = chunk_kib * 1024 / 16;
+        const unsigned g = (unsigned)((n + per - 1) / per);
+        char nm[64];
+        std::snprintf(nm, sizeof nm, "read  chunk %zuK U8", chunk_kib);
+        show(nm, g, 256, timeit([&] { rd_chunk<8><<<g, 256>>>(a, n, per, sink); }), 16.0 * n);
+        std::snprintf(nm, sizeof nm, "copy  chunk %zuK U4", chunk_kib);
+        show(nm, g, 256, timeit([&] { cp_chunk<4, false><<<g, 256>>>(a, o, n, per); }), 32.0 * n);
+        std::snprintf(nm, sizeof nm, "copy  chunk %zuK U8", chunk_kib);
+        show(nm, g, 256, timeit([&] { cp_chunk<8, false><<<g, 256>>>(a, o, n, per); }), 32.0 * n);
+        std::snprintf(nm, sizeof nm, "copy  chunk %zuK U4 1k", chunk_kib);
+        show(nm, g, 1024, timeit([&] { cp_chunk<4, false><<<g, 1024>>>(a, o, n, per); }), 32.0 * n);
+    }
+    {
+        float ms = 0;
+        for (int rep = 0; rep < 6; rep++) {
+            CK(hipEventRecord(e0));
+            CK(hipMemcpyAsync(o, a, bytes, hipMemcpyDeviceToDevice));
+            CK(hipEventRecord(e1));
+            CK(hipEventSynchronize(e1));
+            float t;
+            CK(hipEventElapsedTime(&t, e0, e1));
+            if (rep >= 2) ms += t / 4;
+        }
+        std::printf("hipMemcpy d2d: %.4f ms %6.0f GB/s (frac %.3f)\n", ms, 2.0 * bytes / ms / 1e6, 2.0 * bytes / ms / 8e9);
+    }
+    return 0;
+}
