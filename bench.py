@@ -160,8 +160,11 @@ def measure_traffic(args, kernel):
     paths = []
     with tempfile.TemporaryDirectory(prefix="murr_pmc_") as d:
         for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+            # the interpreter's resolved path after `--` (a `python3` looked up
+            # on PATH may be a wrapper that execs the real one, and rocprofv3
+            # itself execs what follows `--`)
             cmd = [prof, "--pmc", ctr, "--output-format", "csv", "-d", d, "-o", ctr.lower(), "--",
-                   sys.executable, os.path.abspath(__file__), *argv, "--steps", "2", "--warmup", "1",
+                   os.path.realpath(sys.executable), os.path.abspath(__file__), *argv, "--steps", "2", "--warmup", "1",
                    "--no-cpu", "--no-traffic"]
             env = {k: v for k, v in os.environ.items() if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE")}
             pr = subprocess.Popen(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, env=env,
@@ -436,7 +439,7 @@ def run_decode(args, dist, rank, world, local_rank):
 
     # after the timed region: the timed launch's output, checked against the
     # oracle (first and last block); a mismatch fails the run
-    checked = sorted({0, K - 1})
+    checked = sorted({0, K - 1}) if not args.no_verify else []
     bad, want = [], None
     for b in checked:
         bb, want = verify_arrays(ctx, seg, proj, outs, b, host_blob, host_off, want)
@@ -481,7 +484,7 @@ def run_decode(args, dist, rank, world, local_rank):
                      "traffic": traffic, "kernel": ctx.last_kernel(),
                      "kernel_ms_avg": round(k_avg_ms, 5),
                      "algorithmic_bytes_per_launch": (in_block + out_block) * K},
-        "verified": f"blocks {checked} of the timed launch bit-exact vs the oracle",
+        "verified": f"blocks {checked} of the timed launch bit-exact vs the oracle" if checked else "NOT VERIFIED (--no-verify)",
         "no_index_ms": no_index_ms,
         "cpu_baseline": None,
     }
@@ -570,7 +573,7 @@ def run_host(args):
         del dblob, doff
     proj = list(range(len(seg.columns)))
     oseg = O.Segment([int(c.dtype) for c in seg.columns])
-    want = {r: O.decode_block(oseg, proj, blocks[r][0], blocks[r][1]) for r in {0, (args.blocks - 1) % ring}}
+    want = {}
     # the pinned block cache: every ring block copied once into murr_host_alloc memory
     pinned = []
     for blob, off in blocks:
@@ -580,6 +583,8 @@ def run_host(args):
         pinned.append((hb, ho, ho.array.view(np.uint64)))
 
     def check(outs, r):
+        if r not in want:
+            want[r] = O.decode_block(oseg, proj, blocks[r][0], blocks[r][1])
         for p in range(len(proj)):
             g, e = host_array_buffers(outs[p]), want[r][p]
             ok = g["null_count"] == e["null_count"] and (e["validity"] is None or g["validity"] == e["validity"])
@@ -987,6 +992,8 @@ def main():
     ap.add_argument("--table", default="C", choices=["C", "ref"],
                     help="resident mode: config C table, or the reference read benches' dataset (10 x f32)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-verify", action="store_true",
+                    help="skip the oracle check of the timed output (tuning ablations that skip stores only)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--pmc-csv", default=None)
     ap.add_argument("--sync-steps", action="store_true",

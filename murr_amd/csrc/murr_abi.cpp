@@ -2224,12 +2224,17 @@ void murr_builder_free(murr_builder_t* b) {
 }  // extern "C"
 
 // ---- streaming host decode (murr_hstream_*) ----------------------------------
-// Batch reads back to back, host in, host out.  Each slot owns a context (its
-// own stream and decode workspace) and grow-only buffers; a batch is one
-// in-order chain on its slot's stream -- H2D of the blobs and row offsets,
-// the decode, one D2H of the slot's whole (bounded) output region -- so the
-// chains of consecutive batches overlap on the copy engines and the CUs, and
-// the only host wait is next()'s, on the oldest batch.
+// Batch reads back to back, host in, host out.  Three kinds of stream: one H2D
+// stream and one D2H stream shared by all slots (each copy direction one
+// engine, copies of one direction back to back at the link's full rate), and
+// each slot's own context stream for its decode (its own workspace, so
+// `depth` decodes may be in flight).  Batch i: H2D on the H2D stream -> its
+// decode waits on that (event) -> the D2H of its fixed-size arrays (values of
+// fixed-width columns, utf8 offsets, validity) waits on the decode; next()
+// learns the utf8 byte counts from the decode's counters and queues the
+// batch's D2H (fixed-size arrays in one copy, then exactly the utf8 bytes),
+// in batch order.  The only host waits are next()'s; the H2D stream runs
+// ahead through the batches already submitted meanwhile.
 
 struct HSlot {
     murr_ctx* c = nullptr;
@@ -2239,7 +2244,10 @@ struct HSlot {
     uint64_t din_cap = 0;
     HostOut out;
     uint64_t n = 0, h2d_bytes = 0, d2h_bytes = 0;
-    hipEvent_t e0 = nullptr, e1 = nullptr, e2 = nullptr, e3 = nullptr;
+    hipEvent_t e0 = nullptr, e1 = nullptr;  // H2D start / end (H2D stream)
+    hipEvent_t ed = nullptr;                // decode done (slot stream)
+    hipEvent_t e2 = nullptr, e3 = nullptr;  // fixed-size D2H start / end (D2H stream)
+    hipEvent_t e4 = nullptr, e5 = nullptr;  // utf8 bytes D2H start / end (D2H stream)
     int submit_status = MURR_OK;  // an enqueue that failed: next() reports it
     murr_error_t submit_err{};
 };
@@ -2250,15 +2258,16 @@ struct murr_hstream {
     murr_segment_t seg{};
     std::vector<uint32_t> proj;
     std::vector<HSlot> slots;
+    hipStream_t s_h2d = nullptr, s_d2h = nullptr;
     uint64_t head = 0, tail = 0;  // batches submitted / returned
     murr_hstream_stats_t stats{};
 };
 
 namespace {
 
-// Enqueue batch `s` on its slot's stream (everything after the staging copy is
-// asynchronous).  The output region is laid out as decode_to_host's, its utf8
-// parts bounded by the blob bytes past the rows' fixed parts.
+// Enqueue batch `s` (everything after the staging copy is asynchronous).  The
+// output region is laid out as decode_to_host's, its utf8 parts bounded by the
+// blob bytes.
 int hstream_enqueue(murr_hstream* h, HSlot& s, const uint8_t* data, const uint64_t* row_off, uint64_t n,
                     bool pinned, murr_error_t* err) {
     murr_ctx* c = s.c;
@@ -2280,31 +2289,42 @@ int hstream_enqueue(murr_hstream* h, HSlot& s, const uint8_t* data, const uint64
         src_off = (const uint64_t*)(s.hin + dbytes);
     }
     uint64_t* doff = (uint64_t*)(s.din + dbytes);
-    HIPC(hipEventRecord(s.e0, c->stream));
-    if (head + bytes) HIPC(hipMemcpyAsync(s.din, src_data, head + bytes, hipMemcpyHostToDevice, c->stream));
-    HIPC(hipMemcpyAsync(doff, src_off, obytes, hipMemcpyHostToDevice, c->stream));
-    HIPC(hipEventRecord(s.e1, c->stream));
+    HIPC(hipEventRecord(s.e0, h->s_h2d));
+    if (head + bytes) HIPC(hipMemcpyAsync(s.din, src_data, head + bytes, hipMemcpyHostToDevice, h->s_h2d));
+    HIPC(hipMemcpyAsync(doff, src_off, obytes, hipMemcpyHostToDevice, h->s_h2d));
+    HIPC(hipEventRecord(s.e1, h->s_h2d));
+    HIPC(hipStreamWaitEvent(c->stream, s.e1, 0));
     s.h2d_bytes = head + bytes + obytes;
     // row i of the block is data[row_off[i]..]: the block's data pointer sits
     // row_off[0] & ~15 bytes before the staged bytes (16-B aligned)
     murr_block_t blk{s.din - (b0 - head), doff, n, b1};
-    // the blob bytes bound any one utf8 column's string bytes
-    const uint64_t utf8_cap = std::max<uint64_t>(bytes, 8);
+    const uint64_t utf8_cap = std::max<uint64_t>(bytes, 8);  // any one utf8 column's string bytes
     const uint32_t np = (uint32_t)h->proj.size();
     const uint64_t bm = murr_bitmap_bytes(n);
     HostOut& o = s.out;
+    // layout: every fixed-size part first (one D2H right behind the decode),
+    // then the utf8 values (exact bytes, copied in next())
     o.off.assign((size_t)np * 3, 0);
     uint64_t off = 0;
     for (uint32_t p = 0; p < np; p++) {
         const murr_column_t& col = h->seg.cols[h->proj[p]];
-        const uint64_t vb = col.dtype == MURR_UTF8 ? utf8_cap : col.dtype == MURR_BOOL ? bm : n * col.size;
-        o.off[3 * p] = off;
-        off = round_up(off + std::max<uint64_t>(vb, 8), 64);
+        if (col.dtype != MURR_UTF8) {
+            o.off[3 * p] = off;
+            off = round_up(off + std::max<uint64_t>(col.dtype == MURR_BOOL ? bm : n * col.size, 8), 64);
+        }
         o.off[3 * p + 1] = off;
         off = round_up(off + std::max<uint64_t>(bm, 8), 64);
-        o.off[3 * p + 2] = off;
-        if (col.dtype == MURR_UTF8) off = round_up(off + (n + 1) * 4, 64);
+        if (col.dtype == MURR_UTF8) {
+            o.off[3 * p + 2] = off;
+            off = round_up(off + (n + 1) * 4, 64);
+        }
     }
+    const uint64_t fixed_out = std::max<uint64_t>(off, 64);
+    for (uint32_t p = 0; p < np; p++)
+        if (h->seg.cols[h->proj[p]].dtype == MURR_UTF8) {
+            o.off[3 * p] = off;
+            off = round_up(off + utf8_cap, 64);
+        }
     const uint64_t total_out = std::max<uint64_t>(off, 64);
     if (!grow_dev(c, &o.dout, &o.dout_cap, total_out) || !grow_pinned(c, &o.hout, &o.hout_cap, total_out, 0))
         return set_err(err, MURR_E_HIP);
@@ -2318,10 +2338,7 @@ int hstream_enqueue(murr_hstream* h, HSlot& s, const uint8_t* data, const uint64
     }
     const int st = murr_decode_enqueue(c, &h->seg, h->proj.data(), np, &blk, 1, o.arr.data());
     if (st) return set_err(err, st, st == MURR_E_HIP ? (int)hipGetLastError() : 0);
-    HIPC(hipEventRecord(s.e2, c->stream));
-    HIPC(hipMemcpyAsync(o.hout, o.dout, total_out, hipMemcpyDeviceToHost, c->stream));
-    HIPC(hipEventRecord(s.e3, c->stream));
-    s.d2h_bytes = total_out;
+    s.d2h_bytes = fixed_out;  // (the fixed-size part, copied in next() with the utf8 bytes)
     s.n = n;
     return MURR_OK;
 }
@@ -2346,15 +2363,20 @@ int murr_hstream_new(murr_ctx_t* c, const murr_segment_t* seg, const uint32_t* p
     h->seg.cols = h->cols.data();
     h->proj.assign(proj, proj + nproj);
     h->slots.resize(depth);
+    int st = hipSetDevice(c->device) == hipSuccess ? MURR_OK : MURR_E_HIP;
+    if (!st && (hipStreamCreateWithFlags(&h->s_h2d, hipStreamNonBlocking) != hipSuccess ||
+                hipStreamCreateWithFlags(&h->s_d2h, hipStreamNonBlocking) != hipSuccess))
+        st = MURR_E_HIP;
     for (HSlot& s : h->slots) {
-        int st = murr_ctx_create(c->device, &s.c);
+        if (!st) st = murr_ctx_create(c->device, &s.c);
         if (!st) st = murr_ctx_set_opts(s.c, &c->opts);
-        for (hipEvent_t* e : {&s.e0, &s.e1, &s.e2, &s.e3})
+        for (hipEvent_t* e : {&s.e0, &s.e1, &s.e2, &s.e3, &s.e4, &s.e5})
             if (!st && hipEventCreate(e) != hipSuccess) st = MURR_E_HIP;
-        if (st) {
-            murr_hstream_free(h);
-            return st;
-        }
+        if (!st && hipEventCreateWithFlags(&s.ed, hipEventDisableTiming) != hipSuccess) st = MURR_E_HIP;
+    }
+    if (st) {
+        murr_hstream_free(h);
+        return st;
     }
     *out = h;
     return MURR_OK;
@@ -2384,18 +2406,36 @@ int murr_hstream_next(murr_hstream_t* h, murr_host_array_t* outs, murr_error_t* 
         return s.submit_status;
     }
     murr_ctx* c = s.c;
-    // the decode's counters come back behind the D2H on the same stream:
-    // this one synchronisation covers the whole chain
+    HIPC(hipSetDevice(c->device));
+    // the decode and its counters (null counts, utf8 byte counts, errors)
     int st = murr_decode_wait(c, err);
     if (st) return st;
+    // the batch's D2H, in batch order on the D2H stream (a copy queued there
+    // never waits behind a later batch's decode): the fixed-size arrays in
+    // one copy, then exactly the decoded utf8 bytes
+    const HostOut& o = s.out;
+    uint64_t ub = 0;
+    HIPC(hipEventRecord(s.e2, h->s_d2h));
+    HIPC(hipMemcpyAsync(o.hout, o.dout, s.d2h_bytes, hipMemcpyDeviceToHost, h->s_d2h));
+    HIPC(hipEventRecord(s.e3, h->s_d2h));
+    HIPC(hipEventRecord(s.e4, h->s_d2h));
+    for (uint32_t p = 0; p < h->proj.size(); p++) {
+        const murr_array_t& a = o.arr[p];
+        if (a.offsets && a.data_len) {
+            HIPC(hipMemcpyAsync(o.hout + o.off[3 * p], a.values, a.data_len, hipMemcpyDeviceToHost, h->s_d2h));
+            ub += a.data_len;
+        }
+    }
+    HIPC(hipEventRecord(s.e5, h->s_d2h));
+    HIPC(hipEventSynchronize(s.e5));
     float ms = 0;
     if (hipEventElapsedTime(&ms, s.e0, s.e1) == hipSuccess) h->stats.h2d_ms += ms;
     if (murr_ctx_last_kernel_ms(c, &ms) == MURR_OK) h->stats.kernel_ms += ms;
     if (hipEventElapsedTime(&ms, s.e2, s.e3) == hipSuccess) h->stats.d2h_ms += ms;
+    if (ub && hipEventElapsedTime(&ms, s.e4, s.e5) == hipSuccess) h->stats.d2h_ms += ms;
     h->stats.h2d_bytes += s.h2d_bytes;
-    h->stats.d2h_bytes += s.d2h_bytes;
+    h->stats.d2h_bytes += s.d2h_bytes + ub;
     h->stats.batches++;
-    const HostOut& o = s.out;
     for (uint32_t p = 0; p < h->proj.size(); p++) {
         const murr_array_t& a = o.arr[p];
         murr_host_array_t& ha = outs[p];
@@ -2419,6 +2459,9 @@ int murr_hstream_stats(murr_hstream_t* h, murr_hstream_stats_t* out) {
 
 void murr_hstream_free(murr_hstream_t* h) {
     if (!h) return;
+    if (h->owner) (void)hipSetDevice(h->owner->device);
+    if (h->s_h2d) (void)hipStreamSynchronize(h->s_h2d);
+    if (h->s_d2h) (void)hipStreamSynchronize(h->s_d2h);
     for (HSlot& s : h->slots) {
         if (!s.c) continue;
         (void)hipSetDevice(s.c->device);
@@ -2431,10 +2474,13 @@ void murr_hstream_free(murr_hstream_t* h) {
         pool_give(s.c, false, s.din, s.din_cap);
         pool_give(s.c, true, s.out.hout, s.out.hout_cap);
         pool_give(s.c, false, s.out.dout, s.out.dout_cap);
-        for (hipEvent_t e : {s.e0, s.e1, s.e2, s.e3})
+        for (hipEvent_t e : {s.e0, s.e1, s.ed, s.e2, s.e3, s.e4, s.e5})
             if (e) (void)hipEventDestroy(e);
         murr_ctx_destroy(s.c);  // (frees the pooled buffers too)
     }
+    if (h->s_d2h) (void)hipStreamSynchronize(h->s_d2h);
+    if (h->s_h2d) (void)hipStreamDestroy(h->s_h2d);
+    if (h->s_d2h) (void)hipStreamDestroy(h->s_d2h);
     delete h;
 }
 

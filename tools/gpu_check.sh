@@ -5,6 +5,8 @@
 set -u
 mkdir -p gpurun_out
 export TMPDIR=/tmp
+# the resolved interpreter after `--` (rocprofv3 execs it; a `python3` on PATH may be a wrapper)
+PY=$(readlink -f "$(command -v python3)")
 step() {  # step <name> <timeout> <cmd...>
     local name=$1 t=$2; shift 2
     timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1
@@ -15,9 +17,9 @@ step() {  # step <name> <timeout> <cmd...>
 }
 rocm-smi --showproductname > gpurun_out/smi.log 2>&1 || true
 lscpu > gpurun_out/lscpu.log 2>&1 || true
-step smoke 180 python -c "import __graft_entry__ as g; g.smoke()"
-step pytest_gpu 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread ${PYTEST_ARGS:-}
-step bench 380 python bench.py ${BENCH_ARGS:-}
+step smoke 180 "$PY" -c "import __graft_entry__ as g; g.smoke()"
+step pytest_gpu 900 "$PY" -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread ${PYTEST_ARGS:-}
+step bench 380 "$PY" bench.py ${BENCH_ARGS:-}
 if [ -n "${PROFILE:-}" ]; then
-  step rocprof 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o decode -- python3 bench.py --steps 5 --warmup 1 --no-cpu
+  step rocprof 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o decode -- "$PY" bench.py --steps 5 --warmup 1 --no-cpu
 fi

@@ -5,6 +5,8 @@
 # plus the side measurements DESIGN.md quotes.  Everything under gpurun_out/$R.
 set -u
 export TMPDIR=/tmp
+# the resolved interpreter after `--` (rocprofv3 execs it; a `python3` on PATH may be a wrapper)
+PY=$(readlink -f "$(command -v python3)")
 R=${R:-r02}
 out=gpurun_out/$R
 mkdir -p $out
@@ -16,32 +18,32 @@ run() {  # run <name> <timeout> <cmd...>
   [ $rc -eq 0 ] || exit $rc
 }
 # the driver's exact command (bench.py --gpus 1 --steps 20 --warmup 5), traced
-run trace 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out/trace -o decode -- python3 bench.py --gpus 1 --steps 20 --warmup 5 --no-traffic
-run fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $out/pmc -o fetch -- python3 bench.py --steps 3 --warmup 1 --no-cpu --no-traffic
-run write 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $out/pmc -o write -- python3 bench.py --steps 3 --warmup 1 --no-cpu --no-traffic
-run bench 400 python3 bench.py --gpus 1 --steps 20 --warmup 5 --pmc-csv "$out/pmc/fetch_counter_collection.csv,$out/pmc/write_counter_collection.csv"
+run trace 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out/trace -o decode -- "$PY" bench.py --gpus 1 --steps 20 --warmup 5 --no-traffic
+run fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $out/pmc -o fetch -- "$PY" bench.py --steps 3 --warmup 1 --no-cpu --no-traffic
+run write 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $out/pmc -o write -- "$PY" bench.py --steps 3 --warmup 1 --no-cpu --no-traffic
+run bench 400 "$PY" bench.py --gpus 1 --steps 20 --warmup 5 --pmc-csv "$out/pmc/fetch_counter_collection.csv,$out/pmc/write_counter_collection.csv"
 # wide-schema decode (configs C / D one-shard) with their own traffic passes
 for cfg in "C:--config C --blocks 10" "D1:--config D"; do
   n=${cfg%%:*}; a=${cfg#*:}
-  run fetch_$n 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $out/pmc -o fetch_$n -- python3 bench.py $a --steps 3 --warmup 1 --no-cpu --no-traffic
-  run write_$n 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $out/pmc -o write_$n -- python3 bench.py $a --steps 3 --warmup 1 --no-cpu --no-traffic
-  run decode_$n 300 python3 bench.py $a --steps 10 --warmup 2 --no-cpu --pmc-csv "$out/pmc/fetch_${n}_counter_collection.csv,$out/pmc/write_${n}_counter_collection.csv"
+  run fetch_$n 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $out/pmc -o fetch_$n -- "$PY" bench.py $a --steps 3 --warmup 1 --no-cpu --no-traffic
+  run write_$n 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $out/pmc -o write_$n -- "$PY" bench.py $a --steps 3 --warmup 1 --no-cpu --no-traffic
+  run decode_$n 300 "$PY" bench.py $a --steps 10 --warmup 2 --no-cpu --pmc-csv "$out/pmc/fetch_${n}_counter_collection.csv,$out/pmc/write_${n}_counter_collection.csv"
 done
 if [ -z "${QUICK:-}" ]; then
-  run host_B 300 python3 bench.py --mode host --config B --steps 10 --warmup 2
-  run encode_E 300 python3 bench.py --mode encode --steps 10 --warmup 2
-  run decode_C_noindex 300 python3 bench.py --config C --blocks 10 --steps 10 --warmup 2 --no-cpu --uidx-stride 0
-  run decode_D10M 300 python3 bench.py --config D --rows 10000000 --steps 10 --warmup 2 --no-cpu
-  run decode_D1_noindex 300 python3 bench.py --config D --steps 10 --warmup 2 --no-cpu --uidx-stride 0
-  run decode_B_generic 300 python3 bench.py --steps 10 --warmup 2 --no-cpu --opts kernel=generic
-  run host_C 300 python3 bench.py --mode host --config C --rows 1000 --steps 50 --warmup 5
-  run encode_B 300 python3 bench.py --mode encode --enc-config B --steps 10 --warmup 2
-  run encode_C 300 python3 bench.py --mode encode --enc-config C --steps 10 --warmup 2
-  run resident_1000 300 python3 bench.py --mode resident --keys 1000 --steps 30 --warmup 5
-  run resident_read_plain 300 python3 bench.py --mode resident --table ref --rows 10000000 --keys 1000 --steps 200 --warmup 20 --ipc
-  run resident_read_block 400 python3 bench.py --mode resident --table ref --rows 100000000 --keys 1000 --steps 200 --warmup 20
+  run host_B 300 "$PY" bench.py --mode host --config B
+  run encode_E 300 "$PY" bench.py --mode encode --steps 10 --warmup 2
+  run decode_C_noindex 300 "$PY" bench.py --config C --blocks 10 --steps 10 --warmup 2 --no-cpu --uidx-stride 0
+  run decode_D10M 300 "$PY" bench.py --config D --rows 10000000 --steps 10 --warmup 2 --no-cpu
+  run decode_D1_noindex 300 "$PY" bench.py --config D --steps 10 --warmup 2 --no-cpu --uidx-stride 0
+  run decode_B_generic 300 "$PY" bench.py --steps 10 --warmup 2 --no-cpu --opts kernel=generic
+  run host_C 300 "$PY" bench.py --mode host --config C --rows 1000 --blocks 2000 --warmup 50
+  run encode_B 300 "$PY" bench.py --mode encode --enc-config B --steps 10 --warmup 2
+  run encode_C 300 "$PY" bench.py --mode encode --enc-config C --steps 10 --warmup 2
+  run resident_1000 300 "$PY" bench.py --mode resident --keys 1000 --steps 30 --warmup 5
+  run resident_read_plain 300 "$PY" bench.py --mode resident --table ref --rows 10000000 --keys 1000 --steps 200 --warmup 20 --ipc
+  run resident_read_block 400 "$PY" bench.py --mode resident --table ref --rows 100000000 --keys 1000 --steps 200 --warmup 20
   # one-block config D at 2x / 4x the shard: fixed cost per launch (fit over rows)
-  run decode_D1x2 300 python3 bench.py --config D --rows 2500000 --steps 10 --warmup 2 --no-cpu
-  run decode_D1x4 300 python3 bench.py --config D --rows 5000000 --steps 10 --warmup 2 --no-cpu
+  run decode_D1x2 300 "$PY" bench.py --config D --rows 2500000 --steps 10 --warmup 2 --no-cpu
+  run decode_D1x4 300 "$PY" bench.py --config D --rows 5000000 --steps 10 --warmup 2 --no-cpu
   run encode_prof 300 bash tools/enc_prof.sh
 fi

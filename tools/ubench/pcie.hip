@@ -1,0 +1,62 @@
+// Host link probe (round 4): pinned hipMemcpyAsync rates H2D and D2H alone,
+// and both directions at once on two streams, per transfer size -- the
+// ceiling of the streaming host decode (murr_hstream).
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 pcie.hip -o pcie
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+
+#define CK(x)                                                                              \
+    do {                                                                                   \
+        hipError_t e_ = (x);                                                               \
+        if (e_ != hipSuccess) {                                                            \
+            std::fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+            std::exit(1);                                                                  \
+        }                                                                                  \
+    } while (0)
+
+int main() {
+    const size_t maxb = 64ull << 20;
+    void *h1, *h2, *d1, *d2;
+    CK(hipHostMalloc(&h1, maxb, hipHostMallocDefault));
+    CK(hipHostMalloc(&h2, maxb, hipHostMallocDefault));
+    CK(hipMalloc(&d1, maxb));
+    CK(hipMalloc(&d2, maxb));
+    hipStream_t a, b;
+    CK(hipStreamCreateWithFlags(&a, hipStreamNonBlocking));
+    CK(hipStreamCreateWithFlags(&b, hipStreamNonBlocking));
+    hipEvent_t e0, e1, f0, f1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    CK(hipEventCreate(&f0));
+    CK(hipEventCreate(&f1));
+    for (size_t sz : {64ull << 10, 256ull << 10, 1ull << 20, 2730ull << 10, 8ull << 20, 64ull << 20}) {
+        const int reps = sz < (4u << 20) ? 200 : 20;
+        auto run = [&](bool h2d, bool d2h) {
+            CK(hipDeviceSynchronize());
+            CK(hipEventRecord(e0, a));
+            CK(hipEventRecord(f0, b));
+            for (int r = 0; r < reps; r++) {
+                if (h2d) CK(hipMemcpyAsync(d1, h1, sz, hipMemcpyHostToDevice, a));
+                if (d2h) CK(hipMemcpyAsync(h2, d2, sz, hipMemcpyDeviceToHost, b));
+            }
+            CK(hipEventRecord(e1, a));
+            CK(hipEventRecord(f1, b));
+            CK(hipEventSynchronize(e1));
+            CK(hipEventSynchronize(f1));
+            float ta = 0, tb = 0;
+            CK(hipEventElapsedTime(&ta, e0, e1));
+            CK(hipEventElapsedTime(&tb, f0, f1));
+            return std::make_pair(h2d ? ta : 0.f, d2h ? tb : 0.f);
+        };
+        run(true, true);  // warm
+        const auto x = run(true, false), y = run(false, true), z = run(true, true);
+        const double gb = (double)sz * reps / 1e9;
+        std::printf("%8zu KiB: H2D alone %6.1f GB/s  D2H alone %6.1f GB/s  both: H2D %6.1f GB/s D2H %6.1f GB/s  (per copy %.1f / %.1f us)\n",
+                    sz >> 10, gb / (x.first * 1e-3), gb / (y.second * 1e-3), gb / (z.first * 1e-3), gb / (z.second * 1e-3),
+                    x.first * 1e3 / reps, y.second * 1e3 / reps);
+        std::fflush(stdout);
+    }
+    return 0;
+}
