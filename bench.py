@@ -630,15 +630,18 @@ def run_host(args):
         st1 = hs.stats()
         hs.close()
         d = {k: st1[k] - st0[k] for k in st1}
-        nb = d["batches"]
+        nb, nt = d["batches"], max(d["timed_batches"], 1)  # (copies and kernel timed on every eighth batch)
+        h2d_b, d2h_b = d["h2d_bytes"] / nb, d["d2h_bytes"] / nb
         return {"GiB_s_host_to_host": round(out_bytes / el / GIB, 3),
                 "ms_per_batch": round(el / args.blocks * 1e3, 4),
                 "arrow_bytes_out_per_batch": out_bytes // args.blocks,
-                "h2d_GB_s": round(d["h2d_bytes"] / (d["h2d_ms"] * 1e-3) / 1e9, 2) if d["h2d_ms"] else None,
-                "d2h_GB_s": round(d["d2h_bytes"] / (d["d2h_ms"] * 1e-3) / 1e9, 2) if d["d2h_ms"] else None,
-                "h2d_ms_per_batch": round(d["h2d_ms"] / nb, 4), "kernel_ms_per_batch": round(d["kernel_ms"] / nb, 4),
-                "d2h_ms_per_batch": round(d["d2h_ms"] / nb, 4),
-                "h2d_bytes_per_batch": d["h2d_bytes"] // nb, "d2h_bytes_per_batch": d["d2h_bytes"] // nb}
+                "h2d_GB_s": round(h2d_b / (d["h2d_ms"] / nt * 1e-3) / 1e9, 2) if d["h2d_ms"] else None,
+                "d2h_GB_s": round(d2h_b / (d["d2h_ms"] / nt * 1e-3) / 1e9, 2) if d["d2h_ms"] else None,
+                "h2d_ms_per_batch": round(d["h2d_ms"] / nt, 4), "kernel_ms_per_batch": round(d["kernel_ms"] / nt, 4),
+                "d2h_ms_per_batch": round(d["d2h_ms"] / nt, 4),
+                "host_submit_ms_per_batch": round(d["host_submit_ms"] / nb, 4),
+                "host_next_ms_per_batch": round(d["host_next_ms"] / nb, 4),
+                "h2d_bytes_per_batch": int(h2d_b), "d2h_bytes_per_batch": int(d2h_b)}
 
     res = {"pinned_source": stream_run(True), "pageable_source": stream_run(False)}
     # the serial builder path (round 3's number): one batch at a time, rows added one by one

@@ -153,6 +153,10 @@ typedef struct {
                                grid, each workgroup walking several (virtual) blocks);
                                0xFFFFFFFF = one workgroup per (virtual) block, handed to the
                                CUs by the hardware as workgroups finish */
+    uint32_t balance;       /* local mode, several (virtual) blocks per workgroup: 0 auto
+                               (dynamic when the blocks are cut), 1 static deal only,
+                               2 dynamic per-XCD tail with half the blocks dealt statically,
+                               10..90 dynamic with that percentage dealt statically */
 } murr_opts_t;
 int murr_ctx_set_opts(murr_ctx_t* ctx, const murr_opts_t* opts);
 int murr_ctx_get_opts(murr_ctx_t* ctx, murr_opts_t* opts);
@@ -429,13 +433,17 @@ int murr_hstream_new(murr_ctx_t* ctx, const murr_segment_t* seg, const uint32_t*
 int murr_hstream_submit(murr_hstream_t* s, const uint8_t* data, const uint64_t* row_off,
                         uint64_t n_rows, uint32_t flags, murr_error_t* err);
 int murr_hstream_next(murr_hstream_t* s, murr_host_array_t* outs /* nproj */, murr_error_t* err);
-/* Totals since creation: batches returned, device milliseconds of the H2D
- * copies, the decode kernels and the D2H copies (HIP events on the slots'
- * streams), and the bytes each copy direction moved. */
+/* Totals since creation: batches returned; the bytes each copy direction
+ * moved; device milliseconds of the H2D copies, the decode kernels and the
+ * D2H copies of the `timed_batches` batches timed with HIP events (every
+ * eighth: the events cost host time per batch); host milliseconds spent in
+ * submit and in next (API calls and waits). */
 typedef struct {
     uint64_t batches;
     double h2d_ms, kernel_ms, d2h_ms;
     uint64_t h2d_bytes, d2h_bytes;
+    uint64_t timed_batches;
+    double host_submit_ms, host_next_ms;
 } murr_hstream_stats_t;
 int murr_hstream_stats(murr_hstream_t* s, murr_hstream_stats_t* out);
 void murr_hstream_free(murr_hstream_t* s);

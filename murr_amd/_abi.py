@@ -38,7 +38,8 @@ class Error(C.Structure):
 class Opts(C.Structure):
     """murr_opts_t: kernel selection of one context (tests, benchmarks)."""
     _fields_ = [(n, C.c_uint32) for n in ("kernel", "mode", "shape_nw", "shape_r", "seg_tiles", "vrows",
-                                          "lds_budget", "stage", "encode_kernel", "verbose", "grid")]
+                                          "lds_budget", "stage", "encode_kernel", "verbose", "grid",
+                                          "balance")]
 
 
 class CtxStats(C.Structure):
@@ -85,7 +86,8 @@ class HostArray(C.Structure):
 
 class HStreamStats(C.Structure):
     _fields_ = [("batches", C.c_uint64), ("h2d_ms", C.c_double), ("kernel_ms", C.c_double), ("d2h_ms", C.c_double),
-                ("h2d_bytes", C.c_uint64), ("d2h_bytes", C.c_uint64)]
+                ("h2d_bytes", C.c_uint64), ("d2h_bytes", C.c_uint64), ("timed_batches", C.c_uint64),
+                ("host_submit_ms", C.c_double), ("host_next_ms", C.c_double)]
 
 
 class HostColIn(C.Structure):

@@ -123,6 +123,12 @@ namespace {
 
 int hip_fail(murr_error_t* err, hipError_t e) { return set_err(err, MURR_E_HIP, (int)e); }
 
+uint32_t nutf8_of(const murr_segment_t* seg) {
+    uint32_t n = 0;
+    for (uint32_t i = 0; i < seg->ncols; i++) n += seg->cols[i].dtype == MURR_UTF8;
+    return n;
+}
+
 #define HIPC(expr)                                          \
     do {                                                    \
         hipError_t _e = (expr);                             \
@@ -1006,6 +1012,25 @@ int decode_enqueue_jit(murr_ctx* c, const murr_segment_t* seg, const JitLayout* 
     if (O.grid == 0xFFFFFFFFu) grid_local = lsegs.size();
     else if (O.grid) grid_local = std::min<uint64_t>(O.grid, lsegs.size());
     const uint64_t grid = std::max<uint64_t>(1, local ? grid_local : std::min<uint64_t>(G_split, nseg));
+    // Local mode with several (virtual) blocks per workgroup: the first share
+    // dealt statically, the rest claimed at run time from eight per-XCD pools
+    // (murr_jit_kernel.hip dyn_claim), so the launch does not end with its
+    // slowest workgroups.  Auto: when the blocks are cut (similar pieces) and
+    // there is one projection round (the pool counters serve one launch).
+    uint32_t dyn_start = 0, dyn_pool = 0;
+    {
+        const uint32_t bal = O.balance;
+        const uint64_t nv = lsegs.size();
+        const bool want = bal >= 2 || (bal == 0 && cut);
+        if (local && want && nv > grid && nv < 0xFFFFFFFFull) {
+            // (rounds is known below; dynamic needs one round)
+            const uint32_t pct = bal >= 10 && bal <= 90 ? bal : 50;
+            uint64_t per = std::max<uint64_t>(1, (nv * pct / 100) / grid);
+            dyn_start = (uint32_t)std::min<uint64_t>(nv, per * grid);
+            dyn_pool = (uint32_t)((nv - dyn_start + 7) / 8);
+            if (!dyn_pool) dyn_start = 0;
+        }
+    }
     bool emit = false;
     for (uint32_t p = 0; p < nproj; p++) emit |= dp[p].is_utf8;
 
@@ -1014,6 +1039,7 @@ int decode_enqueue_jit(murr_ctx* c, const murr_segment_t* seg, const JitLayout* 
     for (uint32_t p = 0; p < nproj; p++) occ[proj[p]].push_back(p);
     uint32_t rounds = 1;
     for (const auto& v : occ) rounds = std::max<uint32_t>(rounds, (uint32_t)v.size());
+    if (rounds > 1) dyn_start = dyn_pool = 0;
     const uint32_t ncols = seg->ncols, npad = (ncols + 1) & ~1u;
 
     std::vector<DecOut> dout((uint64_t)nblocks * nproj);
@@ -1100,11 +1126,14 @@ int decode_enqueue_jit(murr_ctx* c, const murr_segment_t* seg, const JitLayout* 
     h.ulog = cut && nu_layout ? (uint32_t)__builtin_ctzll(stride) : 0;
     h.mode = local ? 0 : 1;
     h.stage = stage;
+    h.dyn_start = dyn_start;
+    h.dyn_pool = dyn_pool;
     if (verbose)
-        std::fprintf(stderr, "decode launch (jit %ux%us%u): %s grid %llu (%d/CU, %d split) blocks %llu tiles %llu segments %llu (%llu tiles) rows/tile %u stage %u lds %u rounds %u\n",
+        std::fprintf(stderr, "decode launch (jit %ux%us%u): %s grid %llu (%d/CU, %d split) blocks %llu tiles %llu segments %llu (%llu tiles) rows/tile %u stage %u lds %u rounds %u dyn %u+8x%u\n",
                      K.nw, K.r, K.nslot, cut ? "local-cut" : local ? "local" : "split", (unsigned long long)grid, bpc, bpc_safe,
                      (unsigned long long)(local ? lsegs.size() : nonempty),
-                     (unsigned long long)tiles, (unsigned long long)nseg, (unsigned long long)seg_tiles, K.tr, stage, lds, rounds);
+                     (unsigned long long)tiles, (unsigned long long)nseg, (unsigned long long)seg_tiles, K.tr, stage, lds, rounds,
+                     dyn_start, dyn_pool);
 #ifdef MURR_TUNING
     c->tl_off = rep ? 0 : d_sink;
     c->tl_n = grid;
@@ -1196,7 +1225,8 @@ int murr_segment_prepare(murr_ctx_t* c, const murr_segment_t* seg) {
         ec[i] = EncCol{nullptr, nullptr, nullptr, 0, col.dtype, col.index, col.offset, col.size};
     }
     if (seg->ncols &&
-        !jit_encode_kernel(c->device, seg->bitset_size, seg->capacity, ec.data(), seg->ncols, 32768, 256, &why)) {
+        !jit_encode_kernel(c->device, seg->bitset_size, seg->capacity, ec.data(), seg->ncols, 32768, 256,
+                           jit_encode_sbw(0, 0, seg->bitset_size + seg->capacity, nutf8_of(seg)), &why)) {
         std::fprintf(stderr, "murr: JIT encode unavailable: %s\n", why.c_str());
         return MURR_E_INTERNAL;
     }
@@ -1843,7 +1873,8 @@ int murr_encode_batch_at(murr_ctx_t* c, const murr_segment_t* seg, const murr_co
             std::string why;
             const uint32_t tile = jit_encode_tile(n, blob_cap);
             ek = jit_encode_kernel(c->device, seg->bitset_size, seg->capacity, ec.data(), seg->ncols,
-                                   jit_encode_stage(n, blob_cap, tile), tile, &why);
+                                   jit_encode_stage(n, blob_cap, tile), tile,
+                                   jit_encode_sbw(n, blob_cap, seg->bitset_size + seg->capacity, nutf8_of(seg)), &why);
             if (!ek && (c->opts.verbose || ek_mode == 1))
                 std::fprintf(stderr, "murr: JIT encode unavailable: %s\n", why.c_str());
             if (!ek && ek_mode == 1) return set_err(err, MURR_E_INTERNAL);
@@ -2250,6 +2281,7 @@ struct HSlot {
     hipEvent_t e4 = nullptr, e5 = nullptr;  // utf8 bytes D2H start / end (D2H stream)
     int submit_status = MURR_OK;  // an enqueue that failed: next() reports it
     murr_error_t submit_err{};
+    bool timed = false;           // this batch's copies are bracketed by timing events
 };
 
 struct murr_hstream {
@@ -2289,7 +2321,8 @@ int hstream_enqueue(murr_hstream* h, HSlot& s, const uint8_t* data, const uint64
         src_off = (const uint64_t*)(s.hin + dbytes);
     }
     uint64_t* doff = (uint64_t*)(s.din + dbytes);
-    HIPC(hipEventRecord(s.e0, h->s_h2d));
+    s.timed = (h->head & 7) == 0;  // every eighth batch carries timing events
+    if (s.timed) HIPC(hipEventRecord(s.e0, h->s_h2d));
     if (head + bytes) HIPC(hipMemcpyAsync(s.din, src_data, head + bytes, hipMemcpyHostToDevice, h->s_h2d));
     HIPC(hipMemcpyAsync(doff, src_off, obytes, hipMemcpyHostToDevice, h->s_h2d));
     HIPC(hipEventRecord(s.e1, h->s_h2d));
@@ -2386,6 +2419,12 @@ int murr_hstream_submit(murr_hstream_t* h, const uint8_t* data, const uint64_t* 
                         uint32_t flags, murr_error_t* err) {
     if (!h || !row_off || (n_rows && !data) || h->head - h->tail >= h->slots.size())
         return set_err(err, MURR_E_ARGUMENT);
+    const auto t0 = std::chrono::steady_clock::now();
+    struct Clock {  // host time of this call, however it returns
+        murr_hstream* h;
+        std::chrono::steady_clock::time_point t0;
+        ~Clock() { h->stats.host_submit_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(); }
+    } clock{h, t0};
     HSlot& s = h->slots[h->head % h->slots.size()];
     s.submit_err = murr_error_t{};
     s.submit_status = hstream_enqueue(h, s, data, row_off, n_rows, (flags & MURR_HSTREAM_PINNED) != 0, &s.submit_err);
@@ -2399,6 +2438,11 @@ int murr_hstream_submit(murr_hstream_t* h, const uint8_t* data, const uint64_t* 
 
 int murr_hstream_next(murr_hstream_t* h, murr_host_array_t* outs, murr_error_t* err) {
     if (!h || !outs || h->tail == h->head) return set_err(err, MURR_E_ARGUMENT);
+    struct Clock {
+        murr_hstream* h;
+        std::chrono::steady_clock::time_point t0;
+        ~Clock() { h->stats.host_next_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(); }
+    } clock{h, std::chrono::steady_clock::now()};
     HSlot& s = h->slots[h->tail % h->slots.size()];
     h->tail++;
     if (s.submit_status) {
@@ -2415,10 +2459,8 @@ int murr_hstream_next(murr_hstream_t* h, murr_host_array_t* outs, murr_error_t* 
     // one copy, then exactly the decoded utf8 bytes
     const HostOut& o = s.out;
     uint64_t ub = 0;
-    HIPC(hipEventRecord(s.e2, h->s_d2h));
+    if (s.timed) HIPC(hipEventRecord(s.e2, h->s_d2h));
     HIPC(hipMemcpyAsync(o.hout, o.dout, s.d2h_bytes, hipMemcpyDeviceToHost, h->s_d2h));
-    HIPC(hipEventRecord(s.e3, h->s_d2h));
-    HIPC(hipEventRecord(s.e4, h->s_d2h));
     for (uint32_t p = 0; p < h->proj.size(); p++) {
         const murr_array_t& a = o.arr[p];
         if (a.offsets && a.data_len) {
@@ -2426,13 +2468,16 @@ int murr_hstream_next(murr_hstream_t* h, murr_host_array_t* outs, murr_error_t* 
             ub += a.data_len;
         }
     }
-    HIPC(hipEventRecord(s.e5, h->s_d2h));
-    HIPC(hipEventSynchronize(s.e5));
-    float ms = 0;
-    if (hipEventElapsedTime(&ms, s.e0, s.e1) == hipSuccess) h->stats.h2d_ms += ms;
-    if (murr_ctx_last_kernel_ms(c, &ms) == MURR_OK) h->stats.kernel_ms += ms;
-    if (hipEventElapsedTime(&ms, s.e2, s.e3) == hipSuccess) h->stats.d2h_ms += ms;
-    if (ub && hipEventElapsedTime(&ms, s.e4, s.e5) == hipSuccess) h->stats.d2h_ms += ms;
+    if (s.timed) HIPC(hipEventRecord(s.e3, h->s_d2h));
+    // (only this batch's copies are on the D2H stream: they are queued here)
+    HIPC(hipStreamSynchronize(h->s_d2h));
+    if (s.timed) {
+        float ms = 0;
+        if (hipEventElapsedTime(&ms, s.e0, s.e1) == hipSuccess) h->stats.h2d_ms += ms;
+        if (murr_ctx_last_kernel_ms(c, &ms) == MURR_OK) h->stats.kernel_ms += ms;
+        if (hipEventElapsedTime(&ms, s.e2, s.e3) == hipSuccess) h->stats.d2h_ms += ms;
+        h->stats.timed_batches++;
+    }
     h->stats.h2d_bytes += s.h2d_bytes;
     h->stats.d2h_bytes += s.d2h_bytes + ub;
     h->stats.batches++;

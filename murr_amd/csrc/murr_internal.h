@@ -23,10 +23,13 @@ constexpr uint32_t kStage = 32768;
 // Default decode stage (bytes of row blobs per tile held in LDS).
 constexpr uint32_t kDecStage = 36864;
 // Workspace head: the error word, then phase-stamp slots of tuning builds
-// (err[2 .. 2 + kStampSlots)), then the per-(block, column) counters.  The
-// last stamp slot, err[17], is the JIT kernel's virtual-block queue.
+// (err[2 .. 2 + kStampSlots)), then the JIT kernel's eight per-XCD virtual-
+// block pool counters (one 64-B line each, err[kPoolWord + 8 x]), then the
+// per-(block, column) counters.  The last stamp slot, err[17], is the JIT
+// kernel's tuning virtual-block queue.
 constexpr uint32_t kStampSlots = 16;
-constexpr uint64_t kErrBytes = 8 * (2 + kStampSlots);
+constexpr uint32_t kPoolWord = 2 + kStampSlots, kPoolStride = 8;
+constexpr uint64_t kErrBytes = 8 * (kPoolWord + 8 * kPoolStride);
 // Projected columns per decode call (10 bits in the packed error key).
 constexpr uint32_t kMaxProj = 1024;
 
@@ -151,8 +154,10 @@ struct JitArgsHead {               // = mj::Args without its trailing slot[] (mu
     uint32_t zero_words, rb_words;
     unsigned int* ticket;          // prepared launches: workgroups finished (in the counter set)
     unsigned long long* rb_host;   // prepared launches: pinned read-back + done flag (last round only)
+    uint32_t dyn_start;            // local mode: (virtual) blocks [0, dyn_start) dealt statically (0 = all)
+    uint32_t dyn_pool;             // ... the rest in 8 per-XCD pools of dyn_pool, claimed at run time
 };
-static_assert(sizeof(JitArgsHead) == 168, "mj::Args layout");
+static_assert(sizeof(JitArgsHead) == 176, "mj::Args layout");
 // The compiled layout (cached; least recently used beyond 64 are retired).
 // pin: the caller will launch from it and calls jit_layout_unpin after the
 // launch is enqueued; until then no eviction unloads its module.
@@ -173,10 +178,14 @@ struct JitEncKernel {
 struct EncCol;
 // stage: LDS bytes of a tile's blobs (jit_encode_stage), a compile-time size.
 uint32_t jit_encode_stage(uint64_t n_rows, uint64_t blob_cap, uint32_t tile);
+// LDS bytes per wave for the encode's string staging (murr_jit_encode.hip
+// MJE_SBW): a wave's 64 rows of string bytes over every utf8 column with
+// headroom, in powers of two from 512 to 4096; 0 without utf8 columns.
+uint32_t jit_encode_sbw(uint64_t n_rows, uint64_t blob_cap, uint32_t fixed, uint32_t nutf8);
 // tile: rows per encode tile (jit_encode_tile: 256).
 uint32_t jit_encode_tile(uint64_t n_rows, uint64_t blob_cap);
 const JitEncKernel* jit_encode_kernel(int device, uint32_t bs, uint32_t cap, const EncCol* cols, uint32_t ncols,
-                                      uint32_t stage, uint32_t tile, std::string* why);
+                                      uint32_t stage, uint32_t tile, uint32_t sbw, std::string* why);
 struct EncodeArgs;
 // inline_sizes: no utf8 column has a validity buffer (the scan computes the
 // tile totals; no sizes pass).

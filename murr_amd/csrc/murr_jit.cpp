@@ -342,13 +342,13 @@ struct EncEntry {
 std::map<std::string, std::unique_ptr<EncEntry>> g_enc;
 
 std::string enc_prelude(uint32_t bs, uint32_t cap, const EncCol* cols, uint32_t ncols, uint32_t stage,
-                        uint32_t tile) {
+                        uint32_t tile, uint32_t sbw) {
     std::ostringstream o;
     uint32_t nutf8 = 0;
     for (uint32_t c = 0; c < ncols; c++) nutf8 += cols[c].dtype == MURR_UTF8;
     o << "#define MJE_BS " << bs << "\n#define MJE_CAP " << cap << "\n#define MJE_NCOLS " << ncols
       << "\n#define MJE_NUTF8 " << nutf8 << "\n#define MJE_STAGE " << stage << "\n#define MJE_TILE " << tile
-      << "\n#define MJE_SCAN_PER " << kEncScanPer
+      << "\n#define MJE_SCAN_PER " << kEncScanPer << "\n#define MJE_SBW " << sbw
       << "\n#define MJE_COLS(X)";
     for (uint32_t c = 0, u = 0; c < ncols; c++) {
         const uint32_t kind = cols[c].dtype == MURR_UTF8 ? 0u : cols[c].dtype == MURR_BOOL ? 9u : cols[c].width;
@@ -388,9 +388,21 @@ uint32_t jit_encode_tile(uint64_t n_rows, uint64_t blob_cap) {
     return 256u;
 }
 
+uint32_t jit_encode_sbw(uint64_t n_rows, uint64_t blob_cap, uint32_t fixed, uint32_t nutf8) {
+    if (!nutf8) return 0;
+#ifdef MURR_TUNING
+    if (const char* e = std::getenv("MURR_ENC_SBW")) return (uint32_t)std::atoi(e);  // A/B (0 = off)
+#endif
+    const double per_row = n_rows ? std::max(0.0, (double)blob_cap / (double)n_rows - fixed - 4.0 * nutf8) : 16.0;
+    const double want = 1.25 * 64.0 * per_row + 16.0 * (nutf8 + 1);
+    uint32_t b = 512;
+    while (b < 4096 && b < want) b *= 2;
+    return b;
+}
+
 const JitEncKernel* jit_encode_kernel(int device, uint32_t bs, uint32_t cap, const EncCol* cols, uint32_t ncols,
-                                      uint32_t stage, uint32_t tile, std::string* why) {
-    const std::string pre = enc_prelude(bs, cap, cols, ncols, stage, tile);
+                                      uint32_t stage, uint32_t tile, uint32_t sbw, std::string* why) {
+    const std::string pre = enc_prelude(bs, cap, cols, ncols, stage, tile, sbw);
     const std::string key = std::to_string(device) + "\n" + pre;
     std::lock_guard<std::mutex> lk(g_mu);
     auto it = g_enc.find(key);

@@ -239,13 +239,41 @@ DEV void write_out(const LAS uint8_t* buf, GAS uint8_t* out, uint64_t g0, uint64
 #define MJE_PF (MJE_BS + MJE_CAP >= 32 && MJE_NUTF8 <= 2 ? 9 : 5)
 #endif
 constexpr uint32_t PF = MJE_PF;  // aligned dwords of each string loaded with the row (the rest later)
+// String staging (MJE_SBW bytes of LDS per wave, 0 = off).  The strings of a
+// wave's 64 rows in one utf8 column are one contiguous range of the Arrow
+// values buffer: the wave copies each column's range into its part of LDS by
+// LDS-DMA (16-B pieces, 1 KiB per wave-instruction) and every lane reads its
+// string from there -- instead of PF scattered dword loads per lane and
+// column, which made the texture data path the encode's bound (DESIGN.md
+// §3.2).  A wave whose ranges do not fit takes the per-lane loads.
+#ifndef MJE_SBW
+#define MJE_SBW 0
+#endif
+#ifndef MJE_STREAM
+#define MJE_STREAM 1
+#endif
+constexpr uint32_t SBW = NUTF8 && MJE_STREAM ? MJE_SBW : 0;
+DEV void glds16(const GAS void* src, LAS void* dst) {
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(src), "s"(__builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)dst))
+                 : "memory");
+}
+// Where a wave's staged strings are: per utf8 column, the LDS byte offset of
+// its range (in the wave's part) and the 16-B aligned global address it starts at.
+struct StrStage {
+    uint32_t base[NUTF8 ? NUTF8 : 1];
+    uint64_t g0[NUTF8 ? NUTF8 : 1];
+    bool on;
+};
 struct RowBuild {
     Row r;
     uint32_t vmask[(NCOLS + 31) / 32 ? (NCOLS + 31) / 32 : 1];  // valid bits, segment order
     uint32_t pos;
     uint32_t ulen[NUTF8 ? NUTF8 : 1];
     uint64_t ustart[NUTF8 ? NUTF8 : 1];  // Arrow data offset of the string
-    uint32_t pre[NUTF8 ? NUTF8 : 1][PF];  // its first PF aligned dwords
+    uint32_t pre[NUTF8 ? NUTF8 : 1][PF];  // its first PF aligned dwords (without string staging)
     int32_t s0[NUTF8 ? NUTF8 : 1], s1[NUTF8 ? NUTF8 : 1];  // its Arrow offsets
     uint32_t x[NCOLS ? NCOLS : 1], xh[NCOLS ? NCOLS : 1];  // fixed-width values as loaded (xh: high dword of 8-byte ones)
 };
@@ -346,7 +374,7 @@ template <uint32_t C, uint32_t KIND, uint32_t SOFF, uint32_t U> DEV void ld_fixe
 // and the tile scan (an aligned dword never crosses a page: bytes around the
 // string are safe to load and masked later).
 template <uint32_t C, uint32_t KIND, uint32_t SOFF, uint32_t U>
-DEV void ld_str(RowBuild& B, uint64_t rw, uint32_t lane, const Bits& bits) {
+DEV void ld_str(RowBuild& B, uint64_t rw, uint32_t lane, const Bits& bits, bool staged) {
     if constexpr (KIND == 0) {
         const Col c = ldcol(C);
         const bool v = valid_of<C>(c, rw, lane, bits);
@@ -354,11 +382,39 @@ DEV void ld_str(RowBuild& B, uint64_t rw, uint32_t lane, const Bits& bits) {
         const uint64_t a = v ? (uint64_t)(int64_t)B.s0[U] : 0u;
         B.ulen[U] = len;
         B.ustart[U] = a;
+        if constexpr (SBW > 0) return;  // (read at emit time: from the wave's LDS copy, or from HBM when it did not fit)
         const uintptr_t sp = (uintptr_t)(gp(c.values) + a);
         const GAS uint32_t* w = (const GAS uint32_t*)(sp & ~(uintptr_t)3);
         const uint32_t nd = v ? (len + (uint32_t)(sp & 3) + 3) / 4 : 0u;
 #pragma unroll
         for (uint32_t i = 0; i < PF; i++) B.pre[U][i] = i < nd ? w[i] : 0u;
+    }
+}
+
+// The wave's string range of utf8 column C (rows rw .. rw + nact - 1, their
+// Arrow offsets already in B.s0 / B.s1) into its LDS part at S.base[U], by
+// LDS-DMA.  `at`: bytes of the part used so far; S.on drops to false when a
+// range does not fit (then no DMA is issued for it or any later column).
+template <uint32_t C, uint32_t KIND, uint32_t SOFF, uint32_t U>
+DEV void stage_col(const RowBuild& B, LAS uint8_t* part, uint32_t nact, uint32_t lane, uint32_t& at, StrStage& S) {
+    if constexpr (KIND == 0 && SBW > 0) {
+        if (!S.on) return;
+        const Col c = ldcol(C);
+        const int32_t first = __builtin_amdgcn_readfirstlane(B.s0[U]);
+        const int32_t last = __builtin_amdgcn_readlane(B.s1[U], nact - 1);
+        const uint64_t g0 = ((uint64_t)(uintptr_t)gp(c.values) + (uint64_t)(int64_t)first) & ~15ull;
+        const uint64_t g1 = ((uint64_t)(uintptr_t)gp(c.values) + (uint64_t)(int64_t)last + 15) & ~15ull;
+        const uint64_t sz = last >= first ? g1 - g0 : ~0ull;
+        if (sz > SBW - at) {
+            S.on = false;
+            return;
+        }
+        S.base[U] = at;
+        S.g0[U] = g0;
+        for (uint32_t q = 0; q * 1024 < sz; q++)
+            if (q * 1024 + lane * 16 < sz)
+                glds16((const GAS uint8_t*)(uintptr_t)g0 + q * 1024 + lane * 16, part + at + q * 1024);
+        at += (uint32_t)sz;
     }
 }
 
@@ -521,7 +577,25 @@ struct Emit {
 #ifndef MJE_ABL_NOOUT  // ablation (tuning): the stage is not written out
 #define MJE_ABL_NOOUT 0
 #endif
-template <uint32_t C, uint32_t U> DEV void emit_payload(const RowBuild& B, Emit& E) {
+// String bytes [0, n) into the emitter from the aligned dwords w[0..] that
+// cover them (sa = the string's offset in w[0]); dwords past the string are
+// never read (they count as 0).
+template <class W> DEV void emit_str(Emit& E, W* w, uint32_t n, uint32_t sa) {
+    uint32_t cur = n ? w[0] : 0u;
+#pragma unroll 1
+    for (uint32_t q = 0; 4 * q < n; q += 4) {
+        uint32_t x[4];
+#pragma unroll
+        for (uint32_t k = 0; k < 4; k++) x[k] = 4 * (q + 1 + k) < n + sa ? w[q + 1 + k] : 0u;
+#pragma unroll
+        for (uint32_t k = 0; k < 4; k++)
+            if (4 * (q + k) < n) E.put(__builtin_amdgcn_alignbyte(x[k], k ? x[k - 1] : cur, sa), umin(4u, n - 4 * (q + k)));
+        cur = x[3];
+    }
+}
+
+template <uint32_t C, uint32_t U>
+DEV void emit_payload(const RowBuild& B, Emit& E, const StrStage& S, const LAS uint8_t* part) {
     if (!((B.vmask[C / 32] >> (C % 32)) & 1)) return;
     const uint32_t n = B.ulen[U];
     E.put(n, 4);
@@ -529,6 +603,16 @@ template <uint32_t C, uint32_t U> DEV void emit_payload(const RowBuild& B, Emit&
     const Col c = ldcol(C);
     const uintptr_t sa_ptr = (uintptr_t)(gp(c.values) + B.ustart[U]);
     const uint32_t sa = (uint32_t)(sa_ptr & 3);
+    if constexpr (SBW > 0) {
+        // the string's aligned dwords from the wave's LDS copy of its range,
+        // or (a wave whose ranges did not fit) from HBM
+        if (S.on) {
+            emit_str(E, (const LAS uint32_t*)(part + S.base[U] + (uint32_t)((uint64_t)(sa_ptr - sa) - S.g0[U])), n, sa);
+        } else {
+            emit_str(E, (const GAS uint32_t*)(sa_ptr - sa), n, sa);
+        }
+        return;
+    }
     const GAS uint32_t* w = (const GAS uint32_t*)(sa_ptr - sa);
     // chunk q = string bytes [4q, 4q + 4) = alignbyte(w[q + 1], w[q], sa)
 #pragma unroll
@@ -557,6 +641,7 @@ template <uint32_t C, uint32_t U> DEV void emit_payload(const RowBuild& B, Emit&
 extern "C" __global__ void __launch_bounds__(MJE_TILE) MJE_WPE_ATTR murr_jit_encode(mje::Args) {
     using namespace mje;
     __shared__ __attribute__((aligned(16))) uint32_t stage[STAGE / 4 + 8];
+    __shared__ __attribute__((aligned(16))) uint8_t sstr[SBW ? NWAVE * SBW : 16];
     __shared__ uint64_t s_w[8];
     LAS uint32_t* stw = (LAS uint32_t*)stage;
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -583,10 +668,22 @@ extern "C" __global__ void __launch_bounds__(MJE_TILE) MJE_WPE_ATTR murr_jit_enc
         MJE_COLS(MJE_DO_OFFS)
 #undef MJE_DO_OFFS
         const Bits bits = load_bits(rw, lane);
+        // the wave's string ranges into LDS (issued before the fixed-width
+        // loads, so the compiler's counted waits for those cover them too)
+        StrStage S;
+        LAS uint8_t* part = (LAS uint8_t*)sstr + (SBW ? wave * SBW : 0u);
+        S.on = SBW > 0 && rw < n_rows;
+        if (SBW > 0 && S.on) {
+            const uint32_t nact = (uint32_t)min((uint64_t)64, n_rows - rw);
+            uint32_t at = 0;
+#define MJE_DO_STAGE(C, KIND, SOFF, U) stage_col<C, KIND, SOFF, U>(B, part, nact, lane, at, S);
+            MJE_COLS(MJE_DO_STAGE)
+#undef MJE_DO_STAGE
+        }
 #define MJE_DO_FIXED(C, KIND, SOFF, U) ld_fixed<C, KIND, SOFF, U>(B, row);
         MJE_COLS(MJE_DO_FIXED)
 #undef MJE_DO_FIXED
-#define MJE_DO_STR(C, KIND, SOFF, U) ld_str<C, KIND, SOFF, U>(B, rw, lane, bits);
+#define MJE_DO_STR(C, KIND, SOFF, U) ld_str<C, KIND, SOFF, U>(B, rw, lane, bits, S.on);
         MJE_COLS(MJE_DO_STR)
 #undef MJE_DO_STR
 #define MJE_DO_PUT(C, KIND, SOFF, U) put_col<C, KIND, SOFF, U>(B, rw, lane, bits);
@@ -633,12 +730,13 @@ extern "C" __global__ void __launch_bounds__(MJE_TILE) MJE_WPE_ATTR murr_jit_enc
                 __syncthreads();
             }
 #if MJE_STREAM
+            if (SBW > 0 && S.on) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the wave's string DMA landed
             if (active && NUTF8) {
                 Emit E;
                 E.start(stw, (uint32_t)(start - tstart));
 #pragma unroll
                 for (uint32_t k = 0; k < NR; k++) E.put(B.r.w[k], k + 1 < NR ? 4u : FIXED - 4 * (NR - 1));
-#define MJE_DO_EMIT(C, KIND, SOFF, U) if (KIND == 0) emit_payload<C, U>(B, E);
+#define MJE_DO_EMIT(C, KIND, SOFF, U) if (KIND == 0) emit_payload<C, U>(B, E, S, part);
                 MJE_COLS(MJE_DO_EMIT)
 #undef MJE_DO_EMIT
                 E.finish();

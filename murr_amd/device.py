@@ -74,16 +74,19 @@ class Context:
             self.set_opts(**_default_opts)
 
     def set_opts(self, kernel="auto", mode="auto", shape=None, seg_tiles=0, vrows=0, lds_budget=0, stage=0,
-                 encode_kernel="auto", verbose=0, grid=0):
+                 encode_kernel="auto", verbose=0, grid=0, balance=0):
         """murr_ctx_set_opts: kernel selection for this context (all defaults =
         the library's own choice).  kernel / encode_kernel: auto|jit|generic;
         mode: auto|local|split|cut; shape: (waves, chunks) e.g. (5, 3);
-        grid: local-mode workgroups (0 auto, -1 one per virtual block)."""
+        grid: local-mode workgroups (0 auto, -1 one per virtual block);
+        balance: 0 auto, 1 static deal, 2 dynamic per-XCD tail, 10..90 dynamic
+        with that percentage dealt statically."""
         o = _abi.Opts()
         o.kernel, o.mode, o.encode_kernel = KERNELS[kernel], MODES[mode], KERNELS[encode_kernel]
         o.shape_nw, o.shape_r = shape if shape else (0, 0)
         o.seg_tiles, o.vrows, o.lds_budget, o.stage, o.verbose = seg_tiles, vrows, lds_budget, stage, int(verbose)
         o.grid = grid & 0xFFFFFFFF
+        o.balance = balance
         raise_status(self.L.murr_ctx_set_opts(self.h, C.byref(o)), what="murr_ctx_set_opts")
         self.opts_gen = getattr(self, "opts_gen", 0) + 1  # plan caches key on it (no library call per read)
 

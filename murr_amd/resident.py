@@ -156,9 +156,11 @@ def _key_array(keys) -> pa.Array:
 # the rows up and size the block exactly (one 8-byte read-back), then copy.
 TWO_PHASE_BYTES = 64 << 20
 # utf8 index stride of the resident arena (murr_utf8_index_update): every
-# UIDX_STRIDE rows, each utf8 column's string bytes so far (0.016 B per row
-# and column), so a whole-table scan decodes on the whole GPU in one pass.
-UIDX_STRIDE = 512
+# UIDX_STRIDE rows, each utf8 column's string bytes so far (0.0625 B per row
+# and column), so a whole-table scan decodes on the whole GPU in one pass, cut
+# into one-tile virtual blocks that the workgroups claim as they go (the
+# decode's dynamic tail).
+UIDX_STRIDE = 128
 
 
 class ResidentTable:
