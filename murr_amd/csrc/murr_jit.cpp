@@ -272,7 +272,7 @@ uint32_t jit_lds_bytes(uint32_t nw, uint32_t r, uint32_t nslot, uint32_t stage, 
     const uint32_t ro = ((tr + 1) * 4 + 16 + 15) & ~15u;
 #endif
     const uint32_t nu = std::max<uint32_t>(nutf8, 1);
-    return nslot * (ro + stage + 64) + 128 + 256 + 16 + 8 * nu + ((4 * nu * (nw - 1) + 15) & ~15u) + 1024;
+    return nslot * (ro + stage + 64) + 128 + 256 + 32 + 8 * nu + ((8 * nu * (nw - 1) + 15) & ~15u) + 1024;
 }
 
 const JitLayout* jit_layout(int device, const murr_segment_t* seg, std::string* why, bool pin) {
@@ -388,10 +388,18 @@ uint32_t jit_encode_tile(uint64_t n_rows, uint64_t blob_cap) {
     return 256u;
 }
 
+// Off in release builds: staging the strings measured slower than the
+// per-lane prefetch (config C columns 1.24 vs 1.04 ms, B 0.248 vs 0.231 ms;
+// profiles/r04/probes): the LDS round trips at emit time cost more than the
+// scattered loads they replace.  Tuning builds: MURR_ENC_SBW=auto|bytes.
 uint32_t jit_encode_sbw(uint64_t n_rows, uint64_t blob_cap, uint32_t fixed, uint32_t nutf8) {
     if (!nutf8) return 0;
 #ifdef MURR_TUNING
-    if (const char* e = std::getenv("MURR_ENC_SBW")) return (uint32_t)std::atoi(e);  // A/B (0 = off)
+    const char* e = std::getenv("MURR_ENC_SBW");
+    if (!e) return 0;
+    if (std::strcmp(e, "auto")) return (uint32_t)std::atoi(e);
+#else
+    return 0;
 #endif
     const double per_row = n_rows ? std::max(0.0, (double)blob_cap / (double)n_rows - fixed - 4.0 * nutf8) : 16.0;
     const double want = 1.25 * 64.0 * per_row + 16.0 * (nutf8 + 1);

@@ -340,6 +340,11 @@ DEV void wait_vmcnt(uint32_t n) {
 #ifndef MJ_RO64
 #define MJ_RO64 0
 #endif
+// Early release of ring slots in local mode (decode_tile, kernel_body); 0 =
+// one workgroup barrier per tile (tuning A/B).
+#ifndef MJ_ER
+#define MJ_ER 1
+#endif
 constexpr uint32_t RO_STRIDE = MJ_RO64 ? 2 : 1;  // dwords per row offset in LDS
 
 // ---- shape ---------------------------------------------------------------------
@@ -351,9 +356,11 @@ struct Shape {
     // ring slots: 2 (one tile in flight while one decodes) or 3 (two in flight)
     static constexpr uint32_t NSLOT = NSLOT_;
     static_assert(NSLOT == 2 || NSLOT == 3, "ring of 2 or 3 slots");
-    // after the slots: span ring [8][16 B] | tile ring [8][32 B] | counters |
-    // tile prefixes [NU] u64 | wave totals [NU][NC] u32 | prefetch scratch 1 KiB
-    static constexpr uint32_t SPAN_B = 128, INFO_B = 256, CNT_B = 16, PF_B = 1024;
+    // after the slots: span ring [8][16 B] | tile ring [8][32 B] | counters
+    // (8 words: wave totals published, segment prefix ready, epilogue count,
+    // -, slot landed [2], slot released [2]) | tile prefixes [NU] u64 | wave
+    // totals [2 (tile parity)][NU][NC] u32 | prefetch scratch 1 KiB
+    static constexpr uint32_t SPAN_B = 128, INFO_B = 256, CNT_B = 32, PF_B = 1024;
     DEV static uint32_t slot_bytes(uint32_t stage) { return RO_BYTES + stage + 64; }
 };
 
@@ -1054,9 +1061,42 @@ DEV uint64_t look_back(uint64_t t, uint64_t t0, uint32_t u, uint32_t lane, uint6
 // ---- one tile of one decode wave ---------------------------------------------------
 // PH 0: everything (local mode); 1: first pass of a split segment (fixed
 // columns, validity, utf8 lengths); 2: second pass (utf8 offsets and bytes).
-template <class SH, uint32_t PH, class Src>
+// Early release (ER, local mode): the ring slot is handed back (`rel`, an LDS
+// counter the loader polls) as soon as this wave holds in registers all it
+// still needs of the tile -- its row windows, and each utf8 cell's string
+// bytes when the cell is at most 8 bytes, with their OR for the UTF-8 check --
+// so the loader refills the slot while the wave computes and stores.  A wave
+// that would still read the slot (a longer string, a byte >= 0x80 to check,
+// a malformed row, a layout whose fields are not all in the window) hands it
+// back at the end of the tile instead.
+DEV void release_slot(LAS uint32_t* rel, uint32_t lane) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of the slot have returned
+    if (lane == 0) __hip_atomic_fetch_add(rel, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// The n <= 8 case of copy_str from the string's three aligned dwords in registers.
+DEV void copy_str_regs(GAS uint8_t* vb, uint32_t w0, uint32_t w1, uint32_t w2, uint32_t sh, uint32_t n) {
+    const uint32_t head = __builtin_amdgcn_alignbyte(w1, w0, sh);
+    if (n >= 4) {
+        *(GAS u32u*)vb = head;
+        *(GAS u32u*)(vb + n - 4) = pick(w0, w1, w2, sh + n - 4);
+    } else if (n >= 2) {
+        *(GAS u16u*)vb = (uint16_t)head;
+        *(GAS u16u*)(vb + n - 2) = (uint16_t)(pick(w0, w1, w2, sh + n - 2) & 0xFFFFu);
+    } else if (n == 1) {
+        *vb = (uint8_t)head;
+    }
+}
+// OR of a string's bytes (n <= 8) from its three aligned dwords (copy_str's return value).
+DEV uint32_t hib_regs(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t sh, uint32_t n) {
+    const uint32_t head = __builtin_amdgcn_alignbyte(w1, w0, sh);
+    if (n >= 4) return head | pick(w0, w1, w2, sh + n - 4);
+    if (n >= 2) return (head & 0xFFFFu) | (pick(w0, w1, w2, sh + n - 2) & 0xFFFFu);
+    return n == 1 ? head & 0xFFu : 0u;
+}
+
+template <class SH, uint32_t PH, class Src, bool ER = false>
 DEV void decode_tile(const Src& src, const Tile& T, const LAS uint32_t* ro, LAS uint8_t* ctl, uint64_t (&run)[NU],
-                     Lanes& L, uint32_t wave, uint32_t lane, uint32_t it) {
+                     Lanes& L, uint32_t wave, uint32_t lane, uint32_t it, LAS uint32_t* rel = nullptr) {
     constexpr uint32_t R = SH::R, NC = SH::NC;
     unsigned long long* err = args()->err;
     const uint32_t rbase = wave * 64 * R;
@@ -1065,7 +1105,11 @@ DEV void decode_tile(const Src& src, const Tile& T, const LAS uint32_t* ro, LAS 
     LAS uint32_t* pcnt = (LAS uint32_t*)ctl;         // wave totals published (monotone)
     LAS uint32_t* pready = (LAS uint32_t*)ctl + 1;   // segments whose prefix is in tpre (split mode)
     LAS uint64_t* tpre = (LAS uint64_t*)(ctl + SH::CNT_B);
-    LAS uint32_t* wt = (LAS uint32_t*)(ctl + SH::CNT_B + 8 * NU);
+    // wave totals of this tile: one buffer per tile parity (with early
+    // release a wave may publish tile it+1's totals while another still reads
+    // tile it's; it cannot get further ahead, since tile it+1's prefix wait
+    // needs every wave's tile it+1 totals)
+    LAS uint32_t* wt = (LAS uint32_t*)(ctl + SH::CNT_B + 8 * NU) + (it & 1) * NU * NC;
     lanes_block(L, T.b, lane);
 #if MJ_HOIST
     // the projection's slot words, once per tile (one batched scalar load;
@@ -1153,6 +1197,43 @@ DEV void decode_tile(const Src& src, const Tile& T, const LAS uint32_t* ro, LAS 
     MJ_COLS(MJ_U)
 #undef MJ_U
 
+    // early release: strings of <= 8 bytes into registers, then the slot back
+    constexpr bool ERS = ER && PH == 0 && !Src::kHbm;  // (a tile decoded from HBM: its slot held only offsets)
+    uint32_t sw[NU][R][3], shib[NU][R];
+    bool late = false;
+    if constexpr (ER && PH == 0) {
+        if constexpr (Src::kHbm) {
+            release_slot(rel, lane);
+        } else {
+            bool lng = false;
+            uint32_t hi = 0;
+#pragma unroll
+            for (uint32_t u = 0; u < NU; u++)
+#pragma unroll
+                for (uint32_t k = 0; k < R; k++) sw[u][k][0] = sw[u][k][1] = sw[u][k][2] = shib[u][k] = 0;
+#define MJ_P(C, W_, FO, U)                                                                              \
+            if constexpr (W_ == 0) {                                                                    \
+                if (MJ_SLOT(C) != kNone) {                                                              \
+                    _Pragma("unroll") for (uint32_t k = 0; k < R; k++) {                                \
+                        const uint32_t n = ulen[U][k], pay = upay[U][k];                                \
+                        if (n > 8) lng = true;                                                          \
+                        if (n && n <= 8) {                                                              \
+                            src.win3(pay, sw[U][k][0], sw[U][k][1], sw[U][k][2]);                       \
+                            shib[U][k] = hib_regs(sw[U][k][0], sw[U][k][1], sw[U][k][2], pay & 3u, n);  \
+                            hi |= shib[U][k];                                                           \
+                        }                                                                               \
+                    }                                                                                   \
+                }                                                                                       \
+            }
+            MJ_COLS(MJ_P)
+#undef MJ_P
+            late = !WIN || __ballot(lng || (hi & 0x80808080u) || badk || partial) != 0;
+            if (!late) release_slot(rel, lane);
+        }
+    }
+    (void)sw;
+    (void)shib;
+
     // wave totals -> LDS; the tile total and every wave's prefix follow
     if (NUTF8) {
         if (lane == 0) {
@@ -1213,7 +1294,10 @@ DEV void decode_tile(const Src& src, const Tile& T, const LAS uint32_t* ro, LAS 
             report_row(src, W.ra[k], W.rl[k], T.b, T.r0 + i, err);
         }
     }
-    if (!NUTF8) return;
+    if (!NUTF8) {
+        if (ERS && late) release_slot(rel, lane);
+        return;
+    }
 
     // ---- the tile's utf8 prefix
     {
@@ -1303,18 +1387,27 @@ DEV void decode_tile(const Src& src, const Tile& T, const LAS uint32_t* ro, LAS 
                 const uint64_t e = base + uinc[U][k];                                                   \
                 const uint64_t cend = base + (uint32_t)__builtin_amdgcn_readlane(uinc[U][k], 63);                 \
                 uint32_t hib = 0;                                                                       \
+                const bool regs = ERS && !late; /* the bytes are in sw (the slot is gone) */            \
                 if (cend <= 0x7FFFFFFFull && cend <= o.values_cap) { /* wave-uniform fast path */       \
                     if (act) ost(obf + i, (int32_t)e);                                                  \
-                    if (n && !MJ_ABL_NOSTR) hib = copy_str(src, gp(o.values) + (e - n), upay[U][k], n); \
+                    if (regs) {                                                                         \
+                        if (n && !MJ_ABL_NOSTR)                                                         \
+                            copy_str_regs(gp(o.values) + (e - n), sw[U][k][0], sw[U][k][1], sw[U][k][2], \
+                                          upay[U][k] & 3u, n);                                          \
+                        hib = shib[U][k];                                                               \
+                    } else if (n && !MJ_ABL_NOSTR) {                                                    \
+                        hib = copy_str(src, gp(o.values) + (e - n), upay[U][k], n);                     \
+                    }                                                                                   \
                 } else {                                                                                \
                     if (act) {                                                                          \
                         if (e > 0x7FFFFFFFull) report(err, err_key(T.b, T.r0 + i, P, kStOverflow));     \
                         else obf[i] = (int32_t)e;                                                       \
                         if (n && e > o.values_cap) report(err, err_key(T.b, T.r0 + i, P, kStCapacity)); \
                     }                                                                                   \
-                    for (uint32_t q = 0; q < n; q++) hib |= src.u8(upay[U][k] + q);                     \
+                    if (regs) hib = shib[U][k];                                                         \
+                    else for (uint32_t q = 0; q < n; q++) hib |= src.u8(upay[U][k] + q);                \
                 }                                                                                       \
-                if ((hib & 0x80808080u) && !utf8_valid_slow(src, upay[U][k], n))                        \
+                if ((hib & 0x80808080u) && !utf8_valid_slow(src, upay[U][k], n)) /* (never when regs) */ \
                     report(err, err_key(T.b, T.r0 + i, P, kStUtf8));                                    \
             }                                                                                           \
         }                                                                                               \
@@ -1322,6 +1415,7 @@ DEV void decode_tile(const Src& src, const Tile& T, const LAS uint32_t* ro, LAS 
     MJ_COLS(MJ_E)
 #undef MJ_E
 #undef MJ_SLOT
+    if (ERS && late) release_slot(rel, lane);
 }
 
 // ---- read-back epilogue (prepared launches) ---------------------------------------
@@ -1385,8 +1479,13 @@ DEV void kernel_body() {
     LAS uint8_t* spans = lds + NSLOT * SLOT;
     LAS uint8_t* infos = spans + SH::SPAN_B;
     LAS uint8_t* ctl = infos + SH::INFO_B;
-    LAS uint8_t* pf = ctl + SH::CNT_B + 8 * NU + ((4 * NU * NC + 15) & ~15u);
-    if (threadIdx.x < 3) ((LAS uint32_t*)ctl)[threadIdx.x] = 0;
+    LAS uint8_t* pf = ctl + SH::CNT_B + 8 * NU + ((8 * NU * NC + 15) & ~15u);
+    if (threadIdx.x < 8) ((LAS uint32_t*)ctl)[threadIdx.x] = 0;
+    // early release (local mode): slots handed over by LDS counters instead of
+    // a workgroup barrier per tile
+    constexpr bool ER = MODE == 0 && MJ_ER && NSLOT == 2;
+    LAS uint32_t* full = (LAS uint32_t*)ctl + 4;  // [2]: number + 1 of the tile landed in slot s
+    LAS uint32_t* freec = full + 2;               // [2]: decode-wave releases of slot s (cumulative)
     // A prepared launch (murr_decode_run) alternates two counter sets: this
     // launch counts into one and zeroes the other for the next run, so a run
     // needs no memset of its own.
@@ -1413,6 +1512,58 @@ DEV void kernel_body() {
         uint64_t lwait = 0, lvm = 0;  // loader waits: all / the vmcnt part (slot 10)
 #endif
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        if constexpr (ER) {
+            // Up to two tiles in flight: tile t goes into slot t % 2 once every
+            // decode wave has released tile t - 2 from it (freec), lands, and
+            // is published (full).  Between those steps the loader waits only
+            // on its own counted vmcnt and polls one LDS word, never on a
+            // barrier, so a slot is refilled while the decode waves are still
+            // computing and storing the tile it held.
+            lds_barrier();  // B_0: counters zeroed, tiles 0 .. 3 announced
+            uint32_t ti = 0, tl = 0;        // next tile to DMA / to land
+            uint32_t ops[2] = {0, 0}, ann[2] = {0, 0};  // vmem ops issued with tile j % 2: all, its announce part
+            uint32_t claim_t = ~0u;         // tile before whose DMA the claim in flight was issued
+            Wait w;
+            for (;;) {
+                const bool more = tile_valid(infos + (ti & 7) * 32);
+                bool can = more && ti < tl + 2;
+                if (can && ti >= 2)
+                    can = __hip_atomic_load(freec + (ti & 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= NC * (ti >> 1);
+                if (can) {
+                    if (!cl.pend) {
+                        claim_pump(cl, cs.k);
+                        if (cl.pend) claim_t = ti;
+                    }
+                    const uint32_t nd = tile_dma<TR, SH::RO_BYTES>(
+                        tile_read_ptrs(spans + (ti & 7) * 16, infos + (ti & 7) * 32, stage), lds + (ti & 1) * SLOT, lane);
+                    const uint32_t k = ti + NSLOT + 2;
+                    const uint32_t na = tile_announce<TR>(cs, spans + (k & 7) * 16, infos + (k & 7) * 32, lane,
+                                                          pf + (k & 7) * 8 * NU);
+                    cs = cur_next<TR>(cs, cl);
+                    ops[ti & 1] = nd + na;
+                    ann[ti & 1] = na;
+                    ti++;
+                    w = Wait{};
+                    continue;
+                }
+                if (tl < ti) {
+                    // tile tl's DMA: its announce and the later tile's ops are younger
+                    wait_vmcnt(ann[tl & 1] + (ti - tl == 2 ? ops[(tl + 1) & 1] : 0u));
+                    if (cl.pend && claim_t <= tl) cl.ready = 1;
+                    __hip_atomic_store(full + (tl & 1), tl + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    tl++;
+                    w = Wait{};
+                    continue;
+                }
+                if (!more) {  // the end: the decode waves see tile ti invalid and leave
+                    __hip_atomic_store(full + (ti & 1), ti + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    break;
+                }
+                if (w.expired(0, ti)) break;  // (bounded: the decode waves stopped releasing)
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            return;
+        }
         // tiles 0 .. NSLOT - 2 into their slots; B_0 once tile 0 landed
         uint32_t after0 = 0;  // ops issued after tile 0's DMA
 #pragma unroll
@@ -1493,6 +1644,13 @@ DEV void kernel_body() {
     const uint64_t tl_b0 = __builtin_amdgcn_s_memrealtime();
 #endif
     for (uint32_t it = 0;; it++) {
+        if constexpr (ER) {  // tile it landed in its slot (or the loader says there is none)
+            Wait w;
+            bool gone = false;
+            while (__hip_atomic_load(full + (it & 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < it + 1)
+                if (w.expired(0, it)) { gone = true; break; }
+            if (gone) break;
+        }
         const LAS uint8_t* info = infos + (it & 7) * 32;
         if (!tile_valid(info)) break;
 #ifdef MJ_TIMELINE
@@ -1518,6 +1676,7 @@ DEV void kernel_body() {
         }
         if (T.hbm == 2) {  // a tile over 4 GiB of blob bytes (unsupported): report; keep the protocol going
             if (wave == 0 && lane == 0) report(args()->err, err_key(T.b, T.r0, 0, kStMalformed));
+            if constexpr (ER) release_slot(freec + (it & 1), lane);
             if (NUTF8) {
                 if (lane == 0) __hip_atomic_fetch_add((LAS uint32_t*)ctl, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 if (MODE == 1 && ph == 1 && T.seg_last && wave == 0 && args()->emit) {
@@ -1530,7 +1689,7 @@ DEV void kernel_body() {
             Tile Th = T;
             tile_ptrs(Th);
             const HbmSrc src{gp(Th.data) + Th.abase};
-            if (MODE == 0) decode_tile<SH, 0>(src, T, ro, ctl, run, L, wave, lane, it);
+            if (MODE == 0) decode_tile<SH, 0, HbmSrc, ER>(src, T, ro, ctl, run, L, wave, lane, it, freec + (it & 1));
             else if (ph == 1) decode_tile<SH, 1>(src, T, ro, ctl, run, L, wave, lane, it);
             else decode_tile<SH, 2>(src, T, ro, ctl, run, L, wave, lane, it);
             // drain the cold path's loads here (a compiler-visible vmcnt(0)),
@@ -1539,12 +1698,12 @@ DEV void kernel_body() {
         } else {
             const StageSrc src{slot + SH::RO_BYTES};
             MJ_TIC
-            if (MODE == 0) decode_tile<SH, 0>(src, T, ro, ctl, run, L, wave, lane, it);
+            if (MODE == 0) decode_tile<SH, 0, StageSrc, ER>(src, T, ro, ctl, run, L, wave, lane, it, freec + (it & 1));
             else if (ph == 1) decode_tile<SH, 1>(src, T, ro, ctl, run, L, wave, lane, it);
             else decode_tile<SH, 2>(src, T, ro, ctl, run, L, wave, lane, it);
             MJ_TOC(ph == 0 ? 6 : ph == 1 ? 4 : 5)
         }
-        {
+        if constexpr (!ER) {
             MJ_TIC
             lds_barrier();  // B_it+1
             MJ_TOC(0)

@@ -16,6 +16,14 @@
         }                                                                                  \
     } while (0)
 
+// a kernel that copies device memory into pinned host memory (or host to
+// device) with 16-B coalesced accesses: zero-copy over PCIe, no DMA engine
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+__global__ void kcopy(const u32x4* __restrict__ src, u32x4* __restrict__ dst, size_t n) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+        dst[i] = src[i];
+}
+
 int main() {
     const size_t maxb = 64ull << 20;
     void *h1, *h2, *d1, *d2;
@@ -57,6 +65,29 @@ int main() {
                     sz >> 10, gb / (x.first * 1e-3), gb / (y.second * 1e-3), gb / (z.first * 1e-3), gb / (z.second * 1e-3),
                     x.first * 1e3 / reps, y.second * 1e3 / reps);
         std::fflush(stdout);
+    }
+    // kernel copies over PCIe (device -> pinned host, pinned host -> device)
+    for (size_t sz : {256ull << 10, 2730ull << 10, 8ull << 20, 64ull << 20}) {
+        const size_t n = sz / 16;
+        for (int dir = 0; dir < 2; dir++) {
+            for (unsigned grid : {64u, 256u, 1024u}) {
+                const u32x4* src = (const u32x4*)(dir ? h1 : d1);
+                u32x4* dst = (u32x4*)(dir ? d2 : h2);
+                kcopy<<<grid, 256, 0, a>>>(src, dst, n);
+                CK(hipStreamSynchronize(a));
+                const int reps = sz < (4u << 20) ? 100 : 10;
+                CK(hipEventRecord(e0, a));
+                for (int r = 0; r < reps; r++) kcopy<<<grid, 256, 0, a>>>(src, dst, n);
+                CK(hipEventRecord(e1, a));
+                CK(hipEventSynchronize(e1));
+                float t = 0;
+                CK(hipEventElapsedTime(&t, e0, e1));
+                std::printf("%8zu KiB kernel copy %s grid %5u: %6.1f GB/s (%.1f us per copy)\n", sz >> 10,
+                            dir ? "pinned host -> device" : "device -> pinned host", grid,
+                            (double)sz * reps / 1e9 / (t * 1e-3), t * 1e3 / reps);
+                std::fflush(stdout);
+            }
+        }
     }
     return 0;
 }
