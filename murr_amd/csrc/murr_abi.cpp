@@ -928,16 +928,40 @@ int decode_enqueue_jit(murr_ctx* c, const murr_segment_t* seg, const JitLayout* 
     // grid also respects a worst-case register bound: 106 SGPRs allow 6 waves
     // per SIMD (MI355X_MICROARCH.md, residency), the VGPR count allows
     // 512 / alloc, and a 5-wave workgroup may put 2 waves on one SIMD.
+    // (the occupancy and register queries are cached per kernel and LDS size:
+    // each is a runtime call that costs microseconds on every launch)
     auto occupancy = [&](hipFunction_t fn) {
+        static std::mutex mu;
+        static std::map<std::pair<hipFunction_t, uint32_t>, int> cache;
         int n = 0;
-        if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, 64 * K.nw, lds) != hipSuccess || n < 1) n = 1;
+        {
+            std::lock_guard<std::mutex> g(mu);
+            auto it = cache.find({fn, lds});
+            if (it != cache.end()) n = it->second;
+        }
+        if (!n) {
+            if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, 64 * K.nw, lds) != hipSuccess || n < 1) n = 1;
+            std::lock_guard<std::mutex> g(mu);
+            cache[{fn, lds}] = n;
+        }
         return std::min<int>(n, std::max<int>(1, (int)(163840 / std::max<uint32_t>(lds, 1))));
     };
     const int bpc = occupancy(K.fn);
     int bpc_safe = occupancy(K.fn_split);
     {
+        static std::mutex mu;
+        static std::map<hipFunction_t, int> regs;
         int vgprs = 0;
-        if (hipFuncGetAttribute(&vgprs, HIP_FUNC_ATTRIBUTE_NUM_REGS, K.fn_split) != hipSuccess || vgprs < 1) vgprs = 128;
+        {
+            std::lock_guard<std::mutex> g(mu);
+            auto it = regs.find(K.fn_split);
+            if (it != regs.end()) vgprs = it->second;
+        }
+        if (!vgprs) {
+            if (hipFuncGetAttribute(&vgprs, HIP_FUNC_ATTRIBUTE_NUM_REGS, K.fn_split) != hipSuccess || vgprs < 1) vgprs = 128;
+            std::lock_guard<std::mutex> g(mu);
+            regs[K.fn_split] = vgprs;
+        }
         const int alloc = (vgprs + 7) / 8 * 8;
         const int per_simd = std::min(std::min(8, 512 / alloc), 6);
         const int waves_per_simd_per_wg = (int)(K.nw + 3) / 4;
@@ -2282,6 +2306,8 @@ struct HSlot {
     int submit_status = MURR_OK;  // an enqueue that failed: next() reports it
     murr_error_t submit_err{};
     bool timed = false;           // this batch's copies are bracketed by timing events
+    bool drained = false;         // decode waited for, counters read, D2H queued (or its error kept)
+    uint64_t ub = 0;              // utf8 bytes of its D2H
 };
 
 struct murr_hstream {
@@ -2371,9 +2397,61 @@ int hstream_enqueue(murr_hstream* h, HSlot& s, const uint8_t* data, const uint64
     }
     const int st = murr_decode_enqueue(c, &h->seg, h->proj.data(), np, &blk, 1, o.arr.data());
     if (st) return set_err(err, st, st == MURR_E_HIP ? (int)hipGetLastError() : 0);
-    s.d2h_bytes = fixed_out;  // (the fixed-size part, copied in next() with the utf8 bytes)
+    HIPC(hipEventRecord(s.ed, c->stream));  // the decode and its counters' read-back are done
+    s.d2h_bytes = fixed_out;  // (the fixed-size part, queued with the utf8 bytes once the counters are in)
     s.n = n;
+    s.drained = false;
     return MURR_OK;
+}
+
+// Batch s's decode is done: read its counters (null counts, utf8 bytes,
+// errors) and queue its D2H on the D2H stream -- the fixed-size arrays in one
+// copy, then exactly the decoded utf8 bytes -- closed by event e3.  An error
+// is kept for next() (the slot then has nothing to copy).
+void hstream_drain(murr_hstream* h, HSlot& s) {
+    if (s.drained) return;
+    s.drained = true;
+    if (s.submit_status) return;
+    murr_error_t e{};
+    const int st = murr_decode_wait(s.c, &e);
+    if (st) {
+        s.submit_status = st;
+        s.submit_err = e;
+        return;
+    }
+    const HostOut& o = s.out;
+    bool ok = true;
+    if (s.timed) ok = ok && hipEventRecord(s.e2, h->s_d2h) == hipSuccess;
+    ok = ok && hipMemcpyAsync(o.hout, o.dout, s.d2h_bytes, hipMemcpyDeviceToHost, h->s_d2h) == hipSuccess;
+    s.ub = 0;
+    for (uint32_t p = 0; ok && p < h->proj.size(); p++) {
+        const murr_array_t& a = o.arr[p];
+        if (a.offsets && a.data_len) {
+            ok = hipMemcpyAsync(o.hout + o.off[3 * p], a.values, a.data_len, hipMemcpyDeviceToHost, h->s_d2h) == hipSuccess;
+            s.ub += a.data_len;
+        }
+    }
+    ok = ok && hipEventRecord(s.e3, h->s_d2h) == hipSuccess;
+    if (!ok) {
+        s.submit_status = MURR_E_HIP;
+        s.submit_err = murr_error_t{};
+        s.submit_err.status = MURR_E_HIP;
+        s.submit_err.hip_error = (int)hipGetLastError();
+    }
+}
+
+// Queue the D2H of every batch, oldest first, whose decode has finished (no
+// wait): next() then finds its copy under way or done.
+void hstream_progress(murr_hstream* h) {
+    for (uint64_t j = h->tail; j < h->head; j++) {
+        HSlot& s = h->slots[j % h->slots.size()];
+        if (s.drained) continue;
+        if (!s.submit_status) {
+            (void)hipSetDevice(s.c->device);
+            if (hipEventQuery(s.ed) != hipSuccess) break;  // (in order: a later batch waits for this one)
+        }
+        hstream_drain(h, s);
+    }
 }
 
 }  // namespace
@@ -2425,6 +2503,7 @@ int murr_hstream_submit(murr_hstream_t* h, const uint8_t* data, const uint64_t* 
         std::chrono::steady_clock::time_point t0;
         ~Clock() { h->stats.host_submit_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(); }
     } clock{h, t0};
+    hstream_progress(h);  // D2H of the batches whose decode finished, queued early
     HSlot& s = h->slots[h->head % h->slots.size()];
     s.submit_err = murr_error_t{};
     s.submit_status = hstream_enqueue(h, s, data, row_off, n_rows, (flags & MURR_HSTREAM_PINNED) != 0, &s.submit_err);
@@ -2444,33 +2523,18 @@ int murr_hstream_next(murr_hstream_t* h, murr_host_array_t* outs, murr_error_t* 
         ~Clock() { h->stats.host_next_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(); }
     } clock{h, std::chrono::steady_clock::now()};
     HSlot& s = h->slots[h->tail % h->slots.size()];
+    hstream_drain(h, s);  // (waits for its decode if it is still running)
     h->tail++;
+    hstream_progress(h);  // and the next ones' D2H behind it, if their decodes are done
     if (s.submit_status) {
         if (err) *err = s.submit_err;
         return s.submit_status;
     }
     murr_ctx* c = s.c;
     HIPC(hipSetDevice(c->device));
-    // the decode and its counters (null counts, utf8 byte counts, errors)
-    int st = murr_decode_wait(c, err);
-    if (st) return st;
-    // the batch's D2H, in batch order on the D2H stream (a copy queued there
-    // never waits behind a later batch's decode): the fixed-size arrays in
-    // one copy, then exactly the decoded utf8 bytes
+    HIPC(hipEventSynchronize(s.e3));  // its D2H landed
     const HostOut& o = s.out;
-    uint64_t ub = 0;
-    if (s.timed) HIPC(hipEventRecord(s.e2, h->s_d2h));
-    HIPC(hipMemcpyAsync(o.hout, o.dout, s.d2h_bytes, hipMemcpyDeviceToHost, h->s_d2h));
-    for (uint32_t p = 0; p < h->proj.size(); p++) {
-        const murr_array_t& a = o.arr[p];
-        if (a.offsets && a.data_len) {
-            HIPC(hipMemcpyAsync(o.hout + o.off[3 * p], a.values, a.data_len, hipMemcpyDeviceToHost, h->s_d2h));
-            ub += a.data_len;
-        }
-    }
-    if (s.timed) HIPC(hipEventRecord(s.e3, h->s_d2h));
-    // (only this batch's copies are on the D2H stream: they are queued here)
-    HIPC(hipStreamSynchronize(h->s_d2h));
+    const uint64_t ub = s.ub;
     if (s.timed) {
         float ms = 0;
         if (hipEventElapsedTime(&ms, s.e0, s.e1) == hipSuccess) h->stats.h2d_ms += ms;

@@ -18,6 +18,8 @@ timeout -k 10 900 $PY tools/ab.py --reps 2 \
   > $O/ab8.txt 2>&1
 tail -8 $O/ab8.txt
 timeout -k 10 120 tools/ubench/pcie > $O/pcie2.txt 2>&1 || exit 1
+timeout -k 10 300 $PY bench.py --mode host --config B --depth 4 > $O/host_B5.json 2> $O/host_B5.err || exit 1
+timeout -k 10 300 $PY bench.py --mode host --config C --rows 1000 --blocks 2000 --warmup 50 --depth 4 > $O/host_C5.json 2> $O/host_C5.err || exit 1
 for b in 1 0; do
   MURR_LIB=$T MURR_DECODE_VERBOSE=1 MURR_JIT_DEFS=MJ_TIMELINE=1 UIDX_STRIDE=128 timeout -k 10 200 $PY tools/timeline_d.py 1250000 "verbose=1,balance=$((b==1 ? 1 : 0))" > $O/tl_bal$b.log 2>&1 || exit 1
 done
