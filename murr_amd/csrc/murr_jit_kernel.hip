@@ -462,18 +462,23 @@ DEV uint32_t pool_size(uint32_t x) {
 // A claim in flight: a returning add on pool x's counter issued by lane 0
 // (inline asm: the compiler sees neither the load nor its destination, so it
 // inserts no vmcnt wait of its own -- the loader's counted waits cover it).
+// A claim takes kClaim consecutive blocks of a pool: the next claim is issued
+// when the first of them is taken and is not needed before the last of them
+// is, by which time (two tiles in flight at most) a loader wait has covered it.
+constexpr uint32_t kClaim = 3;
 struct Claim {
     uint32_t v;     // lane 0: the counter's old value (valid once `ready`)
     uint32_t x;     // its pool
     uint32_t pend;  // a claim is in flight
     uint32_t ready; // a vmcnt wait of the loader has covered it since
     uint32_t want;  // the static share is (nearly) done: keep one claim in flight
+    uint32_t nxt, nend;  // claimed blocks not yet used: [nxt, nend)
 };
 DEV void claim_issue(Claim& cl, uint32_t x) {
     uint32_t r = 0;
     if (lane_id() == 0) {
         GAS uint32_t* p = pool_cnt(x);
-        asm volatile("global_atomic_add %0, %1, %2, off sc0" : "=v"(r) : "v"(p), "v"(1u) : "memory");
+        asm volatile("global_atomic_add %0, %1, %2, off sc0" : "=v"(r) : "v"(p), "v"(kClaim) : "memory");
     }
     cl.v = r;
     cl.x = x;
@@ -510,9 +515,13 @@ DEV uint32_t dyn_claim() {
 // synchronous claim elsewhere.  Not yet covered by a loader wait: wait here.
 DEV uint32_t claim_take(Claim& cl) {
     if (!cl.ready) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const uint32_t i = (uint32_t)__builtin_amdgcn_readlane(cl.v, 0);
+    const uint32_t i = (uint32_t)__builtin_amdgcn_readlane(cl.v, 0), sz = pool_size(cl.x);
     cl.pend = 0;
-    if (i < pool_size(cl.x)) return pool_lo(cl.x) + i;
+    if (i < sz) {
+        cl.nxt = pool_lo(cl.x) + i + 1;
+        cl.nend = pool_lo(cl.x) + umin32(i + kClaim, sz);
+        return pool_lo(cl.x) + i;
+    }
     return dyn_claim();
 }
 DEV uint32_t next_vblock(uint32_t k, Claim& cl) {
@@ -522,6 +531,7 @@ DEV uint32_t next_vblock(uint32_t k, Claim& cl) {
         if (k + 2 * G >= ds) cl.want = 1;  // the last static block: claims from now on
         return k + G;
     }
+    if (cl.nxt < cl.nend) return cl.nxt++;  // the rest of the last claim
     const uint32_t got = cl.pend ? claim_take(cl) : dyn_claim();
     cl.want = got < args()->norder;  // (pools empty: no more claims)
     return got;
@@ -1501,7 +1511,7 @@ DEV void kernel_body() {
         // for tile i + 1.  It issues no other vector-memory instruction, so
         // its counted vmcnt waits for exactly the DMA it needs.
         Cur cs = cur_first<MODE>();  // next tile to announce
-        Claim cl{0u, 0u, 0u, 0u, MODE == 0 && args()->dyn_start && blockIdx.x + gridDim.x >= args()->dyn_start};
+        Claim cl{0u, 0u, 0u, 0u, MODE == 0 && args()->dyn_start && blockIdx.x + gridDim.x >= args()->dyn_start, 0u, 0u};
 #pragma unroll
         for (uint32_t k = 0; k <= NSLOT + 1; k++) {
             tile_announce<TR>(cs, spans + (k & 7) * 16, infos + (k & 7) * 32, lane, pf + (k & 7) * 8 * NU);
