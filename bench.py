@@ -641,6 +641,7 @@ def run_host(args):
                 "d2h_ms_per_batch": round(d["d2h_ms"] / nt, 4),
                 "host_submit_ms_per_batch": round(d["host_submit_ms"] / nb, 4),
                 "host_next_ms_per_batch": round(d["host_next_ms"] / nb, 4),
+                "host_wait_ms_per_batch": round(d["host_wait_ms"] / nb, 4),
                 "h2d_bytes_per_batch": int(h2d_b), "d2h_bytes_per_batch": int(d2h_b)}
 
     res = {"pinned_source": stream_run(True), "pageable_source": stream_run(False)}

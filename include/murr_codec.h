@@ -154,7 +154,7 @@ typedef struct {
                                0xFFFFFFFF = one workgroup per (virtual) block, handed to the
                                CUs by the hardware as workgroups finish */
     uint32_t balance;       /* local mode, several (virtual) blocks per workgroup: 0 auto
-                               (dynamic when the blocks are cut), 1 static deal only,
+                               (= static: measured faster), 1 static deal only,
                                2 dynamic per-XCD tail with half the blocks dealt statically,
                                10..90 dynamic with that percentage dealt statically */
 } murr_opts_t;
@@ -437,13 +437,15 @@ int murr_hstream_next(murr_hstream_t* s, murr_host_array_t* outs /* nproj */, mu
  * moved; device milliseconds of the H2D copies, the decode kernels and the
  * D2H copies of the `timed_batches` batches timed with HIP events (every
  * eighth: the events cost host time per batch); host milliseconds spent in
- * submit and in next (API calls and waits). */
+ * submit and in next (API calls and waits), and of those the waits for
+ * batches still on the device. */
 typedef struct {
     uint64_t batches;
     double h2d_ms, kernel_ms, d2h_ms;
     uint64_t h2d_bytes, d2h_bytes;
     uint64_t timed_batches;
     double host_submit_ms, host_next_ms;
+    double host_wait_ms;
 } murr_hstream_stats_t;
 int murr_hstream_stats(murr_hstream_t* s, murr_hstream_stats_t* out);
 void murr_hstream_free(murr_hstream_t* s);

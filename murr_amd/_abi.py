@@ -87,7 +87,8 @@ class HostArray(C.Structure):
 class HStreamStats(C.Structure):
     _fields_ = [("batches", C.c_uint64), ("h2d_ms", C.c_double), ("kernel_ms", C.c_double), ("d2h_ms", C.c_double),
                 ("h2d_bytes", C.c_uint64), ("d2h_bytes", C.c_uint64), ("timed_batches", C.c_uint64),
-                ("host_submit_ms", C.c_double), ("host_next_ms", C.c_double)]
+                ("host_submit_ms", C.c_double), ("host_next_ms", C.c_double),
+                ("host_wait_ms", C.c_double)]
 
 
 class HostColIn(C.Structure):

@@ -105,6 +105,14 @@ struct murr_ctx {
     uint64_t aux_cap = 0;     // entries
     hipEvent_t xev = nullptr; // multi-GPU reads: this stream's work, awaited by the home stream
     hipEvent_t hev = nullptr; // multi-GPU reads (as home): the work queued before a read, awaited by the shards
+    // Fused transfers (the streaming host decode, murr_hstream): the next
+    // decode enqueue uploads its descriptors in one segment-copy kernel with
+    // the batch's input (`xin`), and reads its counters back in one with the
+    // decoded buffers (`xout`), instead of two hipMemcpyAsync; with `xtimed`
+    // the caller's events xe[0..3] bracket the two copies (and k0/k1 the decode).
+    bool xfer = false, xtimed = false;
+    std::vector<CopySeg> xin, xout;
+    hipEvent_t xe[4] = {nullptr, nullptr, nullptr, nullptr};
 };
 
 // Device key index (murr_index.hip): the keys' own copy and the slot table.
@@ -824,6 +832,37 @@ int murr_sync(murr_ctx_t* c) {
 // ---- decode ------------------------------------------------------------------
 
 namespace {
+// Copy-kernel grids: reads from pinned host memory saturate PCIe with 64
+// workgroups (more queue up behind the link), writes with 128.
+constexpr uint32_t kCopyGridIn = 64, kCopyGridOut = 128;
+
+// A decode's descriptor upload (c->hs -> dst): one hipMemcpyAsync, or (fused
+// transfers) one segment-copy kernel together with the batch's input.
+hipError_t upload_desc(murr_ctx* c, uint8_t* dst, uint64_t bytes) {
+    if (!c->xfer) return hipMemcpyAsync(dst, c->hs, bytes, hipMemcpyHostToDevice, c->stream);
+    c->xin.push_back(CopySeg{c->hs, dst, bytes, nullptr});
+    hipError_t e = c->xtimed ? hipEventRecord(c->xe[0], c->stream) : hipSuccess;
+    if (e == hipSuccess) e = launch_copy_segs(c->xin.data(), (uint32_t)c->xin.size(), kCopyGridIn, c->stream);
+    if (e == hipSuccess && c->xtimed) e = hipEventRecord(c->xe[1], c->stream);
+    c->xin.clear();
+    return e;
+}
+// Its counter read-back (c->ws -> c->hs + rb): one hipMemcpyAsync, or (fused
+// transfers) one segment-copy kernel together with the decoded buffers.
+hipError_t read_back(murr_ctx* c, uint64_t rb, uint64_t bytes) {
+    if (!c->xfer) return hipMemcpyAsync(c->hs + rb, c->ws, bytes, hipMemcpyDeviceToHost, c->stream);
+    c->xout.insert(c->xout.begin(), CopySeg{c->ws, c->hs + rb, bytes, nullptr});
+    hipError_t e = c->xtimed ? hipEventRecord(c->xe[2], c->stream) : hipSuccess;
+    if (e == hipSuccess) e = launch_copy_segs(c->xout.data(), (uint32_t)c->xout.size(), kCopyGridOut, c->stream);
+    if (e == hipSuccess && c->xtimed) e = hipEventRecord(c->xe[3], c->stream);
+    c->xout.clear();
+    return e;
+}
+// Kernel timing events: always, except untimed fused-transfer batches.
+bool kernel_events(const murr_ctx* c) { return !c->xfer || c->xtimed; }
+}  // namespace
+
+namespace {
 
 // After an enqueue: what murr_decode_wait needs to fill the counts.
 int pending_set(murr_ctx* c, murr_array_t* outs, const murr_block_t* blocks, uint32_t nblocks, uint32_t nproj,
@@ -1039,13 +1078,15 @@ int decode_enqueue_jit(murr_ctx* c, const murr_segment_t* seg, const JitLayout* 
     // Local mode with several (virtual) blocks per workgroup: the first share
     // dealt statically, the rest claimed at run time from eight per-XCD pools
     // (murr_jit_kernel.hip dyn_claim), so the launch does not end with its
-    // slowest workgroups.  Auto: when the blocks are cut (similar pieces) and
-    // there is one projection round (the pool counters serve one launch).
+    // slowest workgroups.  Opt-in (balance >= 2) and with one projection round
+    // (the pool counters serve one launch): measured slower on the D shard,
+    // whose claims wait on device-scope atomics, so auto
+    // deals statically.
     uint32_t dyn_start = 0, dyn_pool = 0;
     {
         const uint32_t bal = O.balance;
         const uint64_t nv = lsegs.size();
-        const bool want = bal >= 2 || (bal == 0 && cut);
+        const bool want = bal >= 2;
         if (local && want && nv > grid && nv < 0xFFFFFFFFull) {
             // (rounds is known below; dynamic needs one round)
             const uint32_t pct = bal >= 10 && bal <= 90 ? bal : 50;
@@ -1120,8 +1161,12 @@ int decode_enqueue_jit(murr_ctx* c, const murr_segment_t* seg, const JitLayout* 
     for (uint32_t p = 0; p < nproj; p++) ((uint16_t*)(hd + (d_projc - zbytes)))[p] = (uint16_t)proj[p];
 
     if (!hz) HIPC(hipMemsetAsync(ws, 0, zbytes, c->stream));
-    HIPC(hipMemcpyAsync(ws + zbytes - hz, c->hs, hz + hdesc, hipMemcpyHostToDevice, c->stream));
-    if (rep) HIPC(hipStreamSynchronize(c->stream));  // c->hs is reused by the next call
+    if (rep) {
+        HIPC(hipMemcpyAsync(ws + zbytes - hz, c->hs, hz + hdesc, hipMemcpyHostToDevice, c->stream));
+        HIPC(hipStreamSynchronize(c->stream));  // c->hs is reused by the next call
+    } else {
+        HIPC(upload_desc(c, ws + zbytes - hz, hz + hdesc));
+    }
     // Empty blocks: utf8 offsets = [0] (StringBuilder starts with offset 0).
     for (uint32_t b = 0; b < nblocks; b++)
         if (blocks[b].n_rows == 0)
@@ -1172,7 +1217,7 @@ int decode_enqueue_jit(murr_ctx* c, const murr_segment_t* seg, const JitLayout* 
         rep->grid = (uint32_t)grid;
         rep->lds = lds;
         rep->mode = cut ? 2u : local ? 1u : 3u;
-    } else {
+    } else if (kernel_events(c)) {
         HIPC(hipEventRecord(c->k0, c->stream));
     }
     if (tiles) {
@@ -1215,10 +1260,10 @@ int decode_enqueue_jit(murr_ctx* c, const murr_segment_t* seg, const JitLayout* 
     c->stats.last_grid = (uint32_t)grid;
     c->stats.last_shape_nw = K.nw;
     c->stats.last_shape_r = K.r;
-    HIPC(hipEventRecord(c->k1, c->stream));
-    c->timed = true;
+    if (kernel_events(c)) HIPC(hipEventRecord(c->k1, c->stream));
+    c->timed = kernel_events(c);
     c->lk0 = c->lk1 = nullptr;
-    HIPC(hipMemcpyAsync(c->hs + rb, c->ws, z_lb, hipMemcpyDeviceToHost, c->stream));
+    HIPC(read_back(c, rb, z_lb));
     c->retry_local = !local && emit && tiles;
     if (c->retry_local) {
         c->r_cols.assign(seg->cols, seg->cols + seg->ncols);
@@ -1454,7 +1499,7 @@ int murr_decode_enqueue_ix(murr_ctx_t* c, const murr_segment_t* seg, const uint3
     std::memcpy(hd + (d_outs - zbytes), dout.data(), sizeof(DecOut) * dout.size());
 
     if (!hz) HIPC(hipMemsetAsync(c->ws, 0, zbytes, c->stream));
-    HIPC(hipMemcpyAsync(c->ws + zbytes - hz, c->hs, hz + hdesc, hipMemcpyHostToDevice, c->stream));
+    HIPC(upload_desc(c, c->ws + zbytes - hz, hz + hdesc));
     // Empty blocks: utf8 offsets = [0] (StringBuilder starts with offset 0).
     for (uint32_t b = 0; b < nblocks; b++)
         if (blocks[b].n_rows == 0)
@@ -1478,7 +1523,7 @@ int murr_decode_enqueue_ix(murr_ctx_t* c, const murr_segment_t* seg, const uint3
     if (verbose)
         std::fprintf(stderr, "decode launch: grid %llu (%d/CU) tiles %llu shape %ux%u rows/tile %u stage %u slots %u depth %u lds %u local %d\n",
                      (unsigned long long)grid, bpc, (unsigned long long)tiles, nw, kc, rows, a.stage, slots, depth, lds, (int)local);
-    HIPC(hipEventRecord(c->k0, c->stream));
+    if (kernel_events(c)) HIPC(hipEventRecord(c->k0, c->stream));
     if (tiles) {
         HIPC(launch_decode(a, nw, kc, (uint32_t)grid, c->stream));
         c->last_kernel = "decode_kernel";
@@ -1487,10 +1532,10 @@ int murr_decode_enqueue_ix(murr_ctx_t* c, const murr_segment_t* seg, const uint3
     c->stats.last_grid = (uint32_t)grid;
     c->stats.last_shape_nw = nw;
     c->stats.last_shape_r = kc;
-    HIPC(hipEventRecord(c->k1, c->stream));
-    c->timed = true;
+    if (kernel_events(c)) HIPC(hipEventRecord(c->k1, c->stream));
+    c->timed = kernel_events(c);
     c->lk0 = c->lk1 = nullptr;
-    HIPC(hipMemcpyAsync(c->hs + rb, c->ws, z_lb, hipMemcpyDeviceToHost, c->stream));
+    HIPC(read_back(c, rb, z_lb));
 
     return pending_set(c, outs, blocks, nblocks, nproj, dp, rb);
 }
@@ -1542,13 +1587,22 @@ int murr_utf8_index_update(murr_ctx_t* c, const murr_segment_t* seg, const murr_
 namespace {
 int finish_counts(murr_ctx* c, const uint8_t* rb, murr_array_t* outs, uint32_t nblocks, uint32_t nproj,
                   const uint64_t* n_rows, const uint32_t* dtypes, murr_error_t* err);
+int decode_collect(murr_ctx* c, murr_error_t* err);
 }  // namespace
 extern "C" {
 
 int murr_decode_wait(murr_ctx_t* c, murr_error_t* err) {
     if (!c || !c->pending) return set_err(err, MURR_E_ARGUMENT);
-    c->pending = false;
     HIPC(hipStreamSynchronize(c->stream));
+    return decode_collect(c, err);
+}
+
+namespace {
+// A pending decode whose stream work (kernel and read-back) has finished:
+// its counts and first error (murr_decode_wait after its synchronisation; the
+// streaming host decode after the batch's event).
+int decode_collect(murr_ctx* c, murr_error_t* err) {
+    c->pending = false;
 #ifdef MURR_TUNING
     if (c->opts.verbose && c->tl_off) print_timeline(c);
 #endif
@@ -1586,6 +1640,7 @@ int murr_decode_wait(murr_ctx_t* c, murr_error_t* err) {
     c->retry_local = false;
     return finish_counts(c, rb, c->outs, c->nblocks, c->nproj, c->n_rows.data(), c->dtypes.data(), err);
 }
+}  // namespace
 
 namespace {
 // The read-back counters of a finished decode -> the arrays' null counts and
@@ -2317,11 +2372,23 @@ struct murr_hstream {
     std::vector<uint32_t> proj;
     std::vector<HSlot> slots;
     hipStream_t s_h2d = nullptr, s_d2h = nullptr;
+    bool fused = true;            // copies by segment-copy kernels on the slot streams (else DMA copies)
     uint64_t head = 0, tail = 0;  // batches submitted / returned
     murr_hstream_stats_t stats{};
 };
 
 namespace {
+
+// The device address of pinned host bytes (hipHostMalloc / hipHostRegister),
+// or null when `p` is not pinned memory the device can read.
+const uint8_t* pinned_dev_view(const void* p) {
+    hipPointerAttribute_t a{};
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    return a.type == hipMemoryTypeHost && a.devicePointer ? (const uint8_t*)a.devicePointer : nullptr;
+}
 
 // Enqueue batch `s` (everything after the staging copy is asynchronous).  The
 // output region is laid out as decode_to_host's, its utf8 parts bounded by the
@@ -2337,6 +2404,17 @@ int hstream_enqueue(murr_hstream* h, HSlot& s, const uint8_t* data, const uint64
     if (!grow_dev(c, &s.din, &s.din_cap, dbytes + obytes)) return set_err(err, MURR_E_HIP);
     const uint8_t* src_data = data + (b0 - head);
     const uint64_t* src_off = row_off;
+    if (pinned && h->fused) {
+        // the copy kernel reads the caller's pinned bytes at their device addresses
+        const uint8_t* dd = pinned_dev_view(src_data);
+        const uint8_t* doo = pinned_dev_view(row_off);
+        if (dd && doo) {
+            src_data = dd;
+            src_off = (const uint64_t*)doo;
+        } else {
+            pinned = false;  // (not pinned after all: staged like pageable bytes)
+        }
+    }
     if (!pinned) {
         // one host copy into the slot's pinned staging (the caller may reuse
         // its buffers as soon as submit returns)
@@ -2348,11 +2426,17 @@ int hstream_enqueue(murr_hstream* h, HSlot& s, const uint8_t* data, const uint64
     }
     uint64_t* doff = (uint64_t*)(s.din + dbytes);
     s.timed = (h->head & 7) == 0;  // every eighth batch carries timing events
-    if (s.timed) HIPC(hipEventRecord(s.e0, h->s_h2d));
-    if (head + bytes) HIPC(hipMemcpyAsync(s.din, src_data, head + bytes, hipMemcpyHostToDevice, h->s_h2d));
-    HIPC(hipMemcpyAsync(doff, src_off, obytes, hipMemcpyHostToDevice, h->s_h2d));
-    HIPC(hipEventRecord(s.e1, h->s_h2d));
-    HIPC(hipStreamWaitEvent(c->stream, s.e1, 0));
+    if (h->fused) {
+        // input copies: with the decode's descriptors, in one kernel (murr_decode_enqueue)
+        c->xin.assign({CopySeg{src_data, s.din, head + bytes, nullptr},
+                       CopySeg{(const uint8_t*)src_off, (uint8_t*)doff, obytes, nullptr}});
+    } else {
+        if (s.timed) HIPC(hipEventRecord(s.e0, h->s_h2d));
+        if (head + bytes) HIPC(hipMemcpyAsync(s.din, src_data, head + bytes, hipMemcpyHostToDevice, h->s_h2d));
+        HIPC(hipMemcpyAsync(doff, src_off, obytes, hipMemcpyHostToDevice, h->s_h2d));
+        HIPC(hipEventRecord(s.e1, h->s_h2d));
+        HIPC(hipStreamWaitEvent(c->stream, s.e1, 0));
+    }
     s.h2d_bytes = head + bytes + obytes;
     // row i of the block is data[row_off[i]..]: the block's data pointer sits
     // row_off[0] & ~15 bytes before the staged bytes (16-B aligned)
@@ -2395,7 +2479,25 @@ int hstream_enqueue(murr_hstream* h, HSlot& s, const uint8_t* data, const uint64
         a.offsets = h->seg.cols[h->proj[p]].dtype == MURR_UTF8 ? (int32_t*)(o.dout + o.off[3 * p + 2]) : nullptr;
         a.values_cap = utf8_cap;
     }
+    if (h->fused) {
+        // output copies: the fixed-size parts, then each utf8 column's bytes
+        // up to its final offset (exactly the decoded bytes), with the
+        // decode's counters, in one kernel behind the decode
+        c->xout.assign({CopySeg{o.dout, o.hout, fixed_out, nullptr}});
+        for (uint32_t p = 0; p < np; p++)
+            if (o.arr[p].offsets)
+                c->xout.push_back(CopySeg{o.dout + o.off[3 * p], o.hout + o.off[3 * p], utf8_cap, o.arr[p].offsets + n});
+        c->xfer = true;
+        c->xtimed = s.timed;
+        c->xe[0] = s.e0;
+        c->xe[1] = s.e1;
+        c->xe[2] = s.e2;
+        c->xe[3] = s.e3;
+    }
     const int st = murr_decode_enqueue(c, &h->seg, h->proj.data(), np, &blk, 1, o.arr.data());
+    c->xfer = false;
+    c->xin.clear();
+    c->xout.clear();
     if (st) return set_err(err, st, st == MURR_E_HIP ? (int)hipGetLastError() : 0);
     HIPC(hipEventRecord(s.ed, c->stream));  // the decode and its counters' read-back are done
     s.d2h_bytes = fixed_out;  // (the fixed-size part, queued with the utf8 bytes once the counters are in)
@@ -2413,7 +2515,8 @@ void hstream_drain(murr_hstream* h, HSlot& s) {
     s.drained = true;
     if (s.submit_status) return;
     murr_error_t e{};
-    const int st = murr_decode_wait(s.c, &e);
+    const uint64_t retries = s.c->stats.split_retries;
+    const int st = decode_collect(s.c, &e);  // (its event `ed` has completed)
     if (st) {
         s.submit_status = st;
         s.submit_err = e;
@@ -2421,6 +2524,26 @@ void hstream_drain(murr_hstream* h, HSlot& s) {
     }
     const HostOut& o = s.out;
     bool ok = true;
+    if (h->fused) {
+        // its copies ran behind the decode; a decode re-run (split mode timed
+        // out, murr_decode_wait) came after them: copy again
+        s.ub = 0;
+        for (uint32_t p = 0; p < h->proj.size(); p++)
+            if (o.arr[p].offsets) s.ub += o.arr[p].data_len;
+        if (s.c->stats.split_retries != retries) {
+            ok = hipMemcpy(o.hout, o.dout, s.d2h_bytes, hipMemcpyDeviceToHost) == hipSuccess;
+            for (uint32_t p = 0; ok && p < h->proj.size(); p++)
+                if (o.arr[p].offsets && o.arr[p].data_len)
+                    ok = hipMemcpy(o.hout + o.off[3 * p], o.arr[p].values, o.arr[p].data_len, hipMemcpyDeviceToHost) == hipSuccess;
+        }
+        if (!ok) {
+            s.submit_status = MURR_E_HIP;
+            s.submit_err = murr_error_t{};
+            s.submit_err.status = MURR_E_HIP;
+            s.submit_err.hip_error = (int)hipGetLastError();
+        }
+        return;
+    }
     if (s.timed) ok = ok && hipEventRecord(s.e2, h->s_d2h) == hipSuccess;
     ok = ok && hipMemcpyAsync(o.hout, o.dout, s.d2h_bytes, hipMemcpyDeviceToHost, h->s_d2h) == hipSuccess;
     s.ub = 0;
@@ -2443,6 +2566,7 @@ void hstream_drain(murr_hstream* h, HSlot& s) {
 // Queue the D2H of every batch, oldest first, whose decode has finished (no
 // wait): next() then finds its copy under way or done.
 void hstream_progress(murr_hstream* h) {
+    if (h->fused) return;  // (nothing to queue: the copies follow the decode on its stream)
     for (uint64_t j = h->tail; j < h->head; j++) {
         HSlot& s = h->slots[j % h->slots.size()];
         if (s.drained) continue;
@@ -2474,6 +2598,9 @@ int murr_hstream_new(murr_ctx_t* c, const murr_segment_t* seg, const uint32_t* p
     h->seg.cols = h->cols.data();
     h->proj.assign(proj, proj + nproj);
     h->slots.resize(depth);
+#ifdef MURR_TUNING
+    if (std::getenv("MURR_HSTREAM_DMA")) h->fused = false;  // A/B: DMA-engine copies
+#endif
     int st = hipSetDevice(c->device) == hipSuccess ? MURR_OK : MURR_E_HIP;
     if (!st && (hipStreamCreateWithFlags(&h->s_h2d, hipStreamNonBlocking) != hipSuccess ||
                 hipStreamCreateWithFlags(&h->s_d2h, hipStreamNonBlocking) != hipSuccess))
@@ -2523,7 +2650,14 @@ int murr_hstream_next(murr_hstream_t* h, murr_host_array_t* outs, murr_error_t* 
         ~Clock() { h->stats.host_next_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(); }
     } clock{h, std::chrono::steady_clock::now()};
     HSlot& s = h->slots[h->tail % h->slots.size()];
-    hstream_drain(h, s);  // (waits for its decode if it is still running)
+    if (!s.drained && !s.submit_status) {  // its decode (fused: and its copies) still running: wait
+        HIPC(hipSetDevice(s.c->device));
+        const auto w0 = std::chrono::steady_clock::now();
+        const hipError_t we = hipEventSynchronize(s.ed);
+        h->stats.host_wait_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - w0).count();
+        HIPC(we);
+    }
+    hstream_drain(h, s);
     h->tail++;
     hstream_progress(h);  // and the next ones' D2H behind it, if their decodes are done
     if (s.submit_status) {
@@ -2532,7 +2666,12 @@ int murr_hstream_next(murr_hstream_t* h, murr_host_array_t* outs, murr_error_t* 
     }
     murr_ctx* c = s.c;
     HIPC(hipSetDevice(c->device));
-    HIPC(hipEventSynchronize(s.e3));  // its D2H landed
+    if (!h->fused) {  // its D2H landed (fused: with the decode's event)
+        const auto w0 = std::chrono::steady_clock::now();
+        const hipError_t we = hipEventSynchronize(s.e3);
+        h->stats.host_wait_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - w0).count();
+        HIPC(we);
+    }
     const HostOut& o = s.out;
     const uint64_t ub = s.ub;
     if (s.timed) {

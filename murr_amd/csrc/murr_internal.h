@@ -296,6 +296,22 @@ hipError_t launch_gather_scan(const IndexArgs& a, hipStream_t s);  // probe + si
 hipError_t launch_gather_copy(const IndexArgs& a, hipStream_t s);  // the copy of a scanned gather
 hipError_t launch_offsets_rebase(int32_t* dst, const int32_t* src, uint64_t n, int64_t add, hipStream_t s);
 
+// Segment copies by a kernel (murr_kernels.hip copy_segs_kernel): pinned host
+// <-> device over PCIe as the CUs' own loads and stores (the streaming host
+// decode's transfers), `grid` workgroups at most.
+struct CopySeg {
+    const uint8_t* src;
+    uint8_t* dst;
+    uint64_t bytes;       // the length, or (len set) its bound
+    const int32_t* len;   // null, or a device int32 holding the length (clamped to [0, bytes])
+};
+constexpr uint32_t kMaxCopySegs = 12;
+struct CopyArgs {
+    CopySeg seg[kMaxCopySegs];
+    uint32_t nseg;
+};
+hipError_t launch_copy_segs(const CopySeg* segs, uint32_t n, uint32_t grid, hipStream_t s);
+
 // Arrow IPC framing (murr_ipc.cpp, murr_ipc.hip).
 enum : uint32_t { kIpcValidity = 0, kIpcOffsets = 1, kIpcValues = 2 };
 struct IpcPlan {

@@ -343,7 +343,14 @@ DEV void wait_vmcnt(uint32_t n) {
 // Early release of ring slots in local mode (decode_tile, kernel_body); 0 =
 // one workgroup barrier per tile (tuning A/B).
 #ifndef MJ_ER
-#define MJ_ER 1
+#define MJ_ER 0
+#endif
+// Fast start (2-slot rings): the loader DMAs its first tile as soon as that
+// tile's span is in and announces the next ones behind the DMA, with the
+// scalar cache warmed for their cursors first; 0 = announce four tiles, then
+// DMA (tuning A/B).
+#ifndef MJ_FASTSTART
+#define MJ_FASTSTART 1
 #endif
 constexpr uint32_t RO_STRIDE = MJ_RO64 ? 2 : 1;  // dwords per row offset in LDS
 
@@ -420,6 +427,27 @@ DEV Cur cur_seg(uint32_t k) {
     return cur_make(ok, k, ok ? sgpr(sp->b) : 0u, ok ? sgpr(sp->first) : 0u, 1, rb, re, rb);
 }
 template <uint32_t MODE> DEV Cur cur_first() { return MODE == 0 ? cur_local(blockIdx.x) : cur_seg(blockIdx.x); }
+// Fast start: the scalar loads behind the first cursors (the segment entries
+// g, g + G, g + 2G, g + 3G, then their block entries) issued side by side, so
+// the dependent chain of cursor loads that follows hits the scalar cache
+// instead of paying two L2 round trips per tile.
+template <uint32_t MODE> DEV void warm_scalar() {
+    const uint32_t G = gridDim.x, n = MODE == 0 ? args()->norder : args()->nseg;
+    if (!n) return;
+    uint32_t b[4];
+#pragma unroll
+    for (uint32_t j = 0; j < 4; j++) {
+        const uint32_t k = blockIdx.x + j * G;
+        b[j] = sgpr(((const CAS Seg*)args()->segs)[k < n ? k : n - 1].b);
+    }
+    uint64_t acc = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < 4; j++) {
+        const CAS Blk* bp = (const CAS Blk*)args()->blocks + b[j];
+        acc += sgpr64((uint64_t)bp->data) ^ sgpr64((uint64_t)bp->uidx);
+    }
+    asm volatile("; warm %0" ::"s"(acc));
+}
 // Tuning (MJ_QUEUE=1): local mode hands out the virtual blocks after each
 // workgroup's first from a queue (a counter beside the error word, zeroed
 // with it), so a workgroup that runs fast takes more of them.  Measured
@@ -1494,6 +1522,7 @@ DEV void kernel_body() {
     // early release (local mode): slots handed over by LDS counters instead of
     // a workgroup barrier per tile
     constexpr bool ER = MODE == 0 && MJ_ER && NSLOT == 2;
+    constexpr bool FAST = MJ_FASTSTART && NSLOT == 2;
     LAS uint32_t* full = (LAS uint32_t*)ctl + 4;  // [2]: number + 1 of the tile landed in slot s
     LAS uint32_t* freec = full + 2;               // [2]: decode-wave releases of slot s (cumulative)
     // A prepared launch (murr_decode_run) alternates two counter sets: this
@@ -1510,10 +1539,13 @@ DEV void kernel_body() {
         // and announces tile i + NSLOT + 2 (its identity and span), then waits
         // for tile i + 1.  It issues no other vector-memory instruction, so
         // its counted vmcnt waits for exactly the DMA it needs.
+        if constexpr (FAST) warm_scalar<MODE>();
         Cur cs = cur_first<MODE>();  // next tile to announce
         Claim cl{0u, 0u, 0u, 0u, MODE == 0 && args()->dyn_start && blockIdx.x + gridDim.x >= args()->dyn_start, 0u, 0u};
+        // tiles announced before the first DMA: 0 .. 3, or (fast start) 0 .. 1 / 0
+        constexpr uint32_t NPRE = !FAST ? NSLOT + 1 : ER ? 1u : 0u;
 #pragma unroll
-        for (uint32_t k = 0; k <= NSLOT + 1; k++) {
+        for (uint32_t k = 0; k <= NPRE; k++) {
             tile_announce<TR>(cs, spans + (k & 7) * 16, infos + (k & 7) * 32, lane, pf + (k & 7) * 8 * NU);
             cs = cur_next<TR>(cs, cl);
         }
@@ -1529,14 +1561,39 @@ DEV void kernel_body() {
             // on its own counted vmcnt and polls one LDS word, never on a
             // barrier, so a slot is refilled while the decode waves are still
             // computing and storing the tile it held.
-            lds_barrier();  // B_0: counters zeroed, tiles 0 .. 3 announced
+            lds_barrier();  // B_0: counters zeroed, tiles 0 .. 3 (FAST: 0 .. 1) announced
             uint32_t ti = 0, tl = 0;        // next tile to DMA / to land
             uint32_t ops[2] = {0, 0}, ann[2] = {0, 0};  // vmem ops issued with tile j % 2: all, its announce part
             uint32_t claim_t = ~0u;         // tile before whose DMA the claim in flight was issued
+            if constexpr (FAST) {
+                // Fast start: tiles 0 and 1 go into their slots as soon as
+                // their spans are in, and tiles 2 and 3 are announced behind
+                // those DMAs.  Their spans are younger than tile 1's DMA, so
+                // tile 1 lands with a full wait (ann[1] = 0), and tiles 2 and 3
+                // are not issued before it has.
+                uint32_t nd1 = 0;
+                if (tile_valid(infos)) {
+                    tile_dma<TR, SH::RO_BYTES>(tile_read_ptrs(spans, infos, stage), lds, lane);
+                    ti = 1;
+                    if (tile_valid(infos + 32)) {
+                        nd1 = tile_dma<TR, SH::RO_BYTES>(tile_read_ptrs(spans + 16, infos + 32, stage), lds + SLOT, lane);
+                        ti = 2;
+                    }
+                }
+                uint32_t na = 0;
+#pragma unroll
+                for (uint32_t k = 2; k <= NSLOT + 1; k++) {
+                    na += tile_announce<TR>(cs, spans + (k & 7) * 16, infos + (k & 7) * 32, lane, pf + (k & 7) * 8 * NU);
+                    cs = cur_next<TR>(cs, cl);
+                }
+                ops[1] = nd1 + na;  // landing tile 0: everything younger than its DMA (or a full wait)
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            }
             Wait w;
             for (;;) {
                 const bool more = tile_valid(infos + (ti & 7) * 32);
                 bool can = more && ti < tl + 2;
+                if (FAST && ti < 4) can = can && tl >= 2;  // (tile 1 landed: the spans of tiles 2, 3 with it)
                 if (can && ti >= 2)
                     can = __hip_atomic_load(freec + (ti & 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= NC * (ti >> 1);
                 if (can) {
@@ -1574,16 +1631,27 @@ DEV void kernel_body() {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             return;
         }
-        // tiles 0 .. NSLOT - 2 into their slots; B_0 once tile 0 landed
-        uint32_t after0 = 0;  // ops issued after tile 0's DMA
+        if constexpr (FAST) {
+            // fast start: tile 0's DMA, then the announcements of tiles 1 .. 3 behind it
+            if (tile_valid(infos)) tile_dma<TR, SH::RO_BYTES>(tile_read_ptrs(spans, infos, stage), lds, lane);
 #pragma unroll
-        for (uint32_t j = 0; j + 1 < NSLOT; j++) {
-            uint32_t n = 0;
-            if (tile_valid(infos + j * 32))
-                n = tile_dma<TR, SH::RO_BYTES>(tile_read_ptrs(spans + j * 16, infos + j * 32, stage), lds + j * SLOT, lane);
-            after0 += j ? n : 0;
+            for (uint32_t k = 1; k <= NSLOT + 1; k++) {
+                tile_announce<TR>(cs, spans + (k & 7) * 16, infos + (k & 7) * 32, lane, pf + (k & 7) * 8 * NU);
+                cs = cur_next<TR>(cs, cl);
+            }
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        } else {
+            // tiles 0 .. NSLOT - 2 into their slots; B_0 once tile 0 landed
+            uint32_t after0 = 0;  // ops issued after tile 0's DMA
+#pragma unroll
+            for (uint32_t j = 0; j + 1 < NSLOT; j++) {
+                uint32_t n = 0;
+                if (tile_valid(infos + j * 32))
+                    n = tile_dma<TR, SH::RO_BYTES>(tile_read_ptrs(spans + j * 16, infos + j * 32, stage), lds + j * SLOT, lane);
+                after0 += j ? n : 0;
+            }
+            wait_vmcnt(after0);
         }
-        wait_vmcnt(after0);
         lds_barrier();  // B_0: tile 0 and the spans of tiles 0 .. NSLOT + 1 landed
         uint32_t pend = 0;  // NSLOT 3: ops issued after tile it+1's DMA before this iteration
         for (uint32_t it = 0;; it++) {

@@ -182,11 +182,92 @@ __global__ void __launch_bounds__(256) encode_kernel(EncodeArgs A) {
     }
 }
 
+
+// ---- segment copies over PCIe (streaming host decode, murr_abi.cpp hstream) ----
+// A list of (src, dst, bytes) copies done by one grid of 256-thread
+// workgroups: pinned host -> device (the batch's blob and row offsets, and
+// the decode's descriptors) or device -> pinned host (the decoded buffers and
+// the decode's counters), the other side of PCIe read or written directly by
+// the CUs -- no copy engine, no per-copy command, no cross-stream event.  A
+// segment may take its length from a device int32 (a utf8 column's final
+// offset: exactly its decoded bytes, clamped to `bytes`).  Each workgroup step
+// moves one 16 KiB chunk: four 16-B loads per lane issued before their
+// stores, so a wave keeps 4 KiB of PCIe reads in flight.
+constexpr uint64_t kCopyChunk = 256 * 4 * 16;
+
+__device__ __forceinline__ uint64_t seg_bytes(const CopySeg& g) {
+    if (!g.len) return g.bytes;
+    const int32_t v = *(const CAS int32_t*)g.len;
+    return v <= 0 ? 0 : ((uint64_t)v < g.bytes ? (uint64_t)v : g.bytes);
+}
+
+__global__ void __launch_bounds__(256) copy_segs_kernel(CopyArgs A) {
+    const uint32_t tid = threadIdx.x;
+    for (uint64_t c = blockIdx.x;; c += gridDim.x) {
+        // the segment holding chunk c (uniform; at most kMaxCopySegs steps)
+        uint32_t s = 0;
+        uint64_t base = 0, nb = 0;
+        for (; s < A.nseg; s++) {
+            nb = seg_bytes(A.seg[s]);
+            const uint64_t nc = (nb + kCopyChunk - 1) / kCopyChunk;
+            if (c < base + nc) break;
+            base += nc;
+        }
+        if (s >= A.nseg) break;
+        const uint64_t off = (c - base) * kCopyChunk;
+        const uint64_t n = nb - off < kCopyChunk ? nb - off : kCopyChunk;
+        const uint8_t* src = A.seg[s].src + off;
+        uint8_t* dst = A.seg[s].dst + off;
+        if ((((uintptr_t)src | (uintptr_t)dst) & 15) == 0) {
+            const uint64_t nv = n >> 4;
+            const u32x4* sv = (const u32x4*)src;
+            u32x4* dv = (u32x4*)dst;
+            u32x4 v[4];
+#pragma unroll
+            for (uint32_t k = 0; k < 4; k++) {
+                const uint64_t i = tid + 256 * k;
+                if (i < nv) v[k] = __builtin_nontemporal_load(sv + i);
+            }
+#pragma unroll
+            for (uint32_t k = 0; k < 4; k++) {
+                const uint64_t i = tid + 256 * k;
+                if (i < nv) __builtin_nontemporal_store(v[k], dv + i);
+            }
+            const uint64_t t0 = nv << 4;
+            if (t0 + tid < n) dst[t0 + tid] = src[t0 + tid];
+        } else if ((((uintptr_t)src | (uintptr_t)dst) & 7) == 0) {
+            const uint64_t nq = n >> 3;
+            for (uint64_t i = tid; i < nq; i += 256) ((uint64_t*)dst)[i] = ((const uint64_t*)src)[i];
+            const uint64_t t0 = nq << 3;
+            if (t0 + tid < n) dst[t0 + tid] = src[t0 + tid];
+        } else {
+            for (uint64_t i = tid; i < n; i += 256) dst[i] = src[i];
+        }
+    }
+}
+
 }  // namespace
 
 hipError_t launch_encode(const EncodeArgs& a, uint32_t grid, hipStream_t s) {
     hipLaunchKernelGGL(encode_kernel, dim3(grid), dim3(kTile), 0, s, a);
     return hipGetLastError();
+}
+
+hipError_t launch_copy_segs(const CopySeg* segs, uint32_t n, uint32_t grid, hipStream_t s) {
+    for (uint32_t i = 0; i < n; i += kMaxCopySegs) {
+        CopyArgs a{};
+        a.nseg = n - i < kMaxCopySegs ? n - i : kMaxCopySegs;
+        uint64_t bound = 0;
+        for (uint32_t k = 0; k < a.nseg; k++) {
+            a.seg[k] = segs[i + k];
+            bound += (segs[i + k].bytes + kCopyChunk - 1) / kCopyChunk;
+        }
+        if (!bound) continue;
+        hipLaunchKernelGGL(copy_segs_kernel, dim3((uint32_t)(bound < grid ? bound : grid)), dim3(256), 0, s, a);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
 }
 
 int encode_blocks_per_cu() {

@@ -165,3 +165,25 @@ def test_stream_malformed_batch_fails_alone(ctx):
         hs.next()
     check(hs.next(), oseg, [0, 1], *good[2], "after")
     hs.close()
+
+
+def test_stream_pinned_buffer_rewritten_between_batches(ctx):
+    # one pinned source buffer refilled with a different batch each time (the
+    # copy reads it over PCIe at its device address: no stale bytes from the
+    # batch before), and batches of every size through the same slots
+    rng = np.random.default_rng(11)
+    dtypes = [D.Utf8, D.Int64, D.Bool, D.Utf8]
+    seg = SegmentSchema([(f"c{i}", d) for i, d in enumerate(dtypes)])
+    oseg = O.Segment([int(d) for d in dtypes])
+    batches = [encode_host(ctx, seg, random_columns(rng, dtypes, n, null_p=0.2, max_str=40), n)
+               for n in (3000, 17, 3000, 2500, 1)]
+    cap = max(d.size for d, _ in batches) + 16
+    hb, ho = HostBuffer(cap, ctx), HostBuffer(8 * 3001, ctx)
+    hs = HostStream(seg, [3, 0, 1, 2], depth=2, ctx=ctx)
+    for k, (data, off) in enumerate(batches):
+        hb.array[:] = 0x5A
+        hb.array[: data.size] = data
+        ho.array[: off.nbytes] = off.view(np.uint8)
+        hs.submit(hb.array, ho.array.view(np.uint64)[: off.size], pinned=True)
+        check(hs.next(), oseg, [3, 0, 1, 2], data, off, f"batch {k}")
+    hs.close()
