@@ -988,7 +988,7 @@ def main():
     ap.add_argument("--table-rows", type=int, default=0,
                     help="config D: one table of this many rows split by key range over the ranks "
                          "(configs[3] as written, strong scaling); default: --rows per rank (weak)")
-    ap.add_argument("--depth", type=int, default=3, help="host mode: pipeline slots (murr_hstream)")
+    ap.add_argument("--depth", type=int, default=4, help="host mode: pipeline slots (murr_hstream)")
     ap.add_argument("--host-ring", type=int, default=16, help="host mode: distinct source blocks in the pinned ring")
     ap.add_argument("--ipc", action="store_true", help="resident mode: also time the Arrow IPC message path")
     ap.add_argument("--uidx-stride", type=int, default=512,

@@ -834,7 +834,15 @@ int murr_sync(murr_ctx_t* c) {
 namespace {
 // Copy-kernel grids: reads from pinned host memory saturate PCIe with 64
 // workgroups (more queue up behind the link), writes with 128.
+#ifdef MURR_TUNING
+uint32_t copy_grid(const char* name, uint32_t dflt) {
+    const char* e = std::getenv(name);
+    return e ? (uint32_t)std::max(1, std::atoi(e)) : dflt;
+}
+const uint32_t kCopyGridIn = copy_grid("MURR_COPY_GRID_IN", 64), kCopyGridOut = copy_grid("MURR_COPY_GRID_OUT", 128);
+#else
 constexpr uint32_t kCopyGridIn = 64, kCopyGridOut = 128;
+#endif
 
 // A decode's descriptor upload (c->hs -> dst): one hipMemcpyAsync, or (fused
 // transfers) one segment-copy kernel together with the batch's input.
@@ -2334,17 +2342,20 @@ void murr_builder_free(murr_builder_t* b) {
 }  // extern "C"
 
 // ---- streaming host decode (murr_hstream_*) ----------------------------------
-// Batch reads back to back, host in, host out.  Three kinds of stream: one H2D
-// stream and one D2H stream shared by all slots (each copy direction one
-// engine, copies of one direction back to back at the link's full rate), and
-// each slot's own context stream for its decode (its own workspace, so
-// `depth` decodes may be in flight).  Batch i: H2D on the H2D stream -> its
-// decode waits on that (event) -> the D2H of its fixed-size arrays (values of
-// fixed-width columns, utf8 offsets, validity) waits on the decode; next()
-// learns the utf8 byte counts from the decode's counters and queues the
-// batch's D2H (fixed-size arrays in one copy, then exactly the utf8 bytes),
-// in batch order.  The only host waits are next()'s; the H2D stream runs
-// ahead through the batches already submitted meanwhile.
+// Batch reads back to back, host in, host out, `depth` batches in flight, each
+// on its own slot: a context (stream, workspace), device input and output
+// buffers, pinned output, all reused.  Batch i runs entirely on its slot's
+// stream: the H2D of its blob and row offsets (copy engine from 1 MiB up,
+// below that a copy kernel with the decode's descriptors), the decode, then
+// one segment-copy kernel (murr_kernels.hip copy_segs_kernel) that writes its
+// fixed-size arrays, exactly the decoded utf8 bytes (each column's length read
+// from its final offset on the device) and the decode's counters into pinned
+// host memory -- no host round trip between the decode and its D2H, and no
+// cross-stream event.  next() waits on the batch's one event.  Measured
+// against the alternatives on one box: copy engines both
+// ways on two shared streams 10.4 GiB/s, kernel copies both ways 11.3, this
+// split 12.4-12.9 (config B, pinned sources).  Tuning builds keep the others:
+// MURR_HSTREAM_DMA=1, MURR_HSTREAM_H2D=kernel.
 
 struct HSlot {
     murr_ctx* c = nullptr;
@@ -2372,12 +2383,15 @@ struct murr_hstream {
     std::vector<uint32_t> proj;
     std::vector<HSlot> slots;
     hipStream_t s_h2d = nullptr, s_d2h = nullptr;
-    bool fused = true;            // copies by segment-copy kernels on the slot streams (else DMA copies)
+    bool fused = true;            // D2H (and H2D unless `h2d_engine`) by segment-copy kernels on the slot streams
+    bool h2d_engine = true;       // (fused) H2D of batches >= kEngineMinBytes by copy-engine copies on the slot stream
     uint64_t head = 0, tail = 0;  // batches submitted / returned
     murr_hstream_stats_t stats{};
 };
 
 namespace {
+
+constexpr uint64_t kEngineMinBytes = 1ull << 20;
 
 // The device address of pinned host bytes (hipHostMalloc / hipHostRegister),
 // or null when `p` is not pinned memory the device can read.
@@ -2404,7 +2418,11 @@ int hstream_enqueue(murr_hstream* h, HSlot& s, const uint8_t* data, const uint64
     if (!grow_dev(c, &s.din, &s.din_cap, dbytes + obytes)) return set_err(err, MURR_E_HIP);
     const uint8_t* src_data = data + (b0 - head);
     const uint64_t* src_off = row_off;
-    if (pinned && h->fused) {
+    // H2D: the copy engine for large batches; below ~1 MiB its fixed cost per
+    // copy (~10 us, two copies) dominates, and the copy kernel takes the bytes
+    // (config C's 1000-key reads: 2.8 -> 3.6 GiB/s)
+    const bool engine = h->fused && h->h2d_engine && head + bytes + obytes >= kEngineMinBytes;
+    if (pinned && h->fused && !engine) {
         // the copy kernel reads the caller's pinned bytes at their device addresses
         const uint8_t* dd = pinned_dev_view(src_data);
         const uint8_t* doo = pinned_dev_view(row_off);
@@ -2426,7 +2444,13 @@ int hstream_enqueue(murr_hstream* h, HSlot& s, const uint8_t* data, const uint64
     }
     uint64_t* doff = (uint64_t*)(s.din + dbytes);
     s.timed = (h->head & 7) == 0;  // every eighth batch carries timing events
-    if (h->fused) {
+    if (engine) {
+        // input copies by the copy engine, on the slot stream ahead of the decode
+        if (s.timed) HIPC(hipEventRecord(s.e0, c->stream));
+        if (head + bytes) HIPC(hipMemcpyAsync(s.din, src_data, head + bytes, hipMemcpyHostToDevice, c->stream));
+        HIPC(hipMemcpyAsync(doff, src_off, obytes, hipMemcpyHostToDevice, c->stream));
+        if (s.timed) HIPC(hipEventRecord(s.e1, c->stream));
+    } else if (h->fused) {
         // input copies: with the decode's descriptors, in one kernel (murr_decode_enqueue)
         c->xin.assign({CopySeg{src_data, s.din, head + bytes, nullptr},
                        CopySeg{(const uint8_t*)src_off, (uint8_t*)doff, obytes, nullptr}});
@@ -2489,8 +2513,8 @@ int hstream_enqueue(murr_hstream* h, HSlot& s, const uint8_t* data, const uint64
                 c->xout.push_back(CopySeg{o.dout + o.off[3 * p], o.hout + o.off[3 * p], utf8_cap, o.arr[p].offsets + n});
         c->xfer = true;
         c->xtimed = s.timed;
-        c->xe[0] = s.e0;
-        c->xe[1] = s.e1;
+        c->xe[0] = engine ? s.e4 : s.e0;  // (engine H2D: e0/e1 bracket the copies above)
+        c->xe[1] = engine ? s.e5 : s.e1;
         c->xe[2] = s.e2;
         c->xe[3] = s.e3;
     }
@@ -2600,6 +2624,7 @@ int murr_hstream_new(murr_ctx_t* c, const murr_segment_t* seg, const uint32_t* p
     h->slots.resize(depth);
 #ifdef MURR_TUNING
     if (std::getenv("MURR_HSTREAM_DMA")) h->fused = false;  // A/B: DMA-engine copies
+    if (const char* e = std::getenv("MURR_HSTREAM_H2D")) h->h2d_engine = std::string(e) != "kernel";
 #endif
     int st = hipSetDevice(c->device) == hipSuccess ? MURR_OK : MURR_E_HIP;
     if (!st && (hipStreamCreateWithFlags(&h->s_h2d, hipStreamNonBlocking) != hipSuccess ||

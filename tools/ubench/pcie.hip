@@ -89,5 +89,42 @@ int main() {
             }
         }
     }
+    // concurrency: a kernel copy in each direction at once (streams a, b), and
+    // a kernel copy beside a copy-engine copy the other way
+    {
+        const size_t sz = 2730ull << 10, n = sz / 16;
+        const int reps = 100;
+        auto kin = [&](hipStream_t st) { kcopy<<<64, 256, 0, st>>>((const u32x4*)h1, (u32x4*)d1, n); };
+        auto kout = [&](hipStream_t st) { kcopy<<<128, 256, 0, st>>>((const u32x4*)d2, (u32x4*)h2, n); };
+        auto din = [&](hipStream_t st) { CK(hipMemcpyAsync(d1, h1, sz, hipMemcpyHostToDevice, st)); };
+        auto dout = [&](hipStream_t st) { CK(hipMemcpyAsync(h2, d2, sz, hipMemcpyDeviceToHost, st)); };
+        auto pair = [&](const char* name, auto fa, auto fb, bool use_b) {
+            CK(hipDeviceSynchronize());
+            CK(hipEventRecord(e0, a));
+            CK(hipEventRecord(f0, b));
+            for (int r = 0; r < reps; r++) {
+                fa(a);
+                if (use_b) fb(b);
+            }
+            CK(hipEventRecord(e1, a));
+            CK(hipEventRecord(f1, b));
+            CK(hipEventSynchronize(e1));
+            CK(hipEventSynchronize(f1));
+            float ta = 0, tb = 0;
+            CK(hipEventElapsedTime(&ta, e0, e1));
+            CK(hipEventElapsedTime(&tb, f0, f1));
+            const double gb = (double)sz * reps / 1e9;
+            std::printf("2730 KiB concurrent %-34s stream a %6.1f GB/s%s", name, gb / (ta * 1e-3), use_b ? "" : "\n");
+            if (use_b) std::printf("  stream b %6.1f GB/s\n", gb / (tb * 1e-3));
+            std::fflush(stdout);
+        };
+        pair("kernel H2D alone", kin, kout, false);
+        pair("kernel D2H alone", kout, kin, false);
+        pair("kernel H2D + kernel D2H", kin, kout, true);
+        pair("kernel H2D + kernel H2D", kin, kin, true);
+        pair("engine H2D + kernel D2H", din, kout, true);
+        pair("kernel H2D + engine D2H", kin, dout, true);
+        pair("engine H2D + engine D2H", din, dout, true);
+    }
     return 0;
 }
