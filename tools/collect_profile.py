@@ -28,7 +28,8 @@ names = {"bench": "bench.json", "decode_C": "decode_C.json", "decode_D1": "decod
          "decode_B_generic": "decode_B_generic.json", "host_C": "host_C.json", "encode_B": "encode_B.json",
          "encode_C": "encode_C.json", "resident_1000": "resident_1000.json",
          "resident_read_plain": "resident_read_plain.json", "resident_read_block": "resident_read_block.json",
-         "decode_D1x2": "decode_D1x2.json", "decode_D1x4": "decode_D1x4.json"}
+         "decode_D1x2": "decode_D1x2.json", "decode_D1x4": "decode_D1x4.json",
+         "decode_D_table10M": "decode_D_table10M.json"}
 for n, out in names.items():
     p = f"{src}/{n}.log"
     if os.path.exists(p):
@@ -36,6 +37,10 @@ for n, out in names.items():
         if j is not None:
             json.dump(j, open(f"{dst}/{out}", "w"))
             print(out)
+for n in ("timeline_D",):
+    if os.path.exists(f"{src}/{n}.log"):
+        shutil.copy(f"{src}/{n}.log", f"{dst}/{n}.log")
+        print(f"{n}.log")
 for pat, out in [("trace/*kernel_stats.csv", "bench_driver_kernel_stats.csv"),
                  ("trace/*domain_stats.csv", "bench_driver_domain_stats.csv")]:
     f = sorted(glob.glob(f"{src}/{pat}"))

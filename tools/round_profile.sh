@@ -7,7 +7,8 @@ set -u
 export TMPDIR=/tmp
 # the resolved interpreter after `--` (rocprofv3 execs it; a `python3` on PATH may be a wrapper)
 PY=$(readlink -f "$(command -v python3)")
-R=${R:-r02}
+R=${R:-r04}
+PART=${PART:-all}  # 1: the headline trace and B/C/D with traffic; 2: the side measurements; all: both
 out=gpurun_out/$R
 mkdir -p $out
 run() {  # run <name> <timeout> <cmd...>
@@ -17,6 +18,7 @@ run() {  # run <name> <timeout> <cmd...>
   echo "$name exit=$rc"; tail -n 2 "$out/$name.log"
   [ $rc -eq 0 ] || exit $rc
 }
+if [ "$PART" != 2 ]; then
 # the driver's exact command (bench.py --gpus 1 --steps 20 --warmup 5), traced
 run trace 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out/trace -o decode -- "$PY" bench.py --gpus 1 --steps 20 --warmup 5 --no-traffic
 run fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $out/pmc -o fetch -- "$PY" bench.py --steps 3 --warmup 1 --no-cpu --no-traffic
@@ -29,7 +31,8 @@ for cfg in "C:--config C --blocks 10" "D1:--config D"; do
   run write_$n 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $out/pmc -o write_$n -- "$PY" bench.py $a --steps 3 --warmup 1 --no-cpu --no-traffic
   run decode_$n 300 "$PY" bench.py $a --steps 10 --warmup 2 --no-cpu --pmc-csv "$out/pmc/fetch_${n}_counter_collection.csv,$out/pmc/write_${n}_counter_collection.csv"
 done
-if [ -z "${QUICK:-}" ]; then
+fi
+if [ "$PART" != 1 ]; then
   run host_B 300 "$PY" bench.py --mode host --config B
   run encode_E 300 "$PY" bench.py --mode encode --steps 10 --warmup 2
   run decode_C_noindex 300 "$PY" bench.py --config C --blocks 10 --steps 10 --warmup 2 --no-cpu --uidx-stride 0
@@ -46,4 +49,9 @@ if [ -z "${QUICK:-}" ]; then
   run decode_D1x2 300 "$PY" bench.py --config D --rows 2500000 --steps 10 --warmup 2 --no-cpu
   run decode_D1x4 300 "$PY" bench.py --config D --rows 5000000 --steps 10 --warmup 2 --no-cpu
   run encode_prof 300 bash tools/enc_prof.sh
+  # configs[3] as written at N = 1 (the whole 10 M-row table on one rank)
+  run decode_D_table10M 400 "$PY" bench.py --config D --table-rows 10000000 --steps 10 --warmup 2 --no-cpu
+  # per-workgroup timeline of the D shard (tuning build)
+  run timeline_D 200 env MURR_LIB=$PWD/murr_amd/libmurr_codec_tuning.so MURR_DECODE_VERBOSE=1 MURR_JIT_DEFS=MJ_TIMELINE=1 \
+    "$PY" tools/timeline_d.py 1250000
 fi
