@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <random>
 #include <atomic>
 #include <map>
 #include <mutex>
@@ -214,16 +215,26 @@ void print_timeline(murr_ctx* c) {
         if (t[4 * g]) t0 = std::min(t0, t[4 * g]);
     std::vector<double> st, b0, en, dur;
     std::map<uint32_t, std::pair<double, int>> by_tiles, by_xcc;
+    std::map<uint32_t, std::vector<double>> by_simd;  // decode wave 0's SIMD: durations
+    FILE* dump = nullptr;
+    if (const char* e = std::getenv("MURR_TIMELINE_DUMP")) dump = std::fopen(e, "a");
     for (uint64_t g = 0; g < c->tl_n; g++) {
         if (!t[4 * g]) continue;
         const double s0 = (t[4 * g] - t0) * 0.01, s1 = (t[4 * g + 1] - t0) * 0.01, s2 = (t[4 * g + 2] - t0) * 0.01;
         st.push_back(s0), b0.push_back(s1 - s0), en.push_back(s2), dur.push_back(s2 - s0);
-        const uint32_t tiles = (uint32_t)(t[4 * g + 3] & 0xFFFF), xcc = (uint32_t)(t[4 * g + 3] >> 48) & 0xF;
+        const uint64_t w = t[4 * g + 3];
+        const uint32_t tiles = (uint32_t)(w & 0xFFFF), xcc = (uint32_t)(w >> 48) & 0xF;
+        const uint32_t hwid = (uint32_t)(w >> 16);  // HW_ID: simd [5:4], cu [11:8], sh [12], se [15:13]
         auto& a = by_tiles[tiles];
         a.first = std::max(a.first, s2), a.second++;
         auto& x = by_xcc[xcc];
         x.first = std::max(x.first, s2), x.second++;
+        by_simd[(hwid >> 4) & 3].push_back(s2 - s0);
+        if (dump)
+            std::fprintf(dump, "%llu,%.2f,%.2f,%.2f,%u,%u,%u,%u,%u,%u\n", (unsigned long long)g, s0, s1, s2, tiles, xcc,
+                         (hwid >> 13) & 7, (hwid >> 12) & 1, (hwid >> 8) & 15, (hwid >> 4) & 3);
     }
+    if (dump) std::fclose(dump);
     auto pct = [](std::vector<double> v, const char* name) {
         std::sort(v.begin(), v.end());
         if (v.empty()) return;
@@ -238,6 +249,11 @@ void print_timeline(murr_ctx* c) {
     pct(en, "end");
     for (auto& kv : by_tiles) std::fprintf(stderr, "  tiles %u: %d workgroups, last end %.2f us\n", kv.first, kv.second.second, kv.second.first);
     for (auto& kv : by_xcc) std::fprintf(stderr, "  xcc %u: %d workgroups, last end %.2f us\n", kv.first, kv.second.second, kv.second.first);
+    for (auto& kv : by_simd) {
+        char nm[32];
+        std::snprintf(nm, sizeof nm, "dur simd%u", kv.first);
+        pct(kv.second, nm);
+    }
 }
 #endif
 
@@ -1044,11 +1060,13 @@ int decode_enqueue_jit(murr_ctx* c, const murr_segment_t* seg, const JitLayout* 
     // (virtual) blocks of local mode: whole blocks, or cuts every V rows (a
     // multiple of the index stride, about 8 per workgroup for balance)
     std::vector<JitSeg> lsegs;
+    uint64_t vrows = 0;  // rows per virtual block (cut mode)
     if (local) {
         const uint64_t S = nu_layout ? std::max<uint32_t>(stride, 1) : K.tr;  // (stride checked when cut)
         uint64_t V = std::max<uint64_t>(K.tr, (total_rows + 8 * G - 1) / (8 * G));
         V = (V + S - 1) / S * S;
         if (O.vrows) V = std::max<uint64_t>(S, (uint64_t)O.vrows / S * S);
+        vrows = V;
         for (uint32_t b = 0; b < nblocks; b++) {
             const uint64_t n = blocks[b].n_rows;
             if (!n) continue;
@@ -1083,6 +1101,45 @@ int decode_enqueue_jit(murr_ctx* c, const murr_segment_t* seg, const JitLayout* 
     if (O.grid == 0xFFFFFFFFu) grid_local = lsegs.size();
     else if (O.grid) grid_local = std::min<uint64_t>(O.grid, lsegs.size());
     const uint64_t grid = std::max<uint64_t>(1, local ? grid_local : std::min<uint64_t>(G_split, nseg));
+    // Cut mode: neighbouring virtual blocks share output lines (a 128-row
+    // piece of a validity bitmap is 16 B of a 128-B line, a string run's ends
+    // are partial lines).  Dealt g, g + G, ... in index order, the eight
+    // pieces of a line came from eight XCDs (workgroup g runs on XCD g % 8),
+    // each L2 writing its piece back as a partial line.  Runs of eight
+    // consecutive virtual blocks go to workgroups of one XCD instead, so a
+    // line's pieces meet in one L2.
+    uint32_t xorder = cut && grid % 8 == 0 && lsegs.size() >= 64 && vrows < 1024 ? 1u : 0u;
+#ifdef MURR_TUNING
+    // 0 index order, 1 runs of 8 round-robin over the XCDs, 2 the same runs
+    // with each 8 runs' XCDs in a pseudo-random order
+    if (const char* e = std::getenv("MURR_XORDER")) xorder = xorder ? (uint32_t)std::atoi(e) : 0u;
+#endif
+    if (xorder) {
+        const uint64_t nv = lsegs.size();
+        std::vector<std::vector<uint64_t>> pos(8), vb(8);
+        for (uint64_t p = 0; p < nv; p++) pos[(p % grid) % 8].push_back(p);
+        uint32_t perm[8] = {0, 1, 2, 3, 4, 5, 6, 7};
+        for (uint64_t k = 0; k < nv; k++) {
+            const uint64_t m = k / 8;
+            if (xorder == 2 && k % 64 == 0) {
+                std::mt19937 rng((uint32_t)(m * 2654435761u + 12345u));
+                std::shuffle(perm, perm + 8, rng);
+            }
+            vb[xorder == 2 ? perm[m % 8] : m % 8].push_back(k);
+        }
+        std::vector<JitSeg> out(nv);
+        std::vector<uint64_t> free_pos, free_vb;
+        for (uint32_t x = 0; x < 8; x++) {
+            const size_t m = std::min(pos[x].size(), vb[x].size());
+            for (size_t i = 0; i < m; i++) out[pos[x][i]] = lsegs[vb[x][i]];
+            free_pos.insert(free_pos.end(), pos[x].begin() + m, pos[x].end());
+            free_vb.insert(free_vb.end(), vb[x].begin() + m, vb[x].end());
+        }
+        std::sort(free_pos.begin(), free_pos.end());
+        std::sort(free_vb.begin(), free_vb.end());
+        for (size_t i = 0; i < free_pos.size(); i++) out[free_pos[i]] = lsegs[free_vb[i]];
+        lsegs.swap(out);
+    }
     // Local mode with several (virtual) blocks per workgroup: the first share
     // dealt statically, the rest claimed at run time from eight per-XCD pools
     // (murr_jit_kernel.hip dyn_claim), so the launch does not end with its
