@@ -1114,14 +1114,18 @@ int decode_enqueue_jit(murr_ctx* c, const murr_segment_t* seg, const JitLayout* 
     // with each 8 runs' XCDs in a pseudo-random order
     if (const char* e = std::getenv("MURR_XORDER")) xorder = xorder ? (uint32_t)std::atoi(e) : 0u;
 #endif
+    uint64_t xrun = 8;  // virtual blocks per run
+#ifdef MURR_TUNING
+    if (const char* e = std::getenv("MURR_XRUN")) xrun = std::max(1, std::atoi(e));
+#endif
     if (xorder) {
         const uint64_t nv = lsegs.size();
         std::vector<std::vector<uint64_t>> pos(8), vb(8);
         for (uint64_t p = 0; p < nv; p++) pos[(p % grid) % 8].push_back(p);
         uint32_t perm[8] = {0, 1, 2, 3, 4, 5, 6, 7};
         for (uint64_t k = 0; k < nv; k++) {
-            const uint64_t m = k / 8;
-            if (xorder == 2 && k % 64 == 0) {
+            const uint64_t m = k / xrun;
+            if (xorder == 2 && k % (8 * xrun) == 0) {
                 std::mt19937 rng((uint32_t)(m * 2654435761u + 12345u));
                 std::shuffle(perm, perm + 8, rng);
             }

@@ -638,6 +638,26 @@ DEV void emit_payload(const RowBuild& B, Emit& E, const StrStage& S, const LAS u
 #else
 #define MJE_WPE_ATTR
 #endif
+// A workgroup per tile: workgroup g runs on XCD (g + c) % 8 for a launch-wide
+// c, so tiles dealt in index order put neighbouring tiles -- whose output
+// spans share a partial line at each end -- on different XCDs.  Runs of
+// MJE_XRUN consecutive tiles can go to workgroups of one XCD instead (a
+// bijection on the first multiple of 8 * MJE_XRUN tiles; the rest as is).
+// Tuning only: neutral on the config B and C column sets, config E 0.335 vs
+// 0.323 ms at runs of 8 (profiles/r04/probes/ab23.txt), so off.
+#ifndef MJE_XRUN
+#define MJE_XRUN 1
+#endif
+namespace mje {
+DEV uint64_t tile_of(uint64_t g, uint64_t total) {
+    if (MJE_XRUN <= 1 || gridDim.x != total) return g;
+    constexpr uint64_t R = MJE_XRUN, P = 8 * R;
+    if (g >= total / P * P) return g;
+    const uint64_t x = g % 8, r = g / 8;  // XCD slot, rank on that XCD
+    return (r / R) * P + x * R + (r % R);
+}
+}  // namespace mje
+
 extern "C" __global__ void __launch_bounds__(MJE_TILE) MJE_WPE_ATTR murr_jit_encode(mje::Args) {
     using namespace mje;
     __shared__ __attribute__((aligned(16))) uint32_t stage[STAGE / 4 + 8];
@@ -648,7 +668,8 @@ extern "C" __global__ void __launch_bounds__(MJE_TILE) MJE_WPE_ATTR murr_jit_enc
     const CAS Args* A = args();
     const uint64_t n_rows = A->n_rows, total_tiles = A->total_tiles, out_cap = A->out_cap;
 
-    for (uint64_t t = blockIdx.x; t < total_tiles; t += gridDim.x) {
+    for (uint64_t t0 = blockIdx.x; t0 < total_tiles; t0 += gridDim.x) {
+        const uint64_t t = tile_of(t0, total_tiles);
         const uint64_t r0 = t * TILE;
         const uint32_t nr = (uint32_t)min((uint64_t)TILE, n_rows - r0);
         const bool active = tid < nr;
