@@ -14,6 +14,8 @@
 #include <mutex>
 #include <set>
 #include <chrono>
+#include <condition_variable>
+#include <thread>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -2418,6 +2420,77 @@ void murr_builder_free(murr_builder_t* b) {
 // split 12.4-12.9 (config B, pinned sources).  Tuning builds keep the others:
 // MURR_HSTREAM_DMA=1, MURR_HSTREAM_H2D=kernel.
 
+// Host copies of pageable batches into pinned staging, split over a few
+// worker threads and the caller (one core copies ~2.6 MB -- a config B batch --
+// in ~130 us, longer than the device needs for the batch).  Workers sleep
+// between batches; a copy is cut into 256 KiB pieces taken off an atomic
+// counter.
+struct CopyPool {
+    struct Piece {
+        uint8_t* dst;
+        const uint8_t* src;
+        uint64_t n;
+    };
+    std::vector<std::thread> th;
+    std::mutex m;
+    std::condition_variable cv;
+    std::vector<Piece> job;
+    std::atomic<size_t> next{0}, done{0};
+    uint64_t gen = 0;
+    bool stop = false;
+
+    explicit CopyPool(unsigned n) {
+        try {
+            for (unsigned i = 0; i < n; i++) th.emplace_back([this] { work(); });
+        } catch (...) {
+            halt();  // (the threads already started end before the exception leaves)
+            throw;
+        }
+    }
+    ~CopyPool() { halt(); }
+    void halt() {
+        {
+            std::lock_guard<std::mutex> g(m);
+            stop = true;
+        }
+        cv.notify_all();
+        for (auto& t : th)
+            if (t.joinable()) t.join();
+    }
+    void drain() {
+        for (size_t i; (i = next.fetch_add(1)) < job.size(); done.fetch_add(1))
+            std::memcpy(job[i].dst, job[i].src, job[i].n);
+    }
+    void work() {
+        uint64_t seen = 0;
+        for (;;) {
+            {
+                std::unique_lock<std::mutex> g(m);
+                cv.wait(g, [&] { return stop || gen != seen; });
+                if (stop) return;
+                seen = gen;
+            }
+            drain();
+        }
+    }
+    // copy every (dst, src, n) of `parts`; returns when all bytes are copied
+    void copy(const std::vector<Piece>& parts) {
+        constexpr uint64_t kPiece = 256 << 10;
+        {
+            std::lock_guard<std::mutex> g(m);
+            job.clear();
+            for (const Piece& p : parts)
+                for (uint64_t o = 0; o < p.n; o += kPiece) job.push_back(Piece{p.dst + o, p.src + o, std::min(kPiece, p.n - o)});
+            next.store(0);
+            done.store(0);
+            gen++;
+        }
+        cv.notify_all();
+        drain();
+        while (done.load() < job.size()) std::this_thread::yield();
+    }
+};
+
 struct HSlot {
     murr_ctx* c = nullptr;
     uint8_t* hin = nullptr;  // pinned staging: blobs | row offsets (unpinned sources)
@@ -2446,6 +2519,8 @@ struct murr_hstream {
     hipStream_t s_h2d = nullptr, s_d2h = nullptr;
     bool fused = true;            // D2H (and H2D unless `h2d_engine`) by segment-copy kernels on the slot streams
     bool h2d_engine = true;       // (fused) H2D of batches >= kEngineMinBytes by copy-engine copies on the slot stream
+    std::unique_ptr<CopyPool> pool;  // pageable batches' staging copies (created on the first large one)
+    bool pool_failed = false;        // (no threads: single-threaded copies)
     uint64_t head = 0, tail = 0;  // batches submitted / returned
     murr_hstream_stats_t stats{};
 };
@@ -2453,6 +2528,8 @@ struct murr_hstream {
 namespace {
 
 constexpr uint64_t kEngineMinBytes = 1ull << 20;
+constexpr uint64_t kPoolMinBytes = 1ull << 20;  // pageable batches from here are staged by the copy pool
+constexpr unsigned kPoolThreads = 3;             // workers (the caller copies too)
 
 // The device address of pinned host bytes (hipHostMalloc / hipHostRegister),
 // or null when `p` is not pinned memory the device can read.
@@ -2498,8 +2575,20 @@ int hstream_enqueue(murr_hstream* h, HSlot& s, const uint8_t* data, const uint64
         // one host copy into the slot's pinned staging (the caller may reuse
         // its buffers as soon as submit returns)
         if (!grow_pinned(c, &s.hin, &s.hin_cap, dbytes + obytes, 0)) return set_err(err, MURR_E_HIP);
-        if (head + bytes) std::memcpy(s.hin, src_data, head + bytes);
-        std::memcpy(s.hin + dbytes, row_off, obytes);
+        if (head + bytes + obytes >= kPoolMinBytes && !h->pool && !h->pool_failed) {
+            try {
+                h->pool.reset(new CopyPool(kPoolThreads));
+            } catch (...) {
+                h->pool_failed = true;
+            }
+        }
+        if (h->pool && head + bytes + obytes >= kPoolMinBytes) {
+            h->pool->copy({CopyPool::Piece{s.hin, src_data, head + bytes},
+                           CopyPool::Piece{s.hin + dbytes, (const uint8_t*)row_off, obytes}});
+        } else {
+            if (head + bytes) std::memcpy(s.hin, src_data, head + bytes);
+            std::memcpy(s.hin + dbytes, row_off, obytes);
+        }
         src_data = s.hin;
         src_off = (const uint64_t*)(s.hin + dbytes);
     }

@@ -217,6 +217,15 @@ std::string prelude(const murr_segment_t* seg) {
           << (w == 0 ? u++ : 0u) << ")";
     }
     o << "\n";
+    // non-temporal value and offset stores for layouts with 1- or 2-byte
+    // columns (a wave's store of such a column is a partial line): C 0.475 ->
+    // 0.465 ms, D shard 0.082 -> 0.074, D at 10 M rows 0.497 -> 0.482; B
+    // (f32 + utf8, whole lines) 0.753 -> 0.772, so plain there
+    // (profiles/r04/probes/ab26.txt)
+    bool narrow = false;
+    for (uint32_t c = 0; c < seg->ncols; c++)
+        narrow |= seg->cols[c].dtype != MURR_UTF8 && seg->cols[c].dtype != MURR_BOOL && seg->cols[c].size <= 2;
+    o << "#define MJ_OUT_NT_LAYOUT " << (narrow ? 1 : 0) << "\n";
     tuning_defs(o);
     return o.str();
 }

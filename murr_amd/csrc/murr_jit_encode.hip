@@ -202,6 +202,11 @@ DEV void or_bytes(LAS uint32_t* stw, uint32_t b, uint32_t v, uint32_t nbytes) {
 // Copy stage[0, span) to out[g0, g0 + span): aligned 16-B stores in the middle,
 // byte stores for the unaligned head and tail (other tiles own their
 // neighbours).
+// The blob stream's whole 16-B pieces: plain stores, or non-temporal
+// (MJE_OUT_NT, tuning).
+#ifndef MJE_OUT_NT
+#define MJE_OUT_NT 0
+#endif
 DEV void write_out(const LAS uint8_t* buf, GAS uint8_t* out, uint64_t g0, uint64_t span, uint32_t tid) {
     const uint64_t g1 = g0 + span;
     const uint64_t a0 = (g0 + 15) & ~15ull, a1 = g1 & ~15ull;
@@ -223,7 +228,11 @@ DEV void write_out(const LAS uint8_t* buf, GAS uint8_t* out, uint64_t g0, uint64
         v.y = __builtin_amdgcn_alignbyte(d2, d1, sh);
         v.z = __builtin_amdgcn_alignbyte(d3, d2, sh);
         v.w = __builtin_amdgcn_alignbyte(d4, d3, sh);
+#if MJE_OUT_NT
+        __builtin_nontemporal_store(v, o + c);
+#else
         o[c] = v;
+#endif
     }
 }
 

@@ -285,12 +285,30 @@ struct HbmSrc {
 #define MJ_ABL_NOFIX 0
 #endif
 // Output stores (written once, read by the caller later): plain, or
-// non-temporal under MJ_OUT_NT (tuning).
+// non-temporal (MJ_OUT_NT 1: fixed-width values and utf8 offsets; the host
+// picks it per layout, murr_jit.cpp prelude; 2: every output store, tuning).
+#ifndef MJ_OUT_NT
+#ifdef MJ_OUT_NT_LAYOUT
+#define MJ_OUT_NT MJ_OUT_NT_LAYOUT
+#else
+#define MJ_OUT_NT 0
+#endif
+#endif
 template <class T> DEV void ost(GAS T* p, T v) {
 #if defined(MJ_OUT_NT) && MJ_OUT_NT
     __builtin_nontemporal_store(v, p);
 #else
     *p = v;
+#endif
+}
+// The other output stores (string bytes at any alignment, validity and bool
+// words): non-temporal from MJ_OUT_NT 2.
+template <class T> DEV void ostu(GAS uint8_t* p, T v) {
+    typedef T __attribute__((aligned(1))) TU;
+#if defined(MJ_OUT_NT) && MJ_OUT_NT >= 2
+    __builtin_nontemporal_store(v, (GAS TU*)p);
+#else
+    *(GAS TU*)p = v;
 #endif
 }
 
@@ -913,8 +931,8 @@ DEV void store_words(Lanes& L, const uint32_t (&vlo)[NCW], const uint32_t (&vhi)
     for (uint32_t j = 0; j < NCW; j++) {
         if (L.proj[j]) {
             const uint64_t v = ((uint64_t)vhi[j] << 32) | vlo[j];
-            gp((uint64_t*)L.vptr[j])[word] = v;
-            if (L.isbool[j]) gp((uint64_t*)L.bptr[j])[word] = ((uint64_t)bhi[j] << 32) | blo[j];
+            ostu<uint64_t>((GAS uint8_t*)gp((uint64_t*)L.vptr[j] + word), v);
+            if (L.isbool[j]) ostu<uint64_t>((GAS uint8_t*)gp((uint64_t*)L.bptr[j] + word), ((uint64_t)bhi[j] << 32) | blo[j]);
             L.nacc[j] += nk - (uint32_t)__popcll(v);
         }
     }
@@ -936,18 +954,18 @@ DEV uint32_t copy_str(const Src& src, GAS uint8_t* vb, uint32_t pay, uint32_t n)
             const uint32_t head = __builtin_amdgcn_alignbyte(w1, w0, sh);
             if (n >= 4) {
                 const uint32_t tail = pick(w0, w1, w2, sh + n - 4);
-                *(GAS u32u*)vb = head;
-                *(GAS u32u*)(vb + n - 4) = tail;
+                ostu<uint32_t>(vb, head);
+                ostu<uint32_t>(vb + n - 4, tail);
                 return head | tail;
             }
             if (n >= 2) {
                 const uint32_t t2 = pick(w0, w1, w2, sh + n - 2) & 0xFFFFu;
-                *(GAS u16u*)vb = (uint16_t)head;
-                *(GAS u16u*)(vb + n - 2) = (uint16_t)t2;
+                ostu<uint16_t>(vb, (uint16_t)head);
+                ostu<uint16_t>(vb + n - 2, (uint16_t)t2);
                 return (head & 0xFFFFu) | t2;
             }
             if (n == 1) {
-                *vb = (uint8_t)head;
+                ostu<uint8_t>(vb, (uint8_t)head);
                 return head & 0xFFu;
             }
             return 0u;
@@ -969,10 +987,10 @@ DEV uint32_t copy_str(const Src& src, GAS uint8_t* vb, uint32_t pay, uint32_t n)
             const uint32_t y0 = p[d1], y1 = p[d1 + 1], y2 = p[d1 + 2];
             const uint32_t lo0 = __builtin_amdgcn_alignbyte(x1, x0, s0), hi0 = __builtin_amdgcn_alignbyte(x2, x1, s0);
             const uint32_t lo1 = __builtin_amdgcn_alignbyte(y1, y0, s1), hi1 = __builtin_amdgcn_alignbyte(y2, y1, s1);
-            *(GAS u64u*)(vb + at0) = ((uint64_t)hi0 << 32) | lo0;
+            ostu<uint64_t>(vb + at0, ((uint64_t)hi0 << 32) | lo0);
             hib |= lo0 | hi0;
             if (two) {
-                *(GAS u64u*)(vb + at1) = ((uint64_t)hi1 << 32) | lo1;
+                ostu<uint64_t>(vb + at1, ((uint64_t)hi1 << 32) | lo1);
                 hib |= lo1 | hi1;
             }
             if (q + 16 >= n) break;
@@ -984,18 +1002,18 @@ DEV uint32_t copy_str(const Src& src, GAS uint8_t* vb, uint32_t pay, uint32_t n)
 #pragma unroll 1
         for (; q + 4 <= n; q += 4) {
             const uint32_t v = src.u32(pay + q);
-            *(GAS u32u*)(vb + q) = v;
+            ostu<uint32_t>(vb + q, v);
             hib |= v;
         }
         if (q < n) {
             const uint32_t v = src.u32(pay + n - 4);
-            *(GAS u32u*)(vb + n - 4) = v;
+            ostu<uint32_t>(vb + n - 4, v);
             hib |= v;
         }
     } else {
         for (; q < n; q++) {
             const uint32_t v = src.u8(pay + q);
-            vb[q] = (uint8_t)v;
+            ostu<uint8_t>(vb + q, (uint8_t)v);
             hib |= v;
         }
     }
@@ -1115,13 +1133,13 @@ DEV void release_slot(LAS uint32_t* rel, uint32_t lane) {
 DEV void copy_str_regs(GAS uint8_t* vb, uint32_t w0, uint32_t w1, uint32_t w2, uint32_t sh, uint32_t n) {
     const uint32_t head = __builtin_amdgcn_alignbyte(w1, w0, sh);
     if (n >= 4) {
-        *(GAS u32u*)vb = head;
-        *(GAS u32u*)(vb + n - 4) = pick(w0, w1, w2, sh + n - 4);
+        ostu<uint32_t>(vb, head);
+        ostu<uint32_t>(vb + n - 4, pick(w0, w1, w2, sh + n - 4));
     } else if (n >= 2) {
-        *(GAS u16u*)vb = (uint16_t)head;
-        *(GAS u16u*)(vb + n - 2) = (uint16_t)(pick(w0, w1, w2, sh + n - 2) & 0xFFFFu);
+        ostu<uint16_t>(vb, (uint16_t)head);
+        ostu<uint16_t>(vb + n - 2, (uint16_t)(pick(w0, w1, w2, sh + n - 2) & 0xFFFFu));
     } else if (n == 1) {
-        *vb = (uint8_t)head;
+        ostu<uint8_t>(vb, (uint8_t)head);
     }
 }
 // OR of a string's bytes (n <= 8) from its three aligned dwords (copy_str's return value).
