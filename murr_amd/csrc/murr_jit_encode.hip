@@ -202,10 +202,11 @@ DEV void or_bytes(LAS uint32_t* stw, uint32_t b, uint32_t v, uint32_t nbytes) {
 // Copy stage[0, span) to out[g0, g0 + span): aligned 16-B stores in the middle,
 // byte stores for the unaligned head and tail (other tiles own their
 // neighbours).
-// The blob stream's whole 16-B pieces: plain stores, or non-temporal
-// (MJE_OUT_NT, tuning).
+// The blob stream's whole 16-B pieces: non-temporal stores (written once,
+// read by the caller's own later work): config B's column set 0.219 -> 0.212
+// ms, C 1.037 -> 1.018, E 0.320 -> 0.310 (profiles/r04/probes/ab27.txt).
 #ifndef MJE_OUT_NT
-#define MJE_OUT_NT 0
+#define MJE_OUT_NT 1
 #endif
 DEV void write_out(const LAS uint8_t* buf, GAS uint8_t* out, uint64_t g0, uint64_t span, uint32_t tid) {
     const uint64_t g1 = g0 + span;
