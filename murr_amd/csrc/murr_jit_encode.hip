@@ -99,6 +99,53 @@ DEV Col ldcol(uint32_t c) {
     return r;
 }
 
+// The columns' descriptors in a lane table: field f (values, validity,
+// offsets, offset) of column c is the u64 in lane (f * NCOLS + c) % 64 of VGPR
+// pair (f * NCOLS + c) / 64 -- one pair for up to 16 columns -- loaded once per
+// workgroup by one vector load per pair; a use is two v_readlane per field
+// with a compile-time lane, instead of a chain of scalar loads (the
+// kernel-argument pointer, then the descriptor) and its wait: about 140 scalar
+// loads per wave on config C's column set.  Past 64 columns: scalar loads.
+// On for eight columns or more: config E's ten 0.308 -> 0.299 ms, C's sixteen
+// neutral, B's two 0.210 -> 0.227 (the table's load opens every one-tile
+// workgroup; profiles/r04/probes/ab29.txt).
+#ifndef MJE_TAB
+#define MJE_TAB (NCOLS >= 8)
+#endif
+constexpr uint32_t TABP = MJE_TAB && NCOLS <= 64 ? (4 * NCOLS + 63) / 64 : 0;  // VGPR pairs (0: scalar loads)
+struct ColTab {
+    uint32_t lo[TABP ? TABP : 1], hi[TABP ? TABP : 1];
+};
+DEV ColTab load_tab(uint32_t lane) {
+    ColTab t;
+#pragma unroll
+    for (uint32_t j = 0; j < TABP; j++) {
+        const uint32_t L = 64 * j + lane, f = L / NCOLS, c = L % NCOLS;
+        uint64_t v = 0;
+        if (f < 4) v = *((const GAS uint64_t*)((const GAS Col*)args()->cols + c) + f);
+        t.lo[j] = (uint32_t)v;
+        t.hi[j] = (uint32_t)(v >> 32);
+    }
+    return t;
+}
+template <uint32_t C> DEV Col tcol(const ColTab& t) {
+    if constexpr (TABP == 0) {
+        return ldcol(C);
+    } else {
+        auto rl64 = [&](uint32_t f) {
+            const uint32_t L = f * NCOLS + C;
+            return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(t.hi[L / 64], L % 64) << 32) |
+                   (uint64_t)(uint32_t)__builtin_amdgcn_readlane(t.lo[L / 64], L % 64);
+        };
+        Col r;
+        r.values = (const uint8_t*)rl64(0);
+        r.validity = (const uint8_t*)rl64(1);
+        r.offsets = (const int32_t*)rl64(2);
+        r.offset = rl64(3);
+        return r;
+    }
+}
+
 // Arrow validity (null buffer absent = all valid).
 DEV bool valid(const Col& c, uint64_t e) {
     if (!c.validity) return true;
@@ -278,6 +325,7 @@ struct StrStage {
     bool on;
 };
 struct RowBuild {
+    ColTab t;  // the columns' descriptors (load_tab)
     Row r;
     uint32_t vmask[(NCOLS + 31) / 32 ? (NCOLS + 31) / 32 : 1];  // valid bits, segment order
     uint32_t pos;
@@ -288,7 +336,7 @@ struct RowBuild {
     uint32_t x[NCOLS ? NCOLS : 1], xh[NCOLS ? NCOLS : 1];  // fixed-width values as loaded (xh: high dword of 8-byte ones)
 };
 
-DEV Bits load_bits(uint64_t rw, uint32_t lane) {
+DEV Bits load_bits(uint64_t rw, uint32_t lane, const ColTab& tab) {
     Bits b{0u, 0u, 0ull};
     if constexpr (VBITS) {
         // lane j's bitmap and element offset, picked from the columns'
@@ -299,7 +347,7 @@ DEV Bits load_bits(uint64_t rw, uint32_t lane) {
         bool any = false;
 #define MJE_BM(C, KIND, SOFF, U)                                                          \
         {                                                                                 \
-            const Col c = ldcol(C);                                                       \
+            const Col c = tcol<C>(tab);                                                   \
             any = any || c.validity || KIND == 9;                                         \
             if (lane == C) { bm = c.validity; eoff = c.offset; }                          \
             if (KIND == 9 && lane == NCOLS + bool_ord(C)) { bm = c.values; eoff = c.offset; } \
@@ -355,7 +403,7 @@ DEV bool valid_of(const Col& c, uint64_t rw, uint32_t lane, const Bits& bits) {
 
 template <uint32_t C, uint32_t KIND, uint32_t SOFF, uint32_t U> DEV void ld_offs(RowBuild& B, uint64_t row) {
     if constexpr (KIND == 0) {
-        const Col c = ldcol(C);
+        const Col c = tcol<C>(B.t);
         const uint64_t e = c.offset + row;
         B.s0[U] = gp(c.offsets)[e];
         B.s1[U] = gp(c.offsets)[e + 1];
@@ -364,7 +412,7 @@ template <uint32_t C, uint32_t KIND, uint32_t SOFF, uint32_t U> DEV void ld_offs
 
 template <uint32_t C, uint32_t KIND, uint32_t SOFF, uint32_t U> DEV void ld_fixed(RowBuild& B, uint64_t row) {
     if constexpr (KIND != 0 && KIND != 9) {
-        const Col c = ldcol(C);
+        const Col c = tcol<C>(B.t);
         const uint64_t e = c.offset + row;
         if constexpr (KIND == 8) {
             const GAS uint32_t* p = (const GAS uint32_t*)(gp(c.values) + e * 8);
@@ -386,7 +434,7 @@ template <uint32_t C, uint32_t KIND, uint32_t SOFF, uint32_t U> DEV void ld_fixe
 template <uint32_t C, uint32_t KIND, uint32_t SOFF, uint32_t U>
 DEV void ld_str(RowBuild& B, uint64_t rw, uint32_t lane, const Bits& bits, bool staged) {
     if constexpr (KIND == 0) {
-        const Col c = ldcol(C);
+        const Col c = tcol<C>(B.t);
         const bool v = valid_of<C>(c, rw, lane, bits);
         const uint32_t len = v ? (uint32_t)(B.s1[U] - B.s0[U]) : 0u;
         const uint64_t a = v ? (uint64_t)(int64_t)B.s0[U] : 0u;
@@ -409,7 +457,7 @@ template <uint32_t C, uint32_t KIND, uint32_t SOFF, uint32_t U>
 DEV void stage_col(const RowBuild& B, LAS uint8_t* part, uint32_t nact, uint32_t lane, uint32_t& at, StrStage& S) {
     if constexpr (KIND == 0 && SBW > 0) {
         if (!S.on) return;
-        const Col c = ldcol(C);
+        const Col c = tcol<C>(B.t);
         const int32_t first = __builtin_amdgcn_readfirstlane(B.s0[U]);
         const int32_t last = __builtin_amdgcn_readlane(B.s1[U], nact - 1);
         const uint64_t g0 = ((uint64_t)(uintptr_t)gp(c.values) + (uint64_t)(int64_t)first) & ~15ull;
@@ -431,7 +479,7 @@ DEV void stage_col(const RowBuild& B, LAS uint8_t* part, uint32_t nact, uint32_t
 // rw: the wave's first row (uniform)
 template <uint32_t C, uint32_t KIND, uint32_t SOFF, uint32_t U>
 DEV void put_col(RowBuild& B, uint64_t rw, uint32_t lane, const Bits& bits) {
-    const Col c = ldcol(C);
+    const Col c = tcol<C>(B.t);
     const bool v = valid_of<C>(c, rw, lane, bits);
     B.vmask[C / 32] |= (uint32_t)v << (C % 32);
     constexpr uint32_t OFF = BS + SOFF;
@@ -481,7 +529,7 @@ DEV void put_payload(const RowBuild& B, LAS uint32_t* stw, uint32_t rb, uint32_t
     if (!((B.vmask[C / 32] >> (C % 32)) & 1)) return;
     or_bytes(stw, rb + p, n, 4);
     p += 4;
-    const Col c = ldcol(C);
+    const Col c = tcol<C>(B.t);
     const uintptr_t sa_ptr = (uintptr_t)(gp(c.values) + B.ustart[U]);
     const uint32_t sa = (uint32_t)(sa_ptr & 3);
     const GAS uint32_t* w = (const GAS uint32_t*)(sa_ptr - sa);
@@ -610,7 +658,7 @@ DEV void emit_payload(const RowBuild& B, Emit& E, const StrStage& S, const LAS u
     const uint32_t n = B.ulen[U];
     E.put(n, 4);
     if (MJE_ABL_NOSTR) return;
-    const Col c = ldcol(C);
+    const Col c = tcol<C>(B.t);
     const uintptr_t sa_ptr = (uintptr_t)(gp(c.values) + B.ustart[U]);
     const uint32_t sa = (uint32_t)(sa_ptr & 3);
     if constexpr (SBW > 0) {
@@ -678,6 +726,7 @@ extern "C" __global__ void __launch_bounds__(MJE_TILE) MJE_WPE_ATTR murr_jit_enc
     const CAS Args* A = args();
     const uint64_t n_rows = A->n_rows, total_tiles = A->total_tiles, out_cap = A->out_cap;
 
+    const ColTab tab = load_tab(lane);
     for (uint64_t t0 = blockIdx.x; t0 < total_tiles; t0 += gridDim.x) {
         const uint64_t t = tile_of(t0, total_tiles);
         const uint64_t r0 = t * TILE;
@@ -689,6 +738,7 @@ extern "C" __global__ void __launch_bounds__(MJE_TILE) MJE_WPE_ATTR murr_jit_enc
         const uint64_t t_pre = NUTF8 ? ((const GAS uint64_t*)A->lookback)[t] : 0;
 
         RowBuild B;
+        B.t = tab;
 #pragma unroll
         for (uint32_t k = 0; k <= NR; k++) B.r.w[k] = 0;
 #pragma unroll
@@ -698,7 +748,7 @@ extern "C" __global__ void __launch_bounds__(MJE_TILE) MJE_WPE_ATTR murr_jit_enc
 #define MJE_DO_OFFS(C, KIND, SOFF, U) ld_offs<C, KIND, SOFF, U>(B, row);
         MJE_COLS(MJE_DO_OFFS)
 #undef MJE_DO_OFFS
-        const Bits bits = load_bits(rw, lane);
+        const Bits bits = load_bits(rw, lane, tab);
         // the wave's string ranges into LDS (issued before the fixed-width
         // loads, so the compiler's counted waits for those cover them too)
         StrStage S;
@@ -807,7 +857,7 @@ extern "C" __global__ void __launch_bounds__(MJE_TILE) MJE_WPE_ATTR murr_jit_enc
     if (KIND == 0 && ((B.vmask[C / 32] >> (C % 32)) & 1)) {                             \
         const uint32_t n = B.ulen[U];                                                   \
         for (uint32_t b = 0; b < 4; b++) o[p + b] = (uint8_t)(n >> (8 * b));            \
-        const GAS uint8_t* s = gp(ldcol(C).values) + B.ustart[U];                       \
+        const GAS uint8_t* s = gp(tcol<C>(B.t).values) + B.ustart[U];                       \
         for (uint32_t b = 0; b < n; b++) o[p + 4 + b] = s[b];                           \
         p += 4 + n;                                                                     \
     }

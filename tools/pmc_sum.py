@@ -1,4 +1,5 @@
-"""Per-dispatch averages of PMC counters for kernels matching a pattern."""
+"""Per-dispatch averages of PMC counters for kernels matching a pattern
+(a substring, or the whole name when the pattern ends with '$')."""
 import csv
 import glob
 import sys
@@ -9,7 +10,8 @@ vals = defaultdict(list)
 for f in sorted(glob.glob(f"{d}/**/*counter_collection.csv", recursive=True)):
     per = defaultdict(float)
     for r in csv.DictReader(open(f)):
-        if pat in r["Kernel_Name"]:
+        name = r["Kernel_Name"]
+        if (name == pat[:-1]) if pat.endswith("$") else (pat in name):
             per[(r["Dispatch_Id"], r["Counter_Name"])] += float(r["Counter_Value"])
     for (_, cn), v in per.items():
         vals[cn].append(v)
