@@ -311,6 +311,22 @@ template <class T> DEV void ostu(GAS uint8_t* p, T v) {
     *(GAS TU*)p = v;
 #endif
 }
+// 1-byte values (a wave's store is half a line): like the wider ones
+// (MJ_OUT_NT_W1 1), or plain (0; tuning).
+#ifndef MJ_OUT_NT_W1
+#define MJ_OUT_NT_W1 1
+#endif
+// Validity and bool words: non-temporal with MJ_OUT_NT 2 or MJ_OUT_NT_VAL (tuning).
+#ifndef MJ_OUT_NT_VAL
+#define MJ_OUT_NT_VAL 0
+#endif
+DEV void ostw(GAS uint64_t* p, uint64_t v) {
+#if (defined(MJ_OUT_NT) && MJ_OUT_NT >= 2) || MJ_OUT_NT_VAL
+    __builtin_nontemporal_store(v, p);
+#else
+    *p = v;
+#endif
+}
 
 // ---- LDS-DMA (inline asm: kept out of the compiler's waitcnt bookkeeping;
 // the loader wave waits for exactly its own DMA with counted vmcnt) ----------
@@ -931,8 +947,8 @@ DEV void store_words(Lanes& L, const uint32_t (&vlo)[NCW], const uint32_t (&vhi)
     for (uint32_t j = 0; j < NCW; j++) {
         if (L.proj[j]) {
             const uint64_t v = ((uint64_t)vhi[j] << 32) | vlo[j];
-            ostu<uint64_t>((GAS uint8_t*)gp((uint64_t*)L.vptr[j] + word), v);
-            if (L.isbool[j]) ostu<uint64_t>((GAS uint8_t*)gp((uint64_t*)L.bptr[j] + word), ((uint64_t)bhi[j] << 32) | blo[j]);
+            ostw(gp((uint64_t*)L.vptr[j]) + word, v);
+            if (L.isbool[j]) ostw(gp((uint64_t*)L.bptr[j]) + word, ((uint64_t)bhi[j] << 32) | blo[j]);
             L.nacc[j] += nk - (uint32_t)__popcll(v);
         }
     }
@@ -1325,7 +1341,8 @@ DEV void decode_tile(const Src& src, const Tile& T, const LAS uint32_t* ro, LAS 
                     if constexpr (W_ == 8) ost(gp((uint64_t*)o.values) + row, ((uint64_t)hi << 32) | lo); \
                     else if constexpr (W_ == 4) ost(gp((uint32_t*)o.values) + row, lo);                 \
                     else if constexpr (W_ == 2) ost(gp((uint16_t*)o.values) + row, (uint16_t)lo);       \
-                    else ost(gp((uint8_t*)o.values) + row, (uint8_t)lo);                                \
+                    else if constexpr (MJ_OUT_NT_W1) ost(gp((uint8_t*)o.values) + row, (uint8_t)lo);    \
+                    else gp((uint8_t*)o.values)[row] = (uint8_t)lo;                                     \
                 }                                                                                       \
             }                                                                                           \
         }                                                                                               \
