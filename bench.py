@@ -30,7 +30,7 @@ sys.path.insert(0, ROOT)
 
 import murr_amd  # noqa: E402  (the HIP library is loaded in main(), after the rank spawn decision)
 from murr_amd import _abi, synth  # noqa: E402
-from murr_amd.device import Context, DecodeOutputs, DecodePlan, DeviceBlock, device_count, encode_batch, \
+from murr_amd.device import Context, DecodeOutputs, DecodePlan, DeviceBlock, DeviceBuffer, device_count, encode_batch, \
     encode_block, parse_opts, set_default_opts  # noqa: E402
 from murr_amd.schema import DTypeName as D, SegmentSchema  # noqa: E402
 from murr_amd.shard import Group, shard_rows  # noqa: E402
@@ -269,6 +269,80 @@ def check_gpus(local_rank, world):
         raise SystemExit(f"local rank {local_rank} has no GPU of its own: {ndev} visible, WORLD_SIZE {world}")
 
 
+class _View(DeviceBuffer):
+    """A piece of an arena buffer (the arena owns the memory)."""
+
+    def __init__(self, parent: DeviceBuffer, offset: int, nbytes: int):
+        self.ctx, self.ptr, self.nbytes, self._parent = parent.ctx, parent.ptr + offset, nbytes, parent
+
+    def free(self):
+        self.ptr = 0
+
+
+class _Arena:
+    """Pieces of one device buffer, each at a multiple of `align` bytes."""
+
+    def __init__(self, ctx, sizes, align: int):
+        self.offs, off = [], 0
+        for n in sizes:
+            self.offs.append(off)
+            off += (n + align - 1) // align * align
+        self.buf = ctx.alloc(max(off, 16))
+        self.sizes = list(sizes)
+
+    def view(self, i: int) -> _View:
+        return _View(self.buf, self.offs[i], self.sizes[i])
+
+
+def arena_blocks(ctx, b0: DeviceBlock, K: int, align: int):
+    """K resident copies of a block in three arenas (blobs, row offsets,
+    utf8 indexes), each piece at a multiple of `align` bytes (--arena)."""
+    nd, no = b0.data_bytes + 16, 8 * (b0.n_rows + 1)
+    ad, ao = _Arena(ctx, [nd] * K, align), _Arena(ctx, [no] * K, align)
+    au = _Arena(ctx, [b0.uidx.nbytes] * K, 256) if b0.uidx is not None else None
+    out = []
+    for i in range(K):
+        d, o = ad.view(i), ao.view(i)
+        d.copy_from(b0.data, b0.data_bytes)
+        o.copy_from(b0.row_off, no)
+        u = None
+        if au is not None:
+            u = au.view(i)
+            u.copy_from(b0.uidx, b0.uidx.nbytes)
+        out.append(DeviceBlock(d, o, b0.n_rows, b0.data_bytes, u, b0.stride))
+    return out
+
+
+class ArenaOutputs(DecodeOutputs):
+    """DecodeOutputs with every buffer a piece of one arena (--arena)."""
+
+    def __init__(self, ctx, segment, proj, blocks, align: int):
+        self.ctx, self.proj, self.blocks = ctx, list(proj), blocks
+        np_ = len(self.proj)
+        self.arrays = (_abi.Array * max(len(blocks) * np_, 1))()
+        L = ctx.L
+        plan = []  # (array index, field, bytes)
+        for b, blk in enumerate(blocks):
+            n = blk.n_rows
+            bm = int(L.murr_bitmap_bytes(n))
+            for p, ci in enumerate(self.proj):
+                col = segment.columns[ci]
+                i = b * np_ + p
+                if col.dtype == D.Utf8:
+                    vb = max(blk.data_bytes, 8)
+                    plan.append((i, "offsets", (n + 1) * 4))
+                    self.arrays[i].values_cap = vb
+                elif col.dtype == D.Bool:
+                    vb = bm
+                else:
+                    vb = n * col.dtype.size()
+                plan += [(i, "values", max(vb, 8)), (i, "validity", max(bm, 8))]
+        self.arena = _Arena(ctx, [x[2] for x in plan], align)
+        self.bufs = [self.arena.buf]
+        for k, (i, field, _) in enumerate(plan):
+            setattr(self.arrays[i], field, self.arena.view(k).ptr)
+
+
 def copy_block(ctx, b: DeviceBlock) -> DeviceBlock:
     """A resident copy of a block (and its index), device to device."""
     data, off = ctx.alloc(b.data_bytes + 16), ctx.alloc(8 * (b.n_rows + 1))
@@ -367,7 +441,10 @@ def run_decode(args, dist, rank, world, local_rank):
             dblob, doff, blen = encode_batch(ctx, seg, dcols, rows)
             b0 = DeviceBlock(dblob, doff, rows, blen)
         del dcols
-        blocks = [b0] + [copy_block(ctx, b0) for _ in range(K - 1)]  # K resident blocks
+        if args.arena:  # K resident blocks in arenas (blobs / row offsets / outputs each one buffer)
+            blocks = arena_blocks(ctx, b0, K, args.arena)
+        else:
+            blocks = [b0] + [copy_block(ctx, b0) for _ in range(K - 1)]  # K resident blocks
         ix_stride = b0.stride
     ctx.sync()
     build_s = time.perf_counter() - t_build
@@ -379,7 +456,10 @@ def run_decode(args, dist, rank, world, local_rank):
     # launch and read-back work overlaps the previous step's kernel, as a
     # serving loop would; on the GPU the steps run one after the other (one
     # stream).  --sync-steps: one set, each step waited for (the A/B).
-    out_sets = [DecodeOutputs(ctx, seg, proj, blocks), DecodeOutputs(ctx, seg, proj, blocks)]
+    if args.arena:
+        out_sets = [ArenaOutputs(ctx, seg, proj, blocks, args.arena) for _ in range(2)]
+    else:
+        out_sets = [DecodeOutputs(ctx, seg, proj, blocks), DecodeOutputs(ctx, seg, proj, blocks)]
     if rt is not None:
         names = [seg.columns[c].name for c in proj]
 
@@ -991,6 +1071,9 @@ def main():
     ap.add_argument("--depth", type=int, default=4, help="host mode: pipeline slots (murr_hstream)")
     ap.add_argument("--host-ring", type=int, default=16, help="host mode: distinct source blocks in the pinned ring")
     ap.add_argument("--ipc", action="store_true", help="resident mode: also time the Arrow IPC message path")
+    ap.add_argument("--arena", type=int, default=0,
+                    help="decode mode: the K blocks and their outputs as pieces of arenas aligned to this many bytes "
+                         "(0: one allocation per buffer)")
     ap.add_argument("--uidx-stride", type=int, default=512,
                     help="decode mode: utf8 index stride of each block (0 = no index)")
     ap.add_argument("--table", default="C", choices=["C", "ref"],
