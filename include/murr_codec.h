@@ -279,9 +279,13 @@ int murr_decode_run(murr_plan_t* plan, murr_error_t* err);   /* synchronous */
  * run of a plan in flight at a time; runs of different plans on one context
  * queue in stream order, so a caller alternating two plans (two output sets)
  * launches the next run while the host finishes the previous one.  The
- * context's last kernel time (murr_ctx_last_kernel_ms) is the waited run's.
+ * context's last kernel time (murr_ctx_last_kernel_ms) is that of the plan's
+ * last timed run: one run in MURR_PLAN_TIME_EVERY, the first included, is
+ * bracketed by timing events (an event between back-to-back launches costs
+ * GPU time; plans on the generic kernel time every run).
  * When _wait returns, the run's kernel has ended: its outputs are visible to
  * the host, to other streams and to peer GPUs, not only in stream order. */
+#define MURR_PLAN_TIME_EVERY 4
 int murr_decode_run_async(murr_plan_t* plan);
 int murr_decode_run_wait(murr_plan_t* plan, murr_error_t* err);
 void murr_plan_free(murr_plan_t* plan);

@@ -14,6 +14,7 @@ ROOT = os.path.dirname(HERE)
 # tools/); announced on stderr whenever it is set, so no run swaps it in silently
 LIB_PATH = os.environ.get("MURR_LIB") or os.path.join(HERE, "libmurr_codec.so")
 HEADER = os.path.join(ROOT, "include", "murr_codec.h")
+PLAN_TIME_EVERY = 4  # MURR_PLAN_TIME_EVERY: a prepared plan times one run in this many
 
 # murr_status_t
 OK, E_INVALID_UTF8, E_DTYPE, E_BAD_COLUMN, E_OFFSET_OVERFLOW, E_MALFORMED_ROW, E_CAPACITY, \

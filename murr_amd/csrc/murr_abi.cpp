@@ -913,6 +913,8 @@ bool stride_ok(uint64_t s) { return s >= 64 && s <= (1ull << 30) && (s & (s - 1)
 // arguments per projection round, and a pinned readback buffer.  A run zeroes
 // the counters, launches, reads back the counts: no host-side preparation and
 // no descriptor upload per launch.
+constexpr uint64_t kTimeEvery = MURR_PLAN_TIME_EVERY;  // prepared plans: one timed run in four
+
 struct JitReplay {
     uint8_t* dws = nullptr;        // device workspace: [counter set 0 | descriptors | sink]
     uint8_t* zb2 = nullptr;        // counter set 1 (runs alternate; each launch zeroes the other set)
@@ -925,7 +927,12 @@ struct JitReplay {
     bool split = false, emit = false;
     uint32_t grid = 0, lds = 0, mode = 0;
     std::vector<int32_t*> empty_offsets;  // utf8 offsets of empty blocks: [0] = 0 per run
-    hipEvent_t e0 = nullptr, e1 = nullptr;  // the run's kernel time
+    // Timing: every kTimeEvery-th run (the first included) is bracketed by
+    // e0/t1, the others end with e1 only -- an event recorded between
+    // back-to-back launches costs ~4 us of GPU time (D shard: 0.0810 vs
+    // 0.0766 ms per run, profiles/r04/probes/ab40.txt).
+    hipEvent_t e0 = nullptr, t1 = nullptr, e1 = nullptr;
+    hipEvent_t end = nullptr;               // the in-flight run's last event (t1 or e1)
     bool inflight = false;                  // murr_decode_run_async issued, murr_decode_run_wait not yet
     int set = 0;                            // the in-flight run's counter set
     void release() {
@@ -933,9 +940,10 @@ struct JitReplay {
         if (zb2) (void)hipFree(zb2);
         if (hrb) (void)hipHostFree(hrb);
         if (e0) (void)hipEventDestroy(e0);
+        if (t1) (void)hipEventDestroy(t1);
         if (e1) (void)hipEventDestroy(e1);
         dws = zb2 = hrb = nullptr;
-        e0 = e1 = nullptr;
+        e0 = t1 = e1 = end = nullptr;
     }
 };
 
@@ -1812,7 +1820,8 @@ int murr_decode_plan(murr_ctx_t* c, const murr_segment_t* seg, const uint32_t* p
                 return st;
             }
             P->replay = true;
-            if (hipEventCreate(&P->r.e0) != hipSuccess || hipEventCreate(&P->r.e1) != hipSuccess) {
+            if (hipEventCreate(&P->r.e0) != hipSuccess || hipEventCreate(&P->r.t1) != hipSuccess ||
+                hipEventCreateWithFlags(&P->r.e1, hipEventDisableTiming) != hipSuccess) {
                 P->r.release();
                 jit_layout_unpin(P->jl);
                 return MURR_E_HIP;
@@ -1844,15 +1853,22 @@ int murr_decode_run_async(murr_plan_t* P) {
     c->stats.decodes++;
     // counter sets alternate: this run counts into `set`, which the previous
     // run zeroed (both were zeroed when the plan was made)
-    const int set = (int)(R.runs++ & 1);
+    const uint64_t run = R.runs++;
+    const int set = (int)(run & 1);
     for (int32_t* o : R.empty_offsets) HIPC(hipMemsetAsync(o, 0, 4, c->stream));
     volatile uint64_t* done = (volatile uint64_t*)(R.hrb + R.z_lb);
     *done = 0;
     std::atomic_thread_fence(std::memory_order_seq_cst);
-    HIPC(hipEventRecord(R.e0, c->stream));
+    uint64_t every = kTimeEvery;
+#ifdef MURR_TUNING
+    if (const char* e = std::getenv("MURR_TIME_EVERY")) every = std::max(1, std::atoi(e));  // A/B of the events' cost
+#endif
+    const bool timed = run % every == 0;
+    if (timed) HIPC(hipEventRecord(R.e0, c->stream));
     for (const auto& ka : R.kargs[set])
         HIPC(jit_decode_launch(R.K, R.split, ka.data(), ka.size(), R.grid, R.lds, c->stream));
-    HIPC(hipEventRecord(R.e1, c->stream));
+    R.end = timed ? R.t1 : R.e1;
+    HIPC(hipEventRecord(R.end, c->stream));
     R.set = set;
     R.inflight = true;
     return MURR_OK;
@@ -1881,7 +1897,7 @@ int murr_decode_run_wait(murr_plan_t* P, murr_error_t* err) {
     if (!R.kargs[set].empty()) {
         for (uint64_t spin = 1;; spin++) {
             if (*done) { flagged = true; break; }
-            if ((spin & 4095) == 0 && hipEventQuery(R.e1) == hipSuccess) {
+            if ((spin & 4095) == 0 && hipEventQuery(R.end) == hipSuccess) {
                 flagged = *done != 0;
                 break;
             }
@@ -1895,15 +1911,15 @@ int murr_decode_run_wait(murr_plan_t* P, murr_error_t* err) {
     // visible to the host, other streams and peer GPUs when this returns.
     // The kernel is in its last workgroup's epilogue by now; a next run queued
     // behind it keeps the GPU busy meanwhile.
-    if (flagged) HIPC(hipEventSynchronize(R.e1));
+    if (flagged) HIPC(hipEventSynchronize(R.end));
     if (!flagged) {
         if (!R.kargs[set].empty()) c->stats.readback_fallbacks++;
         HIPC(hipMemcpyAsync(R.hrb, set ? R.zb2 : R.dws, R.z_lb, hipMemcpyDeviceToHost, c->stream));
         HIPC(hipStreamSynchronize(c->stream));
     }
-    c->timed = true;
+    c->timed = true;  // the plan's last timed run (its first run is one)
     c->lk0 = R.e0;
-    c->lk1 = R.e1;
+    c->lk1 = R.t1;
     if (!R.kargs[0].empty()) c->last_kernel = "murr_jit_decode";
     c->stats.last_mode = R.mode;
     c->stats.last_grid = R.grid;

@@ -20,6 +20,12 @@ def test_library_loads_and_exports_every_header_symbol():
     assert sorted(_abi.SIGNATURES) == syms
 
 
+def test_plan_time_every_mirrors_header():
+    import re
+    m = re.search(r"#define MURR_PLAN_TIME_EVERY (\d+)", open(_abi.HEADER).read())
+    assert m and int(m.group(1)) == _abi.PLAN_TIME_EVERY
+
+
 def test_exports_are_c_symbols():
     out = subprocess.run(["nm", "-D", "--defined-only", _abi.LIB_PATH], capture_output=True,
                          text=True, check=True).stdout

@@ -9,7 +9,7 @@ import pytest
 import oracle as O
 from golden_util import assert_array_equal
 from randgen import random_columns
-from murr_amd import SegmentError, synth
+from murr_amd import SegmentError, _abi, synth
 from murr_amd.device import Context, DecodeOutputs, DecodePlan, DeviceBlock, download_array, set_default_opts
 from murr_amd.schema import DTypeName as D, SegmentSchema
 
@@ -135,6 +135,21 @@ def test_two_plans_alternating_async_runs(ctx, kernel_mode):
         outs = plans[s % 2].wait()
         assert ctx.last_kernel_ms() >= 0.0
         check(ctx, seg, oseg, proj, hosts, outs, f"run {s}")
+    # sampled timing: the plan's timed runs (one in PLAN_TIME_EVERY) report
+    # a kernel time, the others leave the last timed run's in place
+    # (plans[0] has run 3 times: its next runs are numbered 3, 4, ...)
+    e = _abi.PLAN_TIME_EVERY
+    ks = []
+    for r in range(3, 3 + 2 * e + 1):
+        plans[0].run()
+        ks.append((r, ctx.last_kernel_ms()))
+    assert all(k > 0.0 for _, k in ks)
+    last = {}
+    for r, k in ks:
+        last.setdefault(r - r % e, []).append(k)
+    for t, group in last.items():  # (the generic kernel's plans time every run)
+        if kernel_mode != "generic":
+            assert len(set(group)) == 1, (t, group)  # untimed runs repeat the timed run's time
     with pytest.raises(Exception):
         plans[0].wait()  # nothing in flight
     plans[0].run_async()
