@@ -786,6 +786,7 @@ def run_encode(args):
     k = float(np.mean(kms))
     print(json.dumps({"mode": "encode", "config": args.enc_config, "kernel": ctx.last_kernel(), "rows": n, "bytes_in": bytes_in, "bytes_out": bytes_out,
                       "kernel_ms_avg": round(k, 4), "ms_per_step": round(el / args.steps * 1e3, 3),
+                      "recounts": ctx.stats()["encode_recounts"],
                       "GB_s_algorithmic": round((bytes_in + bytes_out) / (k * 1e-3) / 1e9, 1),
                       "frac_of_8TBs": round((bytes_in + bytes_out) / (k * 1e-3) / 8e12, 4),
                       "GiB_s_blob_out": round(bytes_out / (k * 1e-3) / GIB, 2)}))

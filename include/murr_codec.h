@@ -173,6 +173,9 @@ typedef struct {
     uint32_t last_shape_r;
     uint64_t readback_fallbacks;  /* prepared runs whose epilogue read-back flag never came
                                      (counts then copied back the ordinary way; 0 normally) */
+    uint64_t encode_recounts;     /* encodes whose utf8 tile sizes, estimated from the offsets and
+                                     validity (exact when null strings are empty), were off and
+                                     recounted by a sizes pass (the encode then ran twice) */
 } murr_ctx_stats_t;
 int murr_ctx_stats(murr_ctx_t* ctx, murr_ctx_stats_t* out);
 

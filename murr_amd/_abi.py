@@ -46,7 +46,7 @@ class Opts(C.Structure):
 class CtxStats(C.Structure):
     _fields_ = [("decodes", C.c_uint64), ("split_retries", C.c_uint64), ("last_mode", C.c_uint32),
                 ("last_grid", C.c_uint32), ("last_shape_nw", C.c_uint32), ("last_shape_r", C.c_uint32),
-                ("readback_fallbacks", C.c_uint64)]
+                ("readback_fallbacks", C.c_uint64), ("encode_recounts", C.c_uint64)]
 
 
 class Block(C.Structure):

@@ -2076,35 +2076,54 @@ int murr_encode_batch_at(murr_ctx_t* c, const murr_segment_t* seg, const murr_co
     a.nutf8 = nutf8;
     a.bs = seg->bitset_size;
     a.cap = seg->capacity;
+    // utf8 tile totals (murr_internal.h kEncSizes*): a utf8 column with a
+    // validity buffer has them estimated first (exact when its null strings
+    // are empty) and recounted by the sizes pass when the kernel finds one off
+    bool inl = true;
+    for (const EncCol& e : ec) inl = inl && (e.dtype != MURR_UTF8 || e.validity == nullptr);
+    uint32_t sizes = inl ? kEncSizesInline : kEncSizesEstimate;
+#ifdef MURR_TUNING
+    if (std::getenv("MURR_ENC_EXACT")) sizes = inl ? kEncSizesInline : kEncSizesPass;  // A/B of the estimate
+#endif
     HIPC(hipEventRecord(c->k0, c->stream));
-    if (tiles) {
-        // persistent grid, co-resident (the utf8 window prefix waits on tiles t-G+1 .. t-1)
-        const int per_cu = ek ? std::max(1, ek->bpc - 1) : c->enc_grid_per_cu;
-        uint64_t grid = std::min<uint64_t>(tiles, (uint64_t)c->cus * per_cu);
-        if (ek) {
-            bool inl = true;
-            for (const EncCol& e : ec) inl = inl && (e.dtype != MURR_UTF8 || e.validity == nullptr);
-            HIPC(jit_encode_launch(ek, a, (uint32_t)grid, c->stream, inl));
-            c->last_kernel = "murr_jit_encode";
-        } else {
-            HIPC(launch_encode(a, (uint32_t)grid, c->stream));
-            c->last_kernel = "encode_kernel";
+    unsigned long long word = 0;
+    uint64_t total = 0;
+    for (;;) {
+        if (tiles) {
+            // persistent grid, co-resident (the utf8 window prefix waits on tiles t-G+1 .. t-1)
+            const int per_cu = ek ? std::max(1, ek->bpc - 1) : c->enc_grid_per_cu;
+            uint64_t grid = std::min<uint64_t>(tiles, (uint64_t)c->cus * per_cu);
+            if (ek) {
+                HIPC(jit_encode_launch(ek, a, (uint32_t)grid, c->stream, sizes));
+                c->last_kernel = "murr_jit_encode";
+            } else {
+                HIPC(launch_encode(a, (uint32_t)grid, c->stream));
+                c->last_kernel = "encode_kernel";
+            }
         }
+        HIPC(hipEventRecord(c->k1, c->stream));  // (after a recount: both runs)
+        HIPC(hipMemcpyAsync(c->hs + rb, c->ws, 8, hipMemcpyDeviceToHost, c->stream));
+        HIPC(hipMemcpyAsync(c->hs + rb + 8, out_row_off + n, 8, hipMemcpyDeviceToHost, c->stream));
+        HIPC(hipStreamSynchronize(c->stream));
+        std::memcpy(&word, c->hs + rb, 8);
+        std::memcpy(&total, c->hs + rb + 8, 8);
+        // an estimate off (or any error under estimates, which may be the
+        // estimate's doing): recount exactly and encode again
+        if (!(ek && nutf8 && sizes == kEncSizesEstimate && word)) break;
+        c->stats.encode_recounts++;
+        sizes = kEncSizesPass;
+        HIPC(hipMemsetAsync(c->ws, 0, zbytes, c->stream));
     }
-    HIPC(hipEventRecord(c->k1, c->stream));
     c->timed = true;
     c->lk0 = c->lk1 = nullptr;
-    HIPC(hipMemcpyAsync(c->hs + rb, c->ws, 8, hipMemcpyDeviceToHost, c->stream));
-    HIPC(hipMemcpyAsync(c->hs + rb + 8, out_row_off + n, 8, hipMemcpyDeviceToHost, c->stream));
-    HIPC(hipStreamSynchronize(c->stream));
-    unsigned long long word;
-    uint64_t total;
-    std::memcpy(&word, c->hs + rb, 8);
-    std::memcpy(&total, c->hs + rb + 8, 8);
     total -= row_base;
     if (blob_len) *blob_len = total;
     if (err) std::memset(err, 0, sizeof *err);
     st = unpack_err(word, err);
+    if (st == kEncStRecount) {  // an exact recount off: a bug, not the input's
+        st = MURR_E_INTERNAL;
+        if (err) err->status = st;
+    }
     if (err) err->block = 0;
     if (st == MURR_E_CAPACITY && err) err->required = total;
     return st;

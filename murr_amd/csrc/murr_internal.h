@@ -187,10 +187,15 @@ uint32_t jit_encode_tile(uint64_t n_rows, uint64_t blob_cap);
 const JitEncKernel* jit_encode_kernel(int device, uint32_t bs, uint32_t cap, const EncCol* cols, uint32_t ncols,
                                       uint32_t stage, uint32_t tile, uint32_t sbw, std::string* why);
 struct EncodeArgs;
-// inline_sizes: no utf8 column has a validity buffer (the scan computes the
-// tile totals; no sizes pass).
+// Tile totals of utf8 layouts: kEncSizesPass (murr_jit_encode_sizes, exact),
+// kEncSizesInline (no utf8 column has a validity buffer: the scan computes
+// them from the offsets, exact), kEncSizesEstimate (the scan estimates them
+// from the offsets and validity popcounts; exact when every null string is
+// empty, checked by the encode kernel).
+enum : uint32_t { kEncSizesPass = 0, kEncSizesInline = 1, kEncSizesEstimate = 2 };
+constexpr int kEncStRecount = 12;  // murr_jit_encode.hip kStRecount
 hipError_t jit_encode_launch(const JitEncKernel* k, const EncodeArgs& a, uint32_t grid, hipStream_t s,
-                             bool inline_sizes);
+                             uint32_t sizes);
 
 void decode_lds_plan(DecodeArgs& a, uint32_t nw, uint32_t kc, uint32_t slots, uint32_t depth);
 bool decode_shape_ok(uint32_t nw, uint32_t kc);

@@ -354,7 +354,12 @@ std::string enc_prelude(uint32_t bs, uint32_t cap, const EncCol* cols, uint32_t 
                         uint32_t tile, uint32_t sbw) {
     std::ostringstream o;
     uint32_t nutf8 = 0;
-    for (uint32_t c = 0; c < ncols; c++) nutf8 += cols[c].dtype == MURR_UTF8;
+    bool uval = false;  // a utf8 column with a validity buffer: estimated tile sizes, checked
+    for (uint32_t c = 0; c < ncols; c++) {
+        nutf8 += cols[c].dtype == MURR_UTF8;
+        uval = uval || (cols[c].dtype == MURR_UTF8 && cols[c].validity);
+    }
+    o << "#define MJE_CHECK " << (uval ? 1 : 0) << "\n";
     o << "#define MJE_BS " << bs << "\n#define MJE_CAP " << cap << "\n#define MJE_NCOLS " << ncols
       << "\n#define MJE_NUTF8 " << nutf8 << "\n#define MJE_STAGE " << stage << "\n#define MJE_TILE " << tile
       << "\n#define MJE_SCAN_PER " << kEncScanPer << "\n#define MJE_SBW " << sbw
@@ -454,7 +459,7 @@ const JitEncKernel* jit_encode_kernel(int device, uint32_t bs, uint32_t cap, con
 }
 
 hipError_t jit_encode_launch(const JitEncKernel* k, const EncodeArgs& a, uint32_t grid, hipStream_t s,
-                             bool inline_sizes) {
+                             uint32_t sizes) {
     EncodeArgs args = a;
     size_t sz = sizeof(args);
     void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &args, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
@@ -465,12 +470,13 @@ hipError_t jit_encode_launch(const JitEncKernel* k, const EncodeArgs& a, uint32_
         const uint32_t groups = (uint32_t)((a.total_tiles + kEncScanPer - 1) / kEncScanPer);
         // (no utf8 column with a validity buffer: the scan derives the tile
         // totals from the offsets itself, murr_jit_encode.hip sizes_inline)
-        hipError_t e = inline_sizes ? hipSuccess
-                                    : hipModuleLaunchKernel(k->fn_sizes, tiles, 1, 1, k->tile, 1, 1, 0, s, nullptr, cfg);
+        hipError_t e = sizes != kEncSizesPass
+                           ? hipSuccess
+                           : hipModuleLaunchKernel(k->fn_sizes, tiles, 1, 1, k->tile, 1, 1, 0, s, nullptr, cfg);
         struct {
             EncodeArgs a;
             uint32_t pass;
-        } sa{a, 0};
+        } sa{a, sizes == kEncSizesEstimate ? 3u : 0u};
         size_t ssz = sizeof(sa);
         void* scfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &sa, HIP_LAUNCH_PARAM_BUFFER_SIZE, &ssz, HIP_LAUNCH_PARAM_END};
         if (e == hipSuccess) e = hipModuleLaunchKernel(k->fn_scan, groups, 1, 1, 1024, 1, 1, 0, s, nullptr, scfg);

@@ -68,7 +68,9 @@ constexpr uint32_t TILE = MJE_TILE, NWAVE = MJE_TILE / 64, BS = MJE_BS, CAP = MJ
                    STAGE = MJE_STAGE;
 constexpr uint32_t FIXED = BS + CAP;
 constexpr uint32_t NR = (FIXED + 3) / 4;  // dwords of the fixed part
-enum : uint32_t { kStCapacity = 6, kStInternal = 10 };
+// kStRecount: a tile's exact size differs from its estimate (never returned:
+// the host recounts with the sizes pass, murr_encode_batch_at)
+enum : uint32_t { kStCapacity = 6, kStInternal = 10, kStRecount = 12 };
 constexpr uint32_t kSpinLimit = 1u << 22;
 
 DEV uint64_t err_key(uint64_t block, uint64_t row, uint32_t col, uint32_t status) {
@@ -706,6 +708,18 @@ DEV void emit_payload(const RowBuild& B, Emit& E, const StrStage& S, const LAS u
 #ifndef MJE_XRUN
 #define MJE_XRUN 1
 #endif
+#ifndef MJE_CHECK
+#define MJE_CHECK 0
+#endif
+namespace mje {
+DEV bool sizes_inline() {
+    bool ok = true;
+#define MJE_NOVAL(C, KIND, SOFF, U) if (KIND == 0) ok = ok && ((const CAS Col*)args()->cols + C)->validity == nullptr;
+    MJE_COLS(MJE_NOVAL)
+#undef MJE_NOVAL
+    return ok;
+}
+}  // namespace mje
 namespace mje {
 DEV uint64_t tile_of(uint64_t g, uint64_t total) {
     if (MJE_XRUN <= 1 || gridDim.x != total) return g;
@@ -727,6 +741,10 @@ extern "C" __global__ void __launch_bounds__(MJE_TILE) MJE_WPE_ATTR murr_jit_enc
     const uint64_t n_rows = A->n_rows, total_tiles = A->total_tiles, out_cap = A->out_cap;
 
     const ColTab tab = load_tab(lane);
+    // estimated tile sizes to check: only with a utf8 validity buffer (the
+    // prelude's MJE_CHECK; code in the loop costs layouts without one ~10 %,
+    // profiles/r04/probes/ab46.txt)
+    constexpr bool chk = MJE_CHECK != 0 && NUTF8 > 0;
     for (uint64_t t0 = blockIdx.x; t0 < total_tiles; t0 += gridDim.x) {
         const uint64_t t = tile_of(t0, total_tiles);
         const uint64_t r0 = t * TILE;
@@ -735,7 +753,15 @@ extern "C" __global__ void __launch_bounds__(MJE_TILE) MJE_WPE_ATTR murr_jit_enc
         const uint64_t row = r0 + (active ? tid : 0u);
         // the tile's start (murr_jit_encode_sizes + murr_jit_encode_scan left the
         // exclusive prefix of the tile totals in lookback[t]), loaded up front
-        const uint64_t t_pre = NUTF8 ? ((const GAS uint64_t*)A->lookback)[t] : 0;
+        // (checked layouts load it and the next tile's start -- where this one
+        // must end, see tile_bytes_inline -- by scalar loads: written by the
+        // scan's launch before this one.  Measured per layout: config C 0.933
+        // vs 0.970 ms scalar, config B, unchecked, 0.232 vs 0.212 ms vector;
+        // profiles/r04/probes/ab47.txt, ab48.txt)
+        const uint64_t t_pre = NUTF8 == 0 ? 0
+                               : chk      ? ((const CAS uint64_t*)A->lookback)[t]
+                                          : ((const GAS uint64_t*)A->lookback)[t];
+        const uint64_t t_nxt = chk && t + 1 < total_tiles ? ((const CAS uint64_t*)A->lookback)[t + 1] : 0;
 
         RowBuild B;
         B.t = tab;
@@ -794,6 +820,9 @@ extern "C" __global__ void __launch_bounds__(MJE_TILE) MJE_WPE_ATTR murr_jit_enc
             tstart = t_pre;
             start = tstart + before + inc - size;
             span = agg;
+            if (chk && t + 1 < total_tiles && tstart + span != t_nxt) {
+                if (tid == 0) report(A->err, err_key(0, r0, 0, kStRecount));
+            }
         }
         if (active) {
             gp(A->row_off)[row] = A->row_base + start;
@@ -908,14 +937,34 @@ extern "C" __global__ void __launch_bounds__(MJE_TILE) murr_jit_encode_sizes(mje
 // Tile totals without the sizes pass.  When no utf8 column has a validity
 // buffer every row carries every payload, so a tile of nr rows holds
 // nr (FIXED + 4 NUTF8) bytes plus its string bytes: two offsets per column
-// (the host skips murr_jit_encode_sizes on the same condition).
+// (the host skips murr_jit_encode_sizes on the same condition).  With
+// validity buffers (`spec`), a tile holds nr FIXED bytes plus, per utf8
+// column, 4 bytes per valid row and the offsets' span -- exact when every
+// null string is empty, as Arrow writers leave them; the encode kernel checks
+// each tile's exact size against this estimate (kStRecount) and the host
+// recounts with the sizes pass when any differs.
 namespace mje {
-DEV bool sizes_inline() {
-    bool ok = true;
-#define MJE_NOVAL(C, KIND, SOFF, U) if (KIND == 0) ok = ok && ((const CAS Col*)args()->cols + C)->validity == nullptr;
-    MJE_COLS(MJE_NOVAL)
-#undef MJE_NOVAL
-    return ok;
+// Set bits of bitmap bm in [b0, b0 + n): dword loads from bm's aligned
+// base, never past the byte holding bit b0 + n - 1.
+DEV uint32_t popc_bits(const uint8_t* bm, uint64_t b0, uint32_t n) {
+    const uint32_t mis = (uint32_t)((uintptr_t)bm & 3u);
+    const GAS uint32_t* p = (const GAS uint32_t*)(bm - mis);
+    const uint64_t s = b0 + 8 * mis, e = s + n, lim = (b0 + n + 7) / 8 + mis;  // bytes readable from p
+    uint32_t cnt = 0;
+    for (uint64_t w = s >> 5; w < (e + 31) >> 5; w++) {
+        uint32_t v = 0;
+        if (4 * w + 4 <= lim) {
+            v = p[w];
+        } else {
+            for (uint32_t k = 0; k < 4; k++)
+                if (4 * w + k < lim) v |= (uint32_t)((const GAS uint8_t*)p)[4 * w + k] << (8 * k);
+        }
+        uint32_t m = ~0u;
+        if (w == (s >> 5)) m &= ~0u << (s & 31);
+        if (w == ((e - 1) >> 5) && (e & 31)) m &= ~0u >> (32 - (e & 31));
+        cnt += __popc(v & m);
+    }
+    return cnt;
 }
 // Totals of the N consecutive tiles t0 .. t0 + N - 1 (those below hi); each
 // column's descriptor is read once, every offset load issued together.
@@ -926,14 +975,17 @@ template <uint32_t N> DEV void tile_bytes_inline(uint64_t t0, uint64_t hi, uint6
     for (uint32_t q = 0; q < N; q++) {
         const uint64_t r0 = (t0 + q) * TILE;
         nr[q] = t0 + q < hi ? min((uint64_t)TILE, n_rows - r0) : 0;
-        x[q] = nr[q] * (FIXED + 4 * NUTF8);
+        x[q] = nr[q] * FIXED;
     }
 #define MJE_TB(C, KIND, SOFF, U)                                                            \
     if (KIND == 0) {                                                                        \
         const Col c = ldcol(C);                                                             \
         _Pragma("unroll") for (uint32_t q = 0; q < N; q++) {                                \
             const uint64_t e = c.offset + (t0 + q) * TILE;                                  \
-            if (nr[q]) x[q] += (uint64_t)(int64_t)(gp(c.offsets)[e + nr[q]] - gp(c.offsets)[e]); \
+            if (nr[q]) {                                                                    \
+                const uint32_t nv = c.validity ? popc_bits(c.validity, e, (uint32_t)nr[q]) : (uint32_t)nr[q]; \
+                x[q] += 4ull * nv + (uint64_t)(int64_t)(gp(c.offsets)[e + nr[q]] - gp(c.offsets)[e]); \
+            }                                                                               \
         }                                                                                   \
     }
     MJE_COLS(MJE_TB)
@@ -993,8 +1045,9 @@ extern "C" __global__ void __launch_bounds__(1024) murr_jit_encode_scan(mje::Arg
     const uint64_t g = blockIdx.x, lo = g * SCAN_PER, hi = min(T, lo + SCAN_PER);
     constexpr uint32_t PER = SCAN_PER / 1024;  // 4 per thread, contiguous
     uint64_t x[PER], s = 0;
-    if (pass == 0 && sizes_inline()) {
-        // tile totals from the offsets (no sizes pass), kept for pass 1
+    if (pass == 3 || (pass == 0 && sizes_inline())) {
+        // tile totals from the offsets (no sizes pass; pass 3: estimates,
+        // checked by the encode kernel), kept for pass 1
         tile_bytes_inline<PER>(lo + tid * PER, hi, x);
 #pragma unroll
         for (uint32_t q = 0; q < PER; q++)
@@ -1010,7 +1063,7 @@ extern "C" __global__ void __launch_bounds__(1024) murr_jit_encode_scan(mje::Arg
     for (uint32_t q = 0; q < PER; q++) s += x[q];
     uint64_t tot;
     const uint64_t ex = block_excl(s, (LAS uint64_t*)s_t, &tot);
-    if (pass == 0) {
+    if (pass != 1) {
         if (tid == 0) sums[g] = tot;
         return;
     }

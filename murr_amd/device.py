@@ -103,7 +103,8 @@ class Context:
         raise_status(self.L.murr_ctx_stats(self.h, C.byref(s)), what="murr_ctx_stats")
         return {"decodes": s.decodes, "split_retries": s.split_retries,
                 "last_mode": ("generic", "local", "cut", "split")[s.last_mode], "last_grid": s.last_grid,
-                "last_shape": (s.last_shape_nw, s.last_shape_r), "readback_fallbacks": s.readback_fallbacks}
+                "last_shape": (s.last_shape_nw, s.last_shape_r), "readback_fallbacks": s.readback_fallbacks,
+                "encode_recounts": s.encode_recounts}
 
     def close(self):
         if self.h:

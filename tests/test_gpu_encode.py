@@ -194,3 +194,50 @@ def test_bitmaps_not_on_a_dword(ctx, shift):
     wblob, woff = O.encode_batch(O.Segment([int(d) for d in dtypes]), synth.oracle_cols(cols), n)
     assert np.array_equal(row_off.download((n + 1) * 8).view(np.uint64), woff)
     assert blob.download(blen).tobytes() == wblob.tobytes()
+
+
+def _utf8_with_null_bytes(rng, n, null_p, max_str=20):
+    # Arrow lets a null slot span bytes (only the validity bit says null):
+    # every other null string here keeps its bytes
+    valid = rng.random(n) >= null_p
+    lens = rng.integers(0, max_str + 1, size=n)
+    lens[~valid & (np.arange(n) % 2 == 0)] = 0
+    offs = np.zeros(n + 1, np.int64)
+    np.cumsum(lens, out=offs[1:])
+    data = rng.integers(0x20, 0x7F, size=int(offs[-1]), dtype=np.uint8)
+    return synth.column(D.Utf8, valid=valid, offsets=offs.astype(np.int32), data=data, n=n)
+
+
+def test_null_strings_with_bytes_are_recounted(ctx, kernel_mode):
+    # The JIT encode estimates utf8 tile sizes from the offsets and validity
+    # popcounts (exact when null strings are empty); null strings spanning
+    # bytes make the estimate off, the kernel reports it and the host
+    # recounts with the sizes pass: the output is the oracle's either way
+    rng = np.random.default_rng(95)
+    dtypes = [D.Utf8, D.Int32, D.Utf8]
+    n = 50_000 + 3
+    cols = [_utf8_with_null_bytes(rng, n, 0.3), random_columns(rng, [D.Int32], n, null_p=0.2)[0],
+            _utf8_with_null_bytes(rng, n, 0.5)]
+    before = ctx.stats()["encode_recounts"]
+    blob, off = gpu_encode(ctx, dtypes, cols, n)
+    wblob, woff = O.encode_batch(O.Segment([int(d) for d in dtypes]), synth.oracle_cols(cols), n)
+    assert np.array_equal(off, woff) and blob.tobytes() == wblob.tobytes()
+    assert ctx.stats()["encode_recounts"] - before == (1 if kernel_mode == "jit" else 0)
+
+
+@pytest.mark.parametrize("k", [0, 5, 35])
+def test_validity_estimates_exact_for_empty_nulls(ctx, k):
+    # empty null strings (as Arrow writers leave them): the estimated tile
+    # sizes are exact -- no recount -- over several scan groups, sliced
+    rng = np.random.default_rng(96 + k)
+    dtypes = [D.Utf8, D.Float64, D.Utf8, D.Bool]
+    full = 1_100_000 + 41
+    cols = random_columns(rng, dtypes, full, null_p=0.25, max_str=12, unicode=False)
+    n = full - k
+    for c in cols:
+        c["offset"] = k
+    before = ctx.stats()["encode_recounts"]
+    blob, off = gpu_encode(ctx, dtypes, cols, n)
+    wblob, woff = O.encode_batch(O.Segment([int(d) for d in dtypes]), synth.oracle_cols(cols), n)
+    assert np.array_equal(off, woff) and blob.tobytes() == wblob.tobytes()
+    assert ctx.stats()["encode_recounts"] == before
