@@ -465,7 +465,7 @@ hipError_t jit_encode_launch(const JitEncKernel* k, const EncodeArgs& a, uint32_
     void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &args, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
     if (a.nutf8) {
         // tile starts: tile sums (a workgroup per tile), then their exclusive
-        // scan over kEncScanPer-tile groups (sums, one-workgroup scan of the sums, prefixes)
+        // scan over kEncScanPer-tile groups (group sums, then prefixes: each group adds up the sums before it)
         const uint32_t tiles = (uint32_t)std::min<uint64_t>(a.total_tiles, 0x7FFFFFFFull);
         const uint32_t groups = (uint32_t)((a.total_tiles + kEncScanPer - 1) / kEncScanPer);
         // (no utf8 column with a validity buffer: the scan derives the tile
@@ -480,9 +480,15 @@ hipError_t jit_encode_launch(const JitEncKernel* k, const EncodeArgs& a, uint32_
         size_t ssz = sizeof(sa);
         void* scfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &sa, HIP_LAUNCH_PARAM_BUFFER_SIZE, &ssz, HIP_LAUNCH_PARAM_END};
         if (e == hipSuccess) e = hipModuleLaunchKernel(k->fn_scan, groups, 1, 1, 1024, 1, 1, 0, s, nullptr, scfg);
-        sa.pass = 2;
-        if (e == hipSuccess) e = hipModuleLaunchKernel(k->fn_scan, 1, 1, 1, 1024, 1, 1, 0, s, nullptr, scfg);
-        sa.pass = 1;
+        bool scan3 = false;  // the group sums scanned by a launch of their own (A/B)
+#ifdef MURR_TUNING
+        scan3 = std::getenv("MURR_ENC_SCAN3") != nullptr;
+#endif
+        if (scan3) {
+            sa.pass = 2;
+            if (e == hipSuccess) e = hipModuleLaunchKernel(k->fn_scan, 1, 1, 1, 1024, 1, 1, 0, s, nullptr, scfg);
+        }
+        sa.pass = scan3 ? 1u : 4u;
         if (e == hipSuccess) e = hipModuleLaunchKernel(k->fn_scan, groups, 1, 1, 1024, 1, 1, 0, s, nullptr, scfg);
         if (e != hipSuccess) return e;
     }

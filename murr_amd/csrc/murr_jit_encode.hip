@@ -994,9 +994,11 @@ template <uint32_t N> DEV void tile_bytes_inline(uint64_t t0, uint64_t hi, uint6
 }  // namespace mje
 
 // Exclusive prefix of the tile totals in place, in two launches of this
-// kernel over contiguous ranges of SCAN_PER tiles per workgroup: pass 0 sums
-// each range into lookback[T + 1 + g]; pass 1 (after a one-workgroup scan of
-// those sums) rewrites each range as its exclusive prefix.
+// kernel over contiguous ranges of SCAN_PER tiles per workgroup: pass 0 (or
+// 3) sums each range into lookback[T + 1 + g]; pass 4 adds up the sums of the
+// ranges before its own (a few hundred at most) and rewrites its range as
+// its exclusive prefix.  (Passes 2 + 1: the same with a one-workgroup scan of
+// the sums in between, a third launch; tuning MURR_ENC_SCAN3.)
 #ifndef MJE_SCAN_PER
 #define MJE_SCAN_PER 1024
 #endif
@@ -1063,11 +1065,20 @@ extern "C" __global__ void __launch_bounds__(1024) murr_jit_encode_scan(mje::Arg
     for (uint32_t q = 0; q < PER; q++) s += x[q];
     uint64_t tot;
     const uint64_t ex = block_excl(s, (LAS uint64_t*)s_t, &tot);
-    if (pass != 1) {
+    if (pass == 0 || pass == 3) {
         if (tid == 0) sums[g] = tot;
         return;
     }
-    uint64_t run = sums[g] + ex;
+    uint64_t run = ex;
+    if (pass == 1) {
+        run += sums[g];
+    } else {  // pass 4: the ranges before this one
+        for (uint64_t k0 = 0; k0 < g; k0 += 1024) {
+            uint64_t t2;
+            (void)block_excl(k0 + tid < g ? sums[k0 + tid] : 0, (LAS uint64_t*)s_t, &t2);
+            run += t2;
+        }
+    }
 #pragma unroll
     for (uint32_t q = 0; q < PER; q++) {
         const uint64_t j = lo + tid * PER + q;
