@@ -456,10 +456,13 @@ def run_decode(args, dist, rank, world, local_rank):
     # launch and read-back work overlaps the previous step's kernel, as a
     # serving loop would; on the GPU the steps run one after the other (one
     # stream).  --sync-steps: one set, each step waited for (the A/B).
+    # --lanes 2: the second output set's plan on a second context (its own
+    # stream), so step s + 1's workgroups can start on CUs step s has left
+    ctxs = [ctx, Context(local_rank) if args.lanes == 2 and rt is None else ctx]
     if args.arena:
-        out_sets = [ArenaOutputs(ctx, seg, proj, blocks, args.arena) for _ in range(2)]
+        out_sets = [ArenaOutputs(c, seg, proj, blocks, args.arena) for c in ctxs]
     else:
-        out_sets = [DecodeOutputs(ctx, seg, proj, blocks), DecodeOutputs(ctx, seg, proj, blocks)]
+        out_sets = [DecodeOutputs(c, seg, proj, blocks) for c in ctxs]
     if rt is not None:
         names = [seg.columns[c].name for c in proj]
 
@@ -467,7 +470,7 @@ def run_decode(args, dist, rank, world, local_rank):
             return rt.scan_device_async(names, out_sets[i])
     else:
         # the launch prepared once per output set (murr_decode_plan)
-        plans = [DecodePlan(ctx, seg, proj, blocks, o) for o in out_sets]
+        plans = [DecodePlan(c, seg, proj, blocks, o) for c, o in zip(ctxs, out_sets)]
 
         def launch(i):
             plans[i].run_async()
@@ -485,7 +488,7 @@ def run_decode(args, dist, rank, world, local_rank):
 
         def done(i):
             if runs[i] % every == 0:
-                ms.append(ctx.last_kernel_ms())
+                ms.append(ctxs[i].last_kernel_ms())
             runs[i] += 1
 
         if args.sync_steps:
@@ -503,10 +506,12 @@ def run_decode(args, dist, rank, world, local_rank):
 
     wms = run_steps(args.warmup)
     barrier(dist)
-    ctx.sync()
+    for c in ctxs:
+        c.sync()
     t0 = time.perf_counter()
     kms = run_steps(args.steps)
-    ctx.sync()
+    for c in ctxs:
+        c.sync()
     barrier(dist)
     elapsed = time.perf_counter() - t0
     last = 0 if args.sync_steps else (args.steps - 1) % 2
@@ -1098,6 +1103,9 @@ def main():
                     help="skip the oracle check of the timed output (tuning ablations that skip stores only)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--pmc-csv", default=None)
+    ap.add_argument("--lanes", type=int, default=1, choices=[1, 2],
+                    help="decode: 2 = the alternating output sets' plans on two contexts (two streams; "
+                         "block decodes only, not --config D)")
     ap.add_argument("--sync-steps", action="store_true",
                     help="one plan, each step waited for before the next is launched (A/B of the pipelined loop)")
     ap.add_argument("--no-traffic", action="store_true",
