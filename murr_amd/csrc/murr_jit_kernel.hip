@@ -405,6 +405,9 @@ struct Shape {
     DEV static uint32_t slot_bytes(uint32_t stage) { return RO_BYTES + stage + 64; }
 };
 
+#ifndef MJ_LOADER_PRIO
+#define MJ_LOADER_PRIO 0
+#endif
 // One tile as the loader dealt it (tile ring entry, 32 B).
 struct TileInfo {
     uint32_t b, nr;
@@ -1569,6 +1572,9 @@ DEV void kernel_body() {
     }
 
     if (wave == NC) {
+        // (MJ_LOADER_PRIO: the loader wave's issue priority, s_setprio 0-3;
+        // tuning)
+        if constexpr (MJ_LOADER_PRIO > 0) __builtin_amdgcn_s_setprio(MJ_LOADER_PRIO);
         // ---- loader: NSLOT - 1 tiles in flight.  At iteration i (after
         // barrier B_i freed the slot of tile i - 1) it DMAs tile i + NSLOT - 1
         // and announces tile i + NSLOT + 2 (its identity and span), then waits
