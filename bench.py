@@ -297,19 +297,22 @@ class _Arena:
 def arena_blocks(ctx, b0: DeviceBlock, K: int, align: int):
     """K resident copies of a block in three arenas (blobs, row offsets,
     utf8 indexes), each piece at a multiple of `align` bytes (--arena)."""
-    nd, no = b0.data_bytes + 16, 8 * (b0.n_rows + 1)
+    w = b0.offset_width
+    src_off = b0.row_off32 if w == 4 else b0.row_off
+    nd, no = b0.data_bytes + 16, w * (b0.n_rows + 1)
     ad, ao = _Arena(ctx, [nd] * K, align), _Arena(ctx, [no] * K, align)
     au = _Arena(ctx, [b0.uidx.nbytes] * K, 256) if b0.uidx is not None else None
     out = []
     for i in range(K):
         d, o = ad.view(i), ao.view(i)
         d.copy_from(b0.data, b0.data_bytes)
-        o.copy_from(b0.row_off, no)
+        o.copy_from(src_off, no)
         u = None
         if au is not None:
             u = au.view(i)
             u.copy_from(b0.uidx, b0.uidx.nbytes)
-        out.append(DeviceBlock(d, o, b0.n_rows, b0.data_bytes, u, b0.stride))
+        out.append(DeviceBlock(d, None if w == 4 else o, b0.n_rows, b0.data_bytes, u, b0.stride,
+                               o if w == 4 else None))
     return out
 
 
@@ -344,15 +347,18 @@ class ArenaOutputs(DecodeOutputs):
 
 
 def copy_block(ctx, b: DeviceBlock) -> DeviceBlock:
-    """A resident copy of a block (and its index), device to device."""
-    data, off = ctx.alloc(b.data_bytes + 16), ctx.alloc(8 * (b.n_rows + 1))
+    """A resident copy of a block (its offsets at their width, and its
+    index), device to device."""
+    w = b.offset_width
+    data, off = ctx.alloc(b.data_bytes + 16), ctx.alloc(w * (b.n_rows + 1))
     data.copy_from(b.data, b.data_bytes)
-    off.copy_from(b.row_off, 8 * (b.n_rows + 1))
+    off.copy_from(b.row_off32 if w == 4 else b.row_off, w * (b.n_rows + 1))
     ux = None
     if b.uidx is not None:
         ux = ctx.alloc(b.uidx.nbytes)
         ux.copy_from(b.uidx, b.uidx.nbytes)
-    return DeviceBlock(data, off, b.n_rows, b.data_bytes, ux, b.stride)
+    return DeviceBlock(data, None if w == 4 else off, b.n_rows, b.data_bytes, ux, b.stride,
+                       off if w == 4 else None)
 
 
 def config_d_table(ctx, rows: int, start: int, chunk: int = 2_000_000):
@@ -441,6 +447,10 @@ def run_decode(args, dist, rank, world, local_rank):
             dblob, doff, blen = encode_batch(ctx, seg, dcols, rows)
             b0 = DeviceBlock(dblob, doff, rows, blen)
         del dcols
+        if args.offsets == 32:
+            # u32 block-relative row offsets (murr_block_t.row_off32): a
+            # 100k-row block is 1.8 MB, far below 4 GiB
+            b0 = b0.narrow(ctx)
         if args.arena:  # K resident blocks in arenas (blobs / row offsets / outputs each one buffer)
             blocks = arena_blocks(ctx, b0, K, args.arena)
         else:
@@ -449,7 +459,7 @@ def run_decode(args, dist, rank, world, local_rank):
     ctx.sync()
     build_s = time.perf_counter() - t_build
     host_blob = blocks[0].data.download(blocks[0].data_bytes)
-    host_off = blocks[0].row_off.download((rows + 1) * 8).view(np.uint64).copy()
+    host_off = blocks[0].host_offsets()
     ix_bytes = 8 * int(L_len(ctx, seg, rows, ix_stride)) if blocks[0].uidx is not None else 0
     # Two output sets: step s decodes into set s % 2 and is launched
     # (murr_decode_run_async) before step s - 1 is waited for, so the host's
@@ -476,44 +486,67 @@ def run_decode(args, dist, rank, world, local_rank):
             plans[i].run_async()
             return plans[i]
 
-    # A prepared plan times one run in PLAN_TIME_EVERY (its first included):
-    # the kernel time is averaged over those runs only.
+    # Kernel time.  The warm-up samples the plan's own timed runs (one in
+    # PLAN_TIME_EVERY, the first included).  The timed region turns those
+    # per-run events off (each costs GPU time between back-to-back launches)
+    # and brackets all K launches with two marks on the context's stream:
+    # kernel_ms_avg = that GPU time / K, which includes the gaps between the
+    # launches, so it never exceeds ms_per_step (the host's clock around the
+    # same K steps).  With two lanes (two streams) the launches overlap and
+    # the warm-up samples stand in.
     runs = [0, 0]  # runs of each output set's plan so far
     every = _abi.PLAN_TIME_EVERY
     if "MURR_TIME_EVERY" in os.environ and _abi.LIB_PATH.endswith("_tuning.so"):
         every = max(1, int(os.environ["MURR_TIME_EVERY"]))
+    launched = {}  # the prepared plans the steps ran (resident scans make theirs inside the table)
 
-    def run_steps(n):
+    def run_steps(n, sample=True):
         ms = []
 
         def done(i):
-            if runs[i] % every == 0:
+            if sample and runs[i] % every == 0:
                 ms.append(ctxs[i].last_kernel_ms())
             runs[i] += 1
 
+        def go(i):
+            p = launch(i)
+            launched[id(p)] = p
+            return p
+
         if args.sync_steps:
             for _ in range(n):
-                launch(0).wait()
+                go(0).wait()
                 done(0)
             return ms
-        h = launch(0) if n else None
+        h = go(0) if n else None
         for s in range(n):
-            hn = launch((s + 1) % 2) if s + 1 < n else None
+            hn = go((s + 1) % 2) if s + 1 < n else None
             h.wait()
             done(s % 2)
             h = hn
         return ms
 
     wms = run_steps(args.warmup)
+    region = args.lanes == 1
+    if region:
+        for p in launched.values():
+            p.time_every(0)
     barrier(dist)
     for c in ctxs:
         c.sync()
     t0 = time.perf_counter()
-    kms = run_steps(args.steps)
+    if region:
+        ctx.mark(0)
+    kms = run_steps(args.steps, sample=not region)
+    if region:
+        ctx.mark(1)
     for c in ctxs:
         c.sync()
     barrier(dist)
     elapsed = time.perf_counter() - t0
+    region_ms = ctx.mark_ms(0, 1) if region and args.steps else None
+    for p in launched.values():
+        p.time_every(every)
     last = 0 if args.sync_steps else (args.steps - 1) % 2
     outs = out_sets[last]  # the last timed step's output (checked below)
     elapsed = max_over_ranks(dist, elapsed)
@@ -522,11 +555,16 @@ def run_decode(args, dist, rank, world, local_rank):
     a0 = [outs.array(0, p) for p in range(len(proj))]
     out_block = arrow_out_bytes(seg, proj, rows, [a.null_count for a in a0],
                                 [a.data_len for a in a0])
-    in_block = int(host_blob.size) + 8 * (rows + 1) + ix_bytes  # blobs, row offsets, utf8 index
+    off_w = blocks[0].offset_width  # u32 (row_off32) or u64 row offsets
+    in_block = int(host_blob.size) + off_w * (rows + 1) + ix_bytes  # blobs, row offsets, utf8 index
     out_step = out_block * K
     total_out = sum_over_ranks(dist, out_step * args.steps)
     value = total_out / elapsed / GIB
-    k_avg_ms = float(np.mean(kms or wms))  # (a timed region shorter than the period: the warm-up's)
+    warm_ms = wms[1:] or wms  # (the very first run pays one-off costs)
+    if region_ms is not None:
+        k_avg_ms = region_ms / args.steps
+    else:
+        k_avg_ms = float(np.mean(kms or warm_ms))  # (a timed region shorter than the period: the warm-up's)
     achieved = (in_block + out_block) * K / (k_avg_ms * 1e-3) / 1e9
     shape = "%dx%d" % tuple(stats["last_shape"])
     timed_kernel = ("decode_kernel" if stats["last_mode"] == "generic" else
@@ -547,7 +585,7 @@ def run_decode(args, dist, rank, world, local_rank):
     # the same launch without the utf8 index (untimed variant, for DESIGN.md)
     no_index_ms = None
     if ix_bytes:
-        bare = [DeviceBlock(b.data, b.row_off, b.n_rows, b.data_bytes) for b in blocks]
+        bare = [DeviceBlock(b.data, b.row_off, b.n_rows, b.data_bytes, row_off32=b.row_off32) for b in blocks]
         p2 = DecodePlan(ctx, seg, proj, bare, outs)
         nk = []
         for r in range(5 * every):
@@ -573,6 +611,7 @@ def run_decode(args, dist, rank, world, local_rank):
                    "rows_per_rank": [shard_rows(r, world, args.table_rows)[1] for r in range(world)]
                    if args.table_rows else [rows] * world,
                    "utf8_index_stride": ix_stride if ix_bytes else None,
+                   "row_offset_bytes": off_w,
                    "bytes_in_per_step": in_block * K, "bytes_out_per_step": out_step,
                    "parallelism": f"{world} key-range shard(s), no collective",
                    "launch": {"mode": stats["last_mode"], "grid": stats["last_grid"],
@@ -580,8 +619,13 @@ def run_decode(args, dist, rank, world, local_rank):
                    "setup_s": round(build_s, 2)},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     # the same bytes over the driver-visible step (host clock)
+                     "frac_step": round((in_block + out_block) * K / (elapsed / args.steps) / 1e9 / HBM_PEAK_GBS, 4),
                      "traffic": traffic, "kernel": ctx.last_kernel(),
                      "kernel_ms_avg": round(k_avg_ms, 5),
+                     "kernel_ms_timing": "GPU marks around the timed region / steps" if region_ms is not None
+                     else "mean of the plans' timed runs",
+                     "kernel_ms_sampled_warmup": round(float(np.mean(warm_ms)), 5) if warm_ms else None,
                      "algorithmic_bytes_per_launch": (in_block + out_block) * K},
         "verified": f"blocks {checked} of the timed launch bit-exact vs the oracle" if checked else "NOT VERIFIED (--no-verify)",
         "no_index_ms": no_index_ms,
@@ -1094,6 +1138,8 @@ def main():
     ap.add_argument("--arena", type=int, default=0,
                     help="decode mode: the K blocks and their outputs as pieces of arenas aligned to this many bytes "
                          "(0: one allocation per buffer)")
+    ap.add_argument("--offsets", type=int, default=32, choices=[32, 64],
+                    help="row offset width of the decoded blocks (configs A/B/C: u32 row_off32, or u64)")
     ap.add_argument("--uidx-stride", type=int, default=512,
                     help="decode mode: utf8 index stride of each block (0 = no index)")
     ap.add_argument("--table", default="C", choices=["C", "ref"],

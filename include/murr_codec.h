@@ -129,6 +129,11 @@ int  murr_ctx_last_kernel_ms(murr_ctx_t* ctx, float* ms);
  * "encode_kernel" (generic); "" before any.  A static string. */
 const char* murr_ctx_last_kernel(murr_ctx_t* ctx);
 int  murr_device_count(int* n);
+/* Timing marks on the context's stream (benchmarks): murr_ctx_mark records
+ * mark `which` (0-3) behind the work queued so far; murr_ctx_mark_ms waits for
+ * mark b and returns the GPU time from mark a to mark b. */
+int murr_ctx_mark(murr_ctx_t* ctx, uint32_t which);
+int murr_ctx_mark_ms(murr_ctx_t* ctx, uint32_t a, uint32_t b, float* ms);
 
 /* Kernel selection of one context, for tests and benchmarks.  All zero (the
  * state of a new context) = the library's own choice.  Set once; every later
@@ -215,14 +220,28 @@ int murr_segment_prepare(murr_ctx_t* ctx, const murr_segment_t* seg);
  * Row i is data[row_off[i] .. row_off[i+1]); an empty row is a missing key
  * (ReadBatchBuilder::add_empty, src/io/row/read.rs:93-98; a present row is
  * never empty when the segment has >= 1 column, write.rs:21).
- * `data` must be 16-byte aligned; all pointers are device pointers. */
+ * `data` must be 16-byte aligned; all pointers are device pointers.
+ *
+ * Row offsets come in two widths.  `row_off` holds them as u64 (any block,
+ * e.g. a resident table's arena past 4 GiB).  `row_off32`, when non-null,
+ * holds them as u32 instead (4-byte aligned, n_rows + 1 entries, every value
+ * below 2^32; `row_off` is then ignored and may be null): a batch read's block
+ * is far below 4 GiB, and u32 offsets halve the index bytes the decode reads
+ * (and a streamed batch sends over PCIe).  Same values, same meaning. */
 typedef struct {
     const uint8_t*  data;
     const uint64_t* row_off;   /* n_rows + 1 entries, row_off[0] may be > 0 */
     uint64_t        n_rows;
     uint64_t        data_bytes; /* optional: row_off[n] - row_off[0] (0 = unknown);
                                    sizes the tiles, never read past */
+    const uint32_t* row_off32; /* optional: the offsets as u32 (see above) */
 } murr_block_t;
+
+/* u64 row offsets -> u32 (device, n_rows + 1 entries each; `out` 4-byte
+ * aligned).  Fails with MURR_E_OFFSET_OVERFLOW when row_off[n_rows] >= 2^32
+ * (offsets are non-decreasing, so the last one bounds them all).  Enqueued on
+ * the context's stream after one 8-byte read-back of row_off[n_rows]. */
+int murr_row_off_narrow(murr_ctx_t* ctx, const uint64_t* row_off, uint64_t n_rows, uint32_t* out);
 
 /* One output Arrow array (device pointers), arrow-rs 58 builder layout:
  *   fixed W:  values = n*W bytes, null slots zero
@@ -292,6 +311,10 @@ int murr_decode_run(murr_plan_t* plan, murr_error_t* err);   /* synchronous */
 int murr_decode_run_async(murr_plan_t* plan);
 int murr_decode_run_wait(murr_plan_t* plan, murr_error_t* err);
 void murr_plan_free(murr_plan_t* plan);
+/* The plan's timing period: one run in `every` (MURR_PLAN_TIME_EVERY by
+ * default) is bracketed by timing events; 0 times none (a caller timing a
+ * whole loop of runs with murr_ctx_mark instead). */
+int murr_plan_time_every(murr_plan_t* plan, uint32_t every);
 
 /* ---- utf8 index of a block (optional) --------------------------------------
  * For every utf8 column of the layout (column order), the string bytes of the

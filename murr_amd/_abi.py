@@ -50,8 +50,9 @@ class CtxStats(C.Structure):
 
 
 class Block(C.Structure):
+    """murr_block_t: row_off (u64), or row_off32 (u32) when set."""
     _fields_ = [("data", C.c_void_p), ("row_off", C.c_void_p), ("n_rows", C.c_uint64),
-                ("data_bytes", C.c_uint64)]
+                ("data_bytes", C.c_uint64), ("row_off32", C.c_void_p)]
 
 
 class Array(C.Structure):
@@ -124,6 +125,7 @@ SIGNATURES = {
     "murr_memcpy_d2h": (I32, [P, P, P, U64]),
     "murr_memcpy_d2d": (I32, [P, P, P, U64]),
     "murr_memcpy_peer": (I32, [P, P, P, I32, U64]),
+    "murr_row_off_narrow": (I32, [P, P, U64, P]),
     "murr_shard_of": (I32, [P, P, U64, U64, U32, P]),
     "murr_memset_dev": (I32, [P, P, I32, U64]),
     "murr_sync": (I32, [P]),
@@ -143,6 +145,9 @@ SIGNATURES = {
     "murr_decode_run_async": (I32, [P]),
     "murr_decode_run_wait": (I32, [P, C.POINTER(Error)]),
     "murr_plan_free": (None, [P]),
+    "murr_plan_time_every": (I32, [P, U32]),
+    "murr_ctx_mark": (I32, [P, U32]),
+    "murr_ctx_mark_ms": (I32, [P, U32, U32, C.POINTER(C.c_float)]),
     "murr_sst_decode": (I32, [P, C.POINTER(SstBlock), U32, C.POINTER(SstResult), C.POINTER(Error)]),
     "murr_sst_result_free": (None, [P, C.POINTER(SstResult)]),
     "murr_utf8_index": (I32, [P, C.POINTER(Segment), C.POINTER(Block), U32, P]),

@@ -106,6 +106,8 @@ struct murr_ctx {
     std::vector<hipEvent_t> event_pool;
     uint64_t* aux = nullptr;  // device scratch of the gather scan (group sums)
     uint64_t aux_cap = 0;     // entries
+    uint64_t* wide = nullptr; // u32 row offsets widened for the generic decode kernel
+    uint64_t wide_cap = 0;    // entries
     hipEvent_t xev = nullptr; // multi-GPU reads: this stream's work, awaited by the home stream
     hipEvent_t hev = nullptr; // multi-GPU reads (as home): the work queued before a read, awaited by the shards
     // Fused transfers (the streaming host decode, murr_hstream): the next
@@ -116,6 +118,7 @@ struct murr_ctx {
     bool xfer = false, xtimed = false;
     std::vector<CopySeg> xin, xout;
     hipEvent_t xe[4] = {nullptr, nullptr, nullptr, nullptr};
+    hipEvent_t mk[4] = {nullptr, nullptr, nullptr, nullptr};  // murr_ctx_mark: caller's timing marks
 };
 
 // Device key index (murr_index.hip): the keys' own copy and the slot table.
@@ -694,6 +697,7 @@ void murr_ctx_destroy(murr_ctx_t* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->ws) (void)hipFree(c->ws);
     if (c->aux) (void)hipFree(c->aux);
+    if (c->wide) (void)hipFree(c->wide);
     if (c->hs) (void)hipHostFree(c->hs);
     for (const auto& b : c->pool) (void)(b.pinned ? hipHostFree(b.p) : hipFree(b.p));
     for (hipEvent_t e : c->event_pool) (void)hipEventDestroy(e);
@@ -701,6 +705,8 @@ void murr_ctx_destroy(murr_ctx_t* c) {
     if (c->hev) (void)hipEventDestroy(c->hev);
     if (c->k0) (void)hipEventDestroy(c->k0);
     if (c->k1) (void)hipEventDestroy(c->k1);
+    for (hipEvent_t e : c->mk)
+        if (e) (void)hipEventDestroy(e);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -718,6 +724,23 @@ int murr_ctx_last_kernel_ms(murr_ctx_t* c, float* ms) {
 }
 
 const char* murr_ctx_last_kernel(murr_ctx_t* c) { return c ? c->last_kernel : ""; }
+
+int murr_ctx_mark(murr_ctx_t* c, uint32_t which) {
+    murr_error_t* err = nullptr;
+    if (!c || which >= 4) return MURR_E_ARGUMENT;
+    HIPC(hipSetDevice(c->device));
+    if (!c->mk[which]) HIPC(hipEventCreate(&c->mk[which]));
+    HIPC(hipEventRecord(c->mk[which], c->stream));
+    return MURR_OK;
+}
+
+int murr_ctx_mark_ms(murr_ctx_t* c, uint32_t a, uint32_t b, float* ms) {
+    murr_error_t* err = nullptr;
+    if (!c || !ms || a >= 4 || b >= 4 || !c->mk[a] || !c->mk[b]) return MURR_E_ARGUMENT;
+    HIPC(hipEventSynchronize(c->mk[b]));
+    HIPC(hipEventElapsedTime(ms, c->mk[a], c->mk[b]));
+    return MURR_OK;
+}
 
 int murr_ctx_set_opts(murr_ctx_t* c, const murr_opts_t* o) {
     if (!c || !o || o->kernel > 2 || o->mode > 3 || o->encode_kernel > 2 || (!o->shape_nw) != (!o->shape_r))
@@ -799,6 +822,18 @@ int murr_memcpy_d2d(murr_ctx_t* c, void* dst, const void* src, uint64_t n) {
     if (!n) return MURR_OK;
     HIPC(hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToDevice, c->stream));
     HIPC(hipStreamSynchronize(c->stream));
+    return MURR_OK;
+}
+
+int murr_row_off_narrow(murr_ctx_t* c, const uint64_t* row_off, uint64_t n_rows, uint32_t* out) {
+    murr_error_t* err = nullptr;
+    if (!c || !row_off || !out || ((uintptr_t)out & 3) || c->pending) return MURR_E_ARGUMENT;
+    HIPC(hipSetDevice(c->device));
+    uint64_t last = 0;  // offsets never decrease: the last one bounds them all
+    HIPC(hipMemcpyAsync(&last, row_off + n_rows, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPC(hipStreamSynchronize(c->stream));
+    if (last > 0xFFFFFFFFull) return MURR_E_OFFSET_OVERFLOW;
+    HIPC(launch_row_off_narrow(row_off, out, n_rows + 1, c->stream));
     return MURR_OK;
 }
 
@@ -921,7 +956,7 @@ struct JitReplay {
     uint8_t* hrb = nullptr;        // pinned readback (z_lb bytes) + done flag
     uint8_t* hrb_dev = nullptr;    // its device address
     uint64_t zbytes = 0, z_lb = 0;
-    uint64_t runs = 0;
+    uint64_t runs = 0, timed_runs = 0;
     std::vector<std::vector<uint8_t>> kargs[2];  // per counter set: per projection round
     JitShapeK K{};
     bool split = false, emit = false;
@@ -1047,7 +1082,7 @@ int decode_enqueue_jit(murr_ctx* c, const murr_segment_t* seg, const JitLayout* 
     bool cuttable = true;  // every block can be cut into virtual blocks
     for (uint32_t b = 0; b < nblocks; b++) {
         const uint64_t* ux = uidx ? uidx[b] : nullptr;
-        db[b] = DecBlock{blocks[b].data, blocks[b].row_off, blocks[b].n_rows, tiles, ux};
+        db[b] = dec_block(blocks[b], tiles, ux);
         tiles += (blocks[b].n_rows + K.tr - 1) / K.tr;
         nonempty += blocks[b].n_rows != 0;
         total_rows += blocks[b].n_rows;
@@ -1276,6 +1311,7 @@ int decode_enqueue_jit(murr_ctx* c, const murr_segment_t* seg, const JitLayout* 
     h.stage = stage;
     h.dyn_start = dyn_start;
     h.dyn_pool = dyn_pool;
+    h.fast = cut || !local ? 1u : 0u;
     if (verbose)
         std::fprintf(stderr, "decode launch (jit %ux%us%u): %s grid %llu (%d/CU, %d split) blocks %llu tiles %llu segments %llu (%llu tiles) rows/tile %u stage %u lds %u rounds %u dyn %u+8x%u\n",
                      K.nw, K.r, K.nslot, cut ? "local-cut" : local ? "local" : "split", (unsigned long long)grid, bpc, bpc_safe,
@@ -1414,7 +1450,8 @@ int decode_prep(murr_ctx* c, const murr_segment_t* seg, const uint32_t* proj, ui
     }
     for (uint32_t b = 0; b < nblocks; b++) {
         const murr_block_t& bl = blocks[b];
-        if (bl.n_rows && (!bl.data || !bl.row_off || ((uintptr_t)bl.data & 15)))
+        if (bl.n_rows && (!bl.data || (!bl.row_off && !bl.row_off32) || ((uintptr_t)bl.data & 15) ||
+                          ((uintptr_t)bl.row_off32 & 3)))
             return MURR_E_ARGUMENT;
         for (uint32_t p = 0; p < nproj; p++) {
             const murr_array_t& o = outs[(uint64_t)b * nproj + p];
@@ -1531,8 +1568,25 @@ int murr_decode_enqueue_ix(murr_ctx_t* c, const murr_segment_t* seg, const uint3
     std::vector<DecBlock> db(nblocks);
     uint64_t tiles = 0;
     uint32_t nonempty = 0;
+    // this kernel reads u64 offsets: u32 blocks are widened into c->wide first
+    uint64_t nwide = 0;
+    for (uint32_t b = 0; b < nblocks; b++)
+        if (blocks[b].row_off32 && blocks[b].n_rows) nwide += blocks[b].n_rows + 1;
+    if (nwide > c->wide_cap) {
+        if (c->wide) HIPC(hipFree(c->wide));
+        c->wide = nullptr;
+        c->wide_cap = 0;
+        HIPC(hipMalloc(&c->wide, 8 * nwide));
+        c->wide_cap = nwide;
+    }
+    nwide = 0;
     for (uint32_t b = 0; b < nblocks; b++) {
-        db[b] = DecBlock{blocks[b].data, blocks[b].row_off, blocks[b].n_rows, tiles, nullptr};
+        db[b] = DecBlock{blocks[b].data, blocks[b].row_off, blocks[b].n_rows, tiles, nullptr, 0u, 0u};
+        if (blocks[b].row_off32 && blocks[b].n_rows) {
+            HIPC(launch_row_off_widen(blocks[b].row_off32, c->wide + nwide, blocks[b].n_rows + 1, c->stream));
+            db[b].row_off = c->wide + nwide;
+            nwide += blocks[b].n_rows + 1;
+        }
         tiles += (blocks[b].n_rows + R - 1) / R;
         nonempty += blocks[b].n_rows != 0;
     }
@@ -1645,13 +1699,14 @@ int murr_utf8_index_update(murr_ctx_t* c, const murr_segment_t* seg, const murr_
         a.nu++;
     }
     if (!a.nu) return MURR_OK;  // no utf8 column: nothing to index
-    if (!out || (block->n_rows && (!block->data || !block->row_off))) return MURR_E_ARGUMENT;
+    if (!out || (block->n_rows && (!block->data || (!block->row_off && !block->row_off32)))) return MURR_E_ARGUMENT;
     HIPC(hipSetDevice(c->device));
     const uint64_t nwin = utf8_index_windows(from, block->n_rows, stride);
     const int st = ensure_ws(c, 8 * std::max<uint64_t>(nwin, 1) * a.nu, err);
     if (st) return st;
     a.data = block->data;
     a.row_off = block->row_off;
+    a.row_off32 = block->row_off32;
     a.out = out;
     a.part = (uint64_t*)c->ws;
     a.from = from;
@@ -1772,6 +1827,7 @@ struct murr_plan {
     std::vector<uint32_t> dtypes;
     double est_row = 0;
     const JitLayout* jl = nullptr;  // pinned while the plan lives
+    uint32_t every = kTimeEvery;    // one run in `every` bracketed by timing events (0: none)
     bool replay = false;
     JitReplay r;
     bool sync_pending = false;  // (no replay) murr_decode_run_async ran the decode; wait returns its status
@@ -1859,11 +1915,12 @@ int murr_decode_run_async(murr_plan_t* P) {
     volatile uint64_t* done = (volatile uint64_t*)(R.hrb + R.z_lb);
     *done = 0;
     std::atomic_thread_fence(std::memory_order_seq_cst);
-    uint64_t every = kTimeEvery;
+    uint64_t every = P->every;
 #ifdef MURR_TUNING
     if (const char* e = std::getenv("MURR_TIME_EVERY")) every = std::max(1, std::atoi(e));  // A/B of the events' cost
 #endif
-    const bool timed = run % every == 0;
+    const bool timed = every && run % every == 0;
+    if (timed) R.timed_runs++;
     if (timed) HIPC(hipEventRecord(R.e0, c->stream));
     for (const auto& ka : R.kargs[set])
         HIPC(jit_decode_launch(R.K, R.split, ka.data(), ka.size(), R.grid, R.lds, c->stream));
@@ -1917,9 +1974,11 @@ int murr_decode_run_wait(murr_plan_t* P, murr_error_t* err) {
         HIPC(hipMemcpyAsync(R.hrb, set ? R.zb2 : R.dws, R.z_lb, hipMemcpyDeviceToHost, c->stream));
         HIPC(hipStreamSynchronize(c->stream));
     }
-    c->timed = true;  // the plan's last timed run (its first run is one)
-    c->lk0 = R.e0;
-    c->lk1 = R.t1;
+    if (R.timed_runs) {  // the plan's last timed run
+        c->timed = true;
+        c->lk0 = R.e0;
+        c->lk1 = R.t1;
+    }
     if (!R.kargs[0].empty()) c->last_kernel = "murr_jit_decode";
     c->stats.last_mode = R.mode;
     c->stats.last_grid = R.grid;
@@ -1942,6 +2001,12 @@ int murr_decode_run(murr_plan_t* P, murr_error_t* err) {
     const int st = murr_decode_run_async(P);
     if (st) return set_err(err, st);
     return murr_decode_run_wait(P, err);
+}
+
+int murr_plan_time_every(murr_plan_t* P, uint32_t every) {
+    if (!P) return MURR_E_ARGUMENT;
+    P->every = every;
+    return MURR_OK;
 }
 
 void murr_plan_free(murr_plan_t* P) {
@@ -1999,7 +2064,7 @@ int murr_encode_batch_ix(murr_ctx_t* c, const murr_segment_t* seg, const murr_co
     if (!stride_ok(stride) || (murr_utf8_index_len(seg, n, stride) && !uidx)) return set_err(err, MURR_E_ARGUMENT);
     const int st = murr_encode_batch_at(c, seg, cols, n, out_blob, blob_cap, out_row_off, 0, blob_len, err);
     if (st) return st;
-    const murr_block_t blk{out_blob, out_row_off, n, blob_len ? *blob_len : 0};
+    const murr_block_t blk{out_blob, out_row_off, n, blob_len ? *blob_len : 0, nullptr};
     const int ist = murr_utf8_index_update(c, seg, &blk, 0, stride, uidx);
     if (ist) return set_err(err, ist);
     HIPC(hipStreamSynchronize(c->stream));
@@ -2399,7 +2464,7 @@ int murr_builder_build(murr_builder_t* b, murr_host_array_t* outs, murr_error_t*
     if (b->hdata_len) HIPC(hipMemcpyAsync(ddata, b->hdata, b->hdata_len, hipMemcpyHostToDevice, c->stream));
     HIPC(hipMemcpyAsync(doff, b->hoff, obytes, hipMemcpyHostToDevice, c->stream));
     HIPC(hipEventRecord(b->e1, c->stream));
-    murr_block_t blk{ddata, doff, n, b->hdata_len};
+    murr_block_t blk{ddata, doff, n, b->hdata_len, nullptr};
     int st = decode_to_host(c, &b->seg, b->proj.data(), (uint32_t)np, blk, utf8_cap, b->out, b->e2, b->e3, outs, err);
     if (st) return st;
     (void)hipEventElapsedTime(&b->h2d_ms, b->e0, b->e1);
@@ -2649,7 +2714,7 @@ int hstream_enqueue(murr_hstream* h, HSlot& s, const uint8_t* data, const uint64
     s.h2d_bytes = head + bytes + obytes;
     // row i of the block is data[row_off[i]..]: the block's data pointer sits
     // row_off[0] & ~15 bytes before the staged bytes (16-B aligned)
-    murr_block_t blk{s.din - (b0 - head), doff, n, b1};
+    murr_block_t blk{s.din - (b0 - head), doff, n, b1, nullptr};
     const uint64_t utf8_cap = std::max<uint64_t>(bytes, 8);  // any one utf8 column's string bytes
     const uint32_t np = (uint32_t)h->proj.size();
     const uint64_t bm = murr_bitmap_bytes(n);
@@ -3052,7 +3117,7 @@ int murr_reader_read(murr_reader_t* r, const murr_index_t* x, const uint8_t* blo
     // (never read past: rows end at doff[nq]).
     const uint64_t mean = x->n ? blob_bytes / x->n : fixed;
     const uint64_t hint = std::min<uint64_t>(gathered, std::max<uint64_t>(16, mean * nq));
-    murr_block_t blk{w + o_data, doff, nq, two_phase ? std::max<uint64_t>(gathered, 16) : hint};
+    murr_block_t blk{w + o_data, doff, nq, two_phase ? std::max<uint64_t>(gathered, 16) : hint, nullptr};
     const uint64_t utf8_cap = two_phase ? gathered : (max_row > fixed ? nq * (max_row - fixed) : 0);
     return decode_to_host(c, &r->seg, proj, nproj, blk, utf8_cap, r->out, nullptr, nullptr, outs, err);
 }

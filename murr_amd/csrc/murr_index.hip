@@ -543,7 +543,8 @@ __global__ void __launch_bounds__(256) uidx_sums(Utf8IndexArgs A) {
         const uint32_t c = A.col[u], fo = A.fo[u];
         uint64_t sum = 0;
         for (uint64_t i = r0 + threadIdx.x; i < r1; i += 256) {
-            const uint64_t a = gp(A.row_off)[i], e = gp(A.row_off)[i + 1];
+            const uint64_t a = A.row_off32 ? (uint64_t)gp(A.row_off32)[i] : gp(A.row_off)[i];
+            const uint64_t e = A.row_off32 ? (uint64_t)gp(A.row_off32)[i + 1] : gp(A.row_off)[i + 1];
             if (e < a || e - a > 0xFFFFFFFFull) continue;  // the decode reports such a row
             const uint32_t rl = (uint32_t)(e - a);
             const uint8_t* row = A.data + a;

@@ -36,11 +36,18 @@ constexpr uint32_t kMaxProj = 1024;
 
 struct DecBlock {             // one block (batch read) of row blobs
     const uint8_t* data;
-    const uint64_t* row_off;  // n_rows + 1
+    const uint64_t* row_off;  // n_rows + 1 (u64, or u32 when ro32: then really a const uint32_t*)
     uint64_t n_rows;
     uint64_t tile_base;       // first global tile of this block
     const uint64_t* uidx;     // its utf8 index (murr_utf8_index) or null (JIT kernel only)
+    uint32_t ro32, pad;       // row_off holds u32 offsets (murr_block_t.row_off32; JIT kernel only)
 };
+static_assert(sizeof(DecBlock) == 48, "mj::Blk layout");
+// The offsets of a public block as the kernels take them.
+inline DecBlock dec_block(const murr_block_t& b, uint64_t tile_base, const uint64_t* uidx) {
+    return DecBlock{b.data, b.row_off32 ? (const uint64_t*)(const void*)b.row_off32 : b.row_off, b.n_rows, tile_base,
+                    uidx, b.row_off32 ? 1u : 0u, 0u};
+}
 
 struct DecProj {              // one projected column
     uint32_t dtype, bit, offset, width;
@@ -156,8 +163,10 @@ struct JitArgsHead {               // = mj::Args without its trailing slot[] (mu
     unsigned long long* rb_host;   // prepared launches: pinned read-back + done flag (last round only)
     uint32_t dyn_start;            // local mode: (virtual) blocks [0, dyn_start) dealt statically (0 = all)
     uint32_t dyn_pool;             // ... the rest in 8 per-XCD pools of dyn_pool, claimed at run time
+    uint32_t fast;                 // the loader's fast start: cut and split launches (murr_jit_kernel.hip)
+    uint32_t pad_;
 };
-static_assert(sizeof(JitArgsHead) == 176, "mj::Args layout");
+static_assert(sizeof(JitArgsHead) == 184, "mj::Args layout");
 // The compiled layout (cached; least recently used beyond 64 are retired).
 // pin: the caller will launch from it and calls jit_layout_unpin after the
 // launch is enqueued; until then no eviction unloads its module.
@@ -244,6 +253,7 @@ constexpr uint32_t kMaxUidxCols = 64;
 struct Utf8IndexArgs {
     const uint8_t* data;
     const uint64_t* row_off;
+    const uint32_t* row_off32;     // or these (murr_block_t.row_off32)
     uint64_t* out;                 // [(n + stride - 1) / stride + 1][nu]
     uint64_t* part;                // scratch: [windows][nu] window sums
     uint64_t from;                 // rows before `from` are indexed already (their entries, and the
@@ -316,6 +326,9 @@ struct CopyArgs {
     uint32_t nseg;
 };
 hipError_t launch_copy_segs(const CopySeg* segs, uint32_t n, uint32_t grid, hipStream_t s);
+// Row offsets u64 <-> u32, n entries (murr_kernels.hip).
+hipError_t launch_row_off_narrow(const uint64_t* in, uint32_t* out, uint64_t n, hipStream_t s);
+hipError_t launch_row_off_widen(const uint32_t* in, uint64_t* out, uint64_t n, hipStream_t s);
 
 // Arrow IPC framing (murr_ipc.cpp, murr_ipc.hip).
 enum : uint32_t { kIpcValidity = 0, kIpcOffsets = 1, kIpcValues = 2 };

@@ -273,13 +273,7 @@ bool compile(Entry& e, const std::string& pre, int device) {
 // decode waves' utf8 totals and the loader's 1 KiB prefetch scratch.
 uint32_t jit_lds_bytes(uint32_t nw, uint32_t r, uint32_t nslot, uint32_t stage, uint32_t nutf8) {
     const uint32_t tr = 64 * (nw - 1) * r;
-#ifdef MURR_TUNING
-    const char* defs = std::getenv("MURR_JIT_DEFS");
-    const uint32_t rw = defs && std::strstr(defs, "MJ_RO64=1") ? 8 : 4;  // MJ_RO64=1: whole u64 row offsets
-    const uint32_t ro = ((tr + 1) * rw + 16 + 15) & ~15u;
-#else
-    const uint32_t ro = ((tr + 1) * 4 + 16 + 15) & ~15u;
-#endif
+    const uint32_t ro = ((tr + 1) * 4 + 16 + 15) & ~15u;  // = Shape::RO_BYTES
     const uint32_t nu = std::max<uint32_t>(nutf8, 1);
     return nslot * (ro + stage + 64) + 128 + 256 + 32 + 8 * nu + ((8 * nu * (nw - 1) + 15) & ~15u) + 1024;
 }

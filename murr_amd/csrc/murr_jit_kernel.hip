@@ -67,10 +67,11 @@ namespace mj {
 // ---- argument block (layout shared with murr_jit.cpp: JitArgs) -------------
 struct Blk {  // = murr::DecBlock
     const uint8_t* data;
-    const uint64_t* row_off;
+    const uint64_t* row_off;  // u64 offsets, or (ro32) u32 ones
     uint64_t n_rows;
     uint64_t tile_base;    // first global tile of this block (stream mode)
     const uint64_t* uidx;  // utf8 index (murr_utf8_index) or null: [row / 2^ulog][NU] starting offsets
+    uint32_t ro32, pad;    // row_off holds u32 offsets (murr_block_t.row_off32)
 };
 // A segment: rows [r_begin, r_end) of block b; `first` is the index of the
 // block's first segment (split mode).  Local mode walks a table of them too:
@@ -114,6 +115,8 @@ struct Args {
     unsigned long long* rb_host;  // prepared launches: pinned host read-back ([rb_words] + done flag)
     uint32_t dyn_start;           // local mode: (virtual) blocks [0, dyn_start) dealt statically (0 = all)
     uint32_t dyn_pool;            // ... the rest in 8 per-XCD pools of dyn_pool (claimed, dyn_claim)
+    uint32_t fast;                // the loader's fast start (MJ_FASTSTART builds): cut and split launches
+    uint32_t pad_;
     uint16_t slot[(NCOLS + 1) & ~1u];  // output position of column c, 0xFFFF = not decoded
 };
 constexpr uint16_t kNone = 0xFFFF;
@@ -366,14 +369,13 @@ DEV void wait_vmcnt(uint32_t n) {
     }
 }
 
-// Row offsets in the ring slot: their low dwords gathered 64 per LDS-DMA
-// instruction (MJ_RO64 0, the default), or whole u64s, 128 per dwordx4
-// instruction (1: 27 -> 20 loader instructions per 768-row tile, measured
-// neutral on config B; tuning builds only, the host sizes LDS for 4 B per
-// row).  Only the low dwords are read (a tile's span is below 4 GiB).
-#ifndef MJ_RO64
-#define MJ_RO64 0
-#endif
+// Row offsets in the ring slot: 4 B per row.  u64 offsets: their low dwords
+// gathered 64 per LDS-DMA instruction (only the low dwords are read: a tile's
+// span is below 4 GiB).  u32 offsets (murr_block_t.row_off32): loaded
+// linearly, 256 per dwordx4 instruction from the 16-B aligned group at or
+// below the tile's first offset; the tile's offsets start `lead` dwords into
+// the slot.  (Round 2 also measured whole u64s by dwordx4, 128 per
+// instruction: neutral on B, and twice the LDS.)
 // Early release of ring slots in local mode (decode_tile, kernel_body); 0 =
 // one workgroup barrier per tile (tuning A/B).
 #ifndef MJ_ER
@@ -386,14 +388,16 @@ DEV void wait_vmcnt(uint32_t n) {
 #ifndef MJ_FASTSTART
 #define MJ_FASTSTART 1
 #endif
-constexpr uint32_t RO_STRIDE = MJ_RO64 ? 2 : 1;  // dwords per row offset in LDS
 
 // ---- shape ---------------------------------------------------------------------
 template <uint32_t NW_, uint32_t R_, uint32_t NSLOT_>
 struct Shape {
     static constexpr uint32_t NW = NW_, NC = NW_ - 1, R = R_, TR = 64 * (NW_ - 1) * R_;
-    // LDS slot: [row offsets, low dwords: (TR+1)*4 + 16][stage + 64 pad]
-    static constexpr uint32_t RO_BYTES = ((TR + 1) * (MJ_RO64 ? 8 : 4) + 16 + 15) & ~15u;
+    // LDS slot: [row offsets, u32: (TR+1)*4 + 16][stage + 64 pad].  A u32
+    // block's slice lands 16-B groups whole: up to 3 dwords before the tile's
+    // first offset and 3 after its last, (TR + 7) * 4 <= RO_BYTES.
+    static constexpr uint32_t RO_BYTES = ((TR + 1) * 4 + 16 + 15) & ~15u;
+    static_assert((TR + 7) * 4 <= RO_BYTES, "u32 offset groups fit the slot");
     // ring slots: 2 (one tile in flight while one decodes) or 3 (two in flight)
     static constexpr uint32_t NSLOT = NSLOT_;
     static_assert(NSLOT == 2 || NSLOT == 3, "ring of 2 or 3 slots");
@@ -424,7 +428,7 @@ struct Cur {
     const uint64_t* row_off;
     const uint64_t* uidx;
     uint64_t n_rows, r0, r_begin, r_end;
-    uint32_t k, b, first, phase, ok;
+    uint32_t k, b, first, phase, ok, ro32;
 };
 // Cursors are built whole by value (every field assigned on every path: a
 // conditionally stored field would keep the struct on the stack, and stack
@@ -443,6 +447,7 @@ DEV Cur cur_make(uint32_t ok, uint32_t k, uint32_t b, uint32_t first, uint32_t p
     c.row_off = ok ? (const uint64_t*)sgpr64((uint64_t)bp->row_off) : nullptr;
     c.n_rows = ok ? sgpr64(bp->n_rows) : 0;
     c.uidx = ok ? (const uint64_t*)sgpr64((uint64_t)bp->uidx) : nullptr;
+    c.ro32 = ok ? sgpr(bp->ro32) : 0u;
     c.r_begin = r_begin;
     c.r_end = ok && r_end == ~0ull ? c.n_rows : r_end;
     return c;
@@ -658,14 +663,22 @@ DEV uint32_t tile_announce(const Cur& c, LAS uint8_t* span_ent, LAS uint8_t* inf
             ti->r0 = c.r0;
             ti->t = c.k;
             ti->first = c.first;
+            // bit 7: u32 offsets; bits 8-9: the dwords before the tile's
+            // first offset in its aligned 16-B group (tile_dma)
+            const uint32_t lead = c.ro32 ? (uint32_t)(((uintptr_t)((const uint32_t*)c.row_off + c.r0) >> 2) & 3u) : 0u;
             ti->flags = (c.r0 == 0 ? 1u : 0u) | (c.r0 + nr == c.n_rows ? 2u : 0u) | 4u |
-                        (c.r0 == c.r_begin ? 8u : 0u) | (c.r0 + nr == c.r_end ? 16u : 0u) | (c.phase << 5);
+                        (c.r0 == c.r_begin ? 8u : 0u) | (c.r0 + nr == c.r_end ? 16u : 0u) | (c.phase << 5) |
+                        (c.ro32 << 7) | (lead << 8);
         } else {
             ti->flags = 0;
         }
     }
     if (!c.ok) return 0;
-    if (lane < 4) {
+    if (c.ro32) {
+        // the span's two u32 offsets into the low dwords of the two u64
+        // entries (lanes 0 and 2; tile_read masks the high dwords)
+        if (lane == 0 || lane == 2) glds4((const GAS uint32_t*)c.row_off + c.r0 + (lane ? cur_nr<TR>(c) : 0u), span_ent);
+    } else if (lane < 4) {
         const uint64_t r = c.r0 + (lane < 2 ? 0u : cur_nr<TR>(c));
         glds4((const GAS uint8_t*)(c.row_off + r) + (lane & 1) * 4, span_ent);
     }
@@ -685,6 +698,7 @@ struct Tile {
     const uint8_t* data;
     const uint64_t* row_off;
     uint32_t b, nr, hbm, span, first, last, seg_first, seg_last, first_seg;
+    uint32_t ro32, lead;  // u32 offsets; the tile's first offset is dword `lead` of the slot
 };
 DEV Tile tile_read(const LAS uint8_t* span_ent, const LAS uint8_t* info_ent, uint32_t stage) {
     const LAS TileInfo* ti = (const LAS TileInfo*)info_ent;
@@ -698,9 +712,12 @@ DEV Tile tile_read(const LAS uint8_t* span_ent, const LAS uint8_t* info_ent, uin
     T.last = (f >> 1) & 1u;
     T.seg_first = (f >> 3) & 1u;
     T.seg_last = (f >> 4) & 1u;
+    T.ro32 = (f >> 7) & 1u;
+    T.lead = (f >> 8) & 3u;
     T.first_seg = sgpr(ti->first);
-    const uint64_t base = sgpr64(((const LAS uint64_t*)span_ent)[0]);
-    const uint64_t end = sgpr64(((const LAS uint64_t*)span_ent)[1]);
+    const uint64_t m = T.ro32 ? 0xFFFFFFFFull : ~0ull;  // (u32 offsets: the high dwords are stale)
+    const uint64_t base = sgpr64(((const LAS uint64_t*)span_ent)[0]) & m;
+    const uint64_t end = sgpr64(((const LAS uint64_t*)span_ent)[1]) & m;
     T.abase = base & ~15ull;
     const uint64_t span = ((end + 15) & ~15ull) - T.abase;
     T.hbm = end < base || end - T.abase > 0xFFFFFF00ull ? 2u : span > stage ? 1u : 0u;
@@ -725,25 +742,23 @@ DEV Tile tile_read_ptrs(const LAS uint8_t* span_ent, const LAS uint8_t* info_ent
 DEV uint32_t tile_valid(const LAS uint8_t* info_ent) { return sgpr(((const LAS TileInfo*)info_ent)->flags) & 4u; }
 DEV uint32_t tile_phase(const LAS uint8_t* info_ent) { return (sgpr(((const LAS TileInfo*)info_ent)->flags) >> 5) & 3u; }
 
-// The loader wave's LDS-DMA of one tile: its row-offset slice (low dwords,
-// a gather: lane j of piece q fetches row_off[r0 + 64q + j]), then (unless it
-// outgrew the stage) its blob span in 1 KiB pieces.
+// The loader wave's LDS-DMA of one tile: its row-offset slice, then (unless
+// it outgrew the stage) its blob span in 1 KiB pieces.  u64 offsets: their
+// low dwords, a gather (lane j of piece q fetches row_off[r0 + 64q + j]).
+// u32 offsets: the aligned 16-B groups that cover row_off32[r0 .. r0 + nr],
+// a linear dwordx4 stream (lane j of piece q: group 64q + j).  The groups at
+// either end hold only whole dwords of the same 16 B, so they never leave the
+// pages the offsets live in.
 template <uint32_t TR, uint32_t RO_BYTES>
 DEV uint32_t tile_dma(const Tile& T, LAS uint8_t* slot, uint32_t lane) {
     uint32_t n = 0;
-    const GAS uint32_t* ro = (const GAS uint32_t*)(T.row_off + T.r0);
-    if constexpr (MJ_RO64) {
-        // offsets r0 .. r0 + nr: whole pairs as dwordx4 (lane j of piece q:
-        // offsets 128q + 2j, +1), an odd last one as two dwords (lanes 0, 1),
-        // so nothing past row_off[n_rows] is read
-        const uint32_t cnt = T.nr + 1, pairs = cnt >> 1;
-        for (uint32_t q = 0; q * 64 < pairs; q++, n++)  // lane 0 is always active: one instruction each
-            if (q * 64 + lane < pairs) glds16(ro + 4 * (q * 64 + lane), slot + q * 1024);
-        if (cnt & 1) {
-            if (lane < 2) glds4(ro + 2 * (cnt - 1) + lane, slot + 8 * (cnt - 1));
-            n++;
-        }
+    if (T.ro32) {
+        const GAS uint8_t* g = (const GAS uint8_t*)((uintptr_t)((const uint32_t*)T.row_off + T.r0) & ~(uintptr_t)15);
+        const uint32_t groups = (T.lead + T.nr + 1 + 3) >> 2;
+        for (uint32_t q = 0; q * 64 < groups; q++, n++)  // lane 0 is always active: one instruction each
+            if (q * 64 + lane < groups) glds16(g + (q * 64 + lane) * 16, slot + q * 1024);
     } else {
+        const GAS uint32_t* ro = (const GAS uint32_t*)(T.row_off + T.r0);
         for (uint32_t q = 0; q * 64 <= T.nr; q++, n++)  // lane 0 is always active: one instruction each
             if (q * 64 + lane <= T.nr) glds4(ro + 2 * (q * 64 + lane), slot + q * 256);
     }
@@ -1205,7 +1220,7 @@ DEV void decode_tile(const Src& src, const Tile& T, const LAS uint32_t* ro, LAS 
 #pragma unroll
     for (uint32_t k = 0; k < R; k++) {
         const uint32_t i = rbase + k * 64 + lane;
-        const uint32_t a0 = ro[RO_STRIDE * i], a1 = ro[RO_STRIDE * (i + 1)];
+        const uint32_t a0 = ro[i], a1 = ro[i + 1];
         const uint32_t rl = i < T.nr ? a1 - a0 : 0u;
         W.ra[k] = a0 - abase;
         W.rl[k] = rl;
@@ -1580,13 +1595,19 @@ DEV void kernel_body() {
         // and announces tile i + NSLOT + 2 (its identity and span), then waits
         // for tile i + 1.  It issues no other vector-memory instruction, so
         // its counted vmcnt waits for exactly the DMA it needs.
-        if constexpr (FAST) warm_scalar<MODE>();
+        // Fast start for cut and split launches only (args.fast): with many
+        // short virtual blocks per workgroup it took the D shard 0.0866 ->
+        // 0.0852 ms, while whole-block launches (config B) ran 0.758 -> 0.771.
+        const bool fast = ER ? FAST : FAST && args()->fast != 0;
+        if (fast) warm_scalar<MODE>();
         Cur cs = cur_first<MODE>();  // next tile to announce
         Claim cl{0u, 0u, 0u, 0u, MODE == 0 && args()->dyn_start && blockIdx.x + gridDim.x >= args()->dyn_start, 0u, 0u};
         // tiles announced before the first DMA: 0 .. 3, or (fast start) 0 .. 1 / 0
-        constexpr uint32_t NPRE = !FAST ? NSLOT + 1 : ER ? 1u : 0u;
+        constexpr uint32_t NPRE_ER = FAST ? 1u : NSLOT + 1;
+        const uint32_t npre = ER ? NPRE_ER : fast ? 0u : NSLOT + 1;
 #pragma unroll
-        for (uint32_t k = 0; k <= NPRE; k++) {
+        for (uint32_t k = 0; k <= NSLOT + 1; k++) {
+            if (k > npre) break;
             tile_announce<TR>(cs, spans + (k & 7) * 16, infos + (k & 7) * 32, lane, pf + (k & 7) * 8 * NU);
             cs = cur_next<TR>(cs, cl);
         }
@@ -1672,7 +1693,7 @@ DEV void kernel_body() {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             return;
         }
-        if constexpr (FAST) {
+        if (fast) {
             // fast start: tile 0's DMA, then the announcements of tiles 1 .. 3 behind it
             if (tile_valid(infos)) tile_dma<TR, SH::RO_BYTES>(tile_read_ptrs(spans, infos, stage), lds, lane);
 #pragma unroll
@@ -1777,7 +1798,7 @@ DEV void kernel_body() {
 #endif
         LAS uint8_t* slot = lds + (it % NSLOT) * SLOT;
         const Tile T = tile_read(spans + (it & 7) * 16, info, stage);
-        const LAS uint32_t* ro = (const LAS uint32_t*)slot;
+        const LAS uint32_t* ro = (const LAS uint32_t*)slot + T.lead;
         const uint32_t ph = tile_phase(info);
         if (MODE == 0 && T.seg_first) {
             // local mode: a (virtual) block starts at 0, or at its utf8 index

@@ -143,6 +143,16 @@ class Context:
         """Kernel of the last decode: "murr_jit_decode" or "decode_kernel"."""
         return (self.L.murr_ctx_last_kernel(self.h) or b"").decode()
 
+    def mark(self, which: int):
+        """murr_ctx_mark: a timing mark on this context's stream."""
+        raise_status(self.L.murr_ctx_mark(self.h, which), what="murr_ctx_mark")
+
+    def mark_ms(self, a: int, b: int) -> float:
+        """GPU milliseconds from mark a to mark b (waits for b)."""
+        ms = C.c_float()
+        raise_status(self.L.murr_ctx_mark_ms(self.h, a, b, C.byref(ms)), what="murr_ctx_mark_ms")
+        return ms.value
+
     def last_kernel_ms(self) -> float:
         ms = C.c_float()
         raise_status(self.L.murr_ctx_last_kernel_ms(self.h, C.byref(ms)), what="kernel time")
@@ -186,13 +196,46 @@ class DeviceBuffer:
 @dataclass
 class DeviceBlock:
     """murr_block_t: row blobs back to back + row offsets (n_rows + 1), and
-    optionally its utf8 index (murr_utf8_index, built by `index_utf8`)."""
+    optionally its utf8 index (murr_utf8_index, built by `index_utf8`).
+    Offsets are u64 (`row_off`) or u32 (`row_off32`, which the decode then
+    reads instead: half the index bytes; `narrow` makes them)."""
     data: DeviceBuffer
-    row_off: DeviceBuffer
+    row_off: "DeviceBuffer | None"
     n_rows: int
     data_bytes: int
     uidx: "DeviceBuffer | None" = None
     stride: int = 0
+    row_off32: "DeviceBuffer | None" = None
+
+    @property
+    def offset_width(self) -> int:
+        return 4 if self.row_off32 is not None else 8
+
+    def c_block(self, cb=None):
+        """The murr_block_t of this block (filled into `cb` when given)."""
+        cb = cb if cb is not None else _abi.Block()
+        cb.data = self.data.ptr
+        cb.row_off = self.row_off.ptr if self.row_off is not None else None
+        cb.n_rows, cb.data_bytes = self.n_rows, self.data_bytes
+        cb.row_off32 = self.row_off32.ptr if self.row_off32 is not None else None
+        return cb
+
+    def narrow(self, ctx: "Context", keep64: bool = False) -> "DeviceBlock":
+        """The same block with u32 row offsets (murr_row_off_narrow; raises
+        when the block's bytes reach 2^32).  keep64: keep the u64 ones too."""
+        if self.row_off32 is not None:
+            return self
+        buf = ctx.alloc(4 * (self.n_rows + 1))
+        raise_status(ctx.L.murr_row_off_narrow(ctx.h, self.row_off.ptr, self.n_rows, buf.ptr),
+                     what="murr_row_off_narrow")
+        return DeviceBlock(self.data, self.row_off if keep64 else None, self.n_rows, self.data_bytes, self.uidx,
+                           self.stride, buf)
+
+    def host_offsets(self) -> np.ndarray:
+        """The row offsets as host u64 (either width on the device)."""
+        if self.row_off32 is not None:
+            return self.row_off32.download(4 * (self.n_rows + 1)).view(np.uint32).astype(np.uint64)
+        return self.row_off.download(8 * (self.n_rows + 1)).view(np.uint64).copy()
 
     def index_utf8(self, ctx: "Context", segment: SegmentSchema, stride: int = 512) -> "DeviceBlock":
         """Build the block's utf8 index (per `stride` rows, every utf8 column's
@@ -203,15 +246,21 @@ class DeviceBlock:
             self.uidx, self.stride = None, 0
             return self
         buf = ctx.alloc(8 * n)
-        cb = _abi.Block(self.data.ptr, self.row_off.ptr, self.n_rows, self.data_bytes)
+        cb = self.c_block()
         raise_status(ctx.L.murr_utf8_index(ctx.h, C.byref(segment.c), C.byref(cb), stride, buf.ptr),
                      what="murr_utf8_index")
         self.uidx, self.stride = buf, stride
         return self
 
     @classmethod
-    def upload(cls, ctx: Context, data: np.ndarray, row_off: np.ndarray) -> "DeviceBlock":
+    def upload(cls, ctx: Context, data: np.ndarray, row_off: np.ndarray, width: int = 8) -> "DeviceBlock":
+        """A block from host bytes; width 4 uploads the offsets as u32."""
         data = np.ascontiguousarray(data, dtype=np.uint8)
+        if width == 4:
+            ro = np.ascontiguousarray(row_off, dtype=np.uint64)
+            if ro.size and int(ro[-1]) >= 1 << 32:
+                raise ValueError("u32 row offsets: the block's bytes reach 2^32")
+            return cls(ctx.upload(data), None, ro.size - 1, data.nbytes, row_off32=ctx.upload(ro.astype(np.uint32)))
         row_off = np.ascontiguousarray(row_off, dtype=np.uint64)
         return cls(ctx.upload(data), ctx.upload(row_off), row_off.size - 1, data.nbytes)
 
@@ -263,10 +312,7 @@ def decode_blocks(ctx: Context, segment: SegmentSchema, proj, blocks, outs: Deco
     outs = outs or DecodeOutputs(ctx, segment, proj, blocks)
     cb = (_abi.Block * max(len(blocks), 1))()
     for i, blk in enumerate(blocks):
-        cb[i].data = blk.data.ptr
-        cb[i].row_off = blk.row_off.ptr
-        cb[i].n_rows = blk.n_rows
-        cb[i].data_bytes = blk.data_bytes
+        blk.c_block(cb[i])
     pj = (C.c_uint32 * max(len(proj), 1))(*proj)
     err = _abi.Error()
     ix = [b.uidx for b in blocks]
@@ -296,8 +342,7 @@ class DecodePlan:
         k = max(len(self.blocks), 1)
         self._cb = (_abi.Block * k)()
         for i, blk in enumerate(self.blocks):
-            self._cb[i].data, self._cb[i].row_off = blk.data.ptr, blk.row_off.ptr
-            self._cb[i].n_rows, self._cb[i].data_bytes = blk.n_rows, blk.data_bytes
+            blk.c_block(self._cb[i])
         self._pj = (C.c_uint32 * max(len(self.proj), 1))(*self.proj)
         ix = [b.uidx for b in self.blocks]
         self._ux, stride = None, 0
@@ -313,6 +358,10 @@ class DecodePlan:
         raise_status(st, what="murr_decode_plan")
         self.h = h.value
         self._err = _abi.Error()
+
+    def time_every(self, every: int):
+        """murr_plan_time_every: time one run in `every` (0: none)."""
+        raise_status(self.ctx.L.murr_plan_time_every(self.h, every), what="murr_plan_time_every")
 
     def run(self) -> "DecodeOutputs":
         st = self.ctx.L.murr_decode_run(self.h, C.byref(self._err))

@@ -7,8 +7,12 @@ eight distinct sources rotate over the 1000 slots, so a block decoded into
 another block's outputs (or from another block's bytes) shows up.  The first,
 the last, two random blocks and one block of every source are compared with
 the oracle's decode after repeated runs; the launch must not have needed the
-split-abort retry."""
+split-abort retry.  Both offset widths: u32 (row_off32, the bench's default
+since round 5) and u64.  Then bench.py itself, whose line must be
+self-consistent: the kernel time it reports never exceeds its step."""
+import json
 import os
+import subprocess
 import sys
 
 import numpy as np
@@ -26,7 +30,8 @@ pytestmark = pytest.mark.gpu
 ROWS, K, SOURCES, STRIDE = 100_000, 1000, 8, 512
 
 
-def test_bench_config_b_launch_block_by_block():
+@pytest.mark.parametrize("width", [32, 64])
+def test_bench_config_b_launch_block_by_block(width):
     set_default_opts()  # bench's default shape and mode
     ctx = Context(0)
     plan = None
@@ -36,9 +41,14 @@ def test_bench_config_b_launch_block_by_block():
             cols = bench.make_columns("B", ROWS, start=s * ROWS)
             seg = SegmentSchema([(f"c{i}", c["dtype"]) for i, c in enumerate(cols)])
             b = encode_block(ctx, seg, synth.upload_columns(ctx, cols), ROWS, STRIDE)
-            srcs.append(b)
+            if width == 32:
+                b = b.narrow(ctx, keep64=True)
             hosts.append((b.data.download(b.data_bytes),
                           b.row_off.download(8 * (ROWS + 1)).view(np.uint64).copy()))
+            if width == 32:
+                assert np.array_equal(b.host_offsets(), hosts[-1][1])
+                b.row_off = None  # the decode sees the u32 offsets only
+            srcs.append(b)
         blocks = [srcs[i] if i < SOURCES else bench.copy_block(ctx, srcs[i % SOURCES]) for i in range(K)]
         proj = [0, 1]
         outs = DecodeOutputs(ctx, seg, proj, blocks)
@@ -62,3 +72,22 @@ def test_bench_config_b_launch_block_by_block():
         if plan is not None:
             plan.close()
         ctx.close()
+
+
+def test_bench_line_is_self_consistent():
+    """bench.py's own line (a shorter run of the headline launch): verified
+    against the oracle, u32 offsets counted at 4 B per row, and kernel_ms_avg
+    (GPU marks around the timed region / steps) <= ms_per_step (the host
+    clock around the same steps)."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--steps", "12", "--warmup", "3",
+                          "--blocks", "300", "--no-cpu", "--no-traffic"],
+                         capture_output=True, text=True, timeout=240, cwd=root)
+    assert out.returncode == 0, out.stderr[-2000:]
+    line = json.loads(out.stdout.strip().splitlines()[-1])
+    rf = line["roofline"]
+    assert line["verified"].startswith("blocks"), line["verified"]
+    assert line["config"]["row_offset_bytes"] == 4
+    assert rf["kernel_ms_avg"] <= line["ms_per_step"], (rf["kernel_ms_avg"], line["ms_per_step"])
+    assert rf["frac_step"] <= rf["frac"] + 1e-9
+    assert line["config"]["bytes_in_per_step"] == 300 * (1788890 + 4 * 100001 + 1576)

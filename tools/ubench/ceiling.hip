@@ -114,6 +114,32 @@ __global__ void mix_gs(const u32x4* __restrict__ a, const u32x4* __restrict__ b,
     }
 }
 
+// Chunked B-shape mix (round 5): workgroup g owns chunk g, g + G, ... of a
+// launch of `nchunk` chunks; a chunk is `steps` steps, and in one step every
+// lane loads UA 16-B elements of stream a and UB of stream b (contiguous runs,
+// like a block's blob and its row offsets), then stores UW of o (its Arrow
+// outputs).  UA:UB:UW = 4:2:3 is config B's byte mix with u64 row offsets
+// (2.0 : 1), 4:1:3 with u32 offsets (1.67 : 1).
+template <int UA, int UB, int UW>
+__global__ void mixb_chunk(const u32x4* __restrict__ a, const u32x4* __restrict__ b, u32x4* __restrict__ o,
+                           unsigned nchunk, unsigned steps) {
+    const size_t B = blockDim.x;
+    for (unsigned c = blockIdx.x; c < nchunk; c += gridDim.x) {
+        const u32x4* pa = a + (size_t)c * steps * B * UA;
+        const u32x4* pb = b + (size_t)c * steps * B * UB;
+        u32x4* po = o + (size_t)c * steps * B * UW;
+        for (unsigned s = 0; s < steps; s++) {
+            u32x4 v[UA], x[UB];
+#pragma unroll
+            for (int k = 0; k < UA; k++) v[k] = pa[((size_t)s * UA + k) * B + threadIdx.x];
+#pragma unroll
+            for (int k = 0; k < UB; k++) x[k] = pb[((size_t)s * UB + k) * B + threadIdx.x];
+#pragma unroll
+            for (int k = 0; k < UW; k++) po[((size_t)s * UW + k) * B + threadIdx.x] = v[k] ^ x[k % UB];
+        }
+    }
+}
+
 int main(int argc, char** argv) {
     const size_t bytes = (argc > 1 ? std::atoll(argv[1]) : 2048) << 20;  // MiB per buffer
     const size_t n = bytes / 16;
@@ -176,6 +202,24 @@ int main(int argc, char** argv) {
         show(nm, g, 256, timeit([&] { cp_chunk<8, false><<<g, 256>>>(a, o, n, per); }), 32.0 * n);
         std::snprintf(nm, sizeof nm, "copy  chunk %zuK U4 1k", chunk_kib);
         show(nm, g, 1024, timeit([&] { cp_chunk<4, false><<<g, 1024>>>(a, o, n, per); }), 32.0 * n);
+    }
+    // config B's shape: 1000 chunks of ~2.6 MB read / 1.3 MB written (u64
+    // offsets), or ~2.2 / 1.3 MB (u32), over 4 workgroups per CU of 320 or
+    // 256 threads -- a workgroup owns one chunk, as the decode's local mode
+    for (unsigned thr : {256u, 320u}) {
+        for (int ro32 = 0; ro32 < 2; ro32++) {
+            const unsigned nchunk = 1000, g = cus * 4;
+            const size_t per_w = 1288894 / 16;                       // B's Arrow bytes per block, in elements
+            const unsigned steps = (unsigned)(per_w / (thr * 3));    // UW = 3
+            const double moved = (double)nchunk * steps * thr * 16.0 * (ro32 ? 8 : 9);
+            if ((size_t)nchunk * steps * thr * 4 > n) continue;
+            char nm[64];
+            std::snprintf(nm, sizeof nm, "mixB chunk %s t%u", ro32 ? "4:1:3" : "4:2:3", thr);
+            if (ro32)
+                show(nm, g, thr, timeit([&] { mixb_chunk<4, 1, 3><<<g, thr>>>(a, b, o, nchunk, steps); }), moved);
+            else
+                show(nm, g, thr, timeit([&] { mixb_chunk<4, 2, 3><<<g, thr>>>(a, b, o, nchunk, steps); }), moved);
+        }
     }
     {
         float ms = 0;
