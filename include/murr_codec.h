@@ -462,6 +462,11 @@ int murr_hstream_new(murr_ctx_t* ctx, const murr_segment_t* seg, const uint32_t*
                      uint32_t nproj, uint32_t depth, murr_hstream_t** out);
 int murr_hstream_submit(murr_hstream_t* s, const uint8_t* data, const uint64_t* row_off,
                         uint64_t n_rows, uint32_t flags, murr_error_t* err);
+/* The same batch with u32 row offsets (a block below 4 GiB, as every batch
+ * read is): half the offset bytes staged and sent over PCIe, decoded as a
+ * murr_block_t with row_off32. */
+int murr_hstream_submit32(murr_hstream_t* s, const uint8_t* data, const uint32_t* row_off,
+                          uint64_t n_rows, uint32_t flags, murr_error_t* err);
 int murr_hstream_next(murr_hstream_t* s, murr_host_array_t* outs /* nproj */, murr_error_t* err);
 /* Totals since creation: batches returned; the bytes each copy direction
  * moved; device milliseconds of the H2D copies, the decode kernels and the

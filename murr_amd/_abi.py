@@ -169,6 +169,7 @@ SIGNATURES = {
     "murr_builder_free": (None, [P]),
     "murr_hstream_new": (I32, [P, C.POINTER(Segment), C.POINTER(U32), U32, U32, PP]),
     "murr_hstream_submit": (I32, [P, P, P, U64, U32, C.POINTER(Error)]),
+    "murr_hstream_submit32": (I32, [P, P, P, U64, U32, C.POINTER(Error)]),
     "murr_hstream_next": (I32, [P, C.POINTER(HostArray), C.POINTER(Error)]),
     "murr_hstream_stats": (I32, [P, C.POINTER(HStreamStats)]),
     "murr_hstream_free": (None, [P]),

@@ -2531,11 +2531,18 @@ struct CopyPool {
         const uint8_t* src;
         uint64_t n;
     };
+    // One copy() call's pieces and counters.  Each call makes a new one and a
+    // worker takes it under the lock, so a worker that wakes late for an
+    // earlier call works on (and counts into) that call's job only, never on
+    // a job the caller is building.
+    struct Job {
+        std::vector<Piece> pieces;
+        std::atomic<size_t> next{0}, done{0};
+    };
     std::vector<std::thread> th;
     std::mutex m;
     std::condition_variable cv;
-    std::vector<Piece> job;
-    std::atomic<size_t> next{0}, done{0};
+    std::shared_ptr<Job> cur;
     uint64_t gen = 0;
     bool stop = false;
 
@@ -2557,37 +2564,38 @@ struct CopyPool {
         for (auto& t : th)
             if (t.joinable()) t.join();
     }
-    void drain() {
-        for (size_t i; (i = next.fetch_add(1)) < job.size(); done.fetch_add(1))
-            std::memcpy(job[i].dst, job[i].src, job[i].n);
+    static void drain(Job& j) {
+        for (size_t i; (i = j.next.fetch_add(1)) < j.pieces.size(); j.done.fetch_add(1))
+            std::memcpy(j.pieces[i].dst, j.pieces[i].src, j.pieces[i].n);
     }
     void work() {
         uint64_t seen = 0;
         for (;;) {
+            std::shared_ptr<Job> j;
             {
                 std::unique_lock<std::mutex> g(m);
                 cv.wait(g, [&] { return stop || gen != seen; });
                 if (stop) return;
                 seen = gen;
+                j = cur;
             }
-            drain();
+            if (j) drain(*j);
         }
     }
     // copy every (dst, src, n) of `parts`; returns when all bytes are copied
     void copy(const std::vector<Piece>& parts) {
         constexpr uint64_t kPiece = 256 << 10;
+        auto j = std::make_shared<Job>();
+        for (const Piece& p : parts)
+            for (uint64_t o = 0; o < p.n; o += kPiece) j->pieces.push_back(Piece{p.dst + o, p.src + o, std::min(kPiece, p.n - o)});
         {
             std::lock_guard<std::mutex> g(m);
-            job.clear();
-            for (const Piece& p : parts)
-                for (uint64_t o = 0; o < p.n; o += kPiece) job.push_back(Piece{p.dst + o, p.src + o, std::min(kPiece, p.n - o)});
-            next.store(0);
-            done.store(0);
+            cur = j;
             gen++;
         }
         cv.notify_all();
-        drain();
-        while (done.load() < job.size()) std::this_thread::yield();
+        drain(*j);
+        while (j->done.load() < j->pieces.size()) std::this_thread::yield();
     }
 };
 
@@ -2645,17 +2653,32 @@ const uint8_t* pinned_dev_view(const void* p) {
 // Enqueue batch `s` (everything after the staging copy is asynchronous).  The
 // output region is laid out as decode_to_host's, its utf8 parts bounded by the
 // blob bytes.
-int hstream_enqueue(murr_hstream* h, HSlot& s, const uint8_t* data, const uint64_t* row_off, uint64_t n,
+int hstream_enqueue(murr_hstream* h, HSlot& s, const uint8_t* data, const void* row_off, uint32_t w, uint64_t n,
                     bool pinned, murr_error_t* err) {
     murr_ctx* c = s.c;
+    // The context's fused-transfer state is set for one decode enqueue only:
+    // clear it on every way out, so a failed batch leaves nothing behind for
+    // the next one on this slot (a stale `xin` would copy old sources).
+    struct XferReset {
+        murr_ctx* c;
+        ~XferReset() {
+            c->xfer = false;
+            c->xin.clear();
+            c->xout.clear();
+        }
+    } xreset{c};
     HIPC(hipSetDevice(c->device));
-    const uint64_t b0 = n ? row_off[0] : 0, b1 = n ? row_off[n] : 0;
+    // row offsets: u64, or u32 (murr_hstream_submit32: half the index bytes over PCIe)
+    auto off_at = [&](uint64_t i) -> uint64_t {
+        return w == 4 ? ((const uint32_t*)row_off)[i] : ((const uint64_t*)row_off)[i];
+    };
+    const uint64_t b0 = n ? off_at(0) : 0, b1 = n ? off_at(n) : 0;
     if (b1 < b0) return set_err(err, MURR_E_ARGUMENT);
     const uint64_t bytes = b1 - b0, head = b0 & 15;
-    const uint64_t dbytes = round_up(head + bytes + 16, 64), obytes = (n + 1) * 8;
+    const uint64_t dbytes = round_up(head + bytes + 16, 64), obytes = (n + 1) * w;
     if (!grow_dev(c, &s.din, &s.din_cap, dbytes + obytes)) return set_err(err, MURR_E_HIP);
     const uint8_t* src_data = data + (b0 - head);
-    const uint64_t* src_off = row_off;
+    const uint8_t* src_off = (const uint8_t*)row_off;
     // H2D: the copy engine for large batches; below ~1 MiB its fixed cost per
     // copy (~10 us, two copies) dominates, and the copy kernel takes the bytes
     // (config C's 1000-key reads: 2.8 -> 3.6 GiB/s)
@@ -2666,7 +2689,7 @@ int hstream_enqueue(murr_hstream* h, HSlot& s, const uint8_t* data, const uint64
         const uint8_t* doo = pinned_dev_view(row_off);
         if (dd && doo) {
             src_data = dd;
-            src_off = (const uint64_t*)doo;
+            src_off = doo;
         } else {
             pinned = false;  // (not pinned after all: staged like pageable bytes)
         }
@@ -2690,9 +2713,9 @@ int hstream_enqueue(murr_hstream* h, HSlot& s, const uint8_t* data, const uint64
             std::memcpy(s.hin + dbytes, row_off, obytes);
         }
         src_data = s.hin;
-        src_off = (const uint64_t*)(s.hin + dbytes);
+        src_off = s.hin + dbytes;
     }
-    uint64_t* doff = (uint64_t*)(s.din + dbytes);
+    uint8_t* doff = s.din + dbytes;
     s.timed = (h->head & 7) == 0;  // every eighth batch carries timing events
     if (engine) {
         // input copies by the copy engine, on the slot stream ahead of the decode
@@ -2702,8 +2725,7 @@ int hstream_enqueue(murr_hstream* h, HSlot& s, const uint8_t* data, const uint64
         if (s.timed) HIPC(hipEventRecord(s.e1, c->stream));
     } else if (h->fused) {
         // input copies: with the decode's descriptors, in one kernel (murr_decode_enqueue)
-        c->xin.assign({CopySeg{src_data, s.din, head + bytes, nullptr},
-                       CopySeg{(const uint8_t*)src_off, (uint8_t*)doff, obytes, nullptr}});
+        c->xin.assign({CopySeg{src_data, s.din, head + bytes, nullptr}, CopySeg{src_off, doff, obytes, nullptr}});
     } else {
         if (s.timed) HIPC(hipEventRecord(s.e0, h->s_h2d));
         if (head + bytes) HIPC(hipMemcpyAsync(s.din, src_data, head + bytes, hipMemcpyHostToDevice, h->s_h2d));
@@ -2714,7 +2736,8 @@ int hstream_enqueue(murr_hstream* h, HSlot& s, const uint8_t* data, const uint64
     s.h2d_bytes = head + bytes + obytes;
     // row i of the block is data[row_off[i]..]: the block's data pointer sits
     // row_off[0] & ~15 bytes before the staged bytes (16-B aligned)
-    murr_block_t blk{s.din - (b0 - head), doff, n, b1, nullptr};
+    murr_block_t blk{s.din - (b0 - head), w == 8 ? (const uint64_t*)doff : nullptr, n, b1,
+                     w == 4 ? (const uint32_t*)doff : nullptr};
     const uint64_t utf8_cap = std::max<uint64_t>(bytes, 8);  // any one utf8 column's string bytes
     const uint32_t np = (uint32_t)h->proj.size();
     const uint64_t bm = murr_bitmap_bytes(n);
@@ -2769,9 +2792,6 @@ int hstream_enqueue(murr_hstream* h, HSlot& s, const uint8_t* data, const uint64
         c->xe[3] = s.e3;
     }
     const int st = murr_decode_enqueue(c, &h->seg, h->proj.data(), np, &blk, 1, o.arr.data());
-    c->xfer = false;
-    c->xin.clear();
-    c->xout.clear();
     if (st) return set_err(err, st, st == MURR_E_HIP ? (int)hipGetLastError() : 0);
     HIPC(hipEventRecord(s.ed, c->stream));  // the decode and its counters' read-back are done
     s.d2h_bytes = fixed_out;  // (the fixed-size part, queued with the utf8 bytes once the counters are in)
@@ -2895,8 +2915,9 @@ int murr_hstream_new(murr_ctx_t* c, const murr_segment_t* seg, const uint32_t* p
     return MURR_OK;
 }
 
-int murr_hstream_submit(murr_hstream_t* h, const uint8_t* data, const uint64_t* row_off, uint64_t n_rows,
-                        uint32_t flags, murr_error_t* err) {
+namespace {
+int hstream_submit(murr_hstream_t* h, const uint8_t* data, const void* row_off, uint32_t w, uint64_t n_rows,
+                   uint32_t flags, murr_error_t* err) {
     if (!h || !row_off || (n_rows && !data) || h->head - h->tail >= h->slots.size())
         return set_err(err, MURR_E_ARGUMENT);
     const auto t0 = std::chrono::steady_clock::now();
@@ -2908,13 +2929,24 @@ int murr_hstream_submit(murr_hstream_t* h, const uint8_t* data, const uint64_t* 
     hstream_progress(h);  // D2H of the batches whose decode finished, queued early
     HSlot& s = h->slots[h->head % h->slots.size()];
     s.submit_err = murr_error_t{};
-    s.submit_status = hstream_enqueue(h, s, data, row_off, n_rows, (flags & MURR_HSTREAM_PINNED) != 0, &s.submit_err);
+    s.submit_status = hstream_enqueue(h, s, data, row_off, w, n_rows, (flags & MURR_HSTREAM_PINNED) != 0, &s.submit_err);
     if (s.submit_status && s.c->pending) {  // (an enqueue failure after the launch: drain it)
         murr_error_t e2{};
         (void)murr_decode_wait(s.c, &e2);
     }
     h->head++;
     return MURR_OK;
+}
+}  // namespace
+
+int murr_hstream_submit(murr_hstream_t* h, const uint8_t* data, const uint64_t* row_off, uint64_t n_rows,
+                        uint32_t flags, murr_error_t* err) {
+    return hstream_submit(h, data, row_off, 8, n_rows, flags, err);
+}
+
+int murr_hstream_submit32(murr_hstream_t* h, const uint8_t* data, const uint32_t* row_off, uint64_t n_rows,
+                          uint32_t flags, murr_error_t* err) {
+    return hstream_submit(h, data, row_off, 4, n_rows, flags, err);
 }
 
 int murr_hstream_next(murr_hstream_t* h, murr_host_array_t* outs, murr_error_t* err) {

@@ -178,14 +178,19 @@ class HostStream:
         self._err = _abi.Error()
 
     def submit(self, data, row_off, pinned: bool = False):
-        row_off = np.ascontiguousarray(row_off, dtype=np.uint64)
+        """One batch: rows back to back at `data`, row_off (n + 1 entries) as
+        u64, or as u32 (murr_hstream_submit32: half the offset bytes over
+        PCIe) when row_off is a uint32 array."""
+        w32 = getattr(row_off, "dtype", None) == np.uint32
+        row_off = np.ascontiguousarray(row_off, dtype=np.uint32 if w32 else np.uint64)
         n = row_off.size - 1
         if n < 0:
             raise ValueError("row_off needs n_rows + 1 entries")
         dptr = data.ctypes.data if hasattr(data, "ctypes") else int(data)
         err = _abi.Error()
-        raise_status(self.L.murr_hstream_submit(self.h, dptr, row_off.ctypes.data, n, 1 if pinned else 0,
-                                                C.byref(err)), err, "murr_hstream_submit")
+        fn = self.L.murr_hstream_submit32 if w32 else self.L.murr_hstream_submit
+        raise_status(fn(self.h, dptr, row_off.ctypes.data, n, 1 if pinned else 0, C.byref(err)), err,
+                     "murr_hstream_submit")
         self._keep[self._seq] = (data, row_off) if pinned else None
         self._seq += 1
 

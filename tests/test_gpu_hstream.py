@@ -4,7 +4,8 @@ bit-exact against the oracle's ReadBatchBuilder restatement
 (src/io/row/read.rs:62-110), from pinned and from pageable sources, with
 missing rows, empty and one-row batches, blocks that start mid-buffer, and a
 malformed batch that fails alone (ReadBatchBuilder::build's error) while the
-batches around it decode."""
+batches around it decode.  Row offsets as u64 (murr_hstream_submit) and as
+u32 (murr_hstream_submit32)."""
 import numpy as np
 import pytest
 
@@ -38,8 +39,9 @@ def check(outs, oseg, proj, data, off, what):
         assert_array_equal(host_array_buffers(outs[p]), want[p], f"{what} col {p}")
 
 
-@pytest.mark.parametrize("depth,pinned", [(2, False), (3, True), (4, False), (8, True)])
-def test_stream_random_batches_vs_oracle(ctx, depth, pinned):
+@pytest.mark.parametrize("depth,pinned,width", [(2, False, 64), (3, True, 64), (4, False, 64), (8, True, 64),
+                                                (2, False, 32), (3, True, 32), (8, True, 32)])
+def test_stream_random_batches_vs_oracle(ctx, depth, pinned, width):
     rng = np.random.default_rng(100 + depth)
     dtypes = [D.Utf8, D.Int32, D.Bool, D.Float64, D.Utf8, D.UInt8, D.Int16, D.Int64, D.UInt64, D.Float32,
               D.Int8, D.UInt16, D.UInt32]
@@ -56,15 +58,17 @@ def test_stream_random_batches_vs_oracle(ctx, depth, pinned):
         batches.append((data, off))
     hs = HostStream(seg, proj, depth=depth, ctx=ctx)
     keep = []
+    odt = np.uint32 if width == 32 else np.uint64
 
     def submit(k):
         data, off = batches[k]
+        off = off.astype(odt)
         if pinned:
             hb, ho = HostBuffer(data.size + 16, ctx), HostBuffer(off.nbytes, ctx)
             hb.array[: data.size] = data
             ho.array[:] = off.view(np.uint8)
             keep.append((hb, ho))
-            hs.submit(hb.array, ho.array.view(np.uint64), pinned=True)
+            hs.submit(hb.array, ho.array.view(odt), pinned=True)
         else:
             # a scratch copy the caller overwrites right after submit: the
             # library staged it already
@@ -92,33 +96,45 @@ def test_stream_random_batches_vs_oracle(ctx, depth, pinned):
     hs.close()
 
 
-def test_stream_config_b_full_size_every_block(ctx):
+@pytest.mark.parametrize("width,pinned", [(64, True), (32, True), (32, False)])
+def test_stream_config_b_full_size_every_block(ctx, width, pinned):
     # configs[1]'s 100k-row FLOAT32 + UTF8 blocks, 12 batches through three
-    # slots from a pinned ring of four: every block bit-exact
+    # slots from a ring of four: every block bit-exact.  Pageable sources
+    # above 1 MiB are staged by the copy pool's threads, batch after batch
+    # (each copy's pieces are its own job: no worker of an earlier copy can
+    # touch the next one's)
     n, ring = 100_000, 4
+    odt = np.uint32 if width == 32 else np.uint64
     seg = SegmentSchema([("f", D.Float32), ("s", D.Utf8)])
     oseg = O.Segment([int(D.Float32), int(D.Utf8)])
     srcs = []
     for r in range(ring):
         cols = synth.config_b(n, start=r * n, null_frac=0.05 if r % 2 else 0.0, seed=r)
         data, off = encode_host(ctx, seg, cols, n)
-        hb, ho = HostBuffer(data.size + 16, ctx), HostBuffer(off.nbytes, ctx)
+        o = off.astype(odt)
+        hb, ho = HostBuffer(data.size + 16, ctx), HostBuffer(o.nbytes, ctx)
         hb.array[: data.size] = data
-        ho.array[:] = off.view(np.uint8)
+        ho.array[:] = o.view(np.uint8)
         srcs.append((hb, ho, data, off))
     hs = HostStream(seg, [0, 1], depth=3, ctx=ctx)
     total, nxt = 12, 0
+
+    def submit(i):
+        hb, ho, data, off = srcs[i % ring]
+        if pinned:
+            hs.submit(hb.array, ho.array.view(odt), pinned=True)
+        else:
+            hs.submit(data, off.astype(odt))
+
     while nxt < 3:
-        hb, ho, _, _ = srcs[nxt % ring]
-        hs.submit(hb.array, ho.array.view(np.uint64), pinned=True)
+        submit(nxt)
         nxt += 1
     for k in range(total):
         outs = hs.next()
         _, _, data, off = srcs[k % ring]
         check(outs, oseg, [0, 1], data, off, f"batch {k}")
         if nxt < total:
-            hb, ho, _, _ = srcs[nxt % ring]
-            hs.submit(hb.array, ho.array.view(np.uint64), pinned=True)
+            submit(nxt)
             nxt += 1
     hs.close()
 
@@ -133,8 +149,9 @@ def test_stream_block_starting_mid_buffer(ctx):
     cols = random_columns(rng, dtypes, 5000, null_p=0.1)
     data, off = encode_host(ctx, seg, cols, 5000)
     hs = HostStream(seg, [0, 1], depth=2, ctx=ctx)
-    for lo, hi in [(37, 4000), (1, 2), (4999, 5000), (0, 5000)]:
-        sub = off[lo:hi + 1]
+    off32 = off.astype(np.uint32)
+    for lo, hi, w in [(37, 4000, 64), (1, 2, 64), (4999, 5000, 64), (0, 5000, 64), (37, 4000, 32), (3, 5000, 32)]:
+        sub = off[lo:hi + 1] if w == 64 else off32[lo:hi + 1]  # (u32: offsets at any 4-byte alignment)
         hs.submit(data, sub)
         outs = hs.next()
         base = int(off[lo])
