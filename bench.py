@@ -468,7 +468,10 @@ def run_decode(args, dist, rank, world, local_rank):
     # stream).  --sync-steps: one set, each step waited for (the A/B).
     # --lanes 2: the second output set's plan on a second context (its own
     # stream), so step s + 1's workgroups can start on CUs step s has left
-    ctxs = [ctx, Context(local_rank) if args.lanes == 2 and rt is None else ctx]
+    # (config D's default: a resident shard's scan ends with a long tail)
+    if args.lanes is None:
+        args.lanes = 2 if args.config == "D" else 1
+    ctxs = [ctx, Context(local_rank) if args.lanes == 2 else ctx]
     if args.arena:
         out_sets = [ArenaOutputs(c, seg, proj, blocks, args.arena) for c in ctxs]
     else:
@@ -477,7 +480,7 @@ def run_decode(args, dist, rank, world, local_rank):
         names = [seg.columns[c].name for c in proj]
 
         def launch(i):  # the product call (its prepared plan after the first)
-            return rt.scan_device_async(names, out_sets[i])
+            return rt.scan_device_async(names, out_sets[i], ctx=ctxs[i])
     else:
         # the launch prepared once per output set (murr_decode_plan)
         plans = [DecodePlan(c, seg, proj, blocks, o) for c, o in zip(ctxs, out_sets)]
@@ -492,8 +495,9 @@ def run_decode(args, dist, rank, world, local_rank):
     # and brackets all K launches with two marks on the context's stream:
     # kernel_ms_avg = that GPU time / K, which includes the gaps between the
     # launches, so it never exceeds ms_per_step (the host's clock around the
-    # same K steps).  With two lanes (two streams) the launches overlap and
-    # the warm-up samples stand in.
+    # same K steps).  With two lanes (two streams) the region runs from the
+    # first lane's start mark to the later of the two lanes' end marks: the
+    # launches overlap, so this is the GPU time per launch at steady state.
     runs = [0, 0]  # runs of each output set's plan so far
     every = _abi.PLAN_TIME_EVERY
     if "MURR_TIME_EVERY" in os.environ and _abi.LIB_PATH.endswith("_tuning.so"):
@@ -527,24 +531,22 @@ def run_decode(args, dist, rank, world, local_rank):
         return ms
 
     wms = run_steps(args.warmup)
-    region = args.lanes == 1
-    if region:
-        for p in launched.values():
-            p.time_every(0)
+    for p in launched.values():
+        p.time_every(0)
+    lanes = list({id(c): c for c in ctxs}.values())
     barrier(dist)
     for c in ctxs:
         c.sync()
     t0 = time.perf_counter()
-    if region:
-        ctx.mark(0)
-    kms = run_steps(args.steps, sample=not region)
-    if region:
-        ctx.mark(1)
+    ctx.mark(0)
+    kms = run_steps(args.steps, sample=False)
+    for c in lanes:
+        c.mark(1)
     for c in ctxs:
         c.sync()
     barrier(dist)
     elapsed = time.perf_counter() - t0
-    region_ms = ctx.mark_ms(0, 1) if region and args.steps else None
+    region_ms = max(ctx.mark_ms(0, 1, c) for c in lanes) if args.steps else None
     for p in launched.values():
         p.time_every(every)
     last = 0 if args.sync_steps else (args.steps - 1) % 2
@@ -1159,9 +1161,10 @@ def main():
                     help="skip the oracle check of the timed output (tuning ablations that skip stores only)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--pmc-csv", default=None)
-    ap.add_argument("--lanes", type=int, default=1, choices=[1, 2],
-                    help="decode: 2 = the alternating output sets' plans on two contexts (two streams; "
-                         "block decodes only, not --config D)")
+    ap.add_argument("--lanes", type=int, default=None, choices=[1, 2],
+                    help="decode: 2 = the alternating output sets' plans on two contexts (two streams), "
+                         "so a launch starts on the CUs the previous one's tail leaves; default 2 for "
+                         "--config D, else 1")
     ap.add_argument("--sync-steps", action="store_true",
                     help="one plan, each step waited for before the next is launched (A/B of the pipelined loop)")
     ap.add_argument("--no-traffic", action="store_true",

@@ -131,9 +131,10 @@ const char* murr_ctx_last_kernel(murr_ctx_t* ctx);
 int  murr_device_count(int* n);
 /* Timing marks on the context's stream (benchmarks): murr_ctx_mark records
  * mark `which` (0-3) behind the work queued so far; murr_ctx_mark_ms waits for
- * mark b and returns the GPU time from mark a to mark b. */
+ * mark b of context cb and returns the GPU time from mark a of context ca to
+ * it (two contexts of one device: work spread over their streams). */
 int murr_ctx_mark(murr_ctx_t* ctx, uint32_t which);
-int murr_ctx_mark_ms(murr_ctx_t* ctx, uint32_t a, uint32_t b, float* ms);
+int murr_ctx_mark_ms(murr_ctx_t* ca, uint32_t a, murr_ctx_t* cb, uint32_t b, float* ms);
 
 /* Kernel selection of one context, for tests and benchmarks.  All zero (the
  * state of a new context) = the library's own choice.  Set once; every later
@@ -158,10 +159,7 @@ typedef struct {
                                grid, each workgroup walking several (virtual) blocks);
                                0xFFFFFFFF = one workgroup per (virtual) block, handed to the
                                CUs by the hardware as workgroups finish */
-    uint32_t balance;       /* local mode, several (virtual) blocks per workgroup: 0 auto
-                               (= static: measured faster), 1 static deal only,
-                               2 dynamic per-XCD tail with half the blocks dealt statically,
-                               10..90 dynamic with that percentage dealt statically */
+    uint32_t reserved;      /* 0 (round 4's dynamic-tail switch, removed: measured slower) */
 } murr_opts_t;
 int murr_ctx_set_opts(murr_ctx_t* ctx, const murr_opts_t* opts);
 int murr_ctx_get_opts(murr_ctx_t* ctx, murr_opts_t* opts);

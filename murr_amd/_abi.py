@@ -40,7 +40,7 @@ class Opts(C.Structure):
     """murr_opts_t: kernel selection of one context (tests, benchmarks)."""
     _fields_ = [(n, C.c_uint32) for n in ("kernel", "mode", "shape_nw", "shape_r", "seg_tiles", "vrows",
                                           "lds_budget", "stage", "encode_kernel", "verbose", "grid",
-                                          "balance")]
+                                          "reserved")]
 
 
 class CtxStats(C.Structure):
@@ -147,7 +147,7 @@ SIGNATURES = {
     "murr_plan_free": (None, [P]),
     "murr_plan_time_every": (I32, [P, U32]),
     "murr_ctx_mark": (I32, [P, U32]),
-    "murr_ctx_mark_ms": (I32, [P, U32, U32, C.POINTER(C.c_float)]),
+    "murr_ctx_mark_ms": (I32, [P, U32, P, U32, C.POINTER(C.c_float)]),
     "murr_sst_decode": (I32, [P, C.POINTER(SstBlock), U32, C.POINTER(SstResult), C.POINTER(Error)]),
     "murr_sst_result_free": (None, [P, C.POINTER(SstResult)]),
     "murr_utf8_index": (I32, [P, C.POINTER(Segment), C.POINTER(Block), U32, P]),

@@ -734,16 +734,18 @@ int murr_ctx_mark(murr_ctx_t* c, uint32_t which) {
     return MURR_OK;
 }
 
-int murr_ctx_mark_ms(murr_ctx_t* c, uint32_t a, uint32_t b, float* ms) {
+int murr_ctx_mark_ms(murr_ctx_t* ca, uint32_t a, murr_ctx_t* cb, uint32_t b, float* ms) {
     murr_error_t* err = nullptr;
-    if (!c || !ms || a >= 4 || b >= 4 || !c->mk[a] || !c->mk[b]) return MURR_E_ARGUMENT;
-    HIPC(hipEventSynchronize(c->mk[b]));
-    HIPC(hipEventElapsedTime(ms, c->mk[a], c->mk[b]));
+    if (!ca || !cb || !ms || a >= 4 || b >= 4 || !ca->mk[a] || !cb->mk[b] || ca->device != cb->device)
+        return MURR_E_ARGUMENT;
+    HIPC(hipEventSynchronize(cb->mk[b]));
+    HIPC(hipEventElapsedTime(ms, ca->mk[a], cb->mk[b]));
     return MURR_OK;
 }
 
 int murr_ctx_set_opts(murr_ctx_t* c, const murr_opts_t* o) {
-    if (!c || !o || o->kernel > 2 || o->mode > 3 || o->encode_kernel > 2 || (!o->shape_nw) != (!o->shape_r))
+    if (!c || !o || o->kernel > 2 || o->mode > 3 || o->encode_kernel > 2 || (!o->shape_nw) != (!o->shape_r) ||
+        o->reserved)
         return MURR_E_ARGUMENT;
     c->opts = *o;
     return MURR_OK;
@@ -1038,37 +1040,40 @@ int decode_enqueue_jit(murr_ctx* c, const murr_segment_t* seg, const JitLayout* 
     // 512 / alloc, and a 5-wave workgroup may put 2 waves on one SIMD.
     // (the occupancy and register queries are cached per kernel and LDS size:
     // each is a runtime call that costs microseconds on every launch)
-    auto occupancy = [&](hipFunction_t fn) {
+    // (keyed on the shape's uid: a module the JIT cache unloaded may leave its
+    // function address to a later one, which must not inherit its answers)
+    auto occupancy = [&](hipFunction_t fn, bool split) {
         static std::mutex mu;
-        static std::map<std::pair<hipFunction_t, uint32_t>, int> cache;
+        static std::map<std::pair<uint64_t, uint32_t>, int> cache;
+        const std::pair<uint64_t, uint32_t> key{2 * K.uid + (split ? 1 : 0), lds};
         int n = 0;
         {
             std::lock_guard<std::mutex> g(mu);
-            auto it = cache.find({fn, lds});
+            auto it = cache.find(key);
             if (it != cache.end()) n = it->second;
         }
         if (!n) {
             if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, 64 * K.nw, lds) != hipSuccess || n < 1) n = 1;
             std::lock_guard<std::mutex> g(mu);
-            cache[{fn, lds}] = n;
+            cache[key] = n;
         }
         return std::min<int>(n, std::max<int>(1, (int)(163840 / std::max<uint32_t>(lds, 1))));
     };
-    const int bpc = occupancy(K.fn);
-    int bpc_safe = occupancy(K.fn_split);
+    const int bpc = occupancy(K.fn, false);
+    int bpc_safe = occupancy(K.fn_split, true);
     {
         static std::mutex mu;
-        static std::map<hipFunction_t, int> regs;
+        static std::map<uint64_t, int> regs;
         int vgprs = 0;
         {
             std::lock_guard<std::mutex> g(mu);
-            auto it = regs.find(K.fn_split);
+            auto it = regs.find(K.uid);
             if (it != regs.end()) vgprs = it->second;
         }
         if (!vgprs) {
             if (hipFuncGetAttribute(&vgprs, HIP_FUNC_ATTRIBUTE_NUM_REGS, K.fn_split) != hipSuccess || vgprs < 1) vgprs = 128;
             std::lock_guard<std::mutex> g(mu);
-            regs[K.fn_split] = vgprs;
+            regs[K.uid] = vgprs;
         }
         const int alloc = (vgprs + 7) / 8 * 8;
         const int per_simd = std::min(std::min(8, 512 / alloc), 6);
@@ -1189,27 +1194,6 @@ int decode_enqueue_jit(murr_ctx* c, const murr_segment_t* seg, const JitLayout* 
         for (size_t i = 0; i < free_pos.size(); i++) out[free_pos[i]] = lsegs[free_vb[i]];
         lsegs.swap(out);
     }
-    // Local mode with several (virtual) blocks per workgroup: the first share
-    // dealt statically, the rest claimed at run time from eight per-XCD pools
-    // (murr_jit_kernel.hip dyn_claim), so the launch does not end with its
-    // slowest workgroups.  Opt-in (balance >= 2) and with one projection round
-    // (the pool counters serve one launch): measured slower on the D shard,
-    // whose claims wait on device-scope atomics, so auto
-    // deals statically.
-    uint32_t dyn_start = 0, dyn_pool = 0;
-    {
-        const uint32_t bal = O.balance;
-        const uint64_t nv = lsegs.size();
-        const bool want = bal >= 2;
-        if (local && want && nv > grid && nv < 0xFFFFFFFFull) {
-            // (rounds is known below; dynamic needs one round)
-            const uint32_t pct = bal >= 10 && bal <= 90 ? bal : 50;
-            uint64_t per = std::max<uint64_t>(1, (nv * pct / 100) / grid);
-            dyn_start = (uint32_t)std::min<uint64_t>(nv, per * grid);
-            dyn_pool = (uint32_t)((nv - dyn_start + 7) / 8);
-            if (!dyn_pool) dyn_start = 0;
-        }
-    }
     bool emit = false;
     for (uint32_t p = 0; p < nproj; p++) emit |= dp[p].is_utf8;
 
@@ -1218,7 +1202,6 @@ int decode_enqueue_jit(murr_ctx* c, const murr_segment_t* seg, const JitLayout* 
     for (uint32_t p = 0; p < nproj; p++) occ[proj[p]].push_back(p);
     uint32_t rounds = 1;
     for (const auto& v : occ) rounds = std::max<uint32_t>(rounds, (uint32_t)v.size());
-    if (rounds > 1) dyn_start = dyn_pool = 0;
     const uint32_t ncols = seg->ncols, npad = (ncols + 1) & ~1u;
 
     std::vector<DecOut> dout((uint64_t)nblocks * nproj);
@@ -1309,15 +1292,13 @@ int decode_enqueue_jit(murr_ctx* c, const murr_segment_t* seg, const JitLayout* 
     h.ulog = cut && nu_layout ? (uint32_t)__builtin_ctzll(stride) : 0;
     h.mode = local ? 0 : 1;
     h.stage = stage;
-    h.dyn_start = dyn_start;
-    h.dyn_pool = dyn_pool;
     h.fast = cut || !local ? 1u : 0u;
     if (verbose)
-        std::fprintf(stderr, "decode launch (jit %ux%us%u): %s grid %llu (%d/CU, %d split) blocks %llu tiles %llu segments %llu (%llu tiles) rows/tile %u stage %u lds %u rounds %u dyn %u+8x%u\n",
+        std::fprintf(stderr, "decode launch (jit %ux%us%u): %s grid %llu (%d/CU, %d split) blocks %llu tiles %llu segments %llu (%llu tiles) rows/tile %u stage %u lds %u rounds %u fast %u\n",
                      K.nw, K.r, K.nslot, cut ? "local-cut" : local ? "local" : "split", (unsigned long long)grid, bpc, bpc_safe,
                      (unsigned long long)(local ? lsegs.size() : nonempty),
                      (unsigned long long)tiles, (unsigned long long)nseg, (unsigned long long)seg_tiles, K.tr, stage, lds, rounds,
-                     dyn_start, dyn_pool);
+                     h.fast);
 #ifdef MURR_TUNING
     c->tl_off = rep ? 0 : d_sink;
     c->tl_n = grid;

@@ -23,10 +23,9 @@ constexpr uint32_t kStage = 32768;
 // Default decode stage (bytes of row blobs per tile held in LDS).
 constexpr uint32_t kDecStage = 36864;
 // Workspace head: the error word, then phase-stamp slots of tuning builds
-// (err[2 .. 2 + kStampSlots)), then the JIT kernel's eight per-XCD virtual-
-// block pool counters (one 64-B line each, err[kPoolWord + 8 x]), then the
-// per-(block, column) counters.  The last stamp slot, err[17], is the JIT
-// kernel's tuning virtual-block queue.
+// (err[2 .. 2 + kStampSlots)), then eight spare 64-B lines (round 4's
+// per-XCD claim counters, removed in round 5), then the per-(block, column)
+// counters.
 constexpr uint32_t kStampSlots = 16;
 constexpr uint32_t kPoolWord = 2 + kStampSlots, kPoolStride = 8;
 constexpr uint64_t kErrBytes = 8 * (kPoolWord + 8 * kPoolStride);
@@ -130,6 +129,8 @@ struct JitShapeK {
     hipFunction_t fn = nullptr, fn_split = nullptr;  // local / split mode kernels
     uint32_t nw = 0, r = 0, tr = 0;  // waves (nw-1 decode, 1 loads), chunks per decode wave, rows per tile
     uint32_t nslot = 2;              // LDS ring slots (nslot - 1 tiles in flight)
+    uint64_t uid = 0;                // unique per compiled module shape (never reused: keys per-kernel caches,
+                                     // which must not outlive an unloaded module whose address is reused)
 };
 struct JitLayout {
     JitShapeK shapes[kJitShapes];
@@ -161,12 +162,10 @@ struct JitArgsHead {               // = mj::Args without its trailing slot[] (mu
     uint32_t zero_words, rb_words;
     unsigned int* ticket;          // prepared launches: workgroups finished (in the counter set)
     unsigned long long* rb_host;   // prepared launches: pinned read-back + done flag (last round only)
-    uint32_t dyn_start;            // local mode: (virtual) blocks [0, dyn_start) dealt statically (0 = all)
-    uint32_t dyn_pool;             // ... the rest in 8 per-XCD pools of dyn_pool, claimed at run time
     uint32_t fast;                 // the loader's fast start: cut and split launches (murr_jit_kernel.hip)
     uint32_t pad_;
 };
-static_assert(sizeof(JitArgsHead) == 184, "mj::Args layout");
+static_assert(sizeof(JitArgsHead) == 176, "mj::Args layout");
 // The compiled layout (cached; least recently used beyond 64 are retired).
 // pin: the caller will launch from it and calls jit_layout_unpin after the
 // launch is enqueued; until then no eviction unloads its module.

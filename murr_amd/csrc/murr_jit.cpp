@@ -15,6 +15,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -254,6 +255,8 @@ bool compile(Entry& e, const std::string& pre, int device) {
         k.r = kJitShapeTab[s][1];
         k.nslot = kJitShapeTab[s][2];
         k.tr = 64 * (k.nw - 1) * k.r;
+        static std::atomic<uint64_t> g_uid{0};
+        k.uid = ++g_uid;
         const std::string sh = std::to_string(k.nw) + "x" + std::to_string(k.r) + (k.nslot == 2 ? "" : "s3");
         he = hipModuleGetFunction(&k.fn, e.mod, ("murr_jit_decode_" + sh).c_str());
         if (he == hipSuccess) he = hipModuleGetFunction(&k.fn_split, e.mod, ("murr_jit_decode_split_" + sh).c_str());

@@ -113,15 +113,11 @@ struct Args {
     uint32_t zero_words, rb_words;  // ... its dwords; counter words the epilogue copies to rb_host
     unsigned int* ticket;         // prepared launches: workgroups finished (in the counter set)
     unsigned long long* rb_host;  // prepared launches: pinned host read-back ([rb_words] + done flag)
-    uint32_t dyn_start;           // local mode: (virtual) blocks [0, dyn_start) dealt statically (0 = all)
-    uint32_t dyn_pool;            // ... the rest in 8 per-XCD pools of dyn_pool (claimed, dyn_claim)
     uint32_t fast;                // the loader's fast start (MJ_FASTSTART builds): cut and split launches
     uint32_t pad_;
     uint16_t slot[(NCOLS + 1) & ~1u];  // output position of column c, 0xFFFF = not decoded
 };
 constexpr uint16_t kNone = 0xFFFF;
-constexpr uint32_t kQueueWord = 17;  // err[17]: local mode's virtual-block queue (the last stamp slot)
-constexpr uint32_t kPoolWord = 18, kPoolStride = 8;  // err[18 + 8 x]: pool x's claim counter (= murr_internal.h)
 
 enum : uint32_t { kStUtf8 = 1, kStOverflow = 4, kStMalformed = 5, kStCapacity = 6, kStInternal = 10 };
 // Phase stamps of tuning builds (MURR_JIT_DEFS=MJ_STAMPS): shader cycles
@@ -490,143 +486,23 @@ template <uint32_t MODE> DEV void warm_scalar() {
     }
     asm volatile("; warm %0" ::"s"(acc));
 }
-// Tuning (MJ_QUEUE=1): local mode hands out the virtual blocks after each
-// workgroup's first from a queue (a counter beside the error word, zeroed
-// with it), so a workgroup that runs fast takes more of them.  Measured
-// slower: one agent-scope counter serves about one claim per 10 ns, so the
-// D shard's first tiles waited 13 us (512-row virtual blocks, 0.086 -> 0.097
-// ms) and 52 us (128-row ones, 0.167 ms); C gained 1-2 %, B neutral.  The
-// static deal (workgroup g takes g, g + G, ...) stays.
-#ifndef MJ_QUEUE
-#define MJ_QUEUE 0
-#endif
-DEV uint32_t claim_vblock(uint32_t k_static) {
-#if MJ_QUEUE
-    (void)k_static;
-    uint32_t k = 0;
-    if (lane_id() == 0)
-        k = __hip_atomic_fetch_add((GAS uint32_t*)(args()->err + kQueueWord), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return gridDim.x + sgpr(k);
-#else
-    return k_static;
-#endif
-}
-// Local mode's dynamic tail (args.dyn_start != 0).  The (virtual) blocks
-// [0, dyn_start) are dealt statically (workgroup g takes g, g + G, ...); the
-// rest sit in eight pools of dyn_pool consecutive ones, pool x served first
-// to the workgroups running on XCD x.  A loader whose static share is done
-// claims the next one from its own XCD's pool (one returning agent-scope add
-// on the pool's counter, which sits on a 64-B line of its own); once that pool
-// is empty, one sweep of all eight counters (a load per lane) finds a pool
-// that is not, and it claims there.  So a workgroup that runs fast -- on a
-// fast XCD, or a CU with less contention -- takes more of the tail, and the
-// launch ends when the last claimed block does, not when the slowest
-// workgroup's fixed share does (the D shard's end-time spread).
-DEV uint32_t xcc_id() { return __builtin_amdgcn_s_getreg(20 | (3 << 11)) & 7u; }
-DEV GAS uint32_t* pool_cnt(uint32_t x) { return (GAS uint32_t*)((GAS unsigned long long*)args()->err + kPoolWord + kPoolStride * x); }
-DEV uint32_t pool_lo(uint32_t x) { return args()->dyn_start + x * args()->dyn_pool; }
-DEV uint32_t pool_size(uint32_t x) {
-    const uint32_t lo = pool_lo(x), no = args()->norder;
-    return lo < no ? umin32(args()->dyn_pool, no - lo) : 0u;
-}
-// A claim in flight: a returning add on pool x's counter issued by lane 0
-// (inline asm: the compiler sees neither the load nor its destination, so it
-// inserts no vmcnt wait of its own -- the loader's counted waits cover it).
-// A claim takes kClaim consecutive blocks of a pool: the next claim is issued
-// when the first of them is taken and is not needed before the last of them
-// is, by which time (two tiles in flight at most) a loader wait has covered it.
-constexpr uint32_t kClaim = 3;
-struct Claim {
-    uint32_t v;     // lane 0: the counter's old value (valid once `ready`)
-    uint32_t x;     // its pool
-    uint32_t pend;  // a claim is in flight
-    uint32_t ready; // a vmcnt wait of the loader has covered it since
-    uint32_t want;  // the static share is (nearly) done: keep one claim in flight
-    uint32_t nxt, nend;  // claimed blocks not yet used: [nxt, nend)
-};
-DEV void claim_issue(Claim& cl, uint32_t x) {
-    uint32_t r = 0;
-    if (lane_id() == 0) {
-        GAS uint32_t* p = pool_cnt(x);
-        asm volatile("global_atomic_add %0, %1, %2, off sc0" : "=v"(r) : "v"(p), "v"(kClaim) : "memory");
-    }
-    cl.v = r;
-    cl.x = x;
-    cl.pend = 1;
-    cl.ready = 0;
-}
-// A synchronous claim: this XCD's pool, else the first pool a sweep of all
-// eight counters (a load per lane) shows not empty.
-DEV uint32_t dyn_claim() {
-    const uint32_t no = args()->norder;
-    const uint32_t lane = lane_id(), me = xcc_id();
-    uint32_t x = me;
-#pragma unroll 1
-    for (uint32_t attempt = 0; attempt < 24; attempt++) {
-        if (attempt) {
-            const uint32_t sz = lane < 8 ? pool_size(lane) : 0u;
-            uint32_t c = ~0u;
-            if (lane < 8) c = __hip_atomic_load(pool_cnt(lane), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const uint32_t avail = (uint32_t)__ballot(lane < 8 && c < sz) & 0xFFu;
-            if (!avail) return no;
-            const uint32_t rot = ((avail >> me) | (avail << (8 - me))) & 0xFFu;
-            x = (me + (uint32_t)__builtin_ctz(rot)) & 7u;
-        }
-        const uint32_t sz = pool_size(x);
-        if (!sz) continue;
-        uint32_t i = 0;
-        if (lane == 0) i = __hip_atomic_fetch_add(pool_cnt(x), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        i = sgpr(i);
-        if (i < sz) return pool_lo(x) + i;
-    }
-    return no;
-}
-// The claim in flight, resolved: its block, or (its pool ran dry) a
-// synchronous claim elsewhere.  Not yet covered by a loader wait: wait here.
-DEV uint32_t claim_take(Claim& cl) {
-    if (!cl.ready) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const uint32_t i = (uint32_t)__builtin_amdgcn_readlane(cl.v, 0), sz = pool_size(cl.x);
-    cl.pend = 0;
-    if (i < sz) {
-        cl.nxt = pool_lo(cl.x) + i + 1;
-        cl.nend = pool_lo(cl.x) + umin32(i + kClaim, sz);
-        return pool_lo(cl.x) + i;
-    }
-    return dyn_claim();
-}
-DEV uint32_t next_vblock(uint32_t k, Claim& cl) {
-    const uint32_t ds = args()->dyn_start, G = gridDim.x;
-    if (!ds) return claim_vblock(k + G);
-    if (k + G < ds) {
-        if (k + 2 * G >= ds) cl.want = 1;  // the last static block: claims from now on
-        return k + G;
-    }
-    if (cl.nxt < cl.nend) return cl.nxt++;  // the rest of the last claim
-    const uint32_t got = cl.pend ? claim_take(cl) : dyn_claim();
-    cl.want = got < args()->norder;  // (pools empty: no more claims)
-    return got;
-}
-// Loader, top of an iteration: keep one claim in flight (on the pool the last
-// claim came from, or this XCD's own); it is taken a tile later, when a
-// counted wait for a younger DMA has covered it.
-DEV void claim_pump(Claim& cl, uint32_t last_k) {
-    if (!cl.want || cl.pend) return;
-    const uint32_t ds = args()->dyn_start, P = args()->dyn_pool;
-    const uint32_t x = last_k >= ds && P ? umin32((last_k - ds) / P, 7u) : xcc_id();
-    claim_issue(cl, pool_size(x) ? x : xcc_id());
-}
-
+// Local mode deals statically: workgroup g takes (virtual) blocks g, g + G,
+// ...  Rounds 3 and 4 measured dynamic deals against it and dropped them: one
+// queue counter (the D shard's first tiles waited 13-52 us), per-XCD pools
+// claimed a tile ahead with the rest of a launch's blocks (every workgroup's
+// tiles got slower, 0.104-0.112 vs 0.085 ms), and per-position claim words
+// (0.078 vs 0.075 ms); DESIGN.md §7.
 // The next tile: local mode walks the block, then the next block of the
 // order; split mode walks the segment, then walks it again (second pass,
 // when there are utf8 cells to write), then takes segment k + G.
-template <uint32_t TR> DEV Cur cur_next(const Cur& c, Claim& cl) {
+template <uint32_t TR> DEV Cur cur_next(const Cur& c) {
     if (!c.ok) return c;
     if (c.r0 + TR < c.r_end) {
         Cur n = c;
         n.r0 = c.r0 + TR;
         return n;
     }
-    if (c.phase == 0) return cur_local(next_vblock(c.k, cl));
+    if (c.phase == 0) return cur_local(c.k + gridDim.x);
     if (c.phase == 1 && args()->emit) {
         Cur n = c;
         n.phase = 2;
@@ -1601,7 +1477,6 @@ DEV void kernel_body() {
         const bool fast = ER ? FAST : FAST && args()->fast != 0;
         if (fast) warm_scalar<MODE>();
         Cur cs = cur_first<MODE>();  // next tile to announce
-        Claim cl{0u, 0u, 0u, 0u, MODE == 0 && args()->dyn_start && blockIdx.x + gridDim.x >= args()->dyn_start, 0u, 0u};
         // tiles announced before the first DMA: 0 .. 3, or (fast start) 0 .. 1 / 0
         constexpr uint32_t NPRE_ER = FAST ? 1u : NSLOT + 1;
         const uint32_t npre = ER ? NPRE_ER : fast ? 0u : NSLOT + 1;
@@ -1609,7 +1484,7 @@ DEV void kernel_body() {
         for (uint32_t k = 0; k <= NSLOT + 1; k++) {
             if (k > npre) break;
             tile_announce<TR>(cs, spans + (k & 7) * 16, infos + (k & 7) * 32, lane, pf + (k & 7) * 8 * NU);
-            cs = cur_next<TR>(cs, cl);
+            cs = cur_next<TR>(cs);
         }
 #ifdef MJ_STAMPS
         const uint64_t lt0 = __builtin_amdgcn_s_memtime();
@@ -1626,7 +1501,6 @@ DEV void kernel_body() {
             lds_barrier();  // B_0: counters zeroed, tiles 0 .. 3 (FAST: 0 .. 1) announced
             uint32_t ti = 0, tl = 0;        // next tile to DMA / to land
             uint32_t ops[2] = {0, 0}, ann[2] = {0, 0};  // vmem ops issued with tile j % 2: all, its announce part
-            uint32_t claim_t = ~0u;         // tile before whose DMA the claim in flight was issued
             if constexpr (FAST) {
                 // Fast start: tiles 0 and 1 go into their slots as soon as
                 // their spans are in, and tiles 2 and 3 are announced behind
@@ -1646,7 +1520,7 @@ DEV void kernel_body() {
 #pragma unroll
                 for (uint32_t k = 2; k <= NSLOT + 1; k++) {
                     na += tile_announce<TR>(cs, spans + (k & 7) * 16, infos + (k & 7) * 32, lane, pf + (k & 7) * 8 * NU);
-                    cs = cur_next<TR>(cs, cl);
+                    cs = cur_next<TR>(cs);
                 }
                 ops[1] = nd1 + na;  // landing tile 0: everything younger than its DMA (or a full wait)
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1659,16 +1533,12 @@ DEV void kernel_body() {
                 if (can && ti >= 2)
                     can = __hip_atomic_load(freec + (ti & 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= NC * (ti >> 1);
                 if (can) {
-                    if (!cl.pend) {
-                        claim_pump(cl, cs.k);
-                        if (cl.pend) claim_t = ti;
-                    }
                     const uint32_t nd = tile_dma<TR, SH::RO_BYTES>(
                         tile_read_ptrs(spans + (ti & 7) * 16, infos + (ti & 7) * 32, stage), lds + (ti & 1) * SLOT, lane);
                     const uint32_t k = ti + NSLOT + 2;
                     const uint32_t na = tile_announce<TR>(cs, spans + (k & 7) * 16, infos + (k & 7) * 32, lane,
                                                           pf + (k & 7) * 8 * NU);
-                    cs = cur_next<TR>(cs, cl);
+                    cs = cur_next<TR>(cs);
                     ops[ti & 1] = nd + na;
                     ann[ti & 1] = na;
                     ti++;
@@ -1678,7 +1548,6 @@ DEV void kernel_body() {
                 if (tl < ti) {
                     // tile tl's DMA: its announce and the later tile's ops are younger
                     wait_vmcnt(ann[tl & 1] + (ti - tl == 2 ? ops[(tl + 1) & 1] : 0u));
-                    if (cl.pend && claim_t <= tl) cl.ready = 1;
                     __hip_atomic_store(full + (tl & 1), tl + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                     tl++;
                     w = Wait{};
@@ -1699,7 +1568,7 @@ DEV void kernel_body() {
 #pragma unroll
             for (uint32_t k = 1; k <= NSLOT + 1; k++) {
                 tile_announce<TR>(cs, spans + (k & 7) * 16, infos + (k & 7) * 32, lane, pf + (k & 7) * 8 * NU);
-                cs = cur_next<TR>(cs, cl);
+                cs = cur_next<TR>(cs);
             }
             asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
         } else {
@@ -1719,7 +1588,6 @@ DEV void kernel_body() {
         for (uint32_t it = 0;; it++) {
             if (!tile_valid(infos + (it & 7) * 32)) break;  // the decode waves leave too
             const uint32_t tn = it + NSLOT - 1, k = it + NSLOT + 2;
-            if (MODE == 0) claim_pump(cl, cs.k);  // (older than this iteration's DMA: covered by its wait)
             uint32_t nd = 0;
             if (tile_valid(infos + (tn & 7) * 32))
                 nd = tile_dma<TR, SH::RO_BYTES>(tile_read_ptrs(spans + (tn & 7) * 16, infos + (tn & 7) * 32, stage),
@@ -1733,7 +1601,7 @@ DEV void kernel_body() {
 #endif
             const uint32_t ns = tile_announce<TR>(cs, spans + (k & 7) * 16, infos + (k & 7) * 32, lane,
                                                   pf + (k & 7) * 8 * NU) + np;
-            cs = cur_next<TR>(cs, cl);
+            cs = cur_next<TR>(cs);
 #ifdef MJ_STAMPS
             const uint64_t w0 = __builtin_amdgcn_s_memtime();
 #endif
@@ -1741,9 +1609,6 @@ DEV void kernel_body() {
             // an iteration ago, with `pend` ops behind it then (NSLOT 3)
             wait_vmcnt((NSLOT == 2 ? 0u : pend + nd) + ns);
             pend = ns;
-            // a claim issued at this iteration's top is older than tile it+1's
-            // DMA just waited for (NSLOT 2), so it has returned
-            if (NSLOT == 2 && cl.pend) cl.ready = 1;
 #ifdef MJ_STAMPS
             const uint64_t w1 = __builtin_amdgcn_s_memtime();
             lvm += w1 - w0;

@@ -74,19 +74,16 @@ class Context:
             self.set_opts(**_default_opts)
 
     def set_opts(self, kernel="auto", mode="auto", shape=None, seg_tiles=0, vrows=0, lds_budget=0, stage=0,
-                 encode_kernel="auto", verbose=0, grid=0, balance=0):
+                 encode_kernel="auto", verbose=0, grid=0):
         """murr_ctx_set_opts: kernel selection for this context (all defaults =
         the library's own choice).  kernel / encode_kernel: auto|jit|generic;
         mode: auto|local|split|cut; shape: (waves, chunks) e.g. (5, 3);
-        grid: local-mode workgroups (0 auto, -1 one per virtual block);
-        balance: 0 auto, 1 static deal, 2 dynamic per-XCD tail, 10..90 dynamic
-        with that percentage dealt statically."""
+        grid: local-mode workgroups (0 auto, -1 one per virtual block)."""
         o = _abi.Opts()
         o.kernel, o.mode, o.encode_kernel = KERNELS[kernel], MODES[mode], KERNELS[encode_kernel]
         o.shape_nw, o.shape_r = shape if shape else (0, 0)
         o.seg_tiles, o.vrows, o.lds_budget, o.stage, o.verbose = seg_tiles, vrows, lds_budget, stage, int(verbose)
         o.grid = grid & 0xFFFFFFFF
-        o.balance = balance
         raise_status(self.L.murr_ctx_set_opts(self.h, C.byref(o)), what="murr_ctx_set_opts")
         self.opts_gen = getattr(self, "opts_gen", 0) + 1  # plan caches key on it (no library call per read)
 
@@ -147,10 +144,12 @@ class Context:
         """murr_ctx_mark: a timing mark on this context's stream."""
         raise_status(self.L.murr_ctx_mark(self.h, which), what="murr_ctx_mark")
 
-    def mark_ms(self, a: int, b: int) -> float:
-        """GPU milliseconds from mark a to mark b (waits for b)."""
+    def mark_ms(self, a: int, b: int, other: "Context | None" = None) -> float:
+        """GPU milliseconds from this context's mark a to mark b of `other`
+        (default: this context); waits for mark b."""
+        o = other or self
         ms = C.c_float()
-        raise_status(self.L.murr_ctx_mark_ms(self.h, a, b, C.byref(ms)), what="murr_ctx_mark_ms")
+        raise_status(self.L.murr_ctx_mark_ms(self.h, a, o.h, b, C.byref(ms)), what="murr_ctx_mark_ms")
         return ms.value
 
     def last_kernel_ms(self) -> float:

@@ -343,18 +343,25 @@ class ResidentTable:
         decodes its whole shard."""
         return self.scan_device_async(columns, outs).wait()
 
-    def scan_device_async(self, columns, outs: DecodeOutputs | None = None) -> DecodePlan:
+    def scan_device_async(self, columns, outs: DecodeOutputs | None = None, ctx: Context | None = None) -> DecodePlan:
         """scan_device's launch only (murr_decode_run_async): returns the
         prepared plan, whose wait() finishes the scan and returns its outputs.
         A caller alternating two `outs` launches the next scan before waiting
-        for the previous one; each `outs` keeps its own prepared plan."""
+        for the previous one; each `outs` keeps its own prepared plan.
+        `ctx`: another context on the table's device (its own stream) to
+        launch on, so back-to-back scans on two contexts overlap -- the next
+        scan's workgroups start on the CUs the previous one's tail leaves idle
+        (bench.py --config D --lanes 2).  The arena is only read."""
         if self.n == 0:
             self._resolve(columns)  # (an unknown column is reported first)
             raise SegmentError("resident table is empty")
         # the plan's key: columns, table state, the context's options (a
         # repeated scan costs a tuple compare here and one library call)
+        lane = ctx or self.ctx
+        if lane.device != self.ctx.device:
+            raise ValueError("scan_device_async: the context must be on the table's device")
         state = (tuple(columns), self.arena.ptr, self.row_off.ptr, self.uidx.ptr if self.uidx is not None else 0,
-                 self.n, self.used, getattr(self.ctx, "opts_gen", 0))
+                 self.n, self.used, getattr(lane, "opts_gen", 0), id(lane))
         slot = id(outs) if outs is not None else None
         plan = self._scan_plans.get(slot)
         if plan is None or plan[0] != state or (outs is not None and outs is not plan[1].outs):
@@ -374,8 +381,7 @@ class ResidentTable:
                 if cand:
                     self._scan_plans.pop((idle or cand)[0])[1].close()
             blk = self.block()
-            p = DecodePlan(self.ctx, self.segment, proj, [blk],
-                           outs or DecodeOutputs(self.ctx, self.segment, proj, [blk]))
+            p = DecodePlan(lane, self.segment, proj, [blk], outs or DecodeOutputs(lane, self.segment, proj, [blk]))
             self._scan_plans[slot] = plan = (state, p)
         plan[1].run_async()
         return plan[1]

@@ -167,3 +167,34 @@ def test_scan_plan_eviction_with_runs_in_flight(ctx):
             assert_array_equal(download_array(ctx, outs.array(0, p), int(C_DTYPES[p]), n), want[p], f"col {p}")
     with pytest.raises(ValueError):
         hs[0].wait()  # its one result was handed over already
+
+
+def test_scan_device_two_lanes_overlap(ctx):
+    # bench.py --config D's default loop (--lanes 2): the alternating output
+    # sets' scans launched on two contexts of one device (two streams), the
+    # next before the previous is waited for, so they overlap on the GPU.
+    # Every scan of both lanes reads the same arena; both output sets hold
+    # the oracle's arrays after the last scan of each
+    n = 300_000
+    rt = ResidentTable(schema_c(), ctx)
+    rt.write(batch_c(n, seed=11))
+    names = [f"c{i}" for i in range(len(C_DTYPES))]
+    lane2 = Context(ctx.device)
+    try:
+        lanes = [ctx, lane2]
+        sets = [DecodeOutputs(c, rt.segment, list(range(len(C_DTYPES))), [rt.block()]) for c in lanes]
+        h = rt.scan_device_async(names, sets[0], ctx=lanes[0])
+        for s in range(6):
+            hn = rt.scan_device_async(names, sets[(s + 1) % 2], ctx=lanes[(s + 1) % 2]) if s < 5 else None
+            assert h.wait() is sets[s % 2]
+            h = hn
+        data, off = arena(rt)
+        want = O.decode_block(O.Segment([int(d) for d in C_DTYPES]), list(range(len(C_DTYPES))), data, off)
+        for k, outs in enumerate(sets):
+            for p, d in enumerate(C_DTYPES):
+                assert_array_equal(download_array(ctx, outs.array(0, p), int(d), n), want[p], f"lane {k} col {p}")
+    finally:
+        for _, plan in rt._scan_plans.values():  # (plans on lane2 close before it does)
+            plan.close()
+        rt._scan_plans.clear()
+        lane2.close()
