@@ -414,7 +414,7 @@ class ResidentTable:
         them).  A miss is an all-null row (add_empty)."""
         req = self._resolve(columns)
         nq = len(keys)
-        if self.index is None:
+        if self.index is None or nq == 0:
             return req, [_null_dict(c.dtype, nq) for c in req]
         blk, _keep = self.gather(keys)
         proj = [c.index for c in req]

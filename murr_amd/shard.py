@@ -7,16 +7,14 @@ sum-over-ranks bytes the bench reports: every output cell depends on exactly
 one input row (src/io/row/read.rs:85-91) and the utf8 offset prefix is local
 to a block.
 
-Random-key reads (mode 2) across one process per GPU (`merge_reads`,
-`ShardedResidentTable`): every rank reads the caller's keys against its own
-shard and the caller-order batch is the byte-wise sum of the ranks' buffers,
-three all-reduces per read (validity / fixed values / bool bitmaps, utf8
-lengths, utf8 bytes).  That sum is only correct when every key lives on
-exactly one rank, so writes are routed by key (`shard_of`) and `write_shard`
-refuses keys this rank does not own.  The collective-free form of mode 2 (one
-process driving every GPU: keys routed on the host, rows gathered on their
-shard's GPU, one peer-copy gather to the caller's GPU) is
-`murr_amd.multigpu.MultiDeviceTable`.
+Random-key reads (mode 2) across one process per GPU (`gather_reads`,
+`ShardedResidentTable`): every rank reads only the caller's keys it owns
+against its own shard, and sends those rows to the home rank point to point,
+which scatters them into caller order -- no collective on the data path.  Writes
+are routed by key (`shard_of`) and `write_shard` refuses keys this rank does
+not own.  The one-process form of mode 2 (one process driving every GPU: keys
+routed on the host, rows gathered on their shard's GPU, one peer-copy gather
+to the caller's GPU) is `murr_amd.multigpu.MultiDeviceTable`.
 """
 from __future__ import annotations
 
@@ -117,119 +115,153 @@ class Group:
 
 # ---- random-key batch read across key-range shards (SURVEY.md §8(e) mode 2) ----
 #
-# Every rank receives the same keys (the caller's batch) and reads them against
-# its own shard on its own GPU: lookup + gather + decode (ResidentTable), so a
-# key it does not own is a miss -- an all-null row, zero bytes in every buffer
-# (arrow-rs null slots are zero, validity bit 0, utf8 length 0).  A key lives in
-# exactly one shard, so for every row at most one rank contributes non-zero
-# bytes, and the caller-order result (src/io/store/rocksdb/mod.rs:368-399:
-# output row i is key i) is the byte-wise SUM of the ranks' buffers.  That is
-# the one exchange step of the read: fixed-width values, bool bitmaps and
-# validity bitmaps are summed as u8 (disjoint bytes / bits, so no carries),
-# utf8 lengths are summed, every rank places its strings at the merged
-# offsets, and the string bytes are summed.  Three all-reduces per read, each
-# over all projected columns at once (few, large collectives); on GPUs the
-# buffers can stay in HBM and go over RCCL, on CPU (tests) gloo carries them.
+# The caller's keys are known to every rank, and so is each key's owner
+# (shard_of, or a key range).  Every rank reads only the keys it owns against
+# its own shard on its own GPU (lookup + gather + decode: ResidentTable), so
+# the ranks together decode the batch once.  Each rank other than the home
+# rank then SENDS its rows -- every requested column's validity bits, values,
+# or utf8 lengths and bytes, m rows packed into one byte buffer -- to the home
+# rank, point to point; the home rank knows which caller positions each rank
+# owns and scatters the rows back into caller order (the positional contract
+# of src/io/store/rocksdb/mod.rs:368-399: output row i is key i).  Each row
+# crosses the wire once: O(batch) bytes in total, no collective on the data
+# path (round 4's form all-reduced zero-padded full batches from every rank:
+# O(world x batch)).
 
 
-def _bitmap(h, n):
-    nb = (n + 7) // 8
-    if h["validity"] is None:  # no nulls on this rank: every row valid here
-        import numpy as np
-        v = np.full(nb, 0xFF, np.uint8)
-        if n % 8:
-            v[-1] = (1 << (n % 8)) - 1
-        return v
-    import numpy as np
-    return np.frombuffer(bytes(h["validity"][:nb]), np.uint8)
+def _valid_bits(h, m):
+    """Validity of m rows as a bool array (no validity buffer: all valid)."""
+    if h["validity"] is None:
+        return np.ones(m, bool)
+    return np.unpackbits(np.frombuffer(bytes(h["validity"]), np.uint8), bitorder="little")[:m].astype(bool)
 
 
-def merge_reads(group, dtypes, n: int, hs):
-    """Merge this rank's host buffer dicts (one per requested column, caller
-    order, misses all-null) with every other rank's: returns the dicts of the
-    whole read.  `group` is a Group (world 1 returns the input unchanged)."""
+def pack_rows(dtypes, m: int, hs) -> np.ndarray:
+    """This rank's m decoded rows (host buffer dicts, one per requested
+    column) as one u8 buffer: per column the validity bitmap, then its values
+    (fixed: m x W bytes; bool: a bitmap; utf8: m i32 lengths, then the bytes)."""
+    from .schema import DTypeName as D
+    parts = []
+    nb = (m + 7) // 8
+    for dt, h in zip(dtypes, hs):
+        parts.append(np.packbits(_valid_bits(h, m), bitorder="little"))
+        if dt == D.Utf8:
+            o = np.asarray(h["offsets"], np.int64)
+            parts.append(np.diff(o).astype(np.int32).view(np.uint8))
+            parts.append(np.frombuffer(bytes(h["values"]), np.uint8)[: int(o[-1]) - int(o[0])])
+        elif dt == D.Bool:
+            parts.append(np.frombuffer(bytes(h["values"]), np.uint8)[:nb])
+        else:
+            parts.append(np.frombuffer(bytes(h["values"]), np.uint8)[: m * dt.size()])
+    return np.concatenate(parts) if parts else np.zeros(0, np.uint8)
+
+
+def _unpack_rows(dtypes, m: int, buf: np.ndarray):
+    """pack_rows' inverse: per column (valid bool[m], payload)."""
+    from .schema import DTypeName as D
+    out, pos, nb = [], 0, (m + 7) // 8
+    for dt in dtypes:
+        valid = np.unpackbits(buf[pos:pos + nb], bitorder="little")[:m].astype(bool)
+        pos += nb
+        if dt == D.Utf8:
+            lens = buf[pos:pos + 4 * m].view(np.int32).astype(np.int64)
+            pos += 4 * m
+            tot = int(lens.sum())
+            out.append((valid, (lens, buf[pos:pos + tot])))
+            pos += tot
+        elif dt == D.Bool:
+            out.append((valid, np.unpackbits(buf[pos:pos + nb], bitorder="little")[:m].astype(bool)))
+            pos += nb
+        else:
+            w = m * dt.size()
+            out.append((valid, buf[pos:pos + w].reshape(m, dt.size())))
+            pos += w
+    return out
+
+
+def gather_reads(group, dtypes, n: int, owner: np.ndarray, hs, home: int = 0):
+    """Assemble one caller-order read of n keys on the `home` rank.  `owner`
+    (every rank's copy is the same): the rank that owns caller key i; `hs`:
+    this rank's host buffer dicts for ITS keys only, in caller order.  Ranks
+    other than home send their packed rows to home (point to point) and get
+    None; home returns the merged buffer dicts of the whole read.  World 1
+    returns `hs` unchanged."""
+    from .schema import DTypeName as D
     if group.dist is None:
         return hs
-    import numpy as np
     import torch
-    from .schema import DTypeName as D
-    nb = (n + 7) // 8
-    # 1. validity + fixed values + bool bitmaps + utf8 lengths: one u8 buffer
-    parts, lens_parts = [], []
-    for dt, h in zip(dtypes, hs):
-        parts.append(_bitmap(h, n))
-        if dt == D.Utf8:
-            lens_parts.append(np.diff(np.asarray(h["offsets"], np.int64)))
-        else:
-            parts.append(np.frombuffer(bytes(h["values"]), np.uint8)[: (nb if dt == D.Bool else n * dt.size())])
-    flat = torch.from_numpy(np.concatenate(parts) if parts else np.zeros(0, np.uint8))
-    group.dist.all_reduce(flat)
-    lens = None
-    if lens_parts:
-        lens = torch.from_numpy(np.concatenate(lens_parts))
-        group.dist.all_reduce(lens)
-        lens = lens.numpy().reshape(len(lens_parts), n)
-    flat = flat.numpy()
-    # 2. utf8: merged offsets, this rank's strings placed there, summed
-    goffs, data_parts, at, u = [], [], 0, 0
-    for dt, h in zip(dtypes, hs):
-        if dt != D.Utf8:
+    rank, world = group.rank, group.world
+    owner = np.asarray(owner)
+    if rank != home:
+        buf = pack_rows(dtypes, int((owner == rank).sum()), hs)
+        group.dist.send(torch.tensor([buf.size], dtype=torch.int64), dst=home)
+        if buf.size:
+            group.dist.send(torch.from_numpy(buf), dst=home)
+        return None
+    rows = {}
+    for r in range(world):
+        m = int((owner == r).sum())
+        if r == home:
+            rows[r] = _unpack_rows(dtypes, m, pack_rows(dtypes, m, hs))
             continue
-        go = np.zeros(n + 1, np.int64)
-        np.cumsum(lens[u], out=go[1:])
-        if go[-1] > np.iinfo(np.int32).max:
-            from .errors import SegmentError
-            raise SegmentError("byte array offset overflow")
-        lo = np.asarray(h["offsets"], np.int64)
-        mine = np.diff(lo)
-        buf = np.zeros(int(go[-1]), np.uint8)
-        rows = np.flatnonzero(mine)
-        if rows.size:
-            ln = mine[rows]
-            src = np.repeat(lo[rows] - np.cumsum(ln) + ln, ln) + np.arange(int(ln.sum()))
-            dst = np.repeat(go[rows] - np.cumsum(ln) + ln, ln) + np.arange(int(ln.sum()))
-            buf[dst] = np.frombuffer(bytes(h["values"]), np.uint8)[src]
-        goffs.append(go)
-        data_parts.append(buf)
-        u += 1
-    if data_parts:
-        data = torch.from_numpy(np.concatenate(data_parts))
-        group.dist.all_reduce(data)
-        data = data.numpy()
-    # 3. unpack
-    out, pos, dpos, u = [], 0, 0, 0
-    for dt, h in zip(dtypes, hs):
-        valid = flat[pos:pos + nb]
-        pos += nb
-        nulls = n - int(np.unpackbits(valid, bitorder="little")[:n].sum()) if n else 0
-        r = {"dtype": int(dt), "length": n, "null_count": nulls,
-             "validity": valid.tobytes() if nulls else None, "offsets": None}
+        size = torch.zeros(1, dtype=torch.int64)
+        group.dist.recv(size, src=r)
+        buf = torch.zeros(int(size.item()), dtype=torch.uint8)
+        if buf.numel():
+            group.dist.recv(buf, src=r)
+        rows[r] = _unpack_rows(dtypes, m, buf.numpy())
+    where = {r: np.flatnonzero(owner == r) for r in range(world)}
+    out = []
+    for p, dt in enumerate(dtypes):
+        valid = np.zeros(n, bool)
+        for r, idx in where.items():
+            valid[idx] = rows[r][p][0]
+        nulls = int(n - valid.sum())
+        res = {"dtype": int(dt), "length": n, "null_count": nulls,
+               "validity": np.packbits(valid, bitorder="little").tobytes() if nulls else None, "offsets": None}
         if dt == D.Utf8:
-            go = goffs[u]
-            r["offsets"] = go.astype(np.int32)
-            r["values"] = data[dpos:dpos + int(go[-1])].tobytes()
-            dpos += int(go[-1])
-            u += 1
+            lens = np.zeros(n, np.int64)
+            for r, idx in where.items():
+                lens[idx] = rows[r][p][1][0]
+            go = np.zeros(n + 1, np.int64)
+            np.cumsum(lens, out=go[1:])
+            if go[-1] > np.iinfo(np.int32).max:
+                from .errors import SegmentError
+                raise SegmentError("byte array offset overflow")
+            data = np.zeros(int(go[-1]), np.uint8)
+            for r, idx in where.items():
+                ln, src = rows[r][p][1]
+                if not src.size:
+                    continue
+                start = go[idx]  # each of rank r's rows lands at its caller position's offset
+                pos = np.repeat(start - np.cumsum(ln) + ln, ln) + np.arange(int(ln.sum()))
+                data[pos] = src
+            res["offsets"] = go.astype(np.int32)
+            res["values"] = data.tobytes()
+        elif dt == D.Bool:
+            bits = np.zeros(n, bool)
+            for r, idx in where.items():
+                bits[idx] = rows[r][p][1]
+            res["values"] = np.packbits(bits, bitorder="little").tobytes()
         else:
-            w = nb if dt == D.Bool else n * dt.size()
-            r["values"] = flat[pos:pos + w].tobytes()
-            pos += w
-        out.append(r)
+            vals = np.zeros((n, dt.size()), np.uint8)
+            for r, idx in where.items():
+                vals[idx] = rows[r][p][1]
+            res["values"] = vals.tobytes()
+        out.append(res)
     return out
 
 
 class ShardedResidentTable:
     """One key-range shard of a table per rank (one process per GPU), each a
     ResidentTable in that GPU's HBM.  `read` is Table::read over the whole
-    table: every rank passes the same keys and gets the same caller-order
-    batch.
+    table, a collective call: every rank passes the same keys, reads the keys
+    its shard owns, and the home rank gets the caller-order batch (the other
+    ranks get None) -- rows sent to it point to point (gather_reads).
 
-    Not the default multi-GPU read: every rank looks up every key and the
-    ranks byte-sum their host results over the process group (merge_reads),
-    which suits a job whose ranks all want the same batch (a data-parallel
-    reader on gloo or RCCL).  A server that owns all of a node's GPUs reads
-    through MultiDeviceTable (murr_multi_gather: lookups on each GPU at once,
-    one caller-order block on the home GPU, no collective)."""
+    A server that owns all of a node's GPUs reads through MultiDeviceTable
+    instead (murr_multi_gather: lookups on each GPU at once, one caller-order
+    block on the home GPU by peer copies, one process)."""
 
     def __init__(self, table, group: "Group", ctx=None, name: str = "shard"):
         from .resident import ResidentTable
@@ -238,15 +270,18 @@ class ShardedResidentTable:
 
     def write_shard(self, batch):
         """Write this rank's keys (Table::write on its own shard).  Every key
-        must be this rank's (shard_of): a key on two ranks would break the
-        byte-sum merge of reads (route a batch first with route_batch)."""
+        must be this rank's (shard_of): reads look a key up on its owner only
+        (route a batch first with route_batch)."""
         if self.group.world > 1:
             key = self.local.t.table.key
             check_owned(batch.column(batch.schema.get_field_index(key)), self.group.rank, self.group.world)
         self.local.write(batch)
 
-    def read(self, keys, columns):
+    def read(self, keys, columns, home: int = 0):
         from .resident import host_batch
-        req, hs = self.local.read_host(keys, columns)
-        merged = merge_reads(self.group, [c.dtype for c in req], len(keys), hs)
-        return host_batch(req, merged)
+        keys = list(keys)
+        owner = shard_of(keys, self.group.world) if self.group.world > 1 else np.zeros(len(keys), np.uint32)
+        mine = [keys[i] for i in np.flatnonzero(owner == self.group.rank)]
+        req, hs = self.local.read_host(mine, columns)
+        merged = gather_reads(self.group, [c.dtype for c in req], len(keys), owner, hs, home)
+        return None if merged is None else host_batch(req, merged)

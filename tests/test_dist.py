@@ -100,11 +100,11 @@ def test_two_rank_shards_concatenate_to_whole():
 
 
 # ---- random-key batch read across shards (SURVEY.md §8(e) mode 2) -----------------
-# Each rank "reads" the caller's keys against its own shard (here the oracle
-# decodes a block where the keys it does not own are missing rows, exactly what
-# ResidentTable.read_host returns on a GPU), then merge_reads exchanges and
-# restores the whole read in caller order.  It must equal the oracle's decode
-# of the read against the whole table.
+# Each rank "reads" only the caller's keys it owns against its own shard (here
+# the oracle decodes a block of those keys, exactly what ResidentTable.read_host
+# returns on a GPU), then gather_reads sends the rows to the home rank point to
+# point, which restores the whole read in caller order.  It must equal the
+# oracle's decode of the read against the whole table.
 READ_ROWS, READ_KEYS = 3001, 1500
 
 
@@ -123,58 +123,88 @@ def _read_case():
 O_UTF8_EXTRA = 0  # a second utf8 column
 
 
-def _block_for(blob, off, q, owned):
+def _block_for(blob, off, q):
     parts, ro = [], [0]
     for k in q:
         k = int(k)
-        b = blob[int(off[k]):int(off[k + 1])].tobytes() if (k < READ_ROWS and owned(k)) else b""
+        b = blob[int(off[k]):int(off[k + 1])].tobytes() if k < READ_ROWS else b""
         parts.append(b)
         ro.append(ro[-1] + len(b))
     return np.frombuffer(b"".join(parts), np.uint8).copy(), np.array(ro, np.uint64)
 
 
-def _read_worker(rank, world, port, q):
+def _owner(keys, world):
+    """Key-range owners (a key past the table: the last rank, where it misses)."""
+    own = np.full(len(keys), world - 1, np.int64)
+    for r in range(world):
+        start, n = shard_rows(r, world, READ_ROWS)
+        own[(keys >= start) & (keys < start + n)] = r
+    return own
+
+
+def _read_worker(rank, world, port, home, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
     from murr_amd.schema import DTypeName as D
-    from murr_amd.shard import merge_reads
+    from murr_amd.shard import gather_reads
     g = Group("gloo")
     dtypes, seg, blob, off, keys, proj = _read_case()
-    start, n = shard_rows(rank, world, READ_ROWS)
-    data, ro = _block_for(blob, off, keys, lambda k: start <= k < start + n)
+    owner = _owner(keys, world)
+    data, ro = _block_for(blob, off, keys[owner == rank])  # this rank's keys only
     local = O.decode_block(seg, proj, data, ro)
-    merged = merge_reads(g, [D(dtypes[p]) for p in proj], len(keys), local)
-    q.put((rank, [(m["null_count"], m["validity"], m["values"],
-                   None if m["offsets"] is None else m["offsets"].tolist()) for m in merged]))
+    merged = gather_reads(g, [D(dtypes[p]) for p in proj], len(keys), owner, local, home)
+    q.put((rank, None if merged is None else
+           [(m["null_count"], m["validity"], m["values"], None if m["offsets"] is None else m["offsets"].tolist())
+            for m in merged]))
     g.close()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_sharded_random_key_read_restores_caller_order(world):
+@pytest.mark.parametrize("world,home", [(2, 0), (3, 0), (3, 2)])
+def test_sharded_random_key_read_restores_caller_order(world, home):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_read_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_read_worker, args=(r, world, port, home, q)) for r in range(world)]
     for p in procs:
         p.start()
-    got = [q.get(timeout=180) for _ in procs]
+    got = dict(q.get(timeout=180) for _ in procs)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
+    assert all(got[r] is None for r in range(world) if r != home)  # only the home rank holds the read
     dtypes, seg, blob, off, keys, proj = _read_case()
-    data, ro = _block_for(blob, off, keys, lambda k: True)
+    data, ro = _block_for(blob, off, keys)
     want = O.decode_block(seg, proj, data, ro)
     nb = (len(keys) + 7) // 8
-    for rank, cols in got:  # every rank holds the whole read
-        for p, (nulls, validity, values, offsets) in enumerate(cols):
-            w = want[p]
-            assert nulls == w["null_count"], (rank, p)
-            assert (validity is None) == (w["validity"] is None), (rank, p)
-            if validity is not None:
-                assert validity[:nb] == w["validity"], (rank, p)
-            assert values == w["values"], (rank, p)
-            if w["offsets"] is not None:
-                assert offsets == w["offsets"].tolist(), (rank, p)
+    for p, (nulls, validity, values, offsets) in enumerate(got[home]):
+        w = want[p]
+        assert nulls == w["null_count"], p
+        assert (validity is None) == (w["validity"] is None), p
+        if validity is not None:
+            assert validity[:nb] == w["validity"], p
+        assert values == w["values"], p
+        if w["offsets"] is not None:
+            assert offsets == w["offsets"].tolist(), p
+
+
+def test_pack_rows_round_trip():
+    # one rank's packed rows unpack to the same cells (every dtype, nulls,
+    # empty strings, zero rows)
+    from murr_amd.schema import DTypeName as D
+    from murr_amd.shard import _unpack_rows, pack_rows
+    dtypes, seg, blob, off, keys, proj = _read_case()
+    for m in (0, 1, 9, 700):
+        data, ro = _block_for(blob, off, keys[:m])
+        hs = O.decode_block(seg, proj, data, ro)
+        dts = [D(dtypes[p]) for p in proj]
+        cols = _unpack_rows(dts, m, pack_rows(dts, m, hs))
+        for dt, h, (valid, payload) in zip(dts, hs, cols):
+            nulls = m - int(valid.sum())
+            assert nulls == h["null_count"]
+            if dt == D.Utf8:
+                lens, src = payload
+                assert lens.tolist() == np.diff(h["offsets"].astype(np.int64)).tolist()
+                assert src.tobytes() == h["values"]
 
 
 # ---- key routing (murr_shard_of) -----------------------------------------------------
