@@ -435,3 +435,46 @@ def test_layout_without_utf8_cuts_without_index(ctx, kernel_mode):
     want = O.decode_block(oseg, proj, data, off)
     for p, ci in enumerate(proj):
         assert_array_equal(download_array(ctx, outs.array(0, p), int(seg.columns[ci].dtype), n), want[p], f"proj {p}")
+
+
+@pytest.mark.parametrize("shape", ["5x3", "5x2", "3x1"])
+def test_validity_local_whole_blocks(ctx, kernel_mode, shape):
+    # local mode over whole blocks, several per workgroup: a column's first
+    # null at tile edges, in the last row, as a missing row, in one column but
+    # not the others, or none at all; every buffer bit-exact when null_count >
+    # 0 (round 5 measured storing validity lazily from a block's first null
+    # on -- slower on config B; this pins the cases it needed)
+    nw, r = (int(x) for x in shape.split("x"))
+    set_default_opts(kernel=kernel_mode, mode="local", shape=(nw, r))
+    rng = np.random.default_rng(300 + nw * 10 + r)
+    dtypes = [D.Utf8, D.Float32, D.Bool, D.Int16, D.Utf8]
+    oseg = O.Segment([int(d) for d in dtypes])
+    proj = [0, 1, 2, 3, 4, 1]
+    n = 6000
+    blocks, wants = [], []
+    cases = [(None, None), (0, None), (63, None), (64, None), (767, None), (768, 1), (1535, 3),
+             (5000, None), (n - 1, None), ("missing", 2000), (None, 4500)]
+    for first, other in cases:
+        cols = random_columns(rng, dtypes, n, null_p=0.0, max_str=9)
+        miss = set()
+        if first == "missing":
+            miss = {other}  # a missing row: null in every column
+        else:
+            if first is not None:  # column 0's first null
+                v = np.ones(n, bool)
+                v[first] = False
+                v[first + 1:] = rng.random(n - first - 1) >= 0.2
+                cols[0]["validity"] = synth.pack_bits(v)
+            if other is not None:  # column 3 (int16) nulls from row `other` on
+                v = np.ones(n, bool)
+                v[other:] = rng.random(n - other) >= 0.5
+                v[other] = False
+                cols[3]["validity"] = synth.pack_bits(v)
+        _, data, off = oracle_block(dtypes, cols, n, miss)
+        blocks.append((data, off))
+        wants.append(O.decode_block(oseg, proj, data, off))
+    got = gpu_decode(ctx, seg_of(dtypes), proj, blocks * 3)  # 33 blocks: several per workgroup
+    for b in range(len(blocks) * 3):
+        for p in range(len(proj)):
+            assert_array_equal(got[b][p], wants[b % len(blocks)][p], f"block {b} proj {p}")
+            check_padding(got[b][p], n)

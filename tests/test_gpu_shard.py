@@ -1,7 +1,9 @@
 """Random-key batch read over key-range shards on GPUs (SURVEY.md §8(e) mode 2):
 two ranks (gloo, both on device 0 of the one-GPU box, each with its own
-context and shard in HBM) read the same keys; ShardedResidentTable.read must
-equal one ResidentTable holding the whole table, buffer for buffer."""
+context and shard in HBM) read the same keys, each only the keys it owns, and
+send their rows to the home rank; ShardedResidentTable.read on the home rank
+must equal one ResidentTable holding the whole table, buffer for buffer (the
+other rank gets None)."""
 import os
 import socket
 
@@ -39,11 +41,14 @@ def _worker(rank, world, port, q):
     ts, batch, keys = _case()
     t = ShardedResidentTable(ts, g)
     t.write_shard(route_batch(batch, "key", world)[rank])  # keys go to their owner shard
-    rb = t.read(keys, COLS)
-    sink = pa.BufferOutputStream()
-    with pa.ipc.new_stream(sink, rb.schema) as w:
-        w.write_batch(rb)
-    q.put((rank, sink.getvalue().to_pybytes()))
+    rb = t.read(keys, COLS, home=1)
+    if rb is None:
+        q.put((rank, None))
+    else:
+        sink = pa.BufferOutputStream()
+        with pa.ipc.new_stream(sink, rb.schema) as w:
+            w.write_batch(rb)
+        q.put((rank, sink.getvalue().to_pybytes()))
     g.close()
 
 
@@ -63,7 +68,9 @@ def test_two_shards_equal_whole_table():
     whole = ResidentTable(ts)
     whole.write(batch)
     want = whole.read(keys, COLS)
-    for rank, raw in got:
+    got = dict(got)
+    assert got[0] is None and got[1] is not None  # the batch lands on the home rank only
+    for rank, raw in [(1, got[1])]:
         rb = pa.ipc.open_stream(raw).read_next_batch()
         assert rb.schema.equals(want.schema)
         for a, b in zip(rb.columns, want.columns):
