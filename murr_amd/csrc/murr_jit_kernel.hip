@@ -738,6 +738,20 @@ template <uint32_t C> DEV void stash(uint32_t (&lo)[NCW], uint32_t (&hi)[NCW], b
                  : "+v"(lo[C / 64]), "+v"(hi[C / 64])
                  : "s"((uint32_t)m), "s"((uint32_t)(m >> 32)), "i"(C % 64));
 }
+// Merged words: chunk k's ballot of column C into lane k * NCOLS + C (k is a
+// constant once the chunk loop is unrolled, but not a C++ constant, so the
+// lane select goes through M0: an SGPR value and an SGPR lane select in one
+// VOP3 would break the constant-bus limit).  M0 is saved and restored (the
+// loader's LDS-DMA relies on it the same way); the nop covers both the
+// SALU-writes-M0 and the VALU-writes-SGPR (ballot) hazards.
+template <uint32_t C> DEV void stash_k(uint32_t& lo, uint32_t& hi, bool b, uint32_t k) {
+    const uint64_t m = __ballot(b);
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %5\n\ts_nop 4\n\tv_writelane_b32 %1, %3, m0\n\t"
+                 "v_writelane_b32 %2, %4, m0\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep), "+v"(lo), "+v"(hi)
+                 : "s"((uint32_t)m), "s"((uint32_t)(m >> 32)), "s"(k * NCOLS + C));
+}
 
 // ---- per-wave state of a tile --------------------------------------------------
 template <uint32_t R> struct Rows {
@@ -792,29 +806,41 @@ template <uint32_t C> DEV Out lane_out(const Lanes& L, const Out* ob, uint32_t p
 #endif
 }
 
+// Merged validity words (tiles of R > 1 chunks per wave, R x NCOLS <= 64
+// lanes): the words of all R chunks of a wave go out in ONE store -- lane
+// k * NCOLS + c holds chunk k's word of column c -- instead of one store per
+// chunk.  A wave store instruction costs about the same whatever it writes
+// (config B ablation, round 5: its two-lane validity store per chunk was 7.5 %
+// of the kernel).  The per-lane tables then hold column (lane % NCOLS).
+template <uint32_t R> DEV constexpr bool merged_words() { return R > 1 && R * NCOLS <= 64; }
+template <uint32_t R> DEV uint32_t lane_col(uint32_t j, uint32_t lane) {
+    if constexpr (merged_words<R>()) return lane < R * NCOLS ? lane % NCOLS : NCOLS;
+    else return j * 64 + lane;
+}
+
 // Per-lane output pointers of block b (lane c: column c's validity and bool
 // values), reloaded when the block changes; null counts of the previous
 // block flushed first.
-DEV void lanes_flush(Lanes& L, uint32_t lane) {
+template <uint32_t R> DEV void lanes_flush(Lanes& L, uint32_t lane) {
     if (L.blk == ~0u) return;
     unsigned long long* nulls = args()->nulls + (uint64_t)L.blk * args()->nproj;
 #pragma unroll
     for (uint32_t j = 0; j < NCW; j++) {
-        const uint32_t c = j * 64 + lane;
+        const uint32_t c = lane_col<R>(j, lane);
         if (c < NCOLS && L.proj[j] && L.nacc[j])
             __hip_atomic_fetch_add(gp(nulls) + gp(args()->slot_tab)[c], (unsigned long long)L.nacc[j], __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
         L.nacc[j] = 0;
     }
 }
-DEV void lanes_block(Lanes& L, uint32_t b, uint32_t lane) {
+template <uint32_t R> DEV void lanes_block(Lanes& L, uint32_t b, uint32_t lane) {
     if (L.blk == b) return;
-    lanes_flush(L, lane);
+    lanes_flush<R>(L, lane);
     L.blk = b;
     const Out* ob = outs_of(b);
 #pragma unroll
     for (uint32_t j = 0; j < NCW; j++) {
-        const uint32_t c = j * 64 + lane;
+        const uint32_t c = lane_col<R>(j, lane);
         const uint32_t s = c < NCOLS ? (uint32_t)gp(args()->slot_tab)[c] : (uint32_t)kNone;
         L.proj[j] = s != kNone;
         L.isbool[j] = c < NCOLS && kColW[c < NCOLS ? c : 0] == 9;
@@ -845,6 +871,18 @@ DEV void store_words(Lanes& L, const uint32_t (&vlo)[NCW], const uint32_t (&vhi)
             if (L.isbool[j]) ostw(gp((uint64_t*)L.bptr[j]) + word, ((uint64_t)bhi[j] << 32) | blo[j]);
             L.nacc[j] += nk - (uint32_t)__popcll(v);
         }
+    }
+}
+// The merged form: lane k * NCOLS + c stores chunk k's word of column c.
+DEV void store_words_merged(Lanes& L, uint32_t vlo, uint32_t vhi, uint32_t blo, uint32_t bhi, uint64_t r0,
+                            uint32_t rbase, uint32_t nr, uint32_t lane) {
+    const uint32_t c0 = rbase + (lane / NCOLS) * 64;
+    const uint32_t nk = c0 < nr ? umin32(64u, nr - c0) : 0u;
+    if (L.proj[0] && nk) {
+        const uint64_t v = ((uint64_t)vhi << 32) | vlo, word = (r0 + c0) >> 6;
+        ostw(gp((uint64_t*)L.vptr[0]) + word, v);
+        if (L.isbool[0]) ostw(gp((uint64_t*)L.bptr[0]) + word, ((uint64_t)bhi << 32) | blo);
+        L.nacc[0] += nk - (uint32_t)__popcll(v);
     }
 }
 
@@ -1076,7 +1114,13 @@ DEV void decode_tile(const Src& src, const Tile& T, const LAS uint32_t* ro, LAS 
     // tile it's; it cannot get further ahead, since tile it+1's prefix wait
     // needs every wave's tile it+1 totals)
     LAS uint32_t* wt = (LAS uint32_t*)(ctl + SH::CNT_B + 8 * NU) + (it & 1) * NU * NC;
-    lanes_block(L, T.b, lane);
+    lanes_block<R>(L, T.b, lane);
+    constexpr bool MV = merged_words<R>();
+#define MJ_STASH(C, LO, HI, K, B)                        \
+    do {                                                 \
+        if constexpr (MV) stash_k<C>(LO[0][0], HI[0][0], (B), (K)); \
+        else stash<C>(LO[K], HI[K], (B));               \
+    } while (0)
 #if MJ_HOIST
     // the projection's slot words, once per tile (one batched scalar load;
     // slot_of would wait on a kernel-argument load per use)
@@ -1155,7 +1199,7 @@ DEV void decode_tile(const Src& src, const Tile& T, const LAS uint32_t* ro, LAS 
                 ulen[U][k] = good ? l : 0u;                                                             \
                 uinc[U][k] = wave_scan(ulen[U][k]) + wtot;                                              \
                 wtot = (uint32_t)__builtin_amdgcn_readlane(uinc[U][k], 63);                                       \
-                if constexpr (PH != 2) stash<C>(vlo[k], vhi[k], valid);                                 \
+                if constexpr (PH != 2) MJ_STASH(C, vlo, vhi, k, valid);                                 \
             }                                                                                           \
             utot[U] = wtot;                                                                             \
         }                                                                                               \
@@ -1227,9 +1271,9 @@ DEV void decode_tile(const Src& src, const Tile& T, const LAS uint32_t* ro, LAS 
                 const uint32_t m = valid ? ~0u : 0u;                                                    \
                 lo &= m;                                                                                \
                 hi &= m;                                                                                \
-                stash<C>(vlo[k], vhi[k], (W.vb[k][C / 32] >> (C % 32)) & 1u);                           \
+                MJ_STASH(C, vlo, vhi, k, (W.vb[k][C / 32] >> (C % 32)) & 1u);                           \
                 if constexpr (W_ == 9) {                                                                \
-                    stash<C>(blo[k], bhi[k], lo != 0);                                                  \
+                    MJ_STASH(C, blo, bhi, k, lo != 0);                                                  \
                 } else if (i < T.nr && !MJ_ABL_NOFIX) {                                                 \
                     const uint64_t row = T.r0 + i;                                                      \
                     if constexpr (W_ == 8) ost(gp((uint64_t*)o.values) + row, ((uint64_t)hi << 32) | lo); \
@@ -1244,7 +1288,9 @@ DEV void decode_tile(const Src& src, const Tile& T, const LAS uint32_t* ro, LAS 
     MJ_COLS(MJ_F)
 #undef MJ_F
 
-    if constexpr (PH != 2) {
+    if constexpr (PH != 2 && MV) {
+        store_words_merged(L, vlo[0][0], vhi[0][0], blo[0][0], bhi[0][0], T.r0, rbase, T.nr, lane);
+    } else if constexpr (PH != 2) {
 #pragma unroll
         for (uint32_t k = 0; k < R; k++) {
             const uint32_t c0 = rbase + k * 64;
@@ -1252,6 +1298,7 @@ DEV void decode_tile(const Src& src, const Tile& T, const LAS uint32_t* ro, LAS 
             if (nk) store_words(L, vlo[k], vhi[k], blo[k], bhi[k], (T.r0 + c0) >> 6, nk, lane);
         }
     }
+#undef MJ_STASH
 
     if (PH != 2 && args()->report && __ballot(badk != 0)) {  // cold: exact error reports
 #pragma unroll
@@ -1714,7 +1761,7 @@ DEV void kernel_body() {
             MJ_TOC(0)
         }
     }
-    lanes_flush(L, lane);
+    lanes_flush<R>(L, lane);
 #ifdef MJ_STAMPS
     if (lane == 0)
         __hip_atomic_fetch_add((GAS unsigned long long*)args()->err + 2 + 9, (unsigned long long)(__builtin_amdgcn_s_memtime() - ct0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -23,6 +23,12 @@ def test_decode_kernels_use_no_scratch(tmp_path, sample):
     subprocess.run([HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "-include", os.path.join(CSRC, sample),
                     "-S", "--cuda-device-only", "-o", str(out), os.path.join(CSRC, "murr_jit_kernel.hip")],
                    check=True, capture_output=True, timeout=600)
+    # assembled too: operand errors of inline asm (e.g. the constant-bus
+    # limit) show only when the assembler sees them, and at run time hiprtc
+    # would fall back to the generic kernel for that layout
+    subprocess.run([HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "-include", os.path.join(CSRC, sample),
+                    "-c", "--cuda-device-only", "-o", str(tmp_path / "k.o"), os.path.join(CSRC, "murr_jit_kernel.hip")],
+                   check=True, capture_output=True, timeout=600)
     asm = out.read_text()
     names = re.findall(r"\.name:\s+(murr_jit_decode\w*)", asm)
     sizes = re.findall(r"\.private_segment_fixed_size:\s+(\d+)", asm)
