@@ -361,7 +361,7 @@ def copy_block(ctx, b: DeviceBlock) -> DeviceBlock:
                        off if w == 4 else None)
 
 
-def config_d_table(ctx, rows: int, start: int, chunk: int = 2_000_000):
+def config_d_table(ctx, rows: int, start: int, chunk: int = 2_000_000, stride: int = 0):
     """Config D's shard: the config-C schema with keys "key{i}", rows
     [start, start + rows), written into a ResidentTable (device encode, key
     index, utf8 index kept by every write)."""
@@ -370,7 +370,8 @@ def config_d_table(ctx, rows: int, start: int, chunk: int = 2_000_000):
     from murr_amd.resident import ResidentTable
     cols_s = {"key": ColumnSchema(D.Utf8, False)}
     cols_s.update({f"c{i}": ColumnSchema(c["dtype"]) for i, c in enumerate(synth.config_c(1))})
-    rt = ResidentTable(TableSchema("key", cols_s), ctx)
+    from murr_amd.resident import UIDX_STRIDE
+    rt = ResidentTable(TableSchema("key", cols_s), ctx, uidx_stride=stride or UIDX_STRIDE)
     names = [c for c in cols_s if c != "key"]
     for s0 in range(start, start + rows, chunk):
         m = min(chunk, start + rows - s0)
@@ -430,7 +431,7 @@ def run_decode(args, dist, rank, world, local_rank):
         # ResidentTable.scan_device, the whole shard in one launch cut on the
         # table's own utf8 index (kept by every write)
         K = 1
-        rt, names = config_d_table(ctx, rows, start)
+        rt, names = config_d_table(ctx, rows, start, stride=args.resident_stride)
         seg = rt.segment
         proj = parse_proj(args.proj, len(seg.columns))
         blocks = [rt.block()]
@@ -1152,6 +1153,8 @@ def main():
                          "(0: one allocation per buffer)")
     ap.add_argument("--offsets", type=int, default=32, choices=[32, 64],
                     help="row offset width of the decoded blocks (configs A/B/C: u32 row_off32, or u64)")
+    ap.add_argument("--resident-stride", type=int, default=0,
+                    help="config D: the resident table's utf8 index stride (0: ResidentTable's default)")
     ap.add_argument("--uidx-stride", type=int, default=512,
                     help="decode mode: utf8 index stride of each block (0 = no index)")
     ap.add_argument("--table", default="C", choices=["C", "ref"],

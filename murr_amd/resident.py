@@ -158,16 +158,22 @@ TWO_PHASE_BYTES = 64 << 20
 # utf8 index stride of the resident arena (murr_utf8_index_update): every
 # UIDX_STRIDE rows, each utf8 column's string bytes so far (0.0625 B per row
 # and column), so a whole-table scan decodes on the whole GPU in one pass, cut
-# into one-tile virtual blocks that the workgroups claim as they go (the
-# decode's dynamic tail).
+# into virtual blocks on index strides.  The stride bounds how finely the
+# static deal can spread a shard over the grid: config D's 1.25 M rows over
+# 1280 workgroups are 9766 one-tile (128-row) virtual blocks, 7-8 per
+# workgroup, at stride 128; at 512, 2442 blocks of 512 rows, one or two per
+# workgroup -- half the workgroups idle for the last half of the scan
+# (DESIGN.md §6 measures both).  A table can pick another (uidx_stride).
 UIDX_STRIDE = 128
 
 
 class ResidentTable:
     """Table (src/io/table/mod.rs:20-155) whose rows stay in HBM."""
 
-    def __init__(self, table: TableSchema, ctx: Context | None = None, name: str = "resident"):
+    def __init__(self, table: TableSchema, ctx: Context | None = None, name: str = "resident",
+                 uidx_stride: int = UIDX_STRIDE):
         self.t = Table(Store(), name, table, ctx)  # schema, validation, column resolution
+        self.stride = int(uidx_stride)
         self.ctx = self.t.ctx
         self.segment = self.t.segment
         self.t.prepare()  # kernels compiled at open, never on the read path
@@ -180,7 +186,7 @@ class ResidentTable:
         self.n = 0
         self.max_row = 0
         self._reader = None    # murr_reader_t: scratch of the one-call host read
-        self.uidx = None       # utf8 index of the arena (UIDX_STRIDE), kept with every write
+        self.uidx = None       # utf8 index of the arena (every self.stride rows), kept with every write
         self.uidx_cap = 0      # entries
         self._scan_plans = {}  # id(outs) (None: the plan's own outputs) -> (key, DecodePlan) of scan_device
 
@@ -255,18 +261,18 @@ class ResidentTable:
         """Extend the arena's utf8 index over rows n_old .. n (the written
         block's index, kept as the table grows: only the new rows are read)."""
         L, seg = self.ctx.L, self.segment
-        need = int(L.murr_utf8_index_len(C.byref(seg.c), self.n, UIDX_STRIDE))
+        need = int(L.murr_utf8_index_len(C.byref(seg.c), self.n, self.stride))
         if need == 0:
             return
         if need > self.uidx_cap:
             cap = max(need, 2 * self.uidx_cap, 64)
             buf = self.ctx.alloc(8 * cap)
             if self.uidx is not None and n_old:
-                buf.copy_from(self.uidx, 8 * int(L.murr_utf8_index_len(C.byref(seg.c), n_old, UIDX_STRIDE)))
+                buf.copy_from(self.uidx, 8 * int(L.murr_utf8_index_len(C.byref(seg.c), n_old, self.stride)))
                 self.uidx.free()
             self.uidx, self.uidx_cap = buf, cap
         blk = _abi.Block(self.arena.ptr, self.row_off.ptr, self.n, self.used)
-        raise_status(L.murr_utf8_index_update(self.ctx.h, C.byref(seg.c), C.byref(blk), n_old, UIDX_STRIDE,
+        raise_status(L.murr_utf8_index_update(self.ctx.h, C.byref(seg.c), C.byref(blk), n_old, self.stride,
                                               self.uidx.ptr), what="murr_utf8_index_update")
 
     def load_sst(self, entries):
@@ -333,7 +339,7 @@ class ResidentTable:
     def block(self) -> DeviceBlock:
         """The whole arena as one decode block, with its utf8 index."""
         return DeviceBlock(self.arena, self.row_off, self.n, self.used, self.uidx,
-                           UIDX_STRIDE if self.uidx is not None else 0)
+                           self.stride if self.uidx is not None else 0)
 
     def scan_device(self, columns, outs: DecodeOutputs | None = None) -> DecodeOutputs:
         """Every row of the table, decoded on the device in one launch over the
