@@ -156,15 +156,15 @@ def _key_array(keys) -> pa.Array:
 # the rows up and size the block exactly (one 8-byte read-back), then copy.
 TWO_PHASE_BYTES = 64 << 20
 # utf8 index stride of the resident arena (murr_utf8_index_update): every
-# UIDX_STRIDE rows, each utf8 column's string bytes so far (0.0625 B per row
+# UIDX_STRIDE rows, each utf8 column's string bytes so far (0.0156 B per row
 # and column), so a whole-table scan decodes on the whole GPU in one pass, cut
-# into virtual blocks on index strides.  The stride bounds how finely the
-# static deal can spread a shard over the grid: config D's 1.25 M rows over
-# 1280 workgroups are 9766 one-tile (128-row) virtual blocks, 7-8 per
-# workgroup, at stride 128; at 512, 2442 blocks of 512 rows, one or two per
-# workgroup -- half the workgroups idle for the last half of the scan
-# (DESIGN.md §6 measures both).  A table can pick another (uidx_stride).
-UIDX_STRIDE = 128
+# into virtual blocks on index strides.  512, as murr_encode_block's default:
+# round 4 had moved it to 128 for its dynamic tail (one-tile claims); with the
+# static deal the config D shard scans in 0.0748 ms at 512 against 0.0752 at
+# 128 (one lane; 0.0566 vs 0.0578 per step with two), interleaved on one box
+# (profiles/r05/ab_stride.txt), with a quarter of the index.  A table can
+# pick another (uidx_stride).
+UIDX_STRIDE = 512
 
 
 class ResidentTable:

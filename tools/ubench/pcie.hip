@@ -4,6 +4,7 @@
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 pcie.hip -o pcie
 #include <hip/hip_runtime.h>
 
+#include <cstdint>
 #include <cstdio>
 #include <cstdlib>
 
@@ -125,6 +126,51 @@ int main() {
         pair("engine H2D + kernel D2H", din, kout, true);
         pair("kernel H2D + engine D2H", kin, dout, true);
         pair("engine H2D + engine D2H", din, dout, true);
+    }
+    // round 5: the streaming host decode's own shape without the decode --
+    // config B batches with u32 row offsets (2 329 837 B in, 1 451 392 B out
+    // per batch, murr_hstream's h2d_bytes / d2h_bytes), four slots each with
+    // its own stream: H2D by the copy engine, D2H by a 128-workgroup copy
+    // kernel behind it on the slot stream (what murr_hstream issues), or both
+    // by engine / both by kernel; batches back to back, slot s + 4 waiting for
+    // slot s only through its stream.  batch/s x the Arrow bytes of a batch
+    // (1 429 837) is the host-to-host ceiling the stream can reach on this link.
+    {
+        const size_t in_b = 2329837, out_b = 1451392, arrow_b = 1429837;
+        const int depth = 4, batches = 400;
+        hipStream_t ss[4];
+        for (int k = 0; k < depth; k++) CK(hipStreamCreateWithFlags(&ss[k], hipStreamNonBlocking));
+        auto stream_shape = [&](const char* name, int mode) {  // 0 engine+kernel, 1 engine+engine, 2 kernel+kernel
+            CK(hipDeviceSynchronize());
+            CK(hipEventRecord(e0, ss[0]));
+            for (int k = 1; k < depth; k++) CK(hipStreamWaitEvent(ss[k], e0, 0));
+            for (int i = 0; i < batches; i++) {
+                hipStream_t st = ss[i % depth];
+                uint8_t* din = (uint8_t*)d1 + (size_t)(i % depth) * (4u << 20);
+                uint8_t* dout = (uint8_t*)d2 + (size_t)(i % depth) * (4u << 20);
+                uint8_t* hin = (uint8_t*)h1 + (size_t)(i % depth) * (4u << 20);
+                uint8_t* hout = (uint8_t*)h2 + (size_t)(i % depth) * (4u << 20);
+                if (mode == 2) kcopy<<<64, 256, 0, st>>>((const u32x4*)hin, (u32x4*)din, (in_b + 15) / 16);
+                else CK(hipMemcpyAsync(din, hin, in_b, hipMemcpyHostToDevice, st));
+                if (mode == 1) CK(hipMemcpyAsync(hout, dout, out_b, hipMemcpyDeviceToHost, st));
+                else kcopy<<<128, 256, 0, st>>>((const u32x4*)dout, (u32x4*)hout, (out_b + 15) / 16);
+            }
+            for (int k = 0; k < depth; k++) CK(hipStreamSynchronize(ss[k]));
+            CK(hipEventRecord(e1, ss[0]));
+            CK(hipEventSynchronize(e1));
+            float t = 0;
+            CK(hipEventElapsedTime(&t, e0, e1));
+            const double s = t * 1e-3;
+            std::printf("stream shape (B, u32 offsets, depth %d) %-22s %.1f us/batch  in %5.1f GB/s  out %5.1f GB/s  "
+                        "ceiling %5.2f GiB/s Arrow host to host\n",
+                        depth, name, t * 1e3 / batches, in_b * (double)batches / s / 1e9, out_b * (double)batches / s / 1e9,
+                        arrow_b * (double)batches / s / (1024.0 * 1024.0 * 1024.0));
+            std::fflush(stdout);
+        };
+        stream_shape("engine in + kernel out", 0);  // warm
+        stream_shape("engine in + kernel out", 0);
+        stream_shape("engine in + engine out", 1);
+        stream_shape("kernel in + kernel out", 2);
     }
     return 0;
 }
