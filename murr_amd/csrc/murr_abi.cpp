@@ -106,8 +106,6 @@ struct murr_ctx {
     std::vector<hipEvent_t> event_pool;
     uint64_t* aux = nullptr;  // device scratch of the gather scan (group sums)
     uint64_t aux_cap = 0;     // entries
-    uint64_t* wide = nullptr; // u32 row offsets widened for the generic decode kernel
-    uint64_t wide_cap = 0;    // entries
     hipEvent_t xev = nullptr; // multi-GPU reads: this stream's work, awaited by the home stream
     hipEvent_t hev = nullptr; // multi-GPU reads (as home): the work queued before a read, awaited by the shards
     // Fused transfers (the streaming host decode, murr_hstream): the next
@@ -697,7 +695,6 @@ void murr_ctx_destroy(murr_ctx_t* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->ws) (void)hipFree(c->ws);
     if (c->aux) (void)hipFree(c->aux);
-    if (c->wide) (void)hipFree(c->wide);
     if (c->hs) (void)hipHostFree(c->hs);
     for (const auto& b : c->pool) (void)(b.pinned ? hipHostFree(b.p) : hipFree(b.p));
     for (hipEvent_t e : c->event_pool) (void)hipEventDestroy(e);
@@ -1549,25 +1546,8 @@ int murr_decode_enqueue_ix(murr_ctx_t* c, const murr_segment_t* seg, const uint3
     std::vector<DecBlock> db(nblocks);
     uint64_t tiles = 0;
     uint32_t nonempty = 0;
-    // this kernel reads u64 offsets: u32 blocks are widened into c->wide first
-    uint64_t nwide = 0;
-    for (uint32_t b = 0; b < nblocks; b++)
-        if (blocks[b].row_off32 && blocks[b].n_rows) nwide += blocks[b].n_rows + 1;
-    if (nwide > c->wide_cap) {
-        if (c->wide) HIPC(hipFree(c->wide));
-        c->wide = nullptr;
-        c->wide_cap = 0;
-        HIPC(hipMalloc(&c->wide, 8 * nwide));
-        c->wide_cap = nwide;
-    }
-    nwide = 0;
     for (uint32_t b = 0; b < nblocks; b++) {
-        db[b] = DecBlock{blocks[b].data, blocks[b].row_off, blocks[b].n_rows, tiles, nullptr, 0u, 0u};
-        if (blocks[b].row_off32 && blocks[b].n_rows) {
-            HIPC(launch_row_off_widen(blocks[b].row_off32, c->wide + nwide, blocks[b].n_rows + 1, c->stream));
-            db[b].row_off = c->wide + nwide;
-            nwide += blocks[b].n_rows + 1;
-        }
+        db[b] = dec_block(blocks[b], tiles, nullptr);
         tiles += (blocks[b].n_rows + R - 1) / R;
         nonempty += blocks[b].n_rows != 0;
     }

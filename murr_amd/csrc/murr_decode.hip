@@ -70,6 +70,7 @@ __device__ __forceinline__ DecBlock ldblk(const DecodeArgs& A, uint64_t i) {
     const CAS DecBlock* p = (const CAS DecBlock*)A.blocks + i;
     DecBlock r;
     r.data = p->data; r.row_off = p->row_off; r.n_rows = p->n_rows; r.tile_base = p->tile_base;
+    r.ro32 = p->ro32;
     return r;
 }
 __device__ __forceinline__ DecProj ldproj(const DecodeArgs& A, uint64_t i) {
@@ -194,8 +195,8 @@ __device__ __forceinline__ uint32_t wg_tiles(const DecodeArgs& A) {
 struct LCur {
     uint64_t t, tb, te, n_rows;
     const uint8_t* data;
-    const uint64_t* row_off;
-    uint32_t b, ok;
+    const uint64_t* row_off;  // u32 offsets when ro32 (DecBlock)
+    uint32_t b, ok, ro32;
 };
 
 __device__ __forceinline__ void cur_block(const DecodeArgs& A, LCur& c, uint32_t b) {
@@ -206,6 +207,7 @@ __device__ __forceinline__ void cur_block(const DecodeArgs& A, LCur& c, uint32_t
     c.n_rows = blk.n_rows;
     c.data = blk.data;
     c.row_off = blk.row_off;
+    c.ro32 = blk.ro32;
 }
 
 __device__ __forceinline__ LCur cur_first(const DecodeArgs& A) {
@@ -213,6 +215,7 @@ __device__ __forceinline__ LCur cur_first(const DecodeArgs& A) {
     c.t = c.tb = c.te = c.n_rows = 0;
     c.data = nullptr;
     c.row_off = nullptr;
+    c.ro32 = 0;
     c.b = 0;
     c.ok = 0;
     const uint32_t w = blockIdx.x, G = gridDim.x;
@@ -257,7 +260,7 @@ struct SlotDesc {
     uint32_t b, nr, flags;
 };
 static_assert(sizeof(SlotDesc) <= 64, "slot descriptor");
-enum : uint32_t { kFirst = 1, kLast = 2, kHbmTile = 4, kHuge = 8 };
+enum : uint32_t { kFirst = 1, kLast = 2, kHbmTile = 4, kHuge = 8, kRo32 = 16 };
 
 // ---- loader wave ----------------------------------------------------------------
 // LDS-DMA by inline asm: hipcc then keeps these loads out of its s_waitcnt
@@ -293,15 +296,21 @@ __device__ __forceinline__ void dma_1k(const GAS uint8_t* g, uint32_t nb, uint32
 }
 
 // Span DMA for one fill: row_off[r0] and row_off[r0 + nr] (two u64, four
-// dword lanes) into span ring entry e; a dummy for "no such fill".
+// dword lanes; u32 offsets: lanes 0 and 2, the high dwords masked by the
+// reader) into span ring entry e; a dummy for "no such fill".
 __device__ __forceinline__ void span_dma(const DecodeArgs& A, const LCur& c, LAS uint8_t* lds, uint32_t e,
                                          uint32_t lane) {
     LAS uint8_t* dst = lds + A.lds_span + e * 16;
     if (c.ok) {
         const uint64_t r0 = (c.t - c.tb) * A.rows_per_tile;
         const uint64_t nr = min((uint64_t)A.rows_per_tile, c.n_rows - r0);
-        const GAS uint8_t* p = (const GAS uint8_t*)(c.row_off + (lane < 2 ? r0 : r0 + nr)) + (lane & 1) * 4;
-        if (lane < 4) glds4(p, dst);
+        if (c.ro32) {
+            const GAS uint32_t* p = (const GAS uint32_t*)c.row_off + (lane < 2 ? r0 : r0 + nr);
+            if (lane == 0 || lane == 2) glds4(p, dst);
+        } else {
+            const GAS uint8_t* p = (const GAS uint8_t*)(c.row_off + (lane < 2 ? r0 : r0 + nr)) + (lane & 1) * 4;
+            if (lane < 4) glds4(p, dst);
+        }
     } else {
         if (lane == 0) glds4((const GAS void*)A.blocks, lds + A.lds_scratch);
     }
@@ -374,12 +383,13 @@ __device__ __forceinline__ void loader_wave(LAS uint8_t* lds) {
         st.lap(0);
         // this fill's span: landed (step j-P's wait, or the prologue)
         const LAS uint64_t* sp = (const LAS uint64_t*)(lds + A.lds_span + (j % kSpanRing) * 16);
-        const uint64_t base = sgpr64(sp[0]), end = sgpr64(sp[1]);
+        const uint64_t om = ci.ro32 ? 0xFFFFFFFFull : ~0ull;
+        const uint64_t base = sgpr64(sp[0]) & om, end = sgpr64(sp[1]) & om;
         const uint64_t r0 = (ci.t - ci.tb) * F;
         const uint32_t nr = (uint32_t)min((uint64_t)F, ci.n_rows - r0);
         const uint64_t abase = base & ~15ull;
         const uint64_t span = ((end + 15) & ~15ull) - abase;
-        uint32_t flags = (r0 == 0 ? kFirst : 0) | (r0 + nr == ci.n_rows ? kLast : 0);
+        uint32_t flags = (r0 == 0 ? kFirst : 0) | (r0 + nr == ci.n_rows ? kLast : 0) | (ci.ro32 ? kRo32 : 0);
         if (end - abase > 0xFFFFFFF0ull) flags |= kHuge;
         else if (span > A.stage) flags |= kHbmTile;
         if (lane == 0) {
@@ -393,9 +403,10 @@ __device__ __forceinline__ void loader_wave(LAS uint8_t* lds) {
         // fill j+P's span, then fill j's row offsets and blob bytes
         span_dma(A, cs, lds, (j + P) % kSpanRing, lane);
         cur_next(A, cs);
-        const uintptr_t rp = (uintptr_t)(ci.row_off + r0);
+        const uint32_t ow = ci.ro32 ? 4 : 8;  // row offset width
+        const uintptr_t rp = (uintptr_t)ci.row_off + r0 * ow;
         const uintptr_t s0 = rp & ~(uintptr_t)15;
-        const uint32_t nb_ro = (uint32_t)(((rp - s0) + (uint64_t)(nr + 1) * 8 + 15) & ~15ull);
+        const uint32_t nb_ro = (uint32_t)(((rp - s0) + (uint64_t)(nr + 1) * ow + 15) & ~15ull);
         const GAS uint8_t* valid = (const GAS uint8_t*)s0;
         for (uint32_t k = 0; k < A.dro; k++)
             dma_1k((const GAS uint8_t*)s0, nb_ro, k, sb + A.lds_ro, scratch, valid, lane);
@@ -771,7 +782,7 @@ __device__ __forceinline__ void prefixes(const DecodeArgs& A, const Tile& T, LAS
 
 template <int KC, class Src>
 __device__ __forceinline__ void decode_tile(const DecodeArgs& A, const Src& src, const Tile& T,
-                                            const LAS uint32_t* ro, LAS uint8_t* lds, uint32_t s, uint32_t w,
+                                            const LAS uint32_t* ro, uint32_t rs, LAS uint8_t* lds, uint32_t s, uint32_t w,
                                             uint32_t slot, uint32_t NC, LAS uint32_t* wnull, Stamp& st) {
     const uint32_t lane = tidx() & 63;
     const uint32_t bs = A.bs, nproj = A.nproj, nutf8 = A.nutf8;
@@ -785,7 +796,7 @@ __device__ __forceinline__ void decode_tile(const DecodeArgs& A, const Src& src,
 #pragma unroll
     for (int k = 0; k < KC; k++) {
         const uint32_t i = k * 64 + lane;
-        const uint32_t a0 = ro[2 * i], a1 = ro[2 * i + 2];
+        const uint32_t a0 = ro[rs * i], a1 = ro[rs * (i + 1)];
         const uint32_t rl = i < T.nr ? a1 - a0 : 0;
         W.ra[k] = a0 - abase;
         badk |= (uint32_t)(rl != 0 && rl < bs) << k;
@@ -845,7 +856,7 @@ __device__ __forceinline__ void decode_tile(const DecodeArgs& A, const Src& src,
             if (!((badk >> k) & 1)) continue;
             const uint32_t i = k * 64 + lane;
             const uint64_t row = T.r0 + i;
-            const uint32_t ra = W.ra[k], rl = ro[2 * i + 2] - ro[2 * i];
+            const uint32_t ra = W.ra[k], rl = ro[rs * (i + 1)] - ro[rs * i];
             if (rl < bs) { report(A.err, err_key(T.b, row, 0, kStMalformed)); continue; }
             for (uint32_t p = 0; p < nproj; p++) {
                 const DecProj pc = ldproj(A, p);
@@ -932,8 +943,9 @@ __device__ __forceinline__ void consumer_wave(LAS uint8_t* lds, uint32_t w) {
         T.nr = D.nr > s0 ? min(SUB, D.nr - s0) : 0u;
         T.flags = (D.flags & (kHbmTile | kHuge)) | ((D.flags & kFirst) && w == 0 ? kFirst : 0u) |
                   ((D.flags & kLast) && T.nr && s0 + T.nr == D.nr ? kLast : 0u);
+        const uint32_t rs = (D.flags & kRo32) ? 1u : 2u;  // dwords per row offset
         const LAS uint32_t* ro =
-            (const LAS uint32_t*)(sb + A.lds_ro + (((uintptr_t)(D.row_off + D.r0)) & 15)) + 2 * s0;
+            (const LAS uint32_t*)(sb + A.lds_ro + (((uintptr_t)D.row_off + D.r0 * rs * 4) & 15)) + rs * s0;
         if (T.b != cur_b) {  // this wave's null counters belong to one block
             if (cur_b != ~0u) flush_nulls(A, wnull, cur_b);
             cur_b = T.b;
@@ -948,9 +960,9 @@ __device__ __forceinline__ void consumer_wave(LAS uint8_t* lds, uint32_t w) {
                 prefixes(A, T, lds, s, w, slot, NC, pre);
             }
         } else if (T.flags & kHbmTile) {
-            decode_tile<KC>(A, HbmSrc{gp(T.data) + T.abase}, T, ro, lds, s, w, slot, NC, wnull, st);
+            decode_tile<KC>(A, HbmSrc{gp(T.data) + T.abase}, T, ro, rs, lds, s, w, slot, NC, wnull, st);
         } else {
-            decode_tile<KC>(A, StageSrc{sb + A.lds_stage}, T, ro, lds, s, w, slot, NC, wnull, st);
+            decode_tile<KC>(A, StageSrc{sb + A.lds_stage}, T, ro, rs, lds, s, w, slot, NC, wnull, st);
         }
         st.lap(3);
         // every LDS read of the slot has returned: count this wave off the fill

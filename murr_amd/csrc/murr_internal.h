@@ -327,7 +327,6 @@ struct CopyArgs {
 hipError_t launch_copy_segs(const CopySeg* segs, uint32_t n, uint32_t grid, hipStream_t s);
 // Row offsets u64 <-> u32, n entries (murr_kernels.hip).
 hipError_t launch_row_off_narrow(const uint64_t* in, uint32_t* out, uint64_t n, hipStream_t s);
-hipError_t launch_row_off_widen(const uint32_t* in, uint64_t* out, uint64_t n, hipStream_t s);
 
 // Arrow IPC framing (murr_ipc.cpp, murr_ipc.hip).
 enum : uint32_t { kIpcValidity = 0, kIpcOffsets = 1, kIpcValues = 2 };

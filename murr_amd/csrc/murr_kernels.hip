@@ -247,17 +247,12 @@ __global__ void __launch_bounds__(256) copy_segs_kernel(CopyArgs A) {
 }
 
 // ---- row-offset widths (murr_block_t.row_off32) -------------------------------
-// u64 -> u32 (murr_row_off_narrow; the host checked the last offset) and
-// u32 -> u64 (the generic decode kernel reads u64 offsets: a u32 block is
-// widened into the workspace first).
+// u64 -> u32 (murr_row_off_narrow; the host checked the last offset).  Both
+// decode kernels read either width natively.
 __global__ void __launch_bounds__(256) narrow_kernel(const uint64_t* __restrict__ in, uint32_t* __restrict__ out,
                                                      uint64_t n) {
     for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256)
         out[i] = (uint32_t)in[i];
-}
-__global__ void __launch_bounds__(256) widen_kernel(const uint32_t* __restrict__ in, uint64_t* __restrict__ out,
-                                                    uint64_t n) {
-    for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) out[i] = in[i];
 }
 
 }  // namespace
@@ -266,13 +261,6 @@ hipError_t launch_row_off_narrow(const uint64_t* in, uint32_t* out, uint64_t n, 
     if (!n) return hipSuccess;
     const uint64_t g = (n + 255) / 256;
     hipLaunchKernelGGL(narrow_kernel, dim3((uint32_t)(g < 4096 ? g : 4096)), dim3(256), 0, s, in, out, n);
-    return hipGetLastError();
-}
-
-hipError_t launch_row_off_widen(const uint32_t* in, uint64_t* out, uint64_t n, hipStream_t s) {
-    if (!n) return hipSuccess;
-    const uint64_t g = (n + 255) / 256;
-    hipLaunchKernelGGL(widen_kernel, dim3((uint32_t)(g < 4096 ? g : 4096)), dim3(256), 0, s, in, out, n);
     return hipGetLastError();
 }
 

@@ -38,7 +38,7 @@ if [ "$PART" != 1 ]; then
   run decode_C_noindex 300 "$PY" bench.py --config C --blocks 10 --steps 10 --warmup 2 --no-cpu --uidx-stride 0
   run decode_D10M 300 "$PY" bench.py --config D --rows 10000000 --steps 10 --warmup 2 --no-cpu
   run decode_D1_noindex 300 "$PY" bench.py --config D --steps 10 --warmup 2 --no-cpu --uidx-stride 0
-  run decode_B_generic 300 "$PY" bench.py --steps 10 --warmup 2 --no-cpu --opts kernel=generic --offsets 64
+  run decode_B_generic 300 "$PY" bench.py --steps 10 --warmup 2 --no-cpu --opts kernel=generic
   run host_C 300 "$PY" bench.py --mode host --config C --rows 1000 --blocks 2000 --warmup 50
   run encode_B 300 "$PY" bench.py --mode encode --enc-config B --steps 10 --warmup 2
   run encode_C 300 "$PY" bench.py --mode encode --enc-config C --steps 10 --warmup 2
