@@ -239,6 +239,17 @@ constexpr uint32_t kColW[NCOLS] = {  // 0 = utf8, 9 = bool
 #undef MJ_X
 };
 
+// Word lanes per chunk (see store_words).
+#ifndef MJ_FOLDB
+#define MJ_FOLDB 1
+#endif
+constexpr bool has_bool() {
+    for (uint32_t c = 0; c < NCOLS; c++)
+        if (kColW[c] == 9) return true;
+    return false;
+}
+constexpr bool FOLDB = MJ_FOLDB && has_bool() && 2 * NCOLS <= 64;
+constexpr uint32_t WL = FOLDB ? 2 * NCOLS : NCOLS;
 // ---- byte sources ------------------------------------------------------------
 // Tile bytes staged in LDS (hot path).  Aligned dword reads + v_alignbyte (an
 // unaligned ds_read_b32 is correct on gfx950 but far slower).  Reads are
@@ -738,7 +749,7 @@ template <uint32_t C> DEV void stash(uint32_t (&lo)[NCW], uint32_t (&hi)[NCW], b
                  : "+v"(lo[C / 64]), "+v"(hi[C / 64])
                  : "s"((uint32_t)m), "s"((uint32_t)(m >> 32)), "i"(C % 64));
 }
-// Merged words: chunk k's ballot of column C into lane k * NCOLS + C (k is a
+// Merged words: chunk k's ballot of word lane C into lane k * WL + C (k is a
 // constant once the chunk loop is unrolled, but not a C++ constant, so the
 // lane select goes through M0: an SGPR value and an SGPR lane select in one
 // VOP3 would break the constant-bus limit).  M0 is saved and restored (the
@@ -750,7 +761,7 @@ template <uint32_t C> DEV void stash_k(uint32_t& lo, uint32_t& hi, bool b, uint3
     asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %5\n\ts_nop 4\n\tv_writelane_b32 %1, %3, m0\n\t"
                  "v_writelane_b32 %2, %4, m0\n\ts_mov_b32 m0, %0"
                  : "=&s"(keep), "+v"(lo), "+v"(hi)
-                 : "s"((uint32_t)m), "s"((uint32_t)(m >> 32)), "s"(k * NCOLS + C));
+                 : "s"((uint32_t)m), "s"((uint32_t)(m >> 32)), "s"(k * WL + C));
 }
 
 // ---- per-wave state of a tile --------------------------------------------------
@@ -806,28 +817,48 @@ template <uint32_t C> DEV Out lane_out(const Lanes& L, const Out* ob, uint32_t p
 #endif
 }
 
-// Merged validity words (tiles of R > 1 chunks per wave, R x NCOLS <= 64
+// Word lanes.  A chunk's validity words (and the bool columns' value words)
+// go out as one wave store: lane c writes column c's validity word and, with
+// MJ_FOLDB, lane NCOLS + c column c's bool value word (WL = 2 NCOLS word
+// lanes when the layout has a bool column), instead of a second store for the
+// bools.  A wave store instruction costs about the same whatever it writes
+// (the store-shape probe: ~30 cycles of the CU's memory pipeline up to 256 B).
+//
+// Merged validity words (tiles of R > 1 chunks per wave, R x WL <= 64
 // lanes): the words of all R chunks of a wave go out in ONE store -- lane
-// k * NCOLS + c holds chunk k's word of column c -- instead of one store per
-// chunk.  A wave store instruction costs about the same whatever it writes
-// (config B ablation, round 5: its two-lane validity store per chunk was 7.5 %
-// of the kernel).  The per-lane tables then hold column (lane % NCOLS).
-template <uint32_t R> DEV constexpr bool merged_words() { return R > 1 && R * NCOLS <= 64; }
-template <uint32_t R> DEV uint32_t lane_col(uint32_t j, uint32_t lane) {
-    if constexpr (merged_words<R>()) return lane < R * NCOLS ? lane % NCOLS : NCOLS;
-    else return j * 64 + lane;
+// k * WL + c holds chunk k's word c -- instead of one store per chunk (config
+// B ablation, round 5: its two-lane validity store per chunk was 7.5 % of the
+// kernel).  The per-lane tables then hold word lane (lane % WL).
+template <uint32_t R> DEV constexpr bool merged_words() { return R > 1 && R * WL <= 64; }
+// Lane `lane` of lane group j: its column c and whether it is a bool value
+// word (bw); false for a lane with no word.
+template <uint32_t R> DEV bool lane_word(uint32_t j, uint32_t lane, uint32_t& c, uint32_t& bw) {
+    uint32_t x;
+    if constexpr (merged_words<R>()) {
+        if (lane >= R * WL) return false;
+        x = lane % WL;
+    } else if constexpr (FOLDB) {
+        if (lane >= WL) return false;
+        x = lane;
+    } else {
+        x = j * 64 + lane;
+        if (x >= NCOLS) return false;
+    }
+    bw = x >= NCOLS;
+    c = bw ? x - NCOLS : x;
+    return true;
 }
 
-// Per-lane output pointers of block b (lane c: column c's validity and bool
-// values), reloaded when the block changes; null counts of the previous
-// block flushed first.
+// Per-lane output pointers of block b (word lane c: column c's validity, or
+// a bool column's values), reloaded when the block changes; null counts of
+// the previous block flushed first.
 template <uint32_t R> DEV void lanes_flush(Lanes& L, uint32_t lane) {
     if (L.blk == ~0u) return;
     unsigned long long* nulls = args()->nulls + (uint64_t)L.blk * args()->nproj;
 #pragma unroll
     for (uint32_t j = 0; j < NCW; j++) {
-        const uint32_t c = lane_col<R>(j, lane);
-        if (c < NCOLS && L.proj[j] && L.nacc[j])
+        uint32_t c = 0, bw = 0;
+        if (lane_word<R>(j, lane, c, bw) && L.proj[j] && L.nacc[j])  // (nacc stays 0 on bool value lanes)
             __hip_atomic_fetch_add(gp(nulls) + gp(args()->slot_tab)[c], (unsigned long long)L.nacc[j], __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
         L.nacc[j] = 0;
@@ -840,12 +871,14 @@ template <uint32_t R> DEV void lanes_block(Lanes& L, uint32_t b, uint32_t lane) 
     const Out* ob = outs_of(b);
 #pragma unroll
     for (uint32_t j = 0; j < NCW; j++) {
-        const uint32_t c = lane_col<R>(j, lane);
-        const uint32_t s = c < NCOLS ? (uint32_t)gp(args()->slot_tab)[c] : (uint32_t)kNone;
-        L.proj[j] = s != kNone;
-        L.isbool[j] = c < NCOLS && kColW[c < NCOLS ? c : 0] == 9;
+        uint32_t c = 0, bw = 0;
+        const bool ok = lane_word<R>(j, lane, c, bw);
+        const uint32_t s = ok ? (uint32_t)gp(args()->slot_tab)[c] : (uint32_t)kNone;
+        const bool isb = ok && kColW[ok ? c : 0] == 9;
+        L.proj[j] = s != kNone && (!bw || isb);
+        L.isbool[j] = isb && !bw;  // (a separate bool store: layouts without FOLDB)
         const GAS Out* o = (const GAS Out*)ob + (s != kNone ? s : 0u);
-        L.vptr[j] = s != kNone ? (uint64_t)o->validity : 0;
+        L.vptr[j] = s != kNone ? (uint64_t)(bw ? (void*)o->values : (void*)o->validity) : 0;
         L.bptr[j] = s != kNone ? (uint64_t)o->values : 0;
 #if MJ_HOIST >= 2
         L.optr[j] = s != kNone ? (uint64_t)o->offsets : 0;
@@ -860,7 +893,8 @@ template <uint32_t R> DEV void lanes_block(Lanes& L, uint32_t b, uint32_t lane) 
 }
 
 // Validity (and bool values) words of one chunk for every decoded column: one
-// store per lane group, lane c writes column c's word.
+// store per lane group, lane c writes word c.
+template <uint32_t R>
 DEV void store_words(Lanes& L, const uint32_t (&vlo)[NCW], const uint32_t (&vhi)[NCW], const uint32_t (&blo)[NCW],
                      const uint32_t (&bhi)[NCW], uint64_t word, uint32_t nk, uint32_t lane) {
 #pragma unroll
@@ -868,21 +902,21 @@ DEV void store_words(Lanes& L, const uint32_t (&vlo)[NCW], const uint32_t (&vhi)
         if (L.proj[j]) {
             const uint64_t v = ((uint64_t)vhi[j] << 32) | vlo[j];
             ostw(gp((uint64_t*)L.vptr[j]) + word, v);
-            if (L.isbool[j]) ostw(gp((uint64_t*)L.bptr[j]) + word, ((uint64_t)bhi[j] << 32) | blo[j]);
-            L.nacc[j] += nk - (uint32_t)__popcll(v);
+            if constexpr (!FOLDB)
+                if (L.isbool[j]) ostw(gp((uint64_t*)L.bptr[j]) + word, ((uint64_t)bhi[j] << 32) | blo[j]);
+            if (!FOLDB || lane < NCOLS) L.nacc[j] += nk - (uint32_t)__popcll(v);
         }
     }
 }
-// The merged form: lane k * NCOLS + c stores chunk k's word of column c.
-DEV void store_words_merged(Lanes& L, uint32_t vlo, uint32_t vhi, uint32_t blo, uint32_t bhi, uint64_t r0,
-                            uint32_t rbase, uint32_t nr, uint32_t lane) {
-    const uint32_t c0 = rbase + (lane / NCOLS) * 64;
+// The merged form: lane k * WL + c stores chunk k's word c.
+DEV void store_words_merged(Lanes& L, uint32_t vlo, uint32_t vhi, uint64_t r0, uint32_t rbase, uint32_t nr,
+                            uint32_t lane) {
+    const uint32_t c0 = rbase + (lane / WL) * 64;
     const uint32_t nk = c0 < nr ? umin32(64u, nr - c0) : 0u;
     if (L.proj[0] && nk) {
         const uint64_t v = ((uint64_t)vhi << 32) | vlo, word = (r0 + c0) >> 6;
         ostw(gp((uint64_t*)L.vptr[0]) + word, v);
-        if (L.isbool[0]) ostw(gp((uint64_t*)L.bptr[0]) + word, ((uint64_t)bhi << 32) | blo);
-        L.nacc[0] += nk - (uint32_t)__popcll(v);
+        if (lane % WL < NCOLS) L.nacc[0] += nk - (uint32_t)__popcll(v);
     }
 }
 
@@ -1098,6 +1132,25 @@ DEV uint32_t hib_regs(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t sh, uint32
     return n == 1 ? head & 0xFFu : 0u;
 }
 
+// Column C's fixed-width value of chunk k (width WW at row byte FO), 0 for a
+// null or short cell; a valid cell the row is too short for is flagged in badk
+// (primitive.rs:43-56: a null reads as the default value).
+template <uint32_t C, uint32_t WW, uint32_t FO, class Src, uint32_t R>
+DEV uint32_t fixed_val(const Src& src, const Rows<R>& W, uint32_t k, bool safe, uint32_t& badk, uint32_t& hi) {
+    bool valid = (W.vb[k][C / 32] >> (C % 32)) & 1u;
+    if (safe) {
+        const bool have = FO + WW <= W.rl[k];
+        badk |= (uint32_t)(valid && !have) << k;
+        valid = valid && have;
+    }
+    uint32_t lo = 0;
+    hi = 0;
+    field<WW, FO>(src, W.r[k], W.ra[k], valid || !Src::kHbm, lo, hi);
+    const uint32_t m = valid ? ~0u : 0u;
+    hi &= m;
+    return lo & m;
+}
+
 template <class SH, uint32_t PH, class Src, bool ER = false>
 DEV void decode_tile(const Src& src, const Tile& T, const LAS uint32_t* ro, LAS uint8_t* ctl, uint64_t (&run)[NU],
                      Lanes& L, uint32_t wave, uint32_t lane, uint32_t it, LAS uint32_t* rel = nullptr) {
@@ -1120,6 +1173,12 @@ DEV void decode_tile(const Src& src, const Tile& T, const LAS uint32_t* ro, LAS 
     do {                                                 \
         if constexpr (MV) stash_k<C>(LO[0][0], HI[0][0], (B), (K)); \
         else stash<C>(LO[K], HI[K], (B));               \
+    } while (0)
+    // a bool column's value word: word lane NCOLS + C of the validity store
+#define MJ_STASHB(C, K, B)                                                   \
+    do {                                                                     \
+        if constexpr (FOLDB) MJ_STASH(NCOLS + C, vlo, vhi, K, B);            \
+        else MJ_STASH(C, blo, bhi, K, B);                                    \
     } while (0)
 #if MJ_HOIST
     // the projection's slot words, once per tile (one batched scalar load;
@@ -1260,20 +1319,11 @@ DEV void decode_tile(const Src& src, const Tile& T, const LAS uint32_t* ro, LAS 
             const Out o = lane_out<C>(L, ob, MJ_SLOT(C));                                               \
             _Pragma("unroll") for (uint32_t k = 0; k < R; k++) {                                        \
                 const uint32_t i = rbase + k * 64 + lane;                                               \
-                bool valid = (W.vb[k][C / 32] >> (C % 32)) & 1u;                                        \
-                if (safe) {                                                                             \
-                    const bool have = FO + WW <= W.rl[k];                                               \
-                    badk |= (uint32_t)(valid && !have) << k;                                            \
-                    valid = valid && have;                                                              \
-                }                                                                                       \
-                uint32_t lo = 0, hi = 0;                                                                \
-                field<WW, FO>(src, W.r[k], W.ra[k], valid || !Src::kHbm, lo, hi);                       \
-                const uint32_t m = valid ? ~0u : 0u;                                                    \
-                lo &= m;                                                                                \
-                hi &= m;                                                                                \
+                uint32_t hi = 0;                                                                        \
+                const uint32_t lo = fixed_val<C, WW, FO>(src, W, k, safe, badk, hi);                    \
                 MJ_STASH(C, vlo, vhi, k, (W.vb[k][C / 32] >> (C % 32)) & 1u);                           \
                 if constexpr (W_ == 9) {                                                                \
-                    MJ_STASH(C, blo, bhi, k, lo != 0);                                                  \
+                    MJ_STASHB(C, k, lo != 0);                                                           \
                 } else if (i < T.nr && !MJ_ABL_NOFIX) {                                                 \
                     const uint64_t row = T.r0 + i;                                                      \
                     if constexpr (W_ == 8) ost(gp((uint64_t*)o.values) + row, ((uint64_t)hi << 32) | lo); \
@@ -1289,15 +1339,16 @@ DEV void decode_tile(const Src& src, const Tile& T, const LAS uint32_t* ro, LAS 
 #undef MJ_F
 
     if constexpr (PH != 2 && MV) {
-        store_words_merged(L, vlo[0][0], vhi[0][0], blo[0][0], bhi[0][0], T.r0, rbase, T.nr, lane);
+        store_words_merged(L, vlo[0][0], vhi[0][0], T.r0, rbase, T.nr, lane);
     } else if constexpr (PH != 2) {
 #pragma unroll
         for (uint32_t k = 0; k < R; k++) {
             const uint32_t c0 = rbase + k * 64;
             const uint32_t nk = c0 < T.nr ? umin32(64u, T.nr - c0) : 0u;
-            if (nk) store_words(L, vlo[k], vhi[k], blo[k], bhi[k], (T.r0 + c0) >> 6, nk, lane);
+            if (nk) store_words<R>(L, vlo[k], vhi[k], blo[k], bhi[k], (T.r0 + c0) >> 6, nk, lane);
         }
     }
+#undef MJ_STASHB
 #undef MJ_STASH
 
     if (PH != 2 && args()->report && __ballot(badk != 0)) {  // cold: exact error reports

@@ -478,3 +478,36 @@ def test_validity_local_whole_blocks(ctx, kernel_mode, shape):
         for p in range(len(proj)):
             assert_array_equal(got[b][p], wants[b % len(blocks)][p], f"block {b} proj {p}")
             check_padding(got[b][p], n)
+
+
+PAIR_DTYPES = [D.Int8, D.UInt16, D.Bool, D.UInt8, D.Int16, D.Int8, D.Bool, D.Utf8, D.Int64, D.UInt16]
+
+
+@pytest.mark.parametrize("proj", [list(range(10)), [0, 1, 2], [3, 4, 6], [4, 3, 1, 0, 9, 5], [5, 9, 2, 6],
+                                  [0, 3, 0, 3, 1, 4, 7]], ids=["all", "firsts", "seconds", "rev", "odd", "dup"])
+@pytest.mark.parametrize("mode,shape", [("local", "5x3"), ("local", "5x2"), ("local", "3x1"), ("split", "3x1"),
+                                        ("split", "5x2")])
+def test_narrow_pairs_and_bool_words(ctx, kernel_mode, mode, shape, proj):
+    # narrow (1- and 2-byte) columns in pairs and alone, and bool columns,
+    # whose value words the JIT kernel writes in the validity store's lanes
+    # (word lane NCOLS + c); projections holding both, one or neither of a
+    # pair (round 5 measured pairing two narrow columns into one store: no
+    # faster), ragged chunk ends, nulls and missing rows; every
+    # buffer bit-exact against the oracle
+    nw, r = (int(x) for x in shape.split("x"))
+    set_default_opts(kernel=kernel_mode, mode=mode, shape=(nw, r))
+    rng = np.random.default_rng(500 + nw * 10 + r + len(mode) + len(proj))
+    oseg = O.Segment([int(d) for d in PAIR_DTYPES])
+    blocks, wants = [], []
+    for n in [9000, 1, 63, 65, 200, 4097]:
+        cols = random_columns(rng, PAIR_DTYPES, n, null_p=0.2, max_str=12)
+        miss = set(rng.choice(n, size=n // 13, replace=False).tolist()) if n > 13 else set()
+        _, data, off = oracle_block(PAIR_DTYPES, cols, n, miss)
+        blocks.append((data, off))
+        wants.append((n, O.decode_block(oseg, proj, data, off)))
+    got = gpu_decode(ctx, seg_of(PAIR_DTYPES), proj, blocks * 2)
+    for b in range(len(blocks) * 2):
+        n, want = wants[b % len(blocks)]
+        for p in range(len(proj)):
+            assert_array_equal(got[b][p], want[p], f"block {b} proj {p}")
+            check_padding(got[b][p], n)
