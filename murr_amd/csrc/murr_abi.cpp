@@ -3137,9 +3137,9 @@ void murr_sst_result_free(murr_ctx_t* c, murr_sst_result_t* r) {
     std::memset(r, 0, sizeof *r);
 }
 
-// Decode data blocks into entries: sst_count (a lane group per block inflates
-// it in LDS, counts its entries and keeps a tier-0 block in its HBM slot;
-// blocks too large for LDS are flagged tier 2), the scans placing every
+// Decode data blocks into entries: sst_count (a thread per block inflates a
+// tier-0 block into its HBM slot and counts its entries; larger blocks are
+// flagged tier 1 or 2), the scans placing every
 // block's entries, one 40-byte read-back that sizes the outputs, sst_decode.
 // Tier-2 blocks add a raw buffer, sst_big_count and a second read-back.
 // Scratch comes from the context pool.  Synchronous.
@@ -3155,8 +3155,8 @@ int murr_sst_decode(murr_ctx_t* c, const murr_sst_block_t* blocks, uint32_t nblo
     // scratch: err | totals[5] | nlist | descriptors | tier rlen list | ulen uoff ne kb vb eoff koff voff | parts
     const uint64_t o_tot = 8, o_nlist = 56, o_desc = 64, o_tier = round_up(o_desc + sizeof(SstBlock) * nb, 16);
     const uint64_t o_arr = round_up(o_tier + 3 * 4 * nb, 16), o_part = o_arr + 8 * 8 * nb;
-    const uint64_t scratch_bytes = o_part + 8 * std::max<uint64_t>(nparts, 1) + 64;
-    const uint64_t slot_bytes = 1024 * nb + 64;  // tier-0 blocks between sst_count and sst_decode
+    const uint64_t scratch_bytes = o_part + 8 * 4 * std::max<uint64_t>(nparts, 1) + 64;
+    const uint64_t slot_bytes = kSstSlot * nb + 64;  // tier-0 blocks between sst_count and sst_decode
     uint8_t *w = nullptr, *raw = nullptr, *slots = nullptr;
     uint64_t w_cap = 0, raw_cap = 0, slots_cap = 0;
     if (!pool_take(c, false, scratch_bytes, round_up(scratch_bytes, 1 << 20), &w, &w_cap))
@@ -3202,24 +3202,24 @@ int murr_sst_decode(murr_ctx_t* c, const murr_sst_block_t* blocks, uint32_t nblo
     uint64_t* tot = (uint64_t*)(w + o_tot);  // [0] entries [1] key bytes [2] value bytes [3] big bytes
     uint64_t* part = (uint64_t*)(w + o_part);
     uint64_t host[5] = {0, 0, 0, 0, 0};  // err, totals
-    auto scans = [&]() -> hipError_t {
+    // entries, key bytes, value bytes (and after the count pass tier-2 raw bytes)
+    auto scans = [&](bool with_raw) -> hipError_t {
         hipError_t e;
-        if ((e = launch_scan_u64(a.ne, a.eoff, nb, part, tot, c->stream)) != hipSuccess) return e;
-        if ((e = launch_scan_u64(a.kb, a.koff, nb, part, tot + 1, c->stream)) != hipSuccess) return e;
-        if ((e = launch_scan_u64(a.vb, a.voff, nb, part, tot + 2, c->stream)) != hipSuccess) return e;
+        ScanSet S{{a.ne, a.kb, a.vb, a.ulen}, {a.eoff, a.koff, a.voff, a.uoff}, {tot, tot + 1, tot + 2, tot + 3},
+                  part, with_raw ? 4u : 3u, 0u};
+        if ((e = launch_scan_u64_n(S, nb, c->stream)) != hipSuccess) return e;
         if ((e = hipMemcpyAsync(host, w, 40, hipMemcpyDeviceToHost, c->stream)) != hipSuccess) return e;
         return hipStreamSynchronize(c->stream);
     };
     if (nb) {
         SSTC(launch_sst_count(a, c->stream));
-        SSTC(launch_scan_u64(a.ulen, a.uoff, nb, part, tot + 3, c->stream));
-        SSTC(scans());
+        SSTC(scans(true));
         if (host[4]) {  // big blocks: inflated to raw by one thread each, counted, placed again
             if (!pool_take(c, false, host[4] + 16, round_up(host[4] + 16, 1 << 20), &raw, &raw_cap))
                 return fail(set_err(err, MURR_E_HIP, (int)hipErrorOutOfMemory));
             a.raw = raw;
             SSTC(launch_sst_big_count(a, c->stream));
-            SSTC(scans());
+            SSTC(scans(false));
         }
         if (host[0]) return fail(unpack_err(host[0], err));
     }

@@ -218,6 +218,9 @@ struct SstBlock {                  // = murr_sst_block_t
     uint64_t size;
     uint32_t compression, pad;
 };
+// A tier-0 block's HBM slot: up to 1 KiB uncompressed plus a pad the
+// thread-per-block inflate may overrun into (murr_sst.hip, tmatch).
+constexpr uint64_t kSstSlot = 1024 + 64;
 struct SstArgs {
     const SstBlock* blocks;
     uint64_t nblocks;
@@ -225,7 +228,7 @@ struct SstArgs {
     uint64_t* ulen;                // [nblocks] uncompressed size of a tier-2 block (0 otherwise)
     uint64_t* uoff;                // [nblocks] its placement in raw (prefix of ulen)
     uint8_t* raw;                  // tier-2 blocks uncompressed, back to back
-    uint8_t* slots;                // [nblocks][1024] compressed tier-0 blocks, inflated by sst_count
+    uint8_t* slots;                // [nblocks][kSstSlot] compressed tier-0 blocks, inflated by sst_count
     uint32_t* rlen;                // [nblocks] uncompressed size of a tier-0/1 block
     uint32_t* list;                // tier-1 blocks, *nlist of them
     uint32_t* nlist;
@@ -238,14 +241,22 @@ struct SstArgs {
     uint64_t* seqs;
     uint8_t* types;
     unsigned long long* err;
+    uint32_t probe, pad;           // tuning builds (MURR_SST_PROBE): sst_count_t phase ablations; 0
 };
 hipError_t launch_sst_count(const SstArgs& a, hipStream_t s);      // tiers 0 and 1; flags tier 2
 hipError_t launch_sst_big_count(const SstArgs& a, hipStream_t s);  // tier 2: inflate to raw, count
 hipError_t launch_sst_decode(const SstArgs& a, hipStream_t s);     // tiers 0 and 1, after the scans
 hipError_t launch_sst_big_decode(const SstArgs& a, hipStream_t s); // tier 2
-// y[0..n) = exclusive prefix of x[0..n) (y may be x), total -> *total; part: ceil(n / 1024) scratch.
-hipError_t launch_scan_u64(const uint64_t* x, uint64_t* y, uint64_t n, uint64_t* part, uint64_t* total,
-                           hipStream_t s);
+// k <= 4 scans of n-element arrays at once: y[j] = exclusive prefix of x[j],
+// its total -> *total[j]; part: k * ceil(n / 1024) scratch.
+struct ScanSet {
+    const uint64_t* x[4];
+    uint64_t* y[4];
+    uint64_t* total[4];
+    uint64_t* part;
+    uint32_t k, pad;
+};
+hipError_t launch_scan_u64_n(const ScanSet& S, uint64_t n, hipStream_t s);
 
 // utf8 index of a block (murr_index.hip, murr_utf8_index).
 constexpr uint32_t kMaxUidxCols = 64;

@@ -1002,31 +1002,6 @@ DEV uint32_t copy_str(const Src& src, GAS uint8_t* vb, uint32_t pay, uint32_t n)
     return hib;
 }
 
-// Chained string words (MJ_CHAIN; the stage source, every string of the
-// wave's chunks <= 8 bytes).  A chunk's strings are contiguous in the output,
-// so lane i writes the 8 bytes ENDING at its string's end -- its own n bytes
-// after the last 8 - n bytes of row i - 1's string (lane i - 1 by DPP, or lane
-// 63 of the previous chunk) -- in one unaligned dwordx2 store; lane 0 of the
-// first chunk writes the 8 bytes starting at its string, followed by row 1's.
-// Bytes two lanes write are the same bytes, so the overlap is benign.  One
-// store per chunk instead of copy_str's head and tail stores (config B
-// ablation: string stores were 19 % of the kernel); a lane whose neighbour
-// cannot fill the word (null, or n + n_prev < 8) takes copy_str.
-#ifndef MJ_CHAIN
-#define MJ_CHAIN 1
-#endif
-DEV uint64_t bytes_mask(uint32_t n) { return n >= 8 ? ~0ull : (1ull << (8 * n)) - 1; }
-DEV uint32_t from_prev_lane(uint32_t v) {  // lane i: lane i - 1's v (lane 0: 0)
-    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138 /* wave_shr:1 */, 0xF, 0xF, false);
-}
-template <class Src> DEV uint64_t str_word(const Src& src, uint32_t pay, uint32_t n) {  // bytes [0, n) of a string
-    uint32_t w0, w1, w2;
-    src.win3(pay, w0, w1, w2);
-    const uint32_t sh = pay & 3u;
-    const uint64_t v = ((uint64_t)__builtin_amdgcn_alignbyte(w2, w1, sh) << 32) | __builtin_amdgcn_alignbyte(w1, w0, sh);
-    return v & bytes_mask(n);
-}
-
 template <class Src> DEV bool utf8_valid_slow(const Src& src, uint32_t a, uint32_t n) {
     Utf8Dfa dfa;
     for (uint32_t q = 0; q < n; q++) dfa.step(src.u8(a + q));
@@ -1470,19 +1445,6 @@ DEV void decode_tile(const Src& src, const Tile& T, const LAS uint32_t* ro, LAS 
                                    (unsigned long long)(tile_pre[U] + tot[U]), __ATOMIC_RELAXED,        \
                                    __HIP_MEMORY_SCOPE_AGENT); /* write-through: read by the epilogue */ \
             GAS int32_t* obf = gp(o.offsets) + T.r0 + 1;                                                \
-            uint64_t cw[R];                                                                             \
-            bool chain = false;                                                                         \
-            if constexpr (MJ_CHAIN && !Src::kHbm) {                                                     \
-                if (!(ERS && !late)) {                                                                  \
-                    uint32_t big = 0;                                                                   \
-                    _Pragma("unroll") for (uint32_t k = 0; k < R; k++) big |= ulen[U][k] > 8;           \
-                    chain = __ballot(big != 0) == 0;                                                    \
-                    if (chain)                                                                          \
-                        _Pragma("unroll") for (uint32_t k = 0; k < R; k++)                              \
-                            cw[k] = str_word(src, upay[U][k], ulen[U][k]);                              \
-                }                                                                                       \
-            }                                                                                           \
-            (void)cw;                                                                                   \
             _Pragma("unroll") for (uint32_t k = 0; k < R; k++) {                                        \
                 const uint32_t i = rbase + k * 64 + lane;                                               \
                 const bool act = i < T.nr;                                                              \
@@ -1498,33 +1460,6 @@ DEV void decode_tile(const Src& src, const Tile& T, const LAS uint32_t* ro, LAS 
                             copy_str_regs(gp(o.values) + (e - n), sw[U][k][0], sw[U][k][1], sw[U][k][2], \
                                           upay[U][k] & 3u, n);                                          \
                         hib = shib[U][k];                                                               \
-                    } else if (chain) {                                                                 \
-                        /* the previous string: lane i - 1, or lane 63 of chunk k - 1 */                \
-                        uint32_t plo = from_prev_lane((uint32_t)cw[k]);                                 \
-                        uint32_t phi = from_prev_lane((uint32_t)(cw[k] >> 32));                         \
-                        uint32_t pn = from_prev_lane(n);                                                \
-                        if (k > 0 && lane == 0) {                                                       \
-                            plo = __builtin_amdgcn_readlane((uint32_t)cw[k > 0 ? k - 1 : 0], 63);       \
-                            phi = __builtin_amdgcn_readlane((uint32_t)(cw[k > 0 ? k - 1 : 0] >> 32), 63); \
-                            pn = __builtin_amdgcn_readlane(ulen[U][k > 0 ? k - 1 : 0], 63);             \
-                        }                                                                               \
-                        const bool fwd = k == 0 && lane == 0; /* the next string: row 1 (lane 1) */      \
-                        if (fwd) {                                                                      \
-                            plo = __builtin_amdgcn_readlane((uint32_t)cw[0], 1);                        \
-                            phi = __builtin_amdgcn_readlane((uint32_t)(cw[0] >> 32), 1);                \
-                            pn = __builtin_amdgcn_readlane(ulen[U][0], 1);                              \
-                        }                                                                               \
-                        const uint64_t nb = ((uint64_t)phi << 32) | plo;                                \
-                        const bool ok = n >= 8 || n + pn >= 8;                                          \
-                        const uint32_t q = n < 8 ? n : 7u; /* (shift ranges when !ok or n == 8) */       \
-                        const uint64_t word = n >= 8 ? cw[k]                                            \
-                                              : fwd ? cw[k] | (nb << (8 * q))                           \
-                                                    : ((nb >> (8 * ((pn + q - 8) & 7u))) & bytes_mask(8 - q)) | \
-                                                          (cw[k] << (8 * (8 - q)));                     \
-                        const uint64_t at = fwd ? e - n : e - 8;                                        \
-                        if (!MJ_ABL_NOSTR && n && ok) ostu<uint64_t>(gp(o.values) + at, word);          \
-                        if (!MJ_ABL_NOSTR && n && !ok) (void)copy_str(src, gp(o.values) + (e - n), upay[U][k], n); \
-                        hib = (uint32_t)cw[k] | (uint32_t)(cw[k] >> 32);                                \
                     } else if (n && !MJ_ABL_NOSTR) {                                                    \
                         hib = copy_str(src, gp(o.values) + (e - n), upay[U][k], n);                     \
                     }                                                                                   \

@@ -605,7 +605,7 @@ __device__ __forceinline__ void count_block(const SstArgs& A, BlockLds<RAW>& L, 
         if (st == 1) st = wave_walk<G, false>(A, L, r0, ulen, lane, cnt, kbytes, vbytes, 0, 0, 0);
     }
     if (TIER == 0 && st == 1 && blk.compression != 0)
-        store_slot<G>(gp(A.slots) + b * kTier0Raw, L.raw, ulen, lane);
+        store_slot<G>(gp(A.slots) + b * kSstSlot, L.raw, ulen, lane);
     if (lane == 0) {
         if (st == 0) sst_report(A.err, b);
         uint32_t tier = TIER;
@@ -622,6 +622,252 @@ __device__ __forceinline__ void count_block(const SstArgs& A, BlockLds<RAW>& L, 
         gp(A.kb)[b] = st == 1 ? kbytes : 0;
         gp(A.vb)[b] = st == 1 ? vbytes : 0;
     }
+}
+
+// ---- thread-per-block tier-0 count (sst_count_t) ------------------------------
+// One thread per block, every block of the call in flight at once: the block
+// is inflated straight into its HBM slot and its entries are counted from
+// there.  The lane-group kernel (sst_count0) spends its time in the serial tag
+// chain -- a dependent LDS round trip and a group-wide copy per tag, four
+// groups diverging in one wave (PMC, round 5: ~9 k instructions per wave, 47 %
+// issue-active) -- with at most ~56 blocks per CU in flight; here the chain
+// is one thread's, 16-byte steps copy literals and matches (a match closer
+// than 16 bytes stores its repeating 16-byte pattern, overrunning its end by
+// < 16 bytes into the slot's pad, which the next tag overwrites), and the
+// memory latency of ~430 blocks per CU overlaps.  Same results and the same
+// malformed-block rules as count_block<G, 1024, 0>.
+typedef u32x4 __attribute__((aligned(1))) u32x4u;
+typedef unsigned __int128 u128;
+
+__device__ __forceinline__ u128 ld16u(const GAS uint8_t* p) {
+    const u32x4 v = *(const GAS u32x4u*)p;
+    return ((u128)v.w << 96) | ((u128)v.z << 64) | ((u128)v.y << 32) | (u128)v.x;
+}
+__device__ __forceinline__ void st16u(GAS uint8_t* p, u128 x) {
+    u32x4 v;
+    v.x = (uint32_t)x; v.y = (uint32_t)(x >> 32); v.z = (uint32_t)(x >> 64); v.w = (uint32_t)(x >> 96);
+    *(GAS u32x4u*)p = v;
+}
+// up to 8 bytes at p, never reading at or past end
+__device__ __forceinline__ uint64_t ld8b(const GAS uint8_t* p, const GAS uint8_t* end) {
+    if (end - p >= 8) return *(const GAS u64u*)p;
+    uint64_t v = 0;
+    for (uint32_t i = 0; p + i < end; i++) v |= (uint64_t)p[i] << (8 * i);
+    return v;
+}
+// len bytes from src to dst (disjoint, or src < dst with dst - src >= 16), in order
+__device__ __forceinline__ void tcopy(GAS uint8_t* dst, const GAS uint8_t* src, uint32_t len) {
+    if (len >= 16) {
+        uint32_t q = 0;
+        for (; q + 16 <= len; q += 16) st16u(dst + q, ld16u(src + q));
+        if (q < len) st16u(dst + len - 16, ld16u(src + len - 16));
+    } else if (len >= 8) {
+        const uint64_t a = *(const GAS u64u*)src, b = *(const GAS u64u*)(src + len - 8);
+        *(GAS u64u*)dst = a;
+        *(GAS u64u*)(dst + len - 8) = b;
+    } else if (len >= 4) {
+        const uint32_t a = *(const GAS u32u*)src, b = *(const GAS u32u*)(src + len - 4);
+        *(GAS u32u*)dst = a;
+        *(GAS u32u*)(dst + len - 4) = b;
+    } else {
+        for (uint32_t i = 0; i < len; i++) dst[i] = src[i];
+    }
+}
+// out[o, o + len) = out[o - off + (i % off)] (o >= off >= 1); may write up to
+// 15 bytes past o + len (slot pad)
+__device__ __forceinline__ void tmatch(GAS uint8_t* out, uint32_t o, uint32_t off, uint32_t len) {
+    if (off >= 16) {
+        tcopy(out + o, out + o - off, len);
+        return;
+    }
+    u128 w = ld16u(out + o - off) & (((u128)1 << (8 * off)) - 1);
+    for (uint32_t s = off; s < 16; s *= 2) w |= w << (8 * s);  // period off
+    const uint32_t step = (16 / off) * off;
+    for (uint32_t q = 0; q < len; q += step) st16u(out + o + q, w);
+}
+
+// Snappy body c[p, n) into out[0, ulen); false when malformed (the rules of
+// inflate_snappy / winflate_snappy).
+__device__ bool tinflate_snappy(const GAS uint8_t* c, uint32_t p, uint32_t n, GAS uint8_t* out, uint32_t ulen) {
+    uint32_t o = 0;
+    while (p < n) {
+        const uint64_t w = ld8b(c + p, c + n);
+        const uint32_t tag = (uint32_t)w & 0xFFu;
+        p++;
+        uint32_t len, off;
+        const uint32_t kind = tag & 3u;
+        if (kind == 0) {
+            len = tag >> 2;
+            if (len >= 60) {
+                const uint32_t nb = len - 59;
+                if (n - p < nb) return false;
+                len = (uint32_t)(w >> 8) & (nb == 4 ? 0xFFFFFFFFu : ((1u << (8 * nb)) - 1));
+                p += nb;
+            }
+            len += 1;
+            if (n - p < len || o + len > ulen) return false;
+            tcopy(out + o, c + p, len);
+            p += len;
+            o += len;
+            continue;
+        }
+        if (kind == 1) {
+            if (p >= n) return false;
+            len = 4 + ((tag >> 2) & 7u);
+            off = ((tag >> 5) << 8) | ((uint32_t)(w >> 8) & 0xFFu);
+            p += 1;
+        } else if (kind == 2) {
+            if (n - p < 2) return false;
+            len = 1 + (tag >> 2);
+            off = (uint32_t)(w >> 8) & 0xFFFFu;
+            p += 2;
+        } else {
+            if (n - p < 4) return false;
+            len = 1 + (tag >> 2);
+            off = (uint32_t)(w >> 8);
+            p += 4;
+        }
+        if (off == 0 || off > o || o + len > ulen) return false;
+        tmatch(out, o, off, len);
+        o += len;
+    }
+    return o == ulen;
+}
+
+__device__ __forceinline__ bool tlz4_ext(const GAS uint8_t* c, uint32_t& p, uint32_t n, uint32_t& v) {
+    uint32_t b;
+    do {
+        if (p >= n) return false;
+        b = c[p++];
+        v += b;
+    } while (b == 255);
+    return true;
+}
+// LZ4 block c[p, n) into out[0, ulen) (the rules of inflate_lz4).
+__device__ bool tinflate_lz4(const GAS uint8_t* c, uint32_t p, uint32_t n, GAS uint8_t* out, uint32_t ulen) {
+    uint32_t o = 0;
+    for (;;) {
+        if (p >= n) return false;
+        const uint32_t tok = c[p++];
+        uint32_t lit = tok >> 4;
+        if (lit == 15 && !tlz4_ext(c, p, n, lit)) return false;
+        if (n - p < lit || o + lit > ulen) return false;
+        tcopy(out + o, c + p, lit);
+        p += lit;
+        o += lit;
+        if (p == n) break;
+        if (n - p < 2) return false;
+        const uint32_t off = (uint32_t)c[p] | ((uint32_t)c[p + 1] << 8);
+        p += 2;
+        uint32_t ml = tok & 15u;
+        if (ml == 15 && !tlz4_ext(c, p, n, ml)) return false;
+        ml += 4;
+        if (off == 0 || off > o || o + ml > ulen) return false;
+        tmatch(out, o, off, ml);
+        o += ml;
+    }
+    return o == ulen;
+}
+
+// Count the entries of the uncompressed block blk[0, n) (readable to
+// blk + lim): 1 ok, 0 malformed, 3 an internal key past kKeyCap (wave_walk's rules).
+__device__ int twalk(const GAS uint8_t* blk, uint32_t n, const GAS uint8_t* lim, uint64_t& cnt, uint64_t& kbytes,
+                     uint64_t& vbytes) {
+    cnt = kbytes = vbytes = 0;
+    if (n < 4) return 0;
+    const uint32_t footer = *(const GAS u32u*)(blk + n - 4);
+    const uint32_t nr = footer & 0x7FFFFFFFu;
+    uint64_t tail = 4;
+    if (footer >> 31) {
+        if (n < 6) return 0;
+        tail += 2 + (uint32_t)*(const GAS u16u*)(blk + n - 6);
+    }
+    tail += 4ull * nr;
+    if (nr == 0 || tail > n) return 0;
+    const uint32_t end = n - (uint32_t)tail;
+    uint32_t p = 0, pilen = 0;
+    while (p < end) {
+        const uint64_t w0 = ld8b(blk + p, lim), w1 = ld8b(blk + p + 8, lim);
+        uint32_t v[3], i = 0;
+        for (uint32_t k = 0; k < 3; k++) {
+            uint32_t r = 0;
+            bool done = false;
+            for (uint32_t j = 0; j < 5 && !done; j++) {
+                if (p + i >= end) return 0;
+                const uint32_t byte = (uint32_t)(i < 8 ? w0 >> (8 * i) : w1 >> (8 * (i - 8))) & 0xFFu;
+                r |= (byte & 0x7Fu) << (7 * j);
+                done = !(byte & 0x80u);
+                i++;
+            }
+            if (!done) return 0;
+            v[k] = r;
+        }
+        p += i;
+        const uint32_t shared = v[0], nonshared = v[1], vlen = v[2];
+        const uint64_t ilen = (uint64_t)shared + nonshared;
+        if (shared > pilen || ilen < 8 || (uint64_t)(end - p) < (uint64_t)nonshared + vlen) return 0;
+        if (ilen > kKeyCap) return 3;
+        p += nonshared + vlen;
+        pilen = (uint32_t)ilen;
+        kbytes += ilen - 8;
+        vbytes += vlen;
+        cnt++;
+    }
+    return 1;
+}
+
+__global__ void __launch_bounds__(256) sst_count_t(SstArgs A) {
+    const uint64_t b = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (b >= A.nblocks) return;
+    const SstBlock blk = ldblock(A.blocks + b);
+    const GAS uint8_t* c = gp(blk.data);
+    GAS uint8_t* slot = gp(A.slots) + b * kSstSlot;
+    uint64_t cnt = 0, kbytes = 0, vbytes = 0, big_len = 0;
+    uint32_t ulen = 0;
+    int st = 0;  // unknown compression types are malformed
+    if (A.probe & 4) {  // (tuning) pull the stored block's lines into the L2 first
+        uint32_t acc = 0;
+        for (uint64_t q = 0; q < blk.size; q += 64) acc ^= c[q];
+        if (acc == 0x100) sst_report(A.err, b);  // never: keeps the loads
+    }
+    if (blk.compression == 0) {
+        big_len = blk.size;
+        if (blk.size > kTier0Raw) {
+            st = 2;
+        } else {
+            ulen = (uint32_t)blk.size;
+            st = twalk(c, ulen, c + ulen, cnt, kbytes, vbytes);
+        }
+    } else if (blk.compression == 1 || blk.compression == 4 || blk.compression == 5) {
+        const uint8_t* q = blk.data;
+        uint32_t v = 0;
+        if (blk.size && varint32(q, blk.data + blk.size, v) && expansion_ok(v, blk.size)) {
+            big_len = v;
+            if (blk.size > BlockLds<kTier0Raw>::kComp || v > kTier0Raw) {
+                st = 2;
+            } else {
+                ulen = v;
+                const uint32_t n = (uint32_t)blk.size, hl = (uint32_t)(q - blk.data);
+                const bool ok = (A.probe & 2) ? true
+                                : blk.compression == 1 ? tinflate_snappy(c, hl, n, slot, ulen)
+                                                       : tinflate_lz4(c, hl, n, slot, ulen);
+                st = !ok ? 0 : (A.probe & 3) ? 1 : twalk(slot, ulen, slot + kSstSlot, cnt, kbytes, vbytes);
+                if (A.probe & 3) ulen = 0;  // (tuning: an empty block, nothing for the decode)
+            }
+        }
+    }
+    if (st == 0) sst_report(A.err, b);
+    uint32_t tier = 0;
+    if (st == 3) tier = 2;
+    if (st == 2) tier = (big_len <= kTier1Raw && blk.size <= BlockLds<kTier1Raw>::kComp) ? 1 : 2;
+    if (tier == 1)
+        gp(A.list)[__hip_atomic_fetch_add(gp(A.nlist), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)] = (uint32_t)b;
+    gp(A.tier)[b] = tier;
+    gp(A.rlen)[b] = st == 1 ? ulen : 0;
+    gp(A.ulen)[b] = tier == 2 ? (big_len ? big_len : 1) : 0;
+    gp(A.ne)[b] = st == 1 ? cnt : 0;
+    gp(A.kb)[b] = st == 1 ? kbytes : 0;
+    gp(A.vb)[b] = st == 1 ? vbytes : 0;
 }
 
 template <uint32_t G>
@@ -651,7 +897,7 @@ __device__ __forceinline__ void decode_block(const SstArgs& A, Lds& L, uint64_t 
     int st = 1;
     if (FROM_SLOT) {  // tier 0: the stored block if plain, else its slot (inflated by sst_count)
         ulen = gp(A.rlen)[b];
-        r0 = stage<G>(L.raw, blk.compression == 0 ? blk.data : A.slots + b * kTier0Raw, ulen, lane);
+        r0 = stage<G>(L.raw, blk.compression == 0 ? blk.data : A.slots + b * kSstSlot, ulen, lane);
         wave_sync();
     } else {
         st = wave_inflate<G>(blk, L, r0, ulen, big_len, lane);
@@ -680,8 +926,8 @@ __global__ void __launch_bounds__(kThreads) sst_decode1(SstArgs A) {
     }
 }
 
-// Exclusive scan of u64 x[0..n) into y, total at *total: chunk scans of 1024
-// (sums into part[]), one workgroup over the chunk sums, then the add-back.
+// Exclusive scans of u64 arrays (ScanSet): chunk scans of 1024 (sums into
+// part[]), one workgroup per array over its chunk sums, then the add-back.
 __device__ uint64_t block_scan1024(uint64_t v, uint64_t* s_w, uint64_t* total) {
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     uint64_t inc = v;
@@ -700,17 +946,22 @@ __device__ uint64_t block_scan1024(uint64_t v, uint64_t* s_w, uint64_t* total) {
     *total = all;
     return before + inc - v;
 }
-__global__ void __launch_bounds__(1024) scan_chunks(const uint64_t* x, uint64_t* y, uint64_t n, uint64_t* part) {
+// The same over up to four arrays at once (blockIdx.y picks the array): three
+// launches for the count pass's four scans instead of twelve.
+__global__ void __launch_bounds__(1024) scan_chunks_n(ScanSet S, uint64_t n, uint64_t nparts) {
     __shared__ uint64_t s_w[16];
+    const uint32_t k = blockIdx.y;
     const uint64_t i = (uint64_t)blockIdx.x * 1024 + threadIdx.x;
-    const uint64_t v = i < n ? gp(x)[i] : 0;
+    const uint64_t v = i < n ? gp(S.x[k])[i] : 0;
     uint64_t tot;
     const uint64_t ex = block_scan1024(v, s_w, &tot);
-    if (i < n) gp(y)[i] = ex;
-    if (threadIdx.x == 0) gp(part)[blockIdx.x] = tot;
+    if (i < n) gp(S.y[k])[i] = ex;
+    if (threadIdx.x == 0) gp(S.part)[k * nparts + blockIdx.x] = tot;
 }
-__global__ void __launch_bounds__(1024) scan_parts(uint64_t* part, uint64_t nparts, uint64_t* total) {
+__global__ void __launch_bounds__(1024) scan_parts_n(ScanSet S, uint64_t nparts) {
     __shared__ uint64_t s_w[16];
+    const uint32_t k = blockIdx.x;
+    uint64_t* part = S.part + k * nparts;
     uint64_t carry = 0;
     for (uint64_t base = 0; base < nparts; base += 1024) {
         const uint64_t j = base + threadIdx.x;
@@ -720,23 +971,25 @@ __global__ void __launch_bounds__(1024) scan_parts(uint64_t* part, uint64_t npar
         if (j < nparts) gp(part)[j] = carry + ex;
         carry += tot;
     }
-    if (threadIdx.x == 0) gp(total)[0] = carry;
+    if (threadIdx.x == 0) gp(S.total[k])[0] = carry;
 }
-__global__ void __launch_bounds__(1024) scan_add(uint64_t* y, uint64_t n, const uint64_t* part) {
+__global__ void __launch_bounds__(1024) scan_add_n(ScanSet S, uint64_t n, uint64_t nparts) {
+    const uint32_t k = blockIdx.y;
     const uint64_t i = (uint64_t)blockIdx.x * 1024 + threadIdx.x;
-    if (i < n) gp(y)[i] += gp(part)[blockIdx.x];
+    if (i < n) gp(S.y[k])[i] += gp(S.part)[k * nparts + blockIdx.x];
 }
 
 }  // namespace
 
-// Lanes per tier-0 block: kCountLanes for sst_count, kDecodeLanes for
-// sst_decode (tuning builds: MURR_SST_LANES / MURR_SST_DLANES, 4 to 64).
-constexpr uint32_t kCountLanes = 16, kDecodeLanes = 8;
+// Tier-0 count: the thread-per-block kernel (sst_count_t); tuning builds can
+// pick the lane-group one (MURR_SST_LANES 4 to 64).  Lanes per tier-0 block of
+// sst_decode: kDecodeLanes (MURR_SST_DLANES).
+constexpr uint32_t kDecodeLanes = 8;
 uint32_t lanes_env(const char* name, uint32_t dflt) {
 #ifdef MURR_TUNING
     const char* e = std::getenv(name);
     const uint32_t v = e ? (uint32_t)std::atoi(e) : dflt;
-    return (v == 4 || v == 8 || v == 16 || v == 32 || v == 64) ? v : dflt;
+    return (v == 1 || v == 4 || v == 8 || v == 16 || v == 32 || v == 64) ? v : dflt;
 #else
     (void)name;
     return dflt;
@@ -749,11 +1002,21 @@ hipError_t launch_tier0(bool decode, const SstArgs& a, hipStream_t s) {
     else hipLaunchKernelGGL(sst_count0<G>, grid, dim3(kThreads), 0, s, a);
     return hipGetLastError();
 }
-hipError_t launch_tiers(bool decode, const SstArgs& a, hipStream_t s) {
-    static const uint32_t gc = lanes_env("MURR_SST_LANES", kCountLanes);
+hipError_t launch_tiers(bool decode, const SstArgs& a_in, hipStream_t s) {
+    SstArgs a = a_in;
+#ifdef MURR_TUNING
+    // phase ablations of sst_count_t (compressed blocks then read as empty):
+    // 1 no walk, 2 no inflate and no walk, 4 prefetch the stored block
+    static const uint32_t probe = std::getenv("MURR_SST_PROBE") ? (uint32_t)std::atoi(std::getenv("MURR_SST_PROBE")) : 0;
+    a.probe = probe;
+#endif
+    static const uint32_t gc = lanes_env("MURR_SST_LANES", 1);  // 1: the thread-per-block count
     static const uint32_t gd = lanes_env("MURR_SST_DLANES", kDecodeLanes);
     hipError_t e;
-    switch (decode ? gd : gc) {
+    if (!decode && gc == 1) {
+        hipLaunchKernelGGL(sst_count_t, dim3((uint32_t)((a.nblocks + 255) / 256)), dim3(256), 0, s, a);
+        e = hipGetLastError();
+    } else switch (decode ? gd : gc) {
     case 4: e = launch_tier0<4>(decode, a, s); break;
     case 8: e = launch_tier0<8>(decode, a, s); break;
     case 32: e = launch_tier0<32>(decode, a, s); break;
@@ -776,12 +1039,11 @@ hipError_t launch_sst_big_decode(const SstArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(sst_big_decode, dim3((uint32_t)((a.nblocks + 255) / 256)), dim3(256), 0, s, a);
     return hipGetLastError();
 }
-hipError_t launch_scan_u64(const uint64_t* x, uint64_t* y, uint64_t n, uint64_t* part, uint64_t* total,
-                           hipStream_t s) {
+hipError_t launch_scan_u64_n(const ScanSet& S, uint64_t n, hipStream_t s) {
     const uint64_t nparts = (n + 1023) / 1024;
-    if (nparts) hipLaunchKernelGGL(scan_chunks, dim3((uint32_t)nparts), dim3(1024), 0, s, x, y, n, part);
-    hipLaunchKernelGGL(scan_parts, dim3(1), dim3(1024), 0, s, part, nparts, total);
-    if (nparts) hipLaunchKernelGGL(scan_add, dim3((uint32_t)nparts), dim3(1024), 0, s, y, n, (const uint64_t*)part);
+    if (nparts) hipLaunchKernelGGL(scan_chunks_n, dim3((uint32_t)nparts, S.k), dim3(1024), 0, s, S, n, nparts);
+    hipLaunchKernelGGL(scan_parts_n, dim3(S.k), dim3(1024), 0, s, S, nparts);
+    if (nparts) hipLaunchKernelGGL(scan_add_n, dim3((uint32_t)nparts, S.k), dim3(1024), 0, s, S, n, nparts);
     return hipGetLastError();
 }
 
