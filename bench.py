@@ -462,17 +462,21 @@ def run_decode(args, dist, rank, world, local_rank):
     host_blob = blocks[0].data.download(blocks[0].data_bytes)
     host_off = blocks[0].host_offsets()
     ix_bytes = 8 * int(L_len(ctx, seg, rows, ix_stride)) if blocks[0].uidx is not None else 0
-    # Two output sets: step s decodes into set s % 2 and is launched
+    # Output sets: step s decodes into set s % n_sets and is launched
     # (murr_decode_run_async) before step s - 1 is waited for, so the host's
     # launch and read-back work overlaps the previous step's kernel, as a
-    # serving loop would; on the GPU the steps run one after the other (one
-    # stream).  --sync-steps: one set, each step waited for (the A/B).
-    # --lanes 2: the second output set's plan on a second context (its own
-    # stream), so step s + 1's workgroups can start on CUs step s has left
-    # (config D's default: a resident shard's scan ends with a long tail)
-    if args.lanes is None:
-        args.lanes = 2 if args.config == "D" else 1
-    ctxs = [ctx, Context(local_rank) if args.lanes == 2 else ctx]
+    # serving loop would.  One lane: two sets on one context (one stream; on
+    # the GPU the steps run one after the other).  --lanes L > 1: one set per
+    # lane, each lane a context of its own (its own stream), L - 1 steps
+    # launched ahead, so step s + 1's workgroups can start on CUs step s has
+    # left (config D's default, three lanes: a resident shard's scan ends with
+    # a long tail).  --sync-steps: one set, each step waited for (the A/B).
+    if args.lanes is None:  # (config D: 0.0568 -> 0.0510 ms per step from two to three lanes, four no faster)
+        args.lanes = 3 if args.config == "D" else 1
+    # one output set per lane (two on one context with one lane); step s uses
+    # set s % len(ctxs), and len(ctxs) - 1 steps are launched ahead of the
+    # one waited for
+    ctxs = [ctx] + [Context(local_rank) for _ in range(args.lanes - 1)] if args.lanes > 1 else [ctx, ctx]
     if args.arena:
         out_sets = [ArenaOutputs(c, seg, proj, blocks, args.arena) for c in ctxs]
     else:
@@ -496,10 +500,10 @@ def run_decode(args, dist, rank, world, local_rank):
     # and brackets all K launches with two marks on the context's stream:
     # kernel_ms_avg = that GPU time / K, which includes the gaps between the
     # launches, so it never exceeds ms_per_step (the host's clock around the
-    # same K steps).  With two lanes (two streams) the region runs from the
-    # first lane's start mark to the later of the two lanes' end marks: the
+    # same K steps).  With several lanes (streams) the region runs from the
+    # first lane's start mark to the latest of the lanes' end marks: the
     # launches overlap, so this is the GPU time per launch at steady state.
-    runs = [0, 0]  # runs of each output set's plan so far
+    runs = [0] * len(ctxs)  # runs of each output set's plan so far
     every = _abi.PLAN_TIME_EVERY
     if "MURR_TIME_EVERY" in os.environ and _abi.LIB_PATH.endswith("_tuning.so"):
         every = max(1, int(os.environ["MURR_TIME_EVERY"]))
@@ -523,12 +527,13 @@ def run_decode(args, dist, rank, world, local_rank):
                 go(0).wait()
                 done(0)
             return ms
-        h = go(0) if n else None
+        nset = len(ctxs)
+        inflight = [go(s % nset) for s in range(min(n, nset - 1))]
         for s in range(n):
-            hn = go((s + 1) % 2) if s + 1 < n else None
-            h.wait()
-            done(s % 2)
-            h = hn
+            if s + nset - 1 < n:
+                inflight.append(go((s + nset - 1) % nset))
+            inflight.pop(0).wait()
+            done(s % nset)
         return ms
 
     wms = run_steps(args.warmup)
@@ -550,7 +555,7 @@ def run_decode(args, dist, rank, world, local_rank):
     region_ms = max(ctx.mark_ms(0, 1, c) for c in lanes) if args.steps else None
     for p in launched.values():
         p.time_every(every)
-    last = 0 if args.sync_steps else (args.steps - 1) % 2
+    last = 0 if args.sync_steps else (args.steps - 1) % len(ctxs)
     outs = out_sets[last]  # the last timed step's output (checked below)
     elapsed = max_over_ranks(dist, elapsed)
     stats = ctx.stats()
@@ -1164,7 +1169,7 @@ def main():
                     help="skip the oracle check of the timed output (tuning ablations that skip stores only)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--pmc-csv", default=None)
-    ap.add_argument("--lanes", type=int, default=None, choices=[1, 2],
+    ap.add_argument("--lanes", type=int, default=None, choices=[1, 2, 3, 4],
                     help="decode: 2 = the alternating output sets' plans on two contexts (two streams), "
                          "so a launch starts on the CUs the previous one's tail leaves; default 2 for "
                          "--config D, else 1")

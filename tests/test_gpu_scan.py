@@ -169,32 +169,36 @@ def test_scan_plan_eviction_with_runs_in_flight(ctx):
         hs[0].wait()  # its one result was handed over already
 
 
-def test_scan_device_two_lanes_overlap(ctx):
-    # bench.py --config D's default loop (--lanes 2): the alternating output
-    # sets' scans launched on two contexts of one device (two streams), the
-    # next before the previous is waited for, so they overlap on the GPU.
-    # Every scan of both lanes reads the same arena; both output sets hold
-    # the oracle's arrays after the last scan of each
+@pytest.mark.parametrize("nlanes", [2, 3])
+def test_scan_device_lanes_overlap(ctx, nlanes):
+    # bench.py --config D's default loop (--lanes 3): one output set per
+    # lane, each on its own context of one device (its own stream), nlanes - 1
+    # scans launched ahead of the one waited for, so they overlap on the GPU.
+    # Every scan of every lane reads the same arena; each output set holds
+    # the oracle's arrays after its last scan
     n = 300_000
     rt = ResidentTable(schema_c(), ctx)
     rt.write(batch_c(n, seed=11))
     names = [f"c{i}" for i in range(len(C_DTYPES))]
-    lane2 = Context(ctx.device)
+    extra = [Context(ctx.device) for _ in range(nlanes - 1)]
     try:
-        lanes = [ctx, lane2]
+        lanes = [ctx] + extra
         sets = [DecodeOutputs(c, rt.segment, list(range(len(C_DTYPES))), [rt.block()]) for c in lanes]
-        h = rt.scan_device_async(names, sets[0], ctx=lanes[0])
-        for s in range(6):
-            hn = rt.scan_device_async(names, sets[(s + 1) % 2], ctx=lanes[(s + 1) % 2]) if s < 5 else None
-            assert h.wait() is sets[s % 2]
-            h = hn
+        steps = 3 * nlanes
+        inflight = [rt.scan_device_async(names, sets[s], ctx=lanes[s]) for s in range(nlanes - 1)]
+        for s in range(steps):
+            if s + nlanes - 1 < steps:
+                k = (s + nlanes - 1) % nlanes
+                inflight.append(rt.scan_device_async(names, sets[k], ctx=lanes[k]))
+            assert inflight.pop(0).wait() is sets[s % nlanes]
         data, off = arena(rt)
         want = O.decode_block(O.Segment([int(d) for d in C_DTYPES]), list(range(len(C_DTYPES))), data, off)
         for k, outs in enumerate(sets):
             for p, d in enumerate(C_DTYPES):
                 assert_array_equal(download_array(ctx, outs.array(0, p), int(d), n), want[p], f"lane {k} col {p}")
     finally:
-        for _, plan in rt._scan_plans.values():  # (plans on lane2 close before it does)
+        for _, plan in rt._scan_plans.values():  # (plans on the extra lanes close before they do)
             plan.close()
         rt._scan_plans.clear()
-        lane2.close()
+        for c in extra:
+            c.close()
