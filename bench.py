@@ -1027,7 +1027,7 @@ def run_sst(args):
     buf, handles = sst.upload_blocks(ctx, stored)
     in_bytes = sum(len(d) for d, _ in stored)
     t0 = time.perf_counter()
-    table = sst.block_table(buf, handles)  # once per file: murr_sst_block_t[]
+    table = sst.device_table(ctx, buf, handles)  # once per file: murr_sst_block_t[] in HBM
     table_ms = (time.perf_counter() - t0) * 1e3
     for _ in range(args.warmup):
         e = sst.decode(ctx, buf, table)

@@ -635,7 +635,12 @@ void murr_reader_free(murr_reader_t* r);
  * first such block in err->row.  Outputs are allocated by the library (device
  * memory) and freed with murr_sst_result_free, or one by one with
  * murr_dev_free (to keep, e.g., values and value_offsets as a table's
- * arena).  Synchronous. */
+ * arena).  `blocks` is a host array, or a device array (device memory from
+ * murr_dev_alloc / hipMalloc: the descriptor table of a file decoded more
+ * than once, uploaded once -- a 100 k-block host table costs ~0.1 ms of
+ * pageable copy per call); a device table is not read by the host, so a
+ * block with size > 0 and no data is MURR_E_MALFORMED_ROW there rather than
+ * MURR_E_ARGUMENT.  Synchronous. */
 typedef struct {
     const uint8_t* data;   /* device */
     uint64_t size;

@@ -3148,9 +3148,16 @@ int murr_sst_decode(murr_ctx_t* c, const murr_sst_block_t* blocks, uint32_t nblo
     if (err) std::memset(err, 0, sizeof *err);
     if (!c || !out || (nblocks && !blocks) || c->pending) return set_err(err, MURR_E_ARGUMENT);
     std::memset(out, 0, sizeof *out);
-    for (uint32_t b = 0; b < nblocks; b++)
-        if (blocks[b].size && !blocks[b].data) return set_err(err, MURR_E_ARGUMENT);
     HIPC(hipSetDevice(c->device));
+    bool dev_table = false;  // the descriptors in device memory (used in place)
+    if (nblocks) {
+        hipPointerAttribute_t at{};
+        if (hipPointerGetAttributes(&at, blocks) == hipSuccess) dev_table = at.type == hipMemoryTypeDevice;
+        else (void)hipGetLastError();
+    }
+    if (!dev_table)
+        for (uint32_t b = 0; b < nblocks; b++)
+            if (blocks[b].size && !blocks[b].data) return set_err(err, MURR_E_ARGUMENT);
     const uint64_t nb = nblocks, nparts = (nb + 1023) / 1024;
     // scratch: err | totals[5] | nlist | descriptors | tier rlen list | ulen uoff ne kb vb eoff koff voff | parts
     const uint64_t o_tot = 8, o_nlist = 56, o_desc = 64, o_tier = round_up(o_desc + sizeof(SstBlock) * nb, 16);
@@ -3180,9 +3187,10 @@ int murr_sst_decode(murr_ctx_t* c, const murr_sst_block_t* blocks, uint32_t nblo
     } while (0)
     static_assert(sizeof(SstBlock) == sizeof(murr_sst_block_t), "murr_sst_block_t is the device descriptor");
     SSTC(hipMemsetAsync(w, 0, 64, c->stream));
-    if (nb) SSTC(hipMemcpyAsync(w + o_desc, blocks, sizeof(SstBlock) * nb, hipMemcpyHostToDevice, c->stream));
+    if (nb && !dev_table)
+        SSTC(hipMemcpyAsync(w + o_desc, blocks, sizeof(SstBlock) * nb, hipMemcpyHostToDevice, c->stream));
     SstArgs a{};
-    a.blocks = (const SstBlock*)(w + o_desc);
+    a.blocks = dev_table ? (const SstBlock*)blocks : (const SstBlock*)(w + o_desc);
     a.nblocks = nb;
     a.tier = (uint32_t*)(w + o_tier);
     a.rlen = a.tier + nb;

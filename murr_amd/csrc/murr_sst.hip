@@ -599,8 +599,9 @@ __device__ __forceinline__ void count_block(const SstArgs& A, BlockLds<RAW>& L, 
     const SstBlock blk = ldblock(A.blocks + b);
     uint64_t cnt = 0, kbytes = 0, vbytes = 0, big_len = 0;
     uint32_t ulen = 0, r0 = 0;
-    int st = 0;  // unknown compression types are malformed
-    if (blk.compression == 0 || blk.compression == 1 || blk.compression == 4 || blk.compression == 5) {
+    int st = 0;  // unknown compression types, and (device tables) no data, are malformed
+    if ((blk.size == 0 || blk.data) &&
+        (blk.compression == 0 || blk.compression == 1 || blk.compression == 4 || blk.compression == 5)) {
         st = wave_inflate<G>(blk, L, r0, ulen, big_len, lane);
         if (st == 1) st = wave_walk<G, false>(A, L, r0, ulen, lane, cnt, kbytes, vbytes, 0, 0, 0);
     }
@@ -819,12 +820,13 @@ __device__ int twalk(const GAS uint8_t* blk, uint32_t n, const GAS uint8_t* lim,
 __global__ void __launch_bounds__(256) sst_count_t(SstArgs A) {
     const uint64_t b = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (b >= A.nblocks) return;
-    const SstBlock blk = ldblock(A.blocks + b);
+    SstBlock blk = ldblock(A.blocks + b);
     const GAS uint8_t* c = gp(blk.data);
     GAS uint8_t* slot = gp(A.slots) + b * kSstSlot;
     uint64_t cnt = 0, kbytes = 0, vbytes = 0, big_len = 0;
     uint32_t ulen = 0;
-    int st = 0;  // unknown compression types are malformed
+    int st = 0;  // unknown compression types, and (device tables) no data, are malformed
+    if (blk.size && !blk.data) blk.compression = ~0u;
     if (A.probe & 4) {  // (tuning) pull the stored block's lines into the L2 first
         uint32_t acc = 0;
         for (uint64_t q = 0; q < blk.size; q += 64) acc ^= c[q];

@@ -89,16 +89,34 @@ def block_table(buf: DeviceBuffer, handles) -> np.ndarray:
     return desc[:nb]
 
 
+@dataclass
+class SstTable:
+    """A block table in device memory (device_table): murr_sst_decode reads
+    it in place, so a file decoded more than once uploads its descriptors
+    once."""
+    table: DeviceBuffer
+    n: int
+
+
+def device_table(ctx: Context, buf: DeviceBuffer, handles) -> SstTable:
+    """block_table() uploaded once to the device."""
+    desc = block_table(buf, handles)
+    return SstTable(ctx.upload(desc.view(np.uint8) if len(desc) else np.zeros(16, np.uint8)), len(desc))
+
+
 def decode(ctx: Context, buf: DeviceBuffer, handles) -> SstEntries:
     """murr_sst_decode over blocks at buf + offset (handles: [(offset, size,
     compression)], or the block_table() made from them once for a file that is
-    decoded again).  A block that does not parse raises SegmentError
-    (MURR_E_MALFORMED_ROW) naming the first such block."""
-    desc = handles if isinstance(handles, np.ndarray) and handles.dtype == _SST_BLOCK else block_table(buf, handles)
+    decoded again, or its device_table()).  A block that does not parse
+    raises SegmentError (MURR_E_MALFORMED_ROW) naming the first such block."""
+    if isinstance(handles, SstTable):
+        ptr, n = C.cast(C.c_void_p(handles.table.ptr), C.POINTER(_abi.SstBlock)), handles.n
+    else:
+        desc = handles if isinstance(handles, np.ndarray) and handles.dtype == _SST_BLOCK else block_table(buf, handles)
+        ptr, n = desc.ctypes.data_as(C.POINTER(_abi.SstBlock)), len(desc)
     res = _abi.SstResult()
     err = _abi.Error()
-    st = ctx.L.murr_sst_decode(ctx.h, desc.ctypes.data_as(C.POINTER(_abi.SstBlock)), len(desc),
-                               C.byref(res), C.byref(err))
+    st = ctx.L.murr_sst_decode(ctx.h, ptr, n, C.byref(res), C.byref(err))
     raise_status(st, err, "murr_sst_decode")
     n = res.n
     # each output is its own allocation: ownership moves to DeviceBuffers (murr_dev_free)

@@ -227,3 +227,48 @@ def test_rehydrate_duplicate_keys_take_the_highest_seq(layout):
     q = [f"key{i}" for i in rng.integers(2400, 3600, size=1500)] + ["key2500", "key2999", "key0"]
     cols = [f"c{i}" for i in range(16)]
     assert_same(t.read(q, cols), expected([old, new], q, cols))
+
+
+@pytest.mark.parametrize("comp", [G.SNAPPY, G.LZ4])
+def test_short_offset_matches_and_slot_edge(comp):
+    # values repeating with periods 1..17 (matches closer than 16 bytes: the
+    # thread-per-block inflate stores their 16-byte pattern and overruns the
+    # match end into the slot's pad), blocks grown up to the 1 KiB tier-0 edge
+    rng = np.random.default_rng(70 + comp)
+    stored = []
+    for period in range(1, 18):
+        for target in (200, 700, 1000, 1024, 1100):
+            pat = bytes(rng.integers(0, 256, size=period, dtype=np.uint8))
+            entries, size = [], 0
+            i = 0
+            while size < target - 80:
+                v = (pat * (1 + 90 // period))[: 20 + int(rng.integers(0, 70))]
+                entries.append((b"k%06d" % i, 1000 + i, G.TYPE_VALUE, v))
+                size += len(v) + 20
+                i += 1
+            stored.append((G.compress(G.build_block(entries), comp), comp))
+    check(stored)
+
+
+def test_device_block_table_in_place():
+    # the descriptors uploaded once (sst.device_table) decode exactly as the
+    # host table; a device table's block without data is malformed (named),
+    # the host table's an argument error
+    rng = np.random.default_rng(81)
+    blocks = G.blocks_of(G.random_entries(rng, 900, max_val=120), restart_interval=8)
+    stored = [(G.compress(b, c), c) for b, c in zip(blocks, [G.SNAPPY, G.NONE, G.LZ4] * len(blocks))]
+    ctx = default_context()
+    buf, handles = sst.upload_blocks(ctx, stored)
+    want = sst.decode(ctx, buf, handles).to_host()
+    tab = sst.device_table(ctx, buf, handles)
+    for _ in range(2):
+        got = sst.decode(ctx, buf, tab).to_host()
+        assert got[0] == want[0] and got[1] == want[1]
+        assert got[2].tolist() == want[2].tolist() and got[3].tolist() == want[3].tolist()
+    desc = sst.block_table(buf, handles)
+    desc["data"][5] = 0
+    with pytest.raises(Exception):
+        sst.decode(ctx, buf, desc)
+    bad = sst.SstTable(ctx.upload(desc.view(np.uint8)), len(desc))
+    with pytest.raises(SegmentError, match=r"row 5,"):
+        sst.decode(ctx, buf, bad)

@@ -49,6 +49,7 @@ if [ "$PART" != 1 ]; then
   run decode_D1x2 300 "$PY" bench.py --config D --rows 2500000 --steps 10 --warmup 2 --no-cpu
   run decode_D1x4 300 "$PY" bench.py --config D --rows 5000000 --steps 10 --warmup 2 --no-cpu
   run encode_prof 300 bash tools/enc_prof.sh
+  run sst 300 "$PY" bench.py --mode sst --steps 10 --warmup 3
   # configs[3] as written at N = 1 (the whole 10 M-row table on one rank)
   run decode_D_table10M 400 "$PY" bench.py --config D --table-rows 10000000 --steps 10 --warmup 2 --no-cpu
   # per-workgroup timeline of the D shard (tuning build)
