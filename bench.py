@@ -536,6 +536,12 @@ def run_decode(args, dist, rank, world, local_rank):
             done(s % nset)
         return ms
 
+    if rt is not None:
+        # setup: a resident table prepares each lane's scan plan at its first
+        # scan; make those before the warm-up, so a warm-up shorter than the
+        # lane count cannot leave one to the timed region
+        for i in range(len(ctxs)):
+            launch(i).wait()
     wms = run_steps(args.warmup)
     for p in launched.values():
         p.time_every(0)
