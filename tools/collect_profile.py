@@ -9,7 +9,8 @@ import shutil
 import sys
 
 R = sys.argv[1] if len(sys.argv) > 1 else "r02"
-src, dst = f"gpurun_out/{R}", f"profiles/{R}"
+src = f"gpurun_out/{R}"
+dst = f"profiles/{sys.argv[2]}" if len(sys.argv) > 2 else f"profiles/{R}"  # (e.g. r05f -> r05)
 os.makedirs(dst, exist_ok=True)
 
 
@@ -29,7 +30,7 @@ names = {"bench": "bench.json", "decode_C": "decode_C.json", "decode_D1": "decod
          "encode_C": "encode_C.json", "resident_1000": "resident_1000.json",
          "resident_read_plain": "resident_read_plain.json", "resident_read_block": "resident_read_block.json",
          "decode_D1x2": "decode_D1x2.json", "decode_D1x4": "decode_D1x4.json",
-         "decode_D_table10M": "decode_D_table10M.json"}
+         "decode_D_table10M": "decode_D_table10M.json", "sst": "sst_bench.json"}
 for n, out in names.items():
     p = f"{src}/{n}.log"
     if os.path.exists(p):
@@ -37,6 +38,11 @@ for n, out in names.items():
         if j is not None:
             json.dump(j, open(f"{dst}/{out}", "w"))
             print(out)
+if os.path.exists(f"{src}/trace.log"):  # the traced driver command's own line
+    j = last_json(f"{src}/trace.log")
+    if j is not None:
+        open(f"{dst}/bench_driver_traced_line.log", "w").write(json.dumps(j) + "\n")
+        print("bench_driver_traced_line.log")
 for n in ("timeline_D",):
     if os.path.exists(f"{src}/{n}.log"):
         shutil.copy(f"{src}/{n}.log", f"{dst}/{n}.log")
