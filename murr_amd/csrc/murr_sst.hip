@@ -526,6 +526,20 @@ __device__ __forceinline__ int wave_inflate(const SstBlock& blk, Lds& L, uint32_
     return ok ? 1 : 0;
 }
 
+// dst[0, n) = lds[x, x + n) (lds 4-byte aligned, readable to x + n + 11) by
+// the group's lanes: unaligned 8-byte stores (the last one overlapping its
+// neighbour with the same bytes), byte stores under 8 bytes -- a 42-byte row
+// blob is one store instruction instead of six byte stores.
+template <uint32_t G>
+__device__ __forceinline__ void wstore8(GAS uint8_t* dst, const uint8_t* lds, uint32_t x, uint32_t n, uint32_t lane) {
+    if (n >= 8) {
+        for (uint32_t q = 8 * lane; q + 8 <= n; q += 8 * G) *(GAS u64u*)(dst + q) = win8(lds, x + q);
+        if ((n & 7u) && lane == 0) *(GAS u64u*)(dst + n - 8) = win8(lds, x + n - 8);
+    } else {
+        for (uint32_t q = lane; q < n; q += G) dst[q] = lds[x + q];
+    }
+}
+
 // Walk the entries of the block in L.raw[0, n); EMIT writes them at (e0, k0,
 // v0).  1 ok, 0 malformed, 3 an internal key longer than the key buffer.
 template <uint32_t G, bool EMIT, class Lds>
@@ -558,11 +572,8 @@ __device__ __forceinline__ int wave_walk(const SstArgs& A, Lds& L, uint32_t r0, 
             wcopy<G>(L.key + shared, L.raw + p, nonshared, lane);  // the internal key, rebuilt in place
             wave_sync();
             const uint64_t e = e0 + cnt;
-            GAS uint8_t* ko = gp(A.keys) + k0 + kbytes;
-            for (uint32_t q = lane; q < ul; q += G) ko[q] = L.key[q];
-            GAS uint8_t* vo = gp(A.vals) + v0 + vbytes;
-            const uint8_t* vs = L.raw + p + nonshared;
-            for (uint32_t q = lane; q < vlen; q += G) vo[q] = vs[q];
+            wstore8<G>(gp(A.keys) + k0 + kbytes, L.key, 0, ul, lane);
+            wstore8<G>(gp(A.vals) + v0 + vbytes, L.raw, p + nonshared, vlen, lane);
             if (lane == 0) {
                 const uint64_t trailer = win8(L.key, ul);
                 gp(A.key_off)[e + 1] = (int32_t)(k0 + kbytes + ul);
