@@ -189,6 +189,10 @@ int murr_ctx_stats(murr_ctx_t* ctx, murr_ctx_stats_t* out);
  * the layouts held.  The on-disk cache is not affected. */
 int murr_jit_cache_limit(uint32_t max_layouts, uint32_t* limit, uint32_t* cached);
 
+/* Device memory.  murr_dev_free also takes the device outputs the library
+ * allocates for the caller (murr_sst_decode): those go back to the context's
+ * reuse cache (at most 1 GiB, released by murr_ctx_destroy) for its next
+ * call; anything else is freed. */
 int murr_dev_alloc(murr_ctx_t* ctx, uint64_t bytes, void** p);
 int murr_dev_free(murr_ctx_t* ctx, void* p);
 int murr_host_alloc(murr_ctx_t* ctx, uint64_t bytes, void** p); /* pinned */
@@ -633,9 +637,10 @@ void murr_reader_free(murr_reader_t* r);
  * aligned, value_offsets[n + 1] from 0), and each trailer's sequence number
  * and value type.  Blocks that do not parse are MURR_E_MALFORMED_ROW with the
  * first such block in err->row.  Outputs are allocated by the library (device
- * memory) and freed with murr_sst_result_free, or one by one with
- * murr_dev_free (to keep, e.g., values and value_offsets as a table's
- * arena).  `blocks` is a host array, or a device array (device memory from
+ * memory, through the context's reuse cache) and freed with
+ * murr_sst_result_free, or one by one with murr_dev_free (to keep, e.g.,
+ * values and value_offsets as a table's arena); freed ones serve the
+ * context's next call without a hipMalloc.  `blocks` is a host array, or a device array (device memory from
  * murr_dev_alloc / hipMalloc: the descriptor table of a file decoded more
  * than once, uploaded once -- a 100 k-block host table costs ~0.1 ms of
  * pageable copy per call); a device table is not read by the host, so a

@@ -16,6 +16,7 @@
 #include <chrono>
 #include <condition_variable>
 #include <thread>
+#include <unordered_map>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -61,6 +62,13 @@ bool valid_segment(const murr_segment_t* s) {
 }  // namespace
 
 struct murr_ctx {
+    // Library-allocated outputs handed to the caller (murr_sst_decode's
+    // entries) that came back through murr_dev_free / murr_sst_result_free,
+    // kept for reuse (size -> pointer), so a repeated call does not pay six
+    // hipMallocs (~0.1 ms); released at context destroy, or past
+    // kDevCacheMax bytes.  Which pointers are such outputs: g_dcached.
+    std::multimap<uint64_t, void*> dfree;
+    uint64_t dfree_bytes = 0;
     int device = 0;
     int cus = 256;
     int enc_grid_per_cu = 1;
@@ -146,6 +154,68 @@ uint32_t nutf8_of(const murr_segment_t* seg) {
         hipError_t _e = (expr);                             \
         if (_e != hipSuccess) return hip_fail(err, _e);     \
     } while (0)
+
+// Caller-owned device outputs through the context's reuse cache: a freed
+// buffer of at least `bytes` (and at most twice that plus 1 MiB) comes back
+// instead of a new hipMalloc; new ones are rounded to 1 MiB.  hipSuccess or
+// the allocation's error (the cache is released and the call retried once).
+constexpr uint64_t kDevCacheMax = 1ull << 30;
+// process-wide: every buffer dev_alloc_cached made, with its context and size
+// (a pointer freed through another context, or re-allocated by a plain
+// hipMalloc after a direct hipFree, is dropped from it, never reused stale)
+std::mutex g_dc_mu;
+std::unordered_map<void*, std::pair<murr_ctx*, uint64_t>> g_dcached;
+hipError_t dev_alloc_cached(murr_ctx* c, uint64_t bytes, void** out) {
+    std::lock_guard<std::mutex> lk(g_dc_mu);
+    auto it = c->dfree.lower_bound(bytes);
+    if (it != c->dfree.end() && it->first <= 2 * bytes + (1u << 20)) {
+        *out = it->second;
+        c->dfree_bytes -= it->first;
+        c->dfree.erase(it);
+        return hipSuccess;
+    }
+    const uint64_t sz = (bytes + (1u << 20) - 1) & ~(uint64_t)((1u << 20) - 1);
+    hipError_t e = hipMalloc(out, sz);
+    if (e != hipSuccess && !c->dfree.empty()) {
+        (void)hipGetLastError();
+        for (const auto& f : c->dfree) {
+            g_dcached.erase(f.second);
+            (void)hipFree(f.second);
+        }
+        c->dfree.clear();
+        c->dfree_bytes = 0;
+        e = hipMalloc(out, sz);
+    }
+    if (e == hipSuccess) g_dcached[*out] = {c, sz};
+    return e;
+}
+// A buffer dev_alloc_cached handed out goes back to the cache (true); any
+// other pointer is the caller's to hipFree (false).
+bool dev_free_cached(murr_ctx* c, void* p) {
+    std::lock_guard<std::mutex> lk(g_dc_mu);
+    auto it = g_dcached.find(p);
+    if (it == g_dcached.end()) return false;
+    if (it->second.first != c) {  // another context's: released, not cached here
+        g_dcached.erase(it);
+        return false;
+    }
+    c->dfree.emplace(it->second.second, p);
+    c->dfree_bytes += it->second.second;
+    while (c->dfree_bytes > kDevCacheMax && !c->dfree.empty()) {  // the largest go first
+        auto last = std::prev(c->dfree.end());
+        c->dfree_bytes -= last->first;
+        g_dcached.erase(last->second);
+        (void)hipFree(last->second);
+        c->dfree.erase(last);
+    }
+    return true;
+}
+// A plain allocation at `p` (hipMalloc handed the address out again): drop
+// any stale record of it.
+void dev_forget(void* p) {
+    std::lock_guard<std::mutex> lk(g_dc_mu);
+    g_dcached.erase(p);
+}
 
 // Grow a device buffer to at least `need` bytes (doubling), keeping `keep` bytes.
 template <class T>
@@ -693,6 +763,12 @@ void murr_ctx_destroy(murr_ctx_t* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    {
+        std::lock_guard<std::mutex> lk(g_dc_mu);
+        for (const auto& f : c->dfree) (void)hipFree(f.second);
+        for (auto it = g_dcached.begin(); it != g_dcached.end();)  // (outstanding ones: plain buffers from now on)
+            it = it->second.first == c ? g_dcached.erase(it) : std::next(it);
+    }
     if (c->ws) (void)hipFree(c->ws);
     if (c->aux) (void)hipFree(c->aux);
     if (c->hs) (void)hipHostFree(c->hs);
@@ -773,13 +849,14 @@ int murr_dev_alloc(murr_ctx_t* c, uint64_t bytes, void** p) {
     HIPC(hipSetDevice(c->device));
     // Rounded up and padded so 16-B staging loads of the last chunk stay inside.
     HIPC(hipMalloc(p, round_up(bytes ? bytes : 1, 16) + 16));
+    dev_forget(*p);
     return MURR_OK;
 }
 
 int murr_dev_free(murr_ctx_t* c, void* p) {
     murr_error_t* err = nullptr;
     if (!c) return MURR_E_ARGUMENT;
-    if (p) HIPC(hipFree(p));
+    if (p && !dev_free_cached(c, p)) HIPC(hipFree(p));
     return MURR_OK;
 }
 
@@ -3133,7 +3210,7 @@ void murr_sst_result_free(murr_ctx_t* c, murr_sst_result_t* r) {
     if (c) (void)hipSetDevice(c->device);
     for (void* p : {(void*)r->keys, (void*)r->key_offsets, (void*)r->values, (void*)r->value_offsets,
                     (void*)r->seqs, (void*)r->types})
-        if (p) (void)hipFree(p);
+        if (p && !(c && dev_free_cached(c, p))) (void)hipFree(p);
     std::memset(r, 0, sizeof *r);
 }
 
@@ -3234,12 +3311,13 @@ int murr_sst_decode(murr_ctx_t* c, const murr_sst_block_t* blocks, uint32_t nblo
     const uint64_t n = host[1], kbytes = host[2], vbytes = host[3];
     if (kbytes > 0x7FFFFFFFull) return fail(set_err(err, MURR_E_OFFSET_OVERFLOW));
     // outputs (the caller's), then the entries
-    SSTC(hipMalloc((void**)&out->keys, kbytes + 16));
-    SSTC(hipMalloc((void**)&out->key_offsets, 4 * (n + 1)));
-    SSTC(hipMalloc((void**)&out->values, vbytes + 16));
-    SSTC(hipMalloc((void**)&out->value_offsets, 8 * (n + 1)));
-    SSTC(hipMalloc((void**)&out->seqs, 8 * std::max<uint64_t>(n, 1)));
-    SSTC(hipMalloc((void**)&out->types, std::max<uint64_t>(n, 1)));
+    // (through the context's reuse cache: murr_sst_result_free / murr_dev_free give them back)
+    SSTC(dev_alloc_cached(c, kbytes + 16, (void**)&out->keys));
+    SSTC(dev_alloc_cached(c, 4 * (n + 1), (void**)&out->key_offsets));
+    SSTC(dev_alloc_cached(c, vbytes + 16, (void**)&out->values));
+    SSTC(dev_alloc_cached(c, 8 * (n + 1), (void**)&out->value_offsets));
+    SSTC(dev_alloc_cached(c, 8 * std::max<uint64_t>(n, 1), (void**)&out->seqs));
+    SSTC(dev_alloc_cached(c, std::max<uint64_t>(n, 1), (void**)&out->types));
     SSTC(hipMemsetAsync(out->key_offsets, 0, 4, c->stream));
     SSTC(hipMemsetAsync(out->value_offsets, 0, 8, c->stream));
     out->n = n;

@@ -272,3 +272,34 @@ def test_device_block_table_in_place():
     bad = sst.SstTable(ctx.upload(desc.view(np.uint8)), len(desc))
     with pytest.raises(SegmentError, match=r"row 5,"):
         sst.decode(ctx, buf, bad)
+
+
+def test_outputs_reused_after_free_never_while_live():
+    # the entry buffers come from the context's reuse cache: a call made while
+    # an earlier result is alive gets other buffers, one made after it is
+    # freed may get its buffers back; every result reads as the oracle's
+    rng = np.random.default_rng(91)
+    stored = [(G.snappy(b), G.SNAPPY) for b in G.blocks_of(G.random_entries(rng, 700, max_val=90))]
+    want = oracle_entries(stored)
+    ctx = default_context()
+    buf, handles = sst.upload_blocks(ctx, stored)
+
+    def ptrs(e):
+        return {e.keys.ptr, e.key_offsets.ptr, e.values.ptr, e.value_offsets.ptr, e.seqs.ptr, e.types.ptr}
+
+    def same(e):
+        k, v, s, t = e.to_host()
+        assert k == want[0] and v == want[1] and s.tolist() == want[2] and t.tolist() == want[3]
+
+    e1 = sst.decode(ctx, buf, handles)
+    e2 = sst.decode(ctx, buf, handles)
+    assert not (ptrs(e1) & ptrs(e2))
+    same(e1)
+    same(e2)
+    old = ptrs(e1)
+    del e1
+    e3 = sst.decode(ctx, buf, handles)
+    assert not (ptrs(e3) & ptrs(e2))
+    same(e3)
+    same(e2)
+    assert ptrs(e3) & old  # (at least one buffer came back from the cache)
