@@ -27,7 +27,7 @@ import pyarrow as pa
 from . import _abi
 from .device import Context, DecodeOutputs, DecodePlan, DeviceBlock, decode_blocks, download_array
 from .errors import SegmentError, raise_status
-from .row import host_array_to_arrow
+from .row import host_arrays_to_arrow
 from .schema import DTypeName, TableSchema
 from .store import Store
 from .table import Table
@@ -186,6 +186,7 @@ class ResidentTable:
         self.n = 0
         self.max_row = 0
         self._reader = None    # murr_reader_t: scratch of the one-call host read
+        self._schemas = {}     # read(): Arrow schema per requested column list
         self.uidx = None       # utf8 index of the arena (every self.stride rows), kept with every write
         self.uidx_cap = 0      # entries
         self._scan_plans = {}  # id(outs) (None: the plan's own outputs) -> (key, DecodePlan) of scan_device
@@ -450,9 +451,12 @@ class ResidentTable:
                                 self.max_row, kb[2].address if nq and kb[2] is not None else None,
                                 kb[1].address if nq else None, q.offset, nq, proj, len(req), outs, C.byref(err))
         raise_status(st, err, "murr_reader_read")
-        arrays = [host_array_to_arrow(outs[p]) for p in range(len(req))]
-        fields = [pa.field(c.name, c.dtype.arrow_dtype(), True) for c in req]
-        return pa.RecordBatch.from_arrays(arrays, schema=pa.schema(fields))
+        key = tuple(c.index for c in req)
+        schema = self._schemas.get(key)
+        if schema is None:  # (one per column list: a schema costs ~5 us to build)
+            schema = pa.schema([pa.field(c.name, c.dtype.arrow_dtype(), True) for c in req])
+            self._schemas[key] = schema
+        return pa.RecordBatch.from_arrays(host_arrays_to_arrow(outs, len(req)), schema=schema)
 
     def read_ipc(self, keys, columns, alignment: int = 64) -> bytes:
         """read() as the Arrow IPC stream of the HTTP fetch handler's StreamWriter

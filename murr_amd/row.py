@@ -86,12 +86,18 @@ class ReadBatchBuilder:
 
     def build(self) -> pa.RecordBatch:
         outs = self._build_host()
-        arrays, fields = [], []
-        for p, col in enumerate(self.columns):
-            seg_col = col if isinstance(col, SegmentColumnSchema) else self.segment.columns[int(col)]
-            arrays.append(host_array_to_arrow(outs[p]))
-            fields.append(pa.field(seg_col.name, seg_col.dtype.arrow_dtype(), True))
-        return pa.RecordBatch.from_arrays(arrays, schema=pa.schema(fields))
+        return pa.RecordBatch.from_arrays(host_arrays_to_arrow(outs, self._nproj), schema=self._schema())
+
+    def _schema(self) -> pa.Schema:
+        """The batch schema: Field(name, arrow dtype, nullable) per requested
+        column (read.rs:100-109), built once."""
+        if getattr(self, "_arrow_schema", None) is None:
+            fields = []
+            for col in self.columns:
+                seg_col = col if isinstance(col, SegmentColumnSchema) else self.segment.columns[int(col)]
+                fields.append(pa.field(seg_col.name, seg_col.dtype.arrow_dtype(), True))
+            self._arrow_schema = pa.schema(fields)
+        return self._arrow_schema
 
     def last_timing(self):
         tot, h2d, k, d2h = C.c_double(), C.c_float(), C.c_float(), C.c_float()
@@ -120,6 +126,54 @@ class IpcReadBatchBuilder(ReadBatchBuilder):
 
 def _copy(ptr, n) -> pa.Buffer:
     return pa.py_buffer(C.string_at(ptr, n)) if n else pa.py_buffer(b"")
+
+
+_ARROW_TYPE = {int(d): d.arrow_dtype() for d in DTypeName}
+_UTF8 = int(DTypeName.Utf8)
+
+
+_HOST_ARRAY = np.dtype([("values", np.uint64), ("validity", np.uint64), ("offsets", np.uint64), ("length", np.uint64),
+                        ("null_count", np.uint64), ("values_len", np.uint64), ("dtype", np.uint32), ("_pad", np.uint32)])
+assert _HOST_ARRAY.itemsize == C.sizeof(_abi.HostArray)
+
+
+def host_arrays_to_arrow(outs, k: int) -> list:
+    """murr_host_array_t[0..k) -> pyarrow Arrays, copied out of the library's
+    pinned output region (it is reused by the next read).  The descriptors
+    are read as one numpy view; when the arrays' buffers fill most of their
+    span (they lie in one region), one copy of the span and zero-copy slices
+    of it replace a copy per buffer."""
+    if not k:
+        return []
+    t = np.frombuffer((C.c_char * (k * _HOST_ARRAY.itemsize)).from_address(C.addressof(outs)), _HOST_ARRAY, k)
+    vals, valid, offs = t["values"].tolist(), t["validity"].tolist(), t["offsets"].tolist()
+    ns, ncs, vlen, dts = t["length"].tolist(), t["null_count"].tolist(), t["values_len"].tolist(), t["dtype"].tolist()
+    # (pointer, bytes) of every buffer: validity (nulls only), utf8 offsets, values
+    vb = [((n + 7) // 8 if v else 0) for n, v in zip(ns, valid)]
+    ob = [((n + 1) * 4 if d == _UTF8 else 0) for n, d in zip(ns, dts)]
+    spans = [(p, b) for p, b in zip(valid + offs + vals, vb + ob + vlen) if p and b]
+    if spans:
+        lo = min(p for p, _ in spans)
+        hi = max(p + b for p, b in spans)
+        one = hi - lo <= 2 * sum(b for _, b in spans) + 4096
+    else:
+        lo, one = 0, False
+    big = pa.py_buffer(C.string_at(lo, hi - lo)) if one else None
+    empty = pa.py_buffer(b"")
+
+    def buf(p, b):
+        if not (p and b):
+            return empty
+        return big.slice(p - lo, b) if one else pa.py_buffer(C.string_at(p, b))
+
+    out = []
+    for i in range(k):
+        bufs = [buf(valid[i], vb[i]) if valid[i] else None]
+        if dts[i] == _UTF8:
+            bufs.append(buf(offs[i], ob[i]))
+        bufs.append(buf(vals[i], vlen[i]))
+        out.append(pa.Array.from_buffers(_ARROW_TYPE[dts[i]], ns[i], bufs, null_count=ncs[i]))
+    return out
 
 
 def host_array_to_arrow(h) -> pa.Array:
@@ -202,12 +256,13 @@ class HostStream:
         raise_status(st, self._err, "murr_hstream_next")
         if not arrow:
             return outs
-        arrays, fields = [], []
-        for p, col in enumerate(self.columns):
-            seg_col = col if isinstance(col, SegmentColumnSchema) else self.segment.columns[int(col)]
-            arrays.append(host_array_to_arrow(outs[p]))
-            fields.append(pa.field(seg_col.name, seg_col.dtype.arrow_dtype(), True))
-        return pa.RecordBatch.from_arrays(arrays, schema=pa.schema(fields))
+        if getattr(self, "_arrow_schema", None) is None:
+            fields = []
+            for col in self.columns:
+                seg_col = col if isinstance(col, SegmentColumnSchema) else self.segment.columns[int(col)]
+                fields.append(pa.field(seg_col.name, seg_col.dtype.arrow_dtype(), True))
+            self._arrow_schema = pa.schema(fields)
+        return pa.RecordBatch.from_arrays(host_arrays_to_arrow(outs, self._nproj), schema=self._arrow_schema)
 
     @property
     def pending(self) -> int:

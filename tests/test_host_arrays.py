@@ -1,0 +1,60 @@
+"""Host Arrow assembly of a read (murr_amd.row.host_arrays_to_arrow: one copy
+of the output region, zero-copy slices, descriptors read as one numpy view)
+equals the per-column conversion, buffer for buffer (CPU: synthetic
+murr_host_array_t over a host region laid out as the library's)."""
+import numpy as np
+import pytest
+
+from murr_amd import _abi
+from murr_amd.row import host_array_to_arrow, host_arrays_to_arrow
+from murr_amd.schema import DTypeName as D
+
+
+@pytest.mark.parametrize("n", [0, 1, 7, 64, 1000])
+@pytest.mark.parametrize("gap", [64, 1 << 16])  # packed region, or one whose span is mostly gaps
+def test_batched_equals_per_column(n, gap):
+    rng = np.random.default_rng(n + gap)
+    region = np.zeros(16 * (n * 8 + gap + 256), np.uint8)
+    base = region.ctypes.data
+    off = [0]
+
+    def put(arr):
+        b = np.frombuffer(arr.tobytes(), np.uint8)
+        o = off[0]
+        region[o:o + len(b)] = b
+        off[0] = (o + len(b) + gap + 63) // 64 * 64
+        return base + o
+
+    dtypes = [D.Utf8, D.Float32, D.Int64, D.Bool, D.UInt8, D.Utf8, D.Int16, D.Float64]
+    outs = (_abi.HostArray * len(dtypes))()
+    for i, dt in enumerate(dtypes):
+        h = outs[i]
+        if dt == D.Utf8:
+            lens = rng.integers(0, 9, n)
+            o = np.concatenate([[0], np.cumsum(lens)]).astype(np.int32)
+            d = rng.integers(97, 123, int(o[-1]), dtype=np.uint8)
+            h.offsets, h.values, h.values_len = put(o), put(d) if len(d) else base, len(d)
+        else:
+            nb = (n + 7) // 8 if dt == D.Bool else n * {D.Float32: 4, D.Int64: 8, D.UInt8: 1, D.Int16: 2, D.Float64: 8}[dt]
+            v = rng.integers(0, 256, nb, dtype=np.uint8)
+            if dt == D.Bool and n % 8:
+                v[-1] &= 0xFF >> (8 - n % 8)
+            h.offsets, h.values, h.values_len = None, put(v) if nb else base, nb
+        h.dtype = int(dt)
+        if i % 2 == 0 and n:
+            bits = rng.integers(0, 256, (n + 7) // 8, dtype=np.uint8)
+            if n % 8:
+                bits[-1] &= 0xFF >> (8 - n % 8)
+            h.validity = put(bits)
+            h.null_count = int(n - np.unpackbits(bits, bitorder="little")[:n].sum())
+        else:
+            h.validity, h.null_count = None, 0
+        h.length = n
+    got = host_arrays_to_arrow(outs, len(dtypes))
+    for i, (x, y) in enumerate(zip(got, [host_array_to_arrow(outs[i]) for i in range(len(dtypes))])):
+        x.validate(full=True)
+        assert x.type == y.type and len(x) == len(y) and x.null_count == y.null_count, i  # (random floats: NaNs)
+        for bx, by in zip(x.buffers(), y.buffers()):
+            assert (bx is None) == (by is None)
+            if bx is not None:
+                assert bx.to_pybytes() == by.to_pybytes()
