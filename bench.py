@@ -217,6 +217,49 @@ def cpu_baseline(seg, proj, host_blob, host_off, rows, target_s):
                       f"oracle/libmurr_oracle.so (serial ReadBatchBuilder restatement), {dt:.1f} s"}
 
 
+def host_cores():
+    """Host threads this process may really use, and where the number comes
+    from (all cores, stated): the CPU affinity mask, capped by
+    the cgroup's CPU quota (v2 cpu.max or v1 cfs_quota_us / cfs_period_us;
+    the GPU box's share is a quota over a 256-thread host).  Counts hardware
+    threads: two per physical core on an SMT host (`smt` in the source)."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = os.cpu_count() or 1
+    quota, qsrc = None, None
+    for path, kind in (("/sys/fs/cgroup/cpu.max", "v2"), ("/sys/fs/cgroup/cpu/cpu.cfs_quota_us", "v1")):
+        try:
+            with open(path) as f:
+                txt = f.read().split()
+            if kind == "v2":
+                if txt and txt[0] != "max":
+                    quota, qsrc = int(txt[0]) / int(txt[1]), "cgroup v2 cpu.max"
+            else:
+                q = int(txt[0])
+                with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+                    per = int(f.read().split()[0])
+                if q > 0:
+                    quota, qsrc = q / per, "cgroup v1 cfs_quota_us"
+            break
+        except (OSError, ValueError, IndexError):
+            continue
+    smt = 1
+    try:
+        with open("/sys/devices/system/cpu/cpu0/topology/thread_siblings_list") as f:
+            sib = f.read().strip()
+        smt = sum(int(b) - int(a) + 1 if "-" in r else 1
+                  for r in sib.split(",") for a, _, b in [r.partition("-")])
+    except (OSError, ValueError):
+        pass
+    n = aff
+    src = f"sched_getaffinity {aff}"
+    if quota is not None:
+        n = max(1, min(aff, int(quota)))
+        src += f", {qsrc} {quota:g} CPUs"
+    return n, f"{src} -> {n} threads ({smt} hardware thread(s) per core)"
+
+
 def cpu_baseline_threads(seg, proj, host_blob, host_off, rows, target_s, threads):
     """Upper bound the reference does not implement: the
     same oracle on `threads` host threads, each decoding a contiguous row range
@@ -466,102 +509,119 @@ def run_decode(args, dist, rank, world, local_rank):
     # (murr_decode_run_async) before step s - 1 is waited for, so the host's
     # launch and read-back work overlaps the previous step's kernel, as a
     # serving loop would.  One lane: two sets on one context (one stream; on
-    # the GPU the steps run one after the other).  --lanes L > 1: one set per
+    # the GPU the steps run one after the other).  L > 1 lanes: one set per
     # lane, each lane a context of its own (its own stream), L - 1 steps
     # launched ahead, so step s + 1's workgroups can start on CUs step s has
-    # left (config D's default, three lanes: a resident shard's scan ends with
-    # a long tail).  --sync-steps: one set, each step waited for (the A/B).
-    if args.lanes is None:  # (config D: 0.0568 -> 0.0510 ms per step from two to three lanes, four no faster)
-        args.lanes = 3 if args.config == "D" else 1
-    # one output set per lane (two on one context with one lane); step s uses
-    # set s % len(ctxs), and len(ctxs) - 1 steps are launched ahead of the
-    # one waited for
-    ctxs = [ctx] + [Context(local_rank) for _ in range(args.lanes - 1)] if args.lanes > 1 else [ctx, ctx]
-    if args.arena:
-        out_sets = [ArenaOutputs(c, seg, proj, blocks, args.arena) for c in ctxs]
-    else:
-        out_sets = [DecodeOutputs(c, seg, proj, blocks) for c in ctxs]
-    if rt is not None:
-        names = [seg.columns[c].name for c in proj]
-
-        def launch(i):  # the product call (its prepared plan after the first)
-            return rt.scan_device_async(names, out_sets[i], ctx=ctxs[i])
-    else:
-        # the launch prepared once per output set (murr_decode_plan)
-        plans = [DecodePlan(c, seg, proj, blocks, o) for c, o in zip(ctxs, out_sets)]
-
-        def launch(i):
-            plans[i].run_async()
-            return plans[i]
-
-    # Kernel time.  The warm-up samples the plan's own timed runs (one in
-    # PLAN_TIME_EVERY, the first included).  The timed region turns those
-    # per-run events off (each costs GPU time between back-to-back launches)
-    # and brackets all K launches with two marks on the context's stream:
-    # kernel_ms_avg = that GPU time / K, which includes the gaps between the
-    # launches, so it never exceeds ms_per_step (the host's clock around the
-    # same K steps).  With several lanes (streams) the region runs from the
-    # first lane's start mark to the latest of the lanes' end marks: the
-    # launches overlap, so this is the GPU time per launch at steady state.
-    runs = [0] * len(ctxs)  # runs of each output set's plan so far
+    # left.  --sync-steps: one set, each step waited for (the A/B).
+    #
+    # Lane policy, the same for every config: the headline
+    # line is per launch -- one lane, so the roofline's kernel time and a
+    # rocprof trace's kernel duration describe one launch's traffic -- and the
+    # overlapped rate is an extra key (`lanes`: --extra-lanes L, default 3;
+    # config D's shard scan and config B both gain from it), measured after
+    # the headline with every lane's last output checked against the oracle.
+    names = [seg.columns[c].name for c in proj] if rt is not None else None
     every = _abi.PLAN_TIME_EVERY
     if "MURR_TIME_EVERY" in os.environ and _abi.LIB_PATH.endswith("_tuning.so"):
         every = max(1, int(os.environ["MURR_TIME_EVERY"]))
-    launched = {}  # the prepared plans the steps ran (resident scans make theirs inside the table)
 
-    def run_steps(n, sample=True):
-        ms = []
+    def lanes_run(nl, steps, warmup):
+        """Warm-up + timed region over nl lanes; returns the region's state."""
+        # one output set per lane (two on one context with one lane); step s
+        # uses set s % len(ctxs), and len(ctxs) - 1 steps are launched ahead
+        # of the one waited for
+        ctxs = [ctx] + [Context(local_rank) for _ in range(nl - 1)] if nl > 1 else [ctx, ctx]
+        if args.arena:
+            out_sets = [ArenaOutputs(c, seg, proj, blocks, args.arena) for c in ctxs]
+        else:
+            out_sets = [DecodeOutputs(c, seg, proj, blocks) for c in ctxs]
+        plans = None
+        if rt is not None:
+            def launch(i):  # the product call (its prepared plan after the first)
+                return rt.scan_device_async(names, out_sets[i], ctx=ctxs[i])
+        else:
+            # the launch prepared once per output set (murr_decode_plan)
+            plans = [DecodePlan(c, seg, proj, blocks, o) for c, o in zip(ctxs, out_sets)]
 
-        def done(i):
-            if sample and runs[i] % every == 0:
-                ms.append(ctxs[i].last_kernel_ms())
-            runs[i] += 1
+            def launch(i):
+                plans[i].run_async()
+                return plans[i]
 
-        def go(i):
-            p = launch(i)
-            launched[id(p)] = p
-            return p
+        # Kernel time.  The warm-up samples the plan's own timed runs (one in
+        # PLAN_TIME_EVERY, the first included).  The timed region turns those
+        # per-run events off (each costs GPU time between back-to-back
+        # launches) and brackets all K launches with two marks on the context's
+        # stream: kernel_ms_avg = that GPU time / K, which includes the gaps
+        # between the launches, so it never exceeds ms_per_step (the host's
+        # clock around the same K steps).  With several lanes (streams) the
+        # region runs from the first lane's start mark to the latest of the
+        # lanes' end marks: the launches overlap, so this is the GPU time per
+        # launch at steady state.
+        runs = [0] * len(ctxs)  # runs of each output set's plan so far
+        launched = {}  # the prepared plans the steps ran (resident scans make theirs inside the table)
 
-        if args.sync_steps:
-            for _ in range(n):
-                go(0).wait()
-                done(0)
+        def run_steps(n, sample=True):
+            ms = []
+
+            def done(i):
+                if sample and runs[i] % every == 0:
+                    ms.append(ctxs[i].last_kernel_ms())
+                runs[i] += 1
+
+            def go(i):
+                p = launch(i)
+                launched[id(p)] = p
+                return p
+
+            if args.sync_steps:
+                for _ in range(n):
+                    go(0).wait()
+                    done(0)
+                return ms
+            nset = len(ctxs)
+            inflight = [go(s % nset) for s in range(min(n, nset - 1))]
+            for s in range(n):
+                if s + nset - 1 < n:
+                    inflight.append(go((s + nset - 1) % nset))
+                inflight.pop(0).wait()
+                done(s % nset)
             return ms
-        nset = len(ctxs)
-        inflight = [go(s % nset) for s in range(min(n, nset - 1))]
-        for s in range(n):
-            if s + nset - 1 < n:
-                inflight.append(go((s + nset - 1) % nset))
-            inflight.pop(0).wait()
-            done(s % nset)
-        return ms
 
-    if rt is not None:
-        # setup: a resident table prepares each lane's scan plan at its first
-        # scan; make those before the warm-up, so a warm-up shorter than the
-        # lane count cannot leave one to the timed region
-        for i in range(len(ctxs)):
-            launch(i).wait()
-    wms = run_steps(args.warmup)
-    for p in launched.values():
-        p.time_every(0)
-    lanes = list({id(c): c for c in ctxs}.values())
-    barrier(dist)
-    for c in ctxs:
-        c.sync()
-    t0 = time.perf_counter()
-    ctx.mark(0)
-    kms = run_steps(args.steps, sample=False)
-    for c in lanes:
-        c.mark(1)
-    for c in ctxs:
-        c.sync()
-    barrier(dist)
-    elapsed = time.perf_counter() - t0
-    region_ms = max(ctx.mark_ms(0, 1, c) for c in lanes) if args.steps else None
-    for p in launched.values():
-        p.time_every(every)
-    last = 0 if args.sync_steps else (args.steps - 1) % len(ctxs)
+        if rt is not None:
+            # setup: a resident table prepares each lane's scan plan at its
+            # first scan; make those before the warm-up, so a warm-up shorter
+            # than the lane count cannot leave one to the timed region
+            for i in range(len(ctxs)):
+                launch(i).wait()
+        wms = run_steps(warmup)
+        for p in launched.values():
+            p.time_every(0)
+        lanes = list({id(c): c for c in ctxs}.values())
+        barrier(dist)
+        for c in ctxs:
+            c.sync()
+        t0 = time.perf_counter()
+        ctx.mark(0)
+        run_steps(steps, sample=False)
+        for c in lanes:
+            c.mark(1)
+        for c in ctxs:
+            c.sync()
+        barrier(dist)
+        elapsed = time.perf_counter() - t0
+        region_ms = max(ctx.mark_ms(0, 1, c) for c in lanes) if steps else None
+        for p in launched.values():
+            p.time_every(every)
+        nset = 1 if args.sync_steps else len(ctxs)
+        # the set each lane's last timed step wrote (step s used set s % nset)
+        last_of = {i: max(s for s in range(steps) if s % nset == i) for i in range(min(nset, steps))}
+        return {"ctxs": ctxs, "lanes": lanes, "out_sets": out_sets, "plans": plans, "launch": launch,
+                "elapsed": elapsed, "region_ms": region_ms, "wms": wms, "last_of": last_of,
+                "last": (steps - 1) % nset if steps else 0}
+
+    R = lanes_run(1 if args.lanes is None else args.lanes, args.steps, args.warmup)
+    ctxs, out_sets, plans, launch = R["ctxs"], R["out_sets"], R["plans"], R["launch"]
+    elapsed, region_ms, wms, last = R["elapsed"], R["region_ms"], R["wms"], R["last"]
     outs = out_sets[last]  # the last timed step's output (checked below)
     elapsed = max_over_ranks(dist, elapsed)
     stats = ctx.stats()
@@ -578,7 +638,7 @@ def run_decode(args, dist, rank, world, local_rank):
     if region_ms is not None:
         k_avg_ms = region_ms / args.steps
     else:
-        k_avg_ms = float(np.mean(kms or warm_ms))  # (a timed region shorter than the period: the warm-up's)
+        k_avg_ms = float(np.mean(warm_ms))  # (no timed steps: the warm-up's sampled runs)
     achieved = (in_block + out_block) * K / (k_avg_ms * 1e-3) / 1e9
     shape = "%dx%d" % tuple(stats["last_shape"])
     timed_kernel = ("decode_kernel" if stats["last_mode"] == "generic" else
@@ -610,6 +670,32 @@ def run_decode(args, dist, rank, world, local_rank):
         p2.close()
         # leave the indexed output in place
         launch(last).wait()
+    # the overlapped rate (lane policy above): --extra-lanes contexts, every
+    # lane's last timed output checked against the oracle
+    lanes_extra = None
+    if args.extra_lanes > 1 and (args.lanes or 1) == 1 and args.steps:
+        E = lanes_run(args.extra_lanes, args.steps, args.warmup)
+        el = max_over_ranks(dist, E["elapsed"])
+        ebad = []
+        for i in sorted(E["last_of"]):
+            for b in checked:
+                bb, want = verify_arrays(E["ctxs"][i], seg, proj, E["out_sets"][i], b, host_blob, host_off, want)
+                ebad += [f"lane {i}: {x}" for x in bb]
+        if ebad:
+            raise SystemExit("bench: a lane's output differs from the oracle: " + "; ".join(ebad[:8]))
+        lanes_extra = {
+            "lanes": args.extra_lanes, "value": round(total_out / el / GIB, 3),
+            "ms_per_step": round(el / args.steps * 1e3, 4),
+            "frac_step_lanes": round((in_block + out_block) * K / (el / args.steps) / 1e9 / HBM_PEAK_GBS, 4),
+            "gpu_ms_per_step": round(E["region_ms"] / args.steps, 5),
+            "verified": (f"every lane's last timed output, blocks {checked}, bit-exact vs the oracle" if checked
+                         else "NOT VERIFIED (--no-verify)"),
+            "note": "launches on separate streams overlap: a per-launch roofline does not apply"}
+        for pl in E["plans"] or []:
+            pl.close()
+        for c in E["ctxs"][1:]:
+            c.close()
+        del E
     line = {
         "metric": METRIC, "value": round(value, 3), "unit": "GiB/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup,
@@ -643,14 +729,19 @@ def run_decode(args, dist, rank, world, local_rank):
                      "algorithmic_bytes_per_launch": (in_block + out_block) * K},
         "verified": f"blocks {checked} of the timed launch bit-exact vs the oracle" if checked else "NOT VERIFIED (--no-verify)",
         "no_index_ms": no_index_ms,
+        "lane_policy": ("per launch: one stream, steps back to back; the overlapped rate of "
+                        f"{args.extra_lanes} streams is `lanes`" if (args.lanes or 1) == 1 else
+                        f"{args.lanes} lanes (tuning run)"),
+        "lanes": lanes_extra,
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu:
         line["cpu_baseline"] = cpu_baseline(seg, proj, host_blob, host_off, rows, args.cpu_seconds)
-        threads = min(16, os.cpu_count() or 1)  # the GPU box's CPU share is 16
+        threads, src = host_cores()
         if threads > 1:
             line["cpu_baseline_all_cores"] = cpu_baseline_threads(seg, proj, host_blob, host_off, rows,
                                                                   min(5.0, args.cpu_seconds), threads)
+            line["cpu_baseline_all_cores"]["cores_source"] = src
     if rank == 0:
         print(json.dumps(line), flush=True)
     if rt is None:
@@ -936,20 +1027,42 @@ def run_resident(args):
     err = _abi.Error()
     L = ctx.L
 
-    def read(q):
+    def read_unprepared(q):  # (round 5's path: two calls, descriptors uploaded per read)
         st = L.murr_index_gather(ctx.h, rt.index.h, q[0].ptr, q[1].ptr, nq, rt.arena.ptr, rt.row_off.ptr,
                                  data.ptr, cap, roff.ptr, None, needed.ptr)
         assert st == 0, st
         st = L.murr_decode_blocks(ctx.h, C.byref(seg.c), pj, len(proj), cb, 1, outs.arrays, C.byref(err))
         assert st == 0, (st, err.status)
 
-    for i in range(args.warmup):
-        read(dq[i % 4])
-    ts = []
-    for i in range(args.steps):
-        t0 = time.perf_counter()
-        read(dq[i % 4])
-        ts.append(time.perf_counter() - t0)
+    # the product path: the table's prepared read (ReadPlan: lookup + gather +
+    # decode enqueued once, one wait), keys already in HBM
+    rplan = rt.read_plan(names, nq)
+    assert rplan is not None, "read too large for a prepared read"
+
+    def read(q):
+        rplan.run_device(q[0].ptr, q[1].ptr, nq)
+
+    def timed(fn, n):
+        for i in range(args.warmup):
+            fn(dq[i % 4])
+        t = []
+        for i in range(n):
+            t0 = time.perf_counter()
+            fn(dq[i % 4])
+            t.append(time.perf_counter() - t0)
+        return t
+
+    ts = timed(read, args.steps)
+    tu = timed(read_unprepared, args.steps)
+    # the prepared read's output against the unprepared path's (same keys): bit for bit
+    from murr_amd.device import download_array
+    read(dq[0])
+    read_unprepared(dq[0])
+    for p, ci in enumerate(proj):
+        dt = int(seg.columns[ci].dtype)
+        a, b = download_array(ctx, rplan.dev_outs[p], dt, nq), download_array(ctx, outs.array(0, p), dt, nq)
+        assert a["null_count"] == b["null_count"] and a["values"] == b["values"], f"column {p}"
+        assert (a["offsets"] is None and b["offsets"] is None) or np.array_equal(a["offsets"], b["offsets"])
     for i in range(args.warmup):
         rt.read(qsets[i % 4], names)
     th = []
@@ -964,7 +1077,8 @@ def run_resident(args):
         # and one D2H into pinned memory: the HTTP fetch handler's StreamWriter
         # body (src/api/http/handlers.rs:93-101) ready for the socket.
         mlen = C.c_uint64()
-        st = L.murr_ipc_batch_device(ctx.h, C.byref(seg.c), pj, len(proj), outs.arrays, nq, 64, None, 0,
+        read(dq[0])
+        st = L.murr_ipc_batch_device(ctx.h, C.byref(seg.c), pj, len(proj), rplan.dev_outs, nq, 64, None, 0,
                                      C.byref(mlen), C.byref(err))
         assert st == 0, st
         mcap = int(mlen.value) + 4096 * len(proj)  # body sizes vary a little with the key set
@@ -974,7 +1088,7 @@ def run_resident(args):
 
         def read_ipc(q):
             read(q)
-            st = L.murr_ipc_batch_device(ctx.h, C.byref(seg.c), pj, len(proj), outs.arrays, nq, 64, dmsg.ptr,
+            st = L.murr_ipc_batch_device(ctx.h, C.byref(seg.c), pj, len(proj), rplan.dev_outs, nq, 64, dmsg.ptr,
                                          mcap, C.byref(mlen), C.byref(err))
             assert st == 0, (st, err.required)
             assert L.murr_memcpy_d2h(ctx.h, hmsg, dmsg.ptr, mlen.value) == 0
@@ -997,9 +1111,13 @@ def run_resident(args):
                       "arrow_bytes_out": out_bytes,
                       "us_per_read_device_median": round(med * 1e6, 1),
                       "us_per_read_device_p95": round(float(np.percentile(ts, 95)) * 1e6, 1),
+                      "device_path": "ReadPlan.run_device: probe+scan, gather copy, prepared decode; one wait",
+                      "us_per_read_device_unprepared_median": round(float(np.median(tu)) * 1e6, 1),
                       "us_per_read_host_median": round(float(np.median(th)) * 1e6, 1),
                       "GiB_s_arrow_out_device": round(out_bytes / med / GIB, 3),
-                      "kernels": "index_probe/gather_scan, gather_copy, " + ctx.last_kernel(), **ipc_res}))
+                      "host_path": "ResidentTable.read: Python keys -> Arrow -> ReadPlan.run -> RecordBatch",
+                      "kernels": "gather_probe_scan, gather_copy, murr_jit_decode (+ copy_segs_kernel on the host path)",
+                      **ipc_res}))
 
 
 def sst_blocks(rows: int, comp: int, block_size: int = 512):
@@ -1176,9 +1294,12 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--pmc-csv", default=None)
     ap.add_argument("--lanes", type=int, default=None, choices=[1, 2, 3, 4],
-                    help="decode: 2 = the alternating output sets' plans on two contexts (two streams), "
-                         "so a launch starts on the CUs the previous one's tail leaves; default 2 for "
-                         "--config D, else 1")
+                    help="decode: the headline's lanes (tuning A/Bs only; default 1 for every config: the line "
+                         "is per launch).  L > 1 = L contexts (streams), so a launch starts on the CUs the "
+                         "previous one's tail leaves")
+    ap.add_argument("--extra-lanes", type=int, default=3,
+                    help="decode: after the one-lane headline, the same steps over this many lanes, every lane's "
+                         "last output verified, reported as `lanes` (0 or 1: skip)")
     ap.add_argument("--sync-steps", action="store_true",
                     help="one plan, each step waited for before the next is launched (A/B of the pipelined loop)")
     ap.add_argument("--no-traffic", action="store_true",

@@ -32,7 +32,12 @@
 extern "C" {
 #endif
 
-#define MURR_ABI_VERSION 1
+/* ABI version.  2 (round 5): murr_block_t grew row_off32 (32 -> 40 bytes) and
+ * murr_opts_t.balance became `reserved` (must be 0).  A binding checks
+ * murr_abi_version() against the version it was written for before passing
+ * any descriptor array, so a stale caller fails fast
+ * instead of handing over arrays of the old stride. */
+#define MURR_ABI_VERSION 2
 
 /* DTypeName, same members and order as src/core/schema.rs:6-19. */
 typedef enum {
@@ -192,7 +197,11 @@ int murr_jit_cache_limit(uint32_t max_layouts, uint32_t* limit, uint32_t* cached
 /* Device memory.  murr_dev_free also takes the device outputs the library
  * allocates for the caller (murr_sst_decode): those go back to the context's
  * reuse cache (at most 1 GiB, released by murr_ctx_destroy) for its next
- * call; anything else is freed. */
+ * call; anything else is freed.  A cached buffer is handed out again only
+ * after a device synchronisation that follows its free, so work queued before
+ * the free on any stream of the device (another context's scan of an adopted
+ * arena, the caller's own) has finished reading it -- the guarantee hipFree
+ * gives. */
 int murr_dev_alloc(murr_ctx_t* ctx, uint64_t bytes, void** p);
 int murr_dev_free(murr_ctx_t* ctx, void* p);
 int murr_host_alloc(murr_ctx_t* ctx, uint64_t bytes, void** p); /* pinned */
@@ -240,9 +249,10 @@ typedef struct {
 } murr_block_t;
 
 /* u64 row offsets -> u32 (device, n_rows + 1 entries each; `out` 4-byte
- * aligned).  Fails with MURR_E_OFFSET_OVERFLOW when row_off[n_rows] >= 2^32
- * (offsets are non-decreasing, so the last one bounds them all).  Enqueued on
- * the context's stream after one 8-byte read-back of row_off[n_rows]. */
+ * aligned).  Every offset is checked on the device: MURR_E_OFFSET_OVERFLOW
+ * when one is >= 2^32, MURR_E_MALFORMED_ROW when one is below its predecessor
+ * (`out` then holds unspecified values).  One kernel and a 4-byte read-back
+ * on the context's stream; returns once `out` is written. */
 int murr_row_off_narrow(murr_ctx_t* ctx, const uint64_t* row_off, uint64_t n_rows, uint32_t* out);
 
 /* One output Arrow array (device pointers), arrow-rs 58 builder layout:
@@ -622,6 +632,35 @@ int murr_reader_read(murr_reader_t* r, const murr_index_t* idx, const uint8_t* b
                      murr_host_array_t* outs, murr_error_t* err);
 void murr_reader_free(murr_reader_t* r);
 
+/* Prepared resident read: Table::read (src/io/table/mod.rs:114-129 over
+ * src/io/store/memory.rs:28-45) repeated with one projection and at most
+ * `cap` keys -- the loop of benches/read_block.rs / read_plain.rs.  Made once
+ * per (table state, projection, capacity): the gather's device work area, the
+ * decode's outputs and its prepared launch (descriptors resident, counters
+ * handed to pinned memory by the kernel), pinned key staging and arrays.  A
+ * run enqueues lookup + gather + decode (+ the arrays to pinned memory) on the
+ * ctx stream and waits once: no descriptor upload, no read-back copy, no copy
+ * engine; host keys are read by the probe in place.  A run of nq <= cap keys
+ * decodes cap rows (queries past nq are misses) and reports nq.  The table's
+ * arena, row offsets and index must not change while the plan lives (a write
+ * that appends invalidates it).  Fails with MURR_E_ARGUMENT when cap x
+ * max_row passes 64 MiB (murr_reader_read sizes such reads exactly). */
+typedef struct murr_read_plan murr_read_plan_t;
+int murr_read_plan_new(murr_ctx_t* ctx, const murr_segment_t* seg, const murr_index_t* idx,
+                       const uint8_t* blob, const uint64_t* row_off, uint64_t blob_bytes,
+                       uint64_t max_row, const uint32_t* proj, uint32_t nproj, uint64_t cap,
+                       murr_read_plan_t** out);
+/* Keys in device memory (q_offsets[nq + 1], q_data); outs[nproj] are device
+ * arrays in the plan's buffers (n = nq), valid until its next run or free. */
+int murr_read_plan_run_device(murr_read_plan_t* plan, const uint8_t* q_data, const int32_t* q_offsets,
+                              uint64_t nq, murr_array_t* outs, murr_error_t* err);
+/* Keys on the host (Arrow utf8 from key_offset); outs[nproj] point into the
+ * plan's pinned memory, valid until its next run or free.  Synchronous. */
+int murr_read_plan_run(murr_read_plan_t* plan, const uint8_t* key_data, const int32_t* key_offsets,
+                       uint64_t key_offset, uint64_t nq, murr_host_array_t* outs, murr_error_t* err);
+uint64_t murr_read_plan_capacity(const murr_read_plan_t* plan);
+void murr_read_plan_free(murr_read_plan_t* plan);
+
 /* ---- RocksDB data blocks --------------------------- */
 
 /* The data blocks of the block-based SSTs the reference's store writes
@@ -716,6 +755,55 @@ uint64_t murr_ipc_eos(uint8_t* out);
 
 /* Human-readable name of a status code. */
 const char* murr_status_str(int status);
+
+/* MURR_ABI_VERSION of the library (see the define above). */
+uint32_t murr_abi_version(void);
+
+/* ---- Arrow C Data Interface export ------------------------------------------- */
+
+/* The Arrow C Data Interface (arrow/c/abi.h), as arrow-rs' `ffi` module and
+ * pyarrow define it. */
+#ifndef ARROW_C_DATA_INTERFACE
+#define ARROW_C_DATA_INTERFACE
+#define ARROW_FLAG_DICTIONARY_ORDERED 1
+#define ARROW_FLAG_NULLABLE 2
+#define ARROW_FLAG_MAP_KEYS_SORTED 4
+struct ArrowSchema {
+    const char* format;
+    const char* name;
+    const char* metadata;
+    int64_t flags;
+    int64_t n_children;
+    struct ArrowSchema** children;
+    struct ArrowSchema* dictionary;
+    void (*release)(struct ArrowSchema*);
+    void* private_data;
+};
+struct ArrowArray {
+    int64_t length;
+    int64_t null_count;
+    int64_t offset;
+    int64_t n_buffers;
+    int64_t n_children;
+    const void** buffers;
+    struct ArrowArray** children;
+    struct ArrowArray* dictionary;
+    void (*release)(struct ArrowArray*);
+    void* private_data;
+};
+#endif
+
+/* A read's host arrays (all of one length: a build()'s, a reader's, a prepared
+ * read's) as the RecordBatch ReadBatchBuilder::build returns
+ * (src/io/row/read.rs:100-110): a struct array of nullable fields named
+ * names[i] (Arrow C format per dtype: "u" utf8, "b" bool, "c"/"s"/"i"/"l"
+ * int8-64, "C"/"S"/"I"/"L" uint8-64, "f"/"g" float32/64), for
+ * arrow::ffi::from_ffi / pyarrow RecordBatch._import_from_c in one call.
+ * The export owns a compacted copy of the bytes (the arrays' pinned memory is
+ * reused by the next read); its release callbacks free it.  Validity is
+ * exported only when null_count > 0.  Host only. */
+int murr_arrow_export(const murr_host_array_t* arrays, uint32_t n, const char* const* names,
+                      struct ArrowArray* out_array, struct ArrowSchema* out_schema);
 
 #ifdef __cplusplus
 }

@@ -12,6 +12,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 # MURR_LIB: load another build of the same library (the tuning build of
 # tools/); announced on stderr whenever it is set, so no run swaps it in silently
+ABI_VERSION = 2  # include/murr_codec.h MURR_ABI_VERSION
 LIB_PATH = os.environ.get("MURR_LIB") or os.path.join(HERE, "libmurr_codec.so")
 HEADER = os.path.join(ROOT, "include", "murr_codec.h")
 PLAN_TIME_EVERY = 4  # MURR_PLAN_TIME_EVERY: a prepared plan times one run in this many
@@ -53,6 +54,20 @@ class Block(C.Structure):
     """murr_block_t: row_off (u64), or row_off32 (u32) when set."""
     _fields_ = [("data", C.c_void_p), ("row_off", C.c_void_p), ("n_rows", C.c_uint64),
                 ("data_bytes", C.c_uint64), ("row_off32", C.c_void_p)]
+
+
+class ArrowSchema(C.Structure):
+    """struct ArrowSchema (Arrow C Data Interface, include/murr_codec.h)."""
+    _fields_ = [("format", C.c_char_p), ("name", C.c_char_p), ("metadata", C.c_char_p), ("flags", C.c_int64),
+                ("n_children", C.c_int64), ("children", C.c_void_p), ("dictionary", C.c_void_p),
+                ("release", C.c_void_p), ("private_data", C.c_void_p)]
+
+
+class ArrowArray(C.Structure):
+    """struct ArrowArray (Arrow C Data Interface, include/murr_codec.h)."""
+    _fields_ = [("length", C.c_int64), ("null_count", C.c_int64), ("offset", C.c_int64), ("n_buffers", C.c_int64),
+                ("n_children", C.c_int64), ("buffers", C.c_void_p), ("children", C.c_void_p),
+                ("dictionary", C.c_void_p), ("release", C.c_void_p), ("private_data", C.c_void_p)]
 
 
 class Array(C.Structure):
@@ -103,6 +118,8 @@ U32, U64, I32 = C.c_uint32, C.c_uint64, C.c_int
 
 # name -> (restype, argtypes); mirrors include/murr_codec.h one to one.
 SIGNATURES = {
+    "murr_abi_version": (U32, []),
+    "murr_arrow_export": (I32, [C.POINTER(HostArray), U32, C.POINTER(C.c_char_p), P, P]),
     "murr_dtype_size": (I32, [U32]),
     "murr_segment_init": (I32, [C.POINTER(U32), U32, C.POINTER(Column), C.POINTER(Segment)]),
     "murr_segment_prepare": (I32, [P, C.POINTER(Segment)]),
@@ -177,6 +194,11 @@ SIGNATURES = {
     "murr_reader_read": (I32, [P, P, P, P, U64, U64, P, P, U64, U64, C.POINTER(U32), U32,
                                C.POINTER(HostArray), C.POINTER(Error)]),
     "murr_reader_free": (None, [P]),
+    "murr_read_plan_new": (I32, [P, C.POINTER(Segment), P, P, P, U64, U64, C.POINTER(U32), U32, U64, PP]),
+    "murr_read_plan_run_device": (I32, [P, P, P, U64, C.POINTER(Array), C.POINTER(Error)]),
+    "murr_read_plan_run": (I32, [P, P, P, U64, U64, C.POINTER(HostArray), C.POINTER(Error)]),
+    "murr_read_plan_capacity": (U64, [P]),
+    "murr_read_plan_free": (None, [P]),
     "murr_encode_host": (I32, [P, C.POINTER(Segment), C.POINTER(HostColIn), U64,
                                C.POINTER(C.POINTER(C.c_uint8)), C.POINTER(U64),
                                C.POINTER(C.POINTER(C.c_uint64)), C.POINTER(Error)]),
@@ -227,6 +249,9 @@ def lib():
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
+        got = L.murr_abi_version()
+        if got != ABI_VERSION:  # descriptor strides differ: never pass arrays across versions
+            raise ImportError(f"{LIB_PATH}: ABI version {got}, this binding expects {ABI_VERSION}")
         _lib = L
     return _lib
 

@@ -69,6 +69,12 @@ struct murr_ctx {
     // kDevCacheMax bytes.  Which pointers are such outputs: g_dcached.
     std::multimap<uint64_t, void*> dfree;
     uint64_t dfree_bytes = 0;
+    // some buffer entered dfree since the last device synchronisation: work
+    // queued before its free (on any stream of the device: another context's
+    // scan reading an adopted SST arena, the caller's own) may still read it,
+    // so the next reuse first waits for the device, as the hipFree it
+    // replaces did
+    bool dfree_unsynced = false;
     int device = 0;
     int cus = 256;
     int enc_grid_per_cu = 1;
@@ -169,6 +175,12 @@ hipError_t dev_alloc_cached(murr_ctx* c, uint64_t bytes, void** out) {
     std::lock_guard<std::mutex> lk(g_dc_mu);
     auto it = c->dfree.lower_bound(bytes);
     if (it != c->dfree.end() && it->first <= 2 * bytes + (1u << 20)) {
+        if (c->dfree_unsynced) {
+            // every buffer freed so far: its readers queued before the free are done
+            const hipError_t se = hipDeviceSynchronize();
+            if (se != hipSuccess) return se;
+            c->dfree_unsynced = false;
+        }
         *out = it->second;
         c->dfree_bytes -= it->first;
         c->dfree.erase(it);
@@ -201,6 +213,7 @@ bool dev_free_cached(murr_ctx* c, void* p) {
     }
     c->dfree.emplace(it->second.second, p);
     c->dfree_bytes += it->second.second;
+    c->dfree_unsynced = true;
     while (c->dfree_bytes > kDevCacheMax && !c->dfree.empty()) {  // the largest go first
         auto last = std::prev(c->dfree.end());
         c->dfree_bytes -= last->first;
@@ -684,6 +697,8 @@ int murr_index_gather_copy(murr_ctx_t* c, const uint32_t* rows, uint64_t nq, con
     return MURR_OK;
 }
 
+uint32_t murr_abi_version(void) { return MURR_ABI_VERSION; }
+
 const char* murr_status_str(int s) {
     switch (s) {
     case MURR_OK: return "ok";
@@ -905,11 +920,21 @@ int murr_row_off_narrow(murr_ctx_t* c, const uint64_t* row_off, uint64_t n_rows,
     murr_error_t* err = nullptr;
     if (!c || !row_off || !out || ((uintptr_t)out & 3) || c->pending) return MURR_E_ARGUMENT;
     HIPC(hipSetDevice(c->device));
-    uint64_t last = 0;  // offsets never decrease: the last one bounds them all
-    HIPC(hipMemcpyAsync(&last, row_off + n_rows, 8, hipMemcpyDeviceToHost, c->stream));
+    // the kernel checks every offset (a malformed block's interior
+    // offset past 2^32 or below its predecessor is an error, never truncated);
+    // its flag word comes back with one 4-byte read-back
+    int st = ensure_ws(c, 64, err);
+    if (st) return st;
+    st = ensure_hs(c, 64, err);
+    if (st) return st;
+    unsigned int* bad = (unsigned int*)c->ws;
+    HIPC(hipMemsetAsync(bad, 0, 4, c->stream));
+    HIPC(launch_row_off_narrow(row_off, out, n_rows + 1, bad, c->stream));
+    HIPC(hipMemcpyAsync(c->hs, bad, 4, hipMemcpyDeviceToHost, c->stream));
     HIPC(hipStreamSynchronize(c->stream));
-    if (last > 0xFFFFFFFFull) return MURR_E_OFFSET_OVERFLOW;
-    HIPC(launch_row_off_narrow(row_off, out, n_rows + 1, c->stream));
+    const unsigned int f = *(const volatile unsigned int*)c->hs;
+    if (f & 1u) return MURR_E_OFFSET_OVERFLOW;
+    if (f & 2u) return MURR_E_MALFORMED_ROW;
     return MURR_OK;
 }
 
@@ -3203,6 +3228,304 @@ void murr_reader_free(murr_reader_t* r) {
     delete r;
 }
 
+}  // extern "C"
+
+// ---- prepared resident read (murr_read_plan_*) ------------------------------
+// Table::read repeated with one projection and key-count class over a
+// resident table (src/io/table/mod.rs:114-129 over src/io/store/memory.rs:
+// 28-45, the shape benches/read_block.rs / read_plain.rs loop).  Made once:
+// the gather's device work area, the decode's output buffers and its prepared
+// launch (murr_decode_plan: descriptors and kernel arguments resident, the
+// counters handed to pinned host memory by the kernel's last workgroup),
+// pinned key staging and pinned arrays.  A run enqueues on the context's
+// stream: lookup + gather (the probe reads host keys straight from pinned
+// memory: no key copy), the decode, and (host variant) one segment-copy kernel
+// of the arrays into pinned memory; then waits once.  No descriptor upload, no
+// counter read-back copy, no copy engine.  A run of nq <= cap keys decodes cap
+// rows: queries [nq, cap) are misses without a lookup (empty rows), and the
+// arrays are reported at nq rows.
+
+constexpr uint32_t kReadIxStride = 64;  // (the smallest index stride; the decode cuts at whole tiles)
+
+struct murr_read_plan {
+    murr_ctx* ctx = nullptr;
+    std::vector<murr_column_t> cols;
+    murr_segment_t seg{};
+    std::vector<uint32_t> proj;
+    std::vector<uint32_t> dtypes;
+    const murr_index_t* x = nullptr;
+    const uint8_t* blob = nullptr;
+    const uint64_t* row_off = nullptr;
+    uint64_t cap = 0, data_cap = 0, utf8_cap = 0;
+    uint8_t* dwork = nullptr;  // device: gather offsets (cap+1) | rows (cap) | needed | gathered rows
+    uint64_t dwork_cap = 0;
+    uint64_t* doff = nullptr;
+    uint32_t* drows = nullptr;
+    uint64_t* dneed = nullptr;
+    uint8_t* ddata = nullptr;
+    uint8_t* hkeys = nullptr;  // pinned: rebased key offsets (cap + 1), then the key bytes
+    uint64_t hkeys_cap = 0;
+    HostOut out;
+    std::vector<CopySeg> d2h;  // the arrays into pinned memory (host runs)
+    bool ix = false;           // the layout has utf8 columns: the gathered block gets a utf8 index
+    Utf8IndexArgs ua{};        //   (murr_utf8_index's kernels over it), so the decode cuts it into
+                               //   virtual blocks of a tile each, one pass, instead of split mode
+    murr_plan* dplan = nullptr;
+    hipEvent_t ev = nullptr;
+};
+
+namespace {
+int read_plan_gather(murr_read_plan* r, const uint8_t* q_data, const int32_t* q_off, uint64_t nq) {
+    murr_ctx* c = r->ctx;
+    murr_error_t* err = nullptr;
+    const uint64_t groups = gather_scan_groups(r->cap);
+    if (const int st = ensure_aux(c, groups + 1, err)) return st;
+    IndexArgs a = index_args(r->x, q_data, q_off, r->cap);
+    a.nq_live = nq;  // (>= 1: a run of no keys launches nothing)
+    a.rows = r->drows;
+    a.blob = r->blob;
+    a.row_off = r->row_off;
+    a.sizes = r->doff;
+    a.out = r->ddata;
+    a.out_cap = r->data_cap;
+    a.needed = r->dneed;
+    a.scratch = c->aux;
+    HIPC(launch_gather(a, c->stream));
+    if (r->ix) HIPC(launch_utf8_index(r->ua, c->stream));
+    return MURR_OK;
+}
+
+// The plan's arrays at nq rows (padding rows are misses: null in every column).
+void read_plan_report(const murr_read_plan* r, uint64_t nq, murr_array_t* dev, murr_host_array_t* host) {
+    const uint64_t pad = r->cap - nq;
+    for (size_t p = 0; p < r->proj.size(); p++) {
+        const murr_array_t& a = r->out.arr[p];
+        const uint32_t d = r->dtypes[p];
+        const uint64_t nulls = a.null_count >= pad ? a.null_count - pad : 0;
+        const uint64_t vlen = d == MURR_UTF8 ? a.data_len : d == MURR_BOOL ? (nq + 7) / 8 : nq * (uint64_t)dtype_size(d);
+        if (dev) {
+            dev[p] = a;
+            dev[p].null_count = nulls;
+            dev[p].data_len = vlen;
+        }
+        if (host) {
+            murr_host_array_t& h = host[p];
+            h.values = r->out.hout + r->out.off[3 * p];
+            h.validity = nulls ? r->out.hout + r->out.off[3 * p + 1] : nullptr;
+            h.offsets = a.offsets ? (const int32_t*)(r->out.hout + r->out.off[3 * p + 2]) : nullptr;
+            h.length = nq;
+            h.null_count = nulls;
+            h.values_len = vlen;
+            h.dtype = d;
+            h._pad = 0;
+        }
+    }
+}
+}  // namespace
+
+extern "C" {
+
+int murr_read_plan_new(murr_ctx_t* c, const murr_segment_t* seg, const murr_index_t* x, const uint8_t* arena,
+                       const uint64_t* row_off, uint64_t arena_bytes, uint64_t max_row, const uint32_t* proj,
+                       uint32_t nproj, uint64_t cap, murr_read_plan_t** out) {
+    murr_error_t* err = nullptr;
+    if (!out) return MURR_E_ARGUMENT;
+    *out = nullptr;
+    if (!c || !x || !valid_segment(seg) || !row_off || !proj || !nproj || !cap || cap >= kMissing ||
+        x->device != c->device || c->pending || (x->n && !arena))
+        return MURR_E_ARGUMENT;
+    for (uint32_t p = 0; p < nproj; p++)
+        if (proj[p] >= seg->ncols) return MURR_E_BAD_COLUMN;
+    const uint64_t fixed = (uint64_t)seg->bitset_size + seg->capacity;
+    const uint64_t data_cap = std::max<uint64_t>(cap * max_row, 16);
+    if (data_cap > kTwoPhaseBytes) return MURR_E_ARGUMENT;  // (such reads size their gather exactly: murr_reader_read)
+    HIPC(hipSetDevice(c->device));
+    std::unique_ptr<murr_read_plan, void (*)(murr_read_plan*)> r(new (std::nothrow) murr_read_plan(),
+                                                                 [](murr_read_plan* q) { murr_read_plan_free(q); });
+    if (!r) return MURR_E_INTERNAL;
+    r->ctx = c;
+    r->cols.assign(seg->cols, seg->cols + seg->ncols);
+    r->seg = *seg;
+    r->seg.cols = r->cols.data();
+    r->proj.assign(proj, proj + nproj);
+    for (uint32_t p = 0; p < nproj; p++) r->dtypes.push_back(seg->cols[proj[p]].dtype);
+    r->x = x;
+    r->blob = arena;
+    r->row_off = row_off;
+    r->cap = cap;
+    r->data_cap = data_cap;
+    r->utf8_cap = max_row > fixed ? cap * (max_row - fixed) : 0;
+    // the gathered block's utf8 index (stride kReadIxStride): its string
+    // bytes before every kReadIxStride-th row, per utf8 column
+    Utf8IndexArgs& ua = r->ua;
+    for (uint32_t i = 0; i < seg->ncols; i++) {
+        if (seg->cols[i].dtype != MURR_UTF8 || ua.nu == kMaxUidxCols) continue;
+        ua.col[ua.nu] = seg->cols[i].index;
+        ua.fo[ua.nu] = seg->bitset_size + seg->cols[i].offset;
+        ua.nu++;
+    }
+    uint32_t nu_layout = 0;
+    for (uint32_t i = 0; i < seg->ncols; i++) nu_layout += seg->cols[i].dtype == MURR_UTF8;
+    r->ix = nu_layout && nu_layout == ua.nu;  // (more utf8 columns than the index kernel takes: split mode)
+    const uint64_t nwin = utf8_index_windows(0, cap, kReadIxStride);
+    const uint64_t ix_bytes = r->ix ? 8 * ((cap + kReadIxStride - 1) / kReadIxStride + 1) * ua.nu : 0;
+    const uint64_t part_bytes = r->ix ? 8 * std::max<uint64_t>(nwin, 1) * ua.nu : 0;
+    // device work: offsets | rows | needed | utf8 index | its scratch | gathered rows (16-B aligned)
+    const uint64_t o_rows = round_up((cap + 1) * 8, 256), o_need = round_up(o_rows + cap * 4, 256),
+                   o_ix = o_need + 256, o_part = round_up(o_ix + ix_bytes, 256),
+                   o_data = round_up(o_part + part_bytes, 256);
+    if (!grow_dev(c, &r->dwork, &r->dwork_cap, o_data + data_cap + 16)) return MURR_E_HIP;
+    r->doff = (uint64_t*)r->dwork;
+    r->drows = (uint32_t*)(r->dwork + o_rows);
+    r->dneed = (uint64_t*)(r->dwork + o_need);
+    r->ddata = r->dwork + o_data;
+    ua.data = r->ddata;
+    ua.row_off = r->doff;
+    ua.out = (uint64_t*)(r->dwork + o_ix);
+    ua.part = (uint64_t*)(r->dwork + o_part);
+    ua.n = cap;
+    ua.stride = kReadIxStride;
+    ua.bs = seg->bitset_size;
+    // arrays: the fixed-size parts first (values, validity, utf8 offsets), then
+    // the utf8 bytes, so the D2H is one segment plus one per utf8 column
+    HostOut& o = r->out;
+    const uint64_t bm = murr_bitmap_bytes(cap);
+    o.off.assign((size_t)nproj * 3, 0);
+    uint64_t off = 0;
+    for (uint32_t p = 0; p < nproj; p++) {
+        const murr_column_t& col = seg->cols[proj[p]];
+        if (col.dtype != MURR_UTF8) {
+            o.off[3 * p] = off;
+            off = round_up(off + std::max<uint64_t>(col.dtype == MURR_BOOL ? bm : cap * col.size, 8), 64);
+        }
+        o.off[3 * p + 1] = off;
+        off = round_up(off + std::max<uint64_t>(bm, 8), 64);
+        if (col.dtype == MURR_UTF8) {
+            o.off[3 * p + 2] = off;
+            off = round_up(off + (cap + 1) * 4, 64);
+        }
+    }
+    const uint64_t fixed_out = std::max<uint64_t>(off, 64);
+    for (uint32_t p = 0; p < nproj; p++)
+        if (seg->cols[proj[p]].dtype == MURR_UTF8) {
+            o.off[3 * p] = off;
+            off = round_up(off + std::max<uint64_t>(r->utf8_cap, 8), 64);
+        }
+    const uint64_t total_out = std::max<uint64_t>(off, 64);
+    if (!grow_dev(c, &o.dout, &o.dout_cap, total_out) || !grow_pinned(c, &o.hout, &o.hout_cap, total_out, 0))
+        return MURR_E_HIP;
+    o.arr.assign(nproj, murr_array_t{});
+    r->d2h.assign({CopySeg{o.dout, o.hout, fixed_out, nullptr}});
+    for (uint32_t p = 0; p < nproj; p++) {
+        murr_array_t& a = o.arr[p];
+        a.values = o.dout + o.off[3 * p];
+        a.validity = o.dout + o.off[3 * p + 1];
+        a.offsets = seg->cols[proj[p]].dtype == MURR_UTF8 ? (int32_t*)(o.dout + o.off[3 * p + 2]) : nullptr;
+        a.values_cap = r->utf8_cap;
+        if (a.offsets)  // exactly the decoded bytes: the length is the final offset, read on the device
+            r->d2h.push_back(CopySeg{o.dout + o.off[3 * p], o.hout + o.off[3 * p], r->utf8_cap, a.offsets + cap});
+    }
+    // the decode, prepared over the gather's block (its tile-sizing hint: the
+    // table's mean row x cap; rows end at doff[cap], never read past)
+    const uint64_t mean = x->n ? arena_bytes / x->n : fixed;
+    murr_block_t blk{r->ddata, r->doff, cap, std::min<uint64_t>(data_cap, std::max<uint64_t>(16, mean * cap)), nullptr};
+    const uint64_t* ux[1] = {ua.out};
+    int st = murr_decode_plan(c, &r->seg, r->proj.data(), nproj, &blk, 1, r->ix ? ux : nullptr,
+                              r->ix ? kReadIxStride : 0, o.arr.data(), &r->dplan);
+    if (st) return st;
+    (void)murr_plan_time_every(r->dplan, 0);  // (no timing events between the run's kernels)
+    HIPC(hipEventCreateWithFlags(&r->ev, hipEventDisableTiming));
+    *out = r.release();
+    return MURR_OK;
+}
+
+int murr_read_plan_run_device(murr_read_plan_t* r, const uint8_t* q_data, const int32_t* q_offsets, uint64_t nq,
+                              murr_array_t* outs, murr_error_t* err) {
+    if (err) std::memset(err, 0, sizeof *err);
+    if (!r || !outs || nq > r->cap || (nq && (!q_data || !q_offsets))) return set_err(err, MURR_E_ARGUMENT);
+    murr_ctx* c = r->ctx;
+    if (c->pending) return set_err(err, MURR_E_ARGUMENT);
+    if (!nq) {  // no keys: empty arrays, nothing launched
+        for (size_t p = 0; p < r->proj.size(); p++) {
+            outs[p] = r->out.arr[p];
+            outs[p].null_count = outs[p].data_len = 0;
+        }
+        return MURR_OK;
+    }
+    HIPC(hipSetDevice(c->device));
+    int st = read_plan_gather(r, q_data, q_offsets, nq);
+    if (st) return set_err(err, st);
+    st = murr_decode_run_async(r->dplan);
+    if (st) return set_err(err, st);
+    st = murr_decode_run_wait(r->dplan, err);
+    if (st) return st;
+    read_plan_report(r, nq, outs, nullptr);
+    return MURR_OK;
+}
+
+int murr_read_plan_run(murr_read_plan_t* r, const uint8_t* key_data, const int32_t* key_offsets, uint64_t key_offset,
+                       uint64_t nq, murr_host_array_t* outs, murr_error_t* err) {
+    if (err) std::memset(err, 0, sizeof *err);
+    if (!r || !outs || nq > r->cap || (nq && (!key_data || !key_offsets))) return set_err(err, MURR_E_ARGUMENT);
+    murr_ctx* c = r->ctx;
+    if (c->pending) return set_err(err, MURR_E_ARGUMENT);
+    if (!nq) {  // no keys: empty arrays, nothing launched
+        for (size_t p = 0; p < r->proj.size(); p++)
+            outs[p] = murr_host_array_t{r->out.hout, nullptr, r->out.arr[p].offsets ? (const int32_t*)r->out.hout : nullptr,
+                                        0, 0, 0, r->dtypes[p], 0};
+        std::memset(r->out.hout, 0, 8);  // (the one offset of an empty utf8 array: 0)
+        return MURR_OK;
+    }
+    HIPC(hipSetDevice(c->device));
+    // keys: rebased offsets + bytes in pinned staging, read by the probe in place
+    const int32_t k0 = nq ? key_offsets[key_offset] : 0;
+    const uint64_t kbytes = nq ? (uint64_t)(key_offsets[key_offset + nq] - k0) : 0;
+    const uint64_t offb = round_up((nq + 1) * 4, 64);
+    if (!grow_pinned(c, &r->hkeys, &r->hkeys_cap, offb + round_up(kbytes, 16) + 16, 0)) return set_err(err, MURR_E_HIP);
+    int32_t* ho = (int32_t*)r->hkeys;
+    ho[0] = 0;
+    for (uint64_t i = 1; i <= nq; i++) ho[i] = key_offsets[key_offset + i] - k0;
+    if (kbytes) std::memcpy(r->hkeys + offb, key_data + k0, kbytes);
+    std::atomic_thread_fence(std::memory_order_seq_cst);
+    int st = read_plan_gather(r, r->hkeys + offb, ho, nq);
+    if (st) return set_err(err, st);
+    st = murr_decode_run_async(r->dplan);
+    if (st) return set_err(err, st);
+    // the arrays into pinned memory, queued behind the decode on the same stream
+    HIPC(launch_copy_segs(r->d2h.data(), (uint32_t)r->d2h.size(), kCopyGridOut, c->stream));
+    HIPC(hipEventRecord(r->ev, c->stream));
+    st = murr_decode_run_wait(r->dplan, err);
+    if (st) {
+        (void)hipEventSynchronize(r->ev);
+        return st;
+    }
+    HIPC(hipEventSynchronize(r->ev));
+    read_plan_report(r, nq, nullptr, outs);
+    return MURR_OK;
+}
+
+uint64_t murr_read_plan_capacity(const murr_read_plan_t* r) { return r ? r->cap : 0; }
+
+void murr_read_plan_free(murr_read_plan_t* r) {
+    if (!r) return;
+    murr_ctx* c = r->ctx;
+    if (c) {
+        (void)hipSetDevice(c->device);
+        (void)hipStreamSynchronize(c->stream);
+    }
+    if (r->dplan) murr_plan_free(r->dplan);
+    if (r->ev) (void)hipEventDestroy(r->ev);
+    pool_give(c, true, r->hkeys, r->hkeys_cap);
+    pool_give(c, false, r->dwork, r->dwork_cap);
+    pool_give(c, true, r->out.hout, r->out.hout_cap);
+    pool_give(c, false, r->out.dout, r->out.dout_cap);
+    delete r;
+}
+
+}  // extern "C"
+
+extern "C" {
+
 // ---- RocksDB data blocks (murr_sst.hip) --------------
 
 void murr_sst_result_free(murr_ctx_t* c, murr_sst_result_t* r) {
@@ -3210,7 +3533,10 @@ void murr_sst_result_free(murr_ctx_t* c, murr_sst_result_t* r) {
     if (c) (void)hipSetDevice(c->device);
     for (void* p : {(void*)r->keys, (void*)r->key_offsets, (void*)r->values, (void*)r->value_offsets,
                     (void*)r->seqs, (void*)r->types})
-        if (p && !(c && dev_free_cached(c, p))) (void)hipFree(p);
+        if (p && !(c && dev_free_cached(c, p))) {
+            dev_forget(p);  // (no context: a recorded output is released, and its record with it)
+            (void)hipFree(p);
+        }
     std::memset(r, 0, sizeof *r);
 }
 

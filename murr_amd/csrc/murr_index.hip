@@ -190,8 +190,13 @@ __global__ void __launch_bounds__(256) index_seq(IndexArgs A, const uint64_t* se
         __hip_atomic_fetch_max(gp(win) + s, (unsigned long long)(i + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Row of query i, or kMissing.
-__device__ __forceinline__ uint32_t probe_one(const IndexArgs& A, uint64_t i) {
+// Row of query i, or kMissing.  With `size` (a gather): the row's blob
+// length too, its two row offsets loaded beside the candidate's key bytes --
+// a tag match is the row with near certainty, so the lengths need no round
+// trip of their own after the compare (query key, slot + location, stored key
+// and row offsets: three dependent round trips, not four).
+template <bool SIZED = false>
+__device__ __forceinline__ uint32_t probe_one(const IndexArgs& A, uint64_t i, uint64_t* size = nullptr) {
     const GAS int32_t* qo = gp(A.q_off);
     const int32_t q0 = qo[i];
     const uint32_t len = (uint32_t)(qo[i + 1] - q0);
@@ -205,27 +210,37 @@ __device__ __forceinline__ uint32_t probe_one(const IndexArgs& A, uint64_t i) {
     for (uint64_t probe = 0; probe <= A.mask; probe++, s = (s + 1) & A.mask) {
         const uint64_t e = slots[s], l = loc[s];  // independent loads
         if (e == kEmpty) break;
-        if ((e >> 32) == (h >> 32) && (uint32_t)l == len &&
-            key_eq(gp(A.key_data) + (uint32_t)(l >> 32), qc, q, len)) {
-            row = (uint32_t)e;
-            break;
+        if ((e >> 32) == (h >> 32) && (uint32_t)l == len) {
+            uint64_t o0 = 0, o1 = 0;
+            if constexpr (SIZED) {
+                o0 = gp(A.row_off)[(uint32_t)e];
+                o1 = gp(A.row_off)[(uint32_t)e + 1];
+            }
+            if (key_eq(gp(A.key_data) + (uint32_t)(l >> 32), qc, q, len)) {
+                row = (uint32_t)e;
+                if constexpr (SIZED) *size = o1 - o0;
+                break;
+            }
         }
     }
     return row;
 }
 
-__device__ __forceinline__ uint64_t row_size(const IndexArgs& A, uint32_t row) {
-    return row == kMissing ? 0 : gp(A.row_off)[row + 1] - gp(A.row_off)[row];
-}
 
 // One query per thread: rows[i] = the key's row or kMissing; sizes[i] = its
 // blob length (0 for a miss) when a gather follows.
+// Queries that are looked up: [0, nq_live) when nq_live is set (a prepared
+// read padded to its capacity: the rest are misses), else all nq.
+__device__ __forceinline__ uint64_t live_queries(const IndexArgs& A) { return A.nq_live ? A.nq_live : A.nq; }
+
 __global__ void __launch_bounds__(256) index_probe(IndexArgs A) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= A.nq) return;
-    const uint32_t row = probe_one(A, i);
+    uint64_t sz = 0;
+    uint32_t row = kMissing;
+    if (i < live_queries(A)) row = A.sizes ? probe_one<true>(A, i, &sz) : probe_one(A, i);
     if (A.rows) gp(A.rows)[i] = row;
-    if (A.sizes) gp(A.sizes)[i] = row_size(A, row);
+    if (A.sizes) gp(A.sizes)[i] = sz;
 }
 
 // Exclusive scan of sizes[0..nq) in place into block row offsets, in groups
@@ -311,8 +326,8 @@ __global__ void __launch_bounds__(kScanThreads) gather_probe_scan(IndexArgs A) {
     __shared__ uint64_t s_t[kScanThreads / 64];
     const uint32_t tid = threadIdx.x;
     uint32_t row = kMissing;
-    if (tid < A.nq) row = probe_one(A, tid);
-    const uint64_t sz = tid < A.nq ? row_size(A, row) : 0;
+    uint64_t sz = 0;
+    if (tid < live_queries(A)) row = probe_one<true>(A, tid, &sz);
     uint64_t tot;
     const uint64_t ex = block_excl1024(sz, s_t, &tot);
     if (tid < A.nq) {

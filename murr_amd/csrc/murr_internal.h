@@ -299,6 +299,8 @@ struct IndexArgs {
     uint64_t* needed;           //   out (optional): unclamped block bytes
     uint64_t* scratch;          //   scan group sums
     const uint32_t* src;        // multi-shard gather: caller query -> grouped position
+    uint64_t nq_live;           // probe: queries [nq_live, nq) are misses without a lookup (a
+                                //   prepared read's padding to its capacity); 0 = all nq live
 };
 // Shards of a multi-GPU read (murr_multi_gather): arenas, row offsets and the
 // end of each shard's grouped query range.
@@ -337,7 +339,7 @@ struct CopyArgs {
 };
 hipError_t launch_copy_segs(const CopySeg* segs, uint32_t n, uint32_t grid, hipStream_t s);
 // Row offsets u64 <-> u32, n entries (murr_kernels.hip).
-hipError_t launch_row_off_narrow(const uint64_t* in, uint32_t* out, uint64_t n, hipStream_t s);
+hipError_t launch_row_off_narrow(const uint64_t* in, uint32_t* out, uint64_t n, unsigned int* bad, hipStream_t s);
 
 // Arrow IPC framing (murr_ipc.cpp, murr_ipc.hip).
 enum : uint32_t { kIpcValidity = 0, kIpcOffsets = 1, kIpcValues = 2 };

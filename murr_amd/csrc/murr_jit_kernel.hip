@@ -681,25 +681,74 @@ constexpr uint32_t NRA = (FIX + 3) / 4;
 #define MJ_WINMAX 32
 #endif
 constexpr bool WIN = NRA <= MJ_WINMAX;
-constexpr uint32_t NRW = WIN ? NRA : (BS + 3) / 4;  // dwords kept per row
 constexpr uint32_t NBW = (BS + 3) / 4;              // bitset dwords
+// Extended window (round 6, narrow layouts with a utf8 column): the window
+// also covers the first utf8 payload's length word and 8 string bytes (row
+// bytes [0, FIX + 12)).  A row whose first utf8 column is not null has its
+// payload right after the static region (write.rs:40-49: payloads in column
+// order), so for such a row the length and a string of up to 8 bytes come out
+// of the window's registers: two dependent LDS round trips per chunk fewer
+// (length after window, string after the tile's prefix wait) and 6 instead of
+// 9 strided dword reads per row on config B (each a 2-way bank conflict at
+// its 18-B row stride).  Other rows (nulls, longer strings, later utf8
+// columns) read the stage as before.
+#ifndef MJ_XWIN
+#define MJ_XWIN 1
+#endif
+#ifndef MJ_XWMAX
+#define MJ_XWMAX 12
+#endif
+// Ablations (tuning only): MJ_ABL_LDSX re-reads the window (read_window);
+// MJ_ABL_LOADONLY skips the decode, so the decode waves only pass the tile
+// barriers behind the loader (the production ring's own ceiling).
+#ifndef MJ_ABL_LDSX
+#define MJ_ABL_LDSX 0
+#endif
+#ifndef MJ_ABL_LOADONLY
+#define MJ_ABL_LOADONLY 0
+#endif
+constexpr uint32_t S0 = FIX + 4;         // row byte of the first payload's string (when it is first)
+constexpr uint32_t NRX = S0 / 4 + 3;     // realigned dwords that hold row bytes [0, S0 + 8)
+constexpr bool XW = MJ_XWIN && WIN && NUTF8 >= 1 && NRX <= MJ_XWMAX;
+constexpr uint32_t NRW0 = WIN ? NRA : NBW;  // the fixed part's dwords (the window proper)
+constexpr uint32_t NRW = XW ? NRX : NRW0;   // dwords kept per row
+// row bytes the window must hold, and the aligned dwords that cover them at any shift
+constexpr uint32_t NBYTES = XW ? S0 + 8 : 4 * NRW0;
+constexpr uint32_t NRAW = (NBYTES + 3 + 3) / 4;
 
 template <class Src> DEV void read_window(const Src& src, uint32_t ra, bool ok, uint32_t (&r)[NRW]) {
-    // aligned dwords [ra & ~3, (ra & ~3) + 4 (NRW + 1)) cover the row's first
-    // 4 NRW bytes (with ok, every one of them holds a byte of the row)
+    // aligned dwords [ra & ~3, (ra & ~3) + 4 NRAW) cover the row's first
+    // NBYTES bytes (with ok, every one of the window proper's holds a byte of
+    // the row).  From HBM only the window proper (never past the row's own
+    // dwords); the extension is a stage-only read (64 B of pad behind a tile).
     const uint32_t a4 = (Src::kHbm && !ok ? 0u : ra) >> 2, sh = ra & 3u;
-    uint32_t w[NRW + 1];
+    uint32_t w[NRAW];
 #pragma unroll
-    for (uint32_t j = 0; j <= NRW; j++) {
+    for (uint32_t j = 0; j < NRAW; j++) {
         if constexpr (Src::kHbm) {
             // the last dword only when the row reaches into it
-            w[j] = (j < NRW || sh) && ok ? src.w(a4 + j) : 0u;
+            w[j] = j <= NRW0 && (j < NRW0 || sh) && ok ? src.w(a4 + j) : 0u;
         } else {
             w[j] = src.w(a4 + j);
         }
     }
+#if MJ_ABL_LDSX
+    // LDS sensitivity ablation (tuning only): every strided window dword read
+    // a second time (volatile: neither merged nor dropped) and folded in with
+    // a min of two equal values -- the window's bank conflicts and LDS cycles
+    // doubled, both reads on the chain, the data and the rest of the tile
+    // unchanged
+    if constexpr (!Src::kHbm) {
+        const volatile LAS uint32_t* vp = (const volatile LAS uint32_t*)src.s + a4;
 #pragma unroll
-    for (uint32_t j = 0; j < NRW; j++) r[j] = __builtin_amdgcn_alignbyte(w[j + 1], w[j], sh);
+        for (uint32_t j = 0; j < NRAW; j++) {
+            const uint32_t x = vp[j];
+            w[j] = w[j] < x ? w[j] : x;
+        }
+    }
+#endif
+#pragma unroll
+    for (uint32_t j = 0; j < NRW; j++) r[j] = __builtin_amdgcn_alignbyte(j + 1 < NRAW ? w[j + 1] : 0u, w[j], sh);
 }
 // Field at compile-time row byte FO (realigned window).
 template <uint32_t FO> DEV uint32_t get32(const uint32_t (&r)[NRW]) {
@@ -1238,6 +1287,10 @@ DEV void decode_tile(const Src& src, const Tile& T, const LAS uint32_t* ro, LAS 
     uint32_t upay[NU][R], ulen[NU][R], uinc[NU][R], utot[NU];
 #pragma unroll
     for (uint32_t u = 0; u < NU; u++) utot[u] = 0;
+    // extended window (XW): bit k = this lane's first utf8 payload sits right
+    // after the static region, so its length and first 8 bytes are in W.r[k]
+    constexpr bool XWS = XW && !Src::kHbm;
+    uint32_t xin = 0;
 #define MJ_U(C, W_, FO, U)                                                                              \
     if constexpr (W_ == 0) {                                                                            \
         if (MJ_SLOT(C) != kNone) {                                                                      \
@@ -1251,7 +1304,15 @@ DEV void decode_tile(const Src& src, const Tile& T, const LAS uint32_t* ro, LAS 
                 const uint32_t vlen = rl - BS; /* >= 4 when s_ok */                                     \
                 const bool p_ok = s_ok && sl <= vlen - 4;                                               \
                 const uint32_t pa = W.ra[k] + BS + sl;                                                  \
-                const uint32_t l = src.u32(Src::kHbm && !p_ok ? 0u : pa);                               \
+                uint32_t l;                                                                             \
+                if constexpr (XWS && U == 0) {                                                          \
+                    const bool xf = sl == FIX - BS; /* the first payload: in the window */              \
+                    xin |= (uint32_t)xf << k;                                                           \
+                    l = get32<FIX>(W.r[k]);                                                             \
+                    if (s_ok && !xf) l = src.u32(pa);                                                   \
+                } else {                                                                                \
+                    l = src.u32(Src::kHbm && !p_ok ? 0u : pa);                                          \
+                }                                                                                       \
                 const bool good = p_ok && l <= vlen - 4 - sl;                                           \
                 badk |= (uint32_t)(valid && !good) << k;                                                \
                 upay[U][k] = pa + 4;                                                                    \
@@ -1453,6 +1514,8 @@ DEV void decode_tile(const Src& src, const Tile& T, const LAS uint32_t* ro, LAS 
                 const uint64_t cend = base + (uint32_t)__builtin_amdgcn_readlane(uinc[U][k], 63);                 \
                 uint32_t hib = 0;                                                                       \
                 const bool regs = ERS && !late; /* the bytes are in sw (the slot is gone) */            \
+                /* XW: the string is in the window's registers (row bytes S0 ..) */                    \
+                const bool inw = XWS && U == 0 && ((xin >> k) & 1u) && n <= 8;                          \
                 if (cend <= 0x7FFFFFFFull && cend <= o.values_cap) { /* wave-uniform fast path */       \
                     if (act) ost(obf + i, (int32_t)e);                                                  \
                     if (regs) {                                                                         \
@@ -1460,6 +1523,11 @@ DEV void decode_tile(const Src& src, const Tile& T, const LAS uint32_t* ro, LAS 
                             copy_str_regs(gp(o.values) + (e - n), sw[U][k][0], sw[U][k][1], sw[U][k][2], \
                                           upay[U][k] & 3u, n);                                          \
                         hib = shib[U][k];                                                               \
+                    } else if (inw) {                                                                   \
+                        const uint32_t x0 = W.r[k][XW ? S0 / 4 : 0], x1 = W.r[k][XW ? S0 / 4 + 1 : 0];  \
+                        const uint32_t x2 = W.r[k][XW ? S0 / 4 + 2 : 0];                                \
+                        if (!MJ_ABL_NOSTR) copy_str_regs(gp(o.values) + (e - n), x0, x1, x2, S0 % 4, n); \
+                        hib = hib_regs(x0, x1, x2, S0 % 4, n);                                          \
                     } else if (n && !MJ_ABL_NOSTR) {                                                    \
                         hib = copy_str(src, gp(o.values) + (e - n), upay[U][k], n);                     \
                     }                                                                                   \
@@ -1777,7 +1845,11 @@ DEV void kernel_body() {
                     run[u] = NUTF8 && T.r0 ? sgpr64(((const CAS uint64_t*)ux)[(T.r0 >> args()->ulog) * NU + u]) : 0;
             }
         }
-        if (T.hbm == 2) {  // a tile over 4 GiB of blob bytes (unsupported): report; keep the protocol going
+        if (MJ_ABL_LOADONLY) {
+            // ablation: no decode; the totals the prefix protocol counts are
+            // still published so nothing waits on them
+            if (NUTF8 && lane == 0) __hip_atomic_fetch_add((LAS uint32_t*)ctl, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        } else if (T.hbm == 2) {  // a tile over 4 GiB of blob bytes (unsupported): report; keep the protocol going
             if (wave == 0 && lane == 0) report(args()->err, err_key(T.b, T.r0, 0, kStMalformed));
             if constexpr (ER) release_slot(freec + (it & 1), lane);
             if (NUTF8) {

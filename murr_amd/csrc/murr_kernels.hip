@@ -247,20 +247,29 @@ __global__ void __launch_bounds__(256) copy_segs_kernel(CopyArgs A) {
 }
 
 // ---- row-offset widths (murr_block_t.row_off32) -------------------------------
-// u64 -> u32 (murr_row_off_narrow; the host checked the last offset).  Both
-// decode kernels read either width natively.
+// u64 -> u32 (murr_row_off_narrow).  Both decode kernels read either width
+// natively.  Every offset is checked, not only the last (a malformed block's
+// interior offset would otherwise be truncated into a plausible row span):
+// bit 0 of *bad = some offset >= 2^32, bit 1 = some offset below its
+// predecessor.  *bad is zeroed by the host before the launch.
 __global__ void __launch_bounds__(256) narrow_kernel(const uint64_t* __restrict__ in, uint32_t* __restrict__ out,
-                                                     uint64_t n) {
-    for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256)
-        out[i] = (uint32_t)in[i];
+                                                     uint64_t n, unsigned int* __restrict__ bad) {
+    unsigned int f = 0;
+    for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
+        const uint64_t v = in[i];
+        out[i] = (uint32_t)v;
+        f |= (v >> 32) ? 1u : 0u;
+        f |= i && v < in[i - 1] ? 2u : 0u;
+    }
+    if (__any(f != 0)) atomicOr(bad, f);
 }
 
 }  // namespace
 
-hipError_t launch_row_off_narrow(const uint64_t* in, uint32_t* out, uint64_t n, hipStream_t s) {
+hipError_t launch_row_off_narrow(const uint64_t* in, uint32_t* out, uint64_t n, unsigned int* bad, hipStream_t s) {
     if (!n) return hipSuccess;
     const uint64_t g = (n + 255) / 256;
-    hipLaunchKernelGGL(narrow_kernel, dim3((uint32_t)(g < 4096 ? g : 4096)), dim3(256), 0, s, in, out, n);
+    hipLaunchKernelGGL(narrow_kernel, dim3((uint32_t)(g < 4096 ? g : 4096)), dim3(256), 0, s, in, out, n, bad);
     return hipGetLastError();
 }
 

@@ -27,7 +27,7 @@ import pyarrow as pa
 from . import _abi
 from .device import Context, DecodeOutputs, DecodePlan, DeviceBlock, decode_blocks, download_array
 from .errors import SegmentError, raise_status
-from .row import host_arrays_to_arrow
+from .row import c_names, host_arrays_to_arrow, host_arrays_to_batch
 from .schema import DTypeName, TableSchema
 from .store import Store
 from .table import Table
@@ -167,6 +167,60 @@ TWO_PHASE_BYTES = 64 << 20
 UIDX_STRIDE = 512
 
 
+def read_capacity(nq: int) -> int:
+    """The key-count class of a prepared read: 64, or the next power of two
+    (a run of nq keys decodes this many rows; the rest are misses)."""
+    return 64 if nq <= 64 else 1 << (int(nq) - 1).bit_length()
+
+
+class ReadPlan:
+    """murr_read_plan_t: Table::read of up to `cap` keys with one projection,
+    prepared once over a resident table's current state (include/murr_codec.h).
+    run(): host keys -> host arrays (pinned, valid until the next run);
+    run_device(): device keys -> device arrays.  One enqueue and one wait per
+    run, no descriptor upload and no copy engine."""
+
+    def __init__(self, rt: "ResidentTable", proj, cap: int):
+        self.ctx, self.cap, self.nproj = rt.ctx, int(cap), len(proj)
+        L = self.ctx.L
+        pj = (C.c_uint32 * len(proj))(*proj)
+        h = C.c_void_p()
+        raise_status(L.murr_read_plan_new(self.ctx.h, C.byref(rt.segment.c), rt.index.h, rt.arena.ptr,
+                                          rt.row_off.ptr, rt.used, rt.max_row, pj, len(proj), self.cap,
+                                          C.byref(h)), what="murr_read_plan_new")
+        self.h = h
+        self.host_outs = (_abi.HostArray * len(proj))()
+        self.dev_outs = (_abi.Array * len(proj))()
+        self.err = _abi.Error()
+
+    def run(self, q: pa.Array):
+        """Keys as an Arrow utf8/binary array -> the plan's host arrays."""
+        kb = q.buffers()
+        nq = len(q)
+        st = self.ctx.L.murr_read_plan_run(self.h, kb[2].address if nq and kb[2] is not None else None,
+                                           kb[1].address if nq else None, q.offset, nq, self.host_outs,
+                                           C.byref(self.err))
+        raise_status(st, self.err, "murr_read_plan_run")
+        return self.host_outs
+
+    def run_device(self, q_data: int, q_offsets: int, nq: int):
+        """Keys in device memory (Arrow utf8 layout) -> the plan's device arrays (n = nq)."""
+        st = self.ctx.L.murr_read_plan_run_device(self.h, q_data, q_offsets, nq, self.dev_outs, C.byref(self.err))
+        raise_status(st, self.err, "murr_read_plan_run_device")
+        return self.dev_outs
+
+    def close(self):
+        if self.h is not None and self.ctx.h:
+            self.ctx.L.murr_read_plan_free(self.h)
+        self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class ResidentTable:
     """Table (src/io/table/mod.rs:20-155) whose rows stay in HBM."""
 
@@ -186,13 +240,18 @@ class ResidentTable:
         self.n = 0
         self.max_row = 0
         self._reader = None    # murr_reader_t: scratch of the one-call host read
-        self._schemas = {}     # read(): Arrow schema per requested column list
+        self._schemas = {}     # read(): the field names (C strings) per requested column list
         self.uidx = None       # utf8 index of the arena (every self.stride rows), kept with every write
         self.uidx_cap = 0      # entries
         self._scan_plans = {}  # id(outs) (None: the plan's own outputs) -> (key, DecodePlan) of scan_device
+        self._read_plans = {}  # (projection, capacity) -> ReadPlan over the table state _rp_state
+        self._rp_state = None
 
     def __del__(self):
         try:
+            for p in self._read_plans.values():
+                p.close()
+            self._read_plans = {}
             if self._reader is not None and self.ctx.h:
                 self.ctx.L.murr_reader_free(self._reader)
                 self._reader = None
@@ -313,7 +372,10 @@ class ResidentTable:
         if self.index is None:
             raise SegmentError("resident table is empty")
         nq = len(keys)
-        q = pa.array([k.encode() if isinstance(k, str) else bytes(k) for k in keys], pa.binary())
+        if isinstance(keys, pa.Array):  # (an Arrow key array as it is: its bytes are what is hashed)
+            q = keys.view(pa.binary()) if pa.types.is_string(keys.type) else keys
+        else:
+            q = pa.array([k.encode() if isinstance(k, str) else bytes(k) for k in keys], pa.binary())
         qd, qo = _upload_utf8(self.ctx, q.view(pa.string()))
         offs = self.ctx.alloc((nq + 1) * 8)
         needed = self.ctx.alloc(8)
@@ -429,34 +491,68 @@ class ResidentTable:
         decode_blocks(self.ctx, self.segment, proj, [blk], outs)
         return req, [download_array(self.ctx, outs.array(0, p), int(c.dtype), nq) for p, c in enumerate(req)]
 
+    def read_plan(self, columns, nq: int) -> ReadPlan | None:
+        """The prepared read (ReadPlan) for these columns and nq keys over the
+        table as it is now: made at the first read of its key-count class
+        (read_capacity) and reused until a write changes the table.  None
+        when nq x the longest row passes TWO_PHASE_BYTES (such reads size
+        their gather exactly, murr_reader_read)."""
+        if self.index is None or nq == 0:
+            return None
+        proj = tuple(c.index for c in self._resolve(columns))
+        cap = read_capacity(nq)
+        if cap * max(self.max_row, 1) > TWO_PHASE_BYTES:
+            return None
+        state = (self.arena.ptr, self.row_off.ptr, self.n, self.used, self.max_row)
+        if state != self._rp_state:  # a write changed the table: every plan is stale
+            for p in self._read_plans.values():
+                p.close()
+            self._read_plans = {}
+            self._rp_state = state
+        plan = self._read_plans.pop((proj, cap), None)
+        if plan is None:
+            if len(self._read_plans) >= 8:  # least recently used first
+                self._read_plans.pop(next(iter(self._read_plans))).close()
+            plan = ReadPlan(self, list(proj), cap)
+        self._read_plans[(proj, cap)] = plan  # (most recently used last)
+        return plan
+
     def read(self, keys, columns) -> pa.RecordBatch:
         """Table::read (table/mod.rs:114-129) with the store lookup on the
-        device, in one native call (murr_reader_read: one H2D of the keys,
-        lookup + gather + decode, one D2H of the arrays)."""
+        device: a prepared read (ReadPlan: lookup + gather + decode + the
+        arrays to pinned memory, one enqueue and one wait), or for a read too
+        large for one (murr_reader_read) the one-call read with exact sizing."""
         req = self._resolve(columns)
         nq = len(keys)
         if self.index is None:
             return host_batch(req, [_null_dict(c.dtype, nq) for c in req])
         L = self.ctx.L
-        if self._reader is None:
-            h = C.c_void_p()
-            raise_status(L.murr_reader_new(self.ctx.h, C.byref(self.segment.c), C.byref(h)), what="murr_reader_new")
-            self._reader = h
         q = keys if isinstance(keys, pa.Array) else _key_array(keys)
-        kb = q.buffers()
-        proj = (C.c_uint32 * len(req))(*[c.index for c in req])
-        outs = (_abi.HostArray * len(req))()
-        err = _abi.Error()
-        st = L.murr_reader_read(self._reader, self.index.h, self.arena.ptr, self.row_off.ptr, self.used,
-                                self.max_row, kb[2].address if nq and kb[2] is not None else None,
-                                kb[1].address if nq else None, q.offset, nq, proj, len(req), outs, C.byref(err))
-        raise_status(st, err, "murr_reader_read")
-        key = tuple(c.index for c in req)
-        schema = self._schemas.get(key)
-        if schema is None:  # (one per column list: a schema costs ~5 us to build)
-            schema = pa.schema([pa.field(c.name, c.dtype.arrow_dtype(), True) for c in req])
-            self._schemas[key] = schema
-        return pa.RecordBatch.from_arrays(host_arrays_to_arrow(outs, len(req)), schema=schema)
+        plan = self.read_plan(columns, nq)
+        if plan is not None:
+            outs = plan.run(q)
+        else:
+            if self._reader is None:
+                h = C.c_void_p()
+                raise_status(L.murr_reader_new(self.ctx.h, C.byref(self.segment.c), C.byref(h)),
+                             what="murr_reader_new")
+                self._reader = h
+            kb = q.buffers()
+            proj = (C.c_uint32 * len(req))(*[c.index for c in req])
+            outs = (_abi.HostArray * len(req))()
+            err = _abi.Error()
+            st = L.murr_reader_read(self._reader, self.index.h, self.arena.ptr, self.row_off.ptr, self.used,
+                                    self.max_row, kb[2].address if nq and kb[2] is not None else None,
+                                    kb[1].address if nq else None, q.offset, nq, proj, len(req), outs, C.byref(err))
+            raise_status(st, err, "murr_reader_read")
+        # the RecordBatch through the Arrow C Data Interface: the library
+        # copies the arrays out of its pinned memory into an export pyarrow
+        # imports in one call (one Array.from_buffers per column cost ~4x more)
+        key = tuple(c.name for c in req)
+        names = self._schemas.get(key)
+        if names is None:  # (the field names as C strings, once per column list)
+            names = self._schemas[key] = c_names(list(key))
+        return host_arrays_to_batch(outs, len(req), names)
 
     def read_ipc(self, keys, columns, alignment: int = 64) -> bytes:
         """read() as the Arrow IPC stream of the HTTP fetch handler's StreamWriter

@@ -8,6 +8,7 @@ order (read.rs:100-109).
 """
 from __future__ import annotations
 
+import bisect
 import ctypes as C
 
 import numpy as np
@@ -86,7 +87,9 @@ class ReadBatchBuilder:
 
     def build(self) -> pa.RecordBatch:
         outs = self._build_host()
-        return pa.RecordBatch.from_arrays(host_arrays_to_arrow(outs, self._nproj), schema=self._schema())
+        if getattr(self, "_cnames", None) is None:
+            self._cnames = c_names(self._schema().names)
+        return host_arrays_to_batch(outs, self._nproj, self._cnames)
 
     def _schema(self) -> pa.Schema:
         """The batch schema: Field(name, arrow dtype, nullable) per requested
@@ -151,20 +154,25 @@ def host_arrays_to_arrow(outs, k: int) -> list:
     # (pointer, bytes) of every buffer: validity (nulls only), utf8 offsets, values
     vb = [((n + 7) // 8 if v else 0) for n, v in zip(ns, valid)]
     ob = [((n + 1) * 4 if d == _UTF8 else 0) for n, d in zip(ns, dts)]
-    spans = [(p, b) for p, b in zip(valid + offs + vals, vb + ob + vlen) if p and b]
-    if spans:
-        lo = min(p for p, _ in spans)
-        hi = max(p + b for p, b in spans)
-        one = hi - lo <= 2 * sum(b for _, b in spans) + 4096
-    else:
-        lo, one = 0, False
-    big = pa.py_buffer(C.string_at(lo, hi - lo)) if one else None
+    spans = sorted((p, b) for p, b in zip(valid + offs + vals, vb + ob + vlen) if p and b)
+    # runs of buffers no more than 4 KiB apart are copied as one span each (a
+    # prepared read lays the fixed-size buffers out back to back and each utf8
+    # column's bytes in a region of its own, sized for the longest rows)
+    runs = []  # [lo, hi]
+    for p, b in spans:
+        if runs and p <= runs[-1][1] + 4096:
+            runs[-1][1] = max(runs[-1][1], p + b)
+        else:
+            runs.append([p, p + b])
+    los = [lo for lo, _ in runs]
+    bigs = [pa.py_buffer(C.string_at(lo, hi - lo)) for lo, hi in runs]
     empty = pa.py_buffer(b"")
 
     def buf(p, b):
         if not (p and b):
             return empty
-        return big.slice(p - lo, b) if one else pa.py_buffer(C.string_at(p, b))
+        j = bisect.bisect_right(los, p) - 1
+        return bigs[j].slice(p - los[j], b)
 
     out = []
     for i in range(k):
@@ -174,6 +182,24 @@ def host_arrays_to_arrow(outs, k: int) -> list:
         bufs.append(buf(vals[i], vlen[i]))
         out.append(pa.Array.from_buffers(_ARROW_TYPE[dts[i]], ns[i], bufs, null_count=ncs[i]))
     return out
+
+
+def host_arrays_to_batch(outs, k: int, names, schema: pa.Schema | None = None) -> pa.RecordBatch:
+    """murr_host_array_t[0..k) -> one pyarrow RecordBatch through the Arrow C
+    Data Interface (murr_arrow_export: the library copies the bytes out of its
+    pinned region into an export it owns; pyarrow imports it in one call).
+    `names`: a ctypes array of k c_char_p (built once per column list).
+    `schema`: the batch's schema, when the caller has it (checked equal)."""
+    arr, sch = _abi.ArrowArray(), _abi.ArrowSchema()
+    L = _abi.lib()
+    raise_status(L.murr_arrow_export(outs, k, names, C.byref(arr), C.byref(sch)), what="murr_arrow_export")
+    rb = pa.RecordBatch._import_from_c(C.addressof(arr), C.addressof(sch))
+    return rb
+
+
+def c_names(names) -> "C.Array":
+    """Column names as the const char* const* murr_arrow_export takes."""
+    return (C.c_char_p * max(len(names), 1))(*[n.encode() for n in names])
 
 
 def host_array_to_arrow(h) -> pa.Array:
@@ -262,7 +288,8 @@ class HostStream:
                 seg_col = col if isinstance(col, SegmentColumnSchema) else self.segment.columns[int(col)]
                 fields.append(pa.field(seg_col.name, seg_col.dtype.arrow_dtype(), True))
             self._arrow_schema = pa.schema(fields)
-        return pa.RecordBatch.from_arrays(host_arrays_to_arrow(outs, self._nproj), schema=self._arrow_schema)
+            self._cnames = c_names(self._arrow_schema.names)
+        return host_arrays_to_batch(outs, self._nproj, self._cnames)
 
     @property
     def pending(self) -> int:

@@ -279,9 +279,14 @@ class ShardedResidentTable:
 
     def read(self, keys, columns, home: int = 0):
         from .resident import host_batch
-        keys = list(keys)
+        import pyarrow as pa
+        if not isinstance(keys, pa.Array):
+            keys = list(keys)
+        # owners from the keys as given (shard_of takes an Arrow array: its
+        # scalars would not survive list())
         owner = shard_of(keys, self.group.world) if self.group.world > 1 else np.zeros(len(keys), np.uint32)
-        mine = [keys[i] for i in np.flatnonzero(owner == self.group.rank)]
+        sel = np.flatnonzero(owner == self.group.rank)
+        mine = keys.take(pa.array(sel, pa.int64())) if isinstance(keys, pa.Array) else [keys[i] for i in sel]
         req, hs = self.local.read_host(mine, columns)
         merged = gather_reads(self.group, [c.dtype for c in req], len(keys), owner, hs, home)
         return None if merged is None else host_batch(req, merged)

@@ -26,6 +26,16 @@ def test_plan_time_every_mirrors_header():
     assert m and int(m.group(1)) == _abi.PLAN_TIME_EVERY
 
 
+def test_abi_version_mirrors_header_and_library():
+    # murr_block_t grew to 40 bytes in round 5, so the version moved
+    # to 2 and the loader refuses a library of another version
+    import re
+    m = re.search(r"#define MURR_ABI_VERSION (\d+)", open(_abi.HEADER).read())
+    assert m and int(m.group(1)) == _abi.ABI_VERSION == 2
+    assert _abi.lib().murr_abi_version() == _abi.ABI_VERSION
+    assert C.sizeof(_abi.Block) == 40
+
+
 def test_exports_are_c_symbols():
     out = subprocess.run(["nm", "-D", "--defined-only", _abi.LIB_PATH], capture_output=True,
                          text=True, check=True).stdout

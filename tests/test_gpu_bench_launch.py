@@ -91,3 +91,26 @@ def test_bench_line_is_self_consistent():
     assert rf["kernel_ms_avg"] <= line["ms_per_step"], (rf["kernel_ms_avg"], line["ms_per_step"])
     assert rf["frac_step"] <= rf["frac"] + 1e-9
     assert line["config"]["bytes_in_per_step"] == 300 * (1788890 + 4 * 100001 + 1576)
+    _lane_policy(line)
+
+
+def _lane_policy(line):
+    # one rule for every config -- the line is per launch (one
+    # stream), the overlapped rate is the extra `lanes` key with every lane's
+    # last output verified
+    assert line["lane_policy"].startswith("per launch"), line["lane_policy"]
+    ln = line["lanes"]
+    assert ln["lanes"] == 3 and ln["verified"].startswith("every lane"), ln
+    assert ln["frac_step_lanes"] > 0 and ln["ms_per_step"] > 0
+
+
+def test_bench_line_config_d_same_lane_policy():
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--config", "D", "--rows", "300000",
+                          "--steps", "9", "--warmup", "3", "--no-cpu", "--no-traffic"],
+                         capture_output=True, text=True, timeout=240, cwd=root)
+    assert out.returncode == 0, out.stderr[-2000:]
+    line = json.loads(out.stdout.strip().splitlines()[-1])
+    assert line["verified"].startswith("blocks"), line["verified"]
+    assert line["roofline"]["kernel_ms_avg"] <= line["ms_per_step"]
+    _lane_policy(line)

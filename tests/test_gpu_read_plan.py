@@ -1,0 +1,123 @@
+"""The prepared resident read (murr_read_plan_*, ResidentTable.read's path):
+lookup + gather + decode (+ the arrays to pinned memory) enqueued once and
+waited for once.  Checked against the MemoryStore restatement of
+src/io/store/memory.rs:28-45 (a miss is an all-null row), against the
+builder path bit for bit, and against round 5's unprepared device path, at key
+counts around the plan's capacity classes (a run of nq keys decodes
+read_capacity(nq) rows, the rest misses)."""
+import ctypes as C
+
+import numpy as np
+import pyarrow as pa
+import pytest
+
+from murr_amd import _abi
+from murr_amd.device import DecodeOutputs, DeviceBlock, decode_blocks, download_array
+from murr_amd.resident import ReadPlan, ResidentTable, _upload_utf8, read_capacity
+from murr_amd.store import MemoryStore
+from murr_amd.table import Table
+
+from test_gpu_resident import assert_same, batch_c, expected, schema_c
+
+pytestmark = pytest.mark.gpu
+
+COLS = [f"c{i}" for i in range(16)]
+
+
+@pytest.fixture(scope="module")
+def table():
+    rt = ResidentTable(schema_c())
+    b0 = batch_c(6000, seed=42)
+    rt.write(b0)
+    return rt, b0
+
+
+def test_capacity_classes():
+    assert [read_capacity(n) for n in (1, 63, 64, 65, 1000, 1024, 1025, 5000)] == \
+        [64, 64, 64, 128, 1024, 1024, 2048, 8192]
+
+
+@pytest.mark.parametrize("nq", [1, 5, 63, 64, 65, 700, 1000, 1025, 3000])
+def test_plan_reads_match_store_semantics(table, nq):
+    rt, b0 = table
+    rng = np.random.default_rng(1000 + nq)
+    keys = [f"key{i}" for i in rng.integers(0, 6300, size=nq)]  # ~5 % misses
+    got = rt.read(keys, COLS)
+    assert_same(got, expected([b0], keys, COLS))
+    plan = rt.read_plan(COLS, nq)
+    assert isinstance(plan, ReadPlan) and plan.cap == read_capacity(nq)
+    assert rt.ctx.L.murr_read_plan_capacity(plan.h) == plan.cap
+
+
+def test_plan_bit_exact_vs_builder_path(table):
+    rt, b0 = table
+    mt = Table.create(MemoryStore(), "t", schema_c())
+    mt.write(b0)
+    rng = np.random.default_rng(8)
+    keys = [f"key{i}" for i in rng.integers(0, 6300, size=1000)]
+    got, want = rt.read(keys, COLS), mt.read(keys, COLS)
+    for a, b in zip(got.columns, want.columns):
+        ba, bb = a.buffers(), b.buffers()
+        assert a.null_count == b.null_count
+        for x, y in zip(ba[1:], bb[1:]):
+            assert x.to_pybytes() == y.to_pybytes()
+        if a.null_count:
+            nb = (len(a) + 7) // 8
+            assert ba[0].to_pybytes()[:nb] == bb[0].to_pybytes()[:nb]
+
+
+def test_plan_reused_across_key_sets_and_replaced_after_a_write():
+    rt = ResidentTable(schema_c())
+    b0 = batch_c(3000, seed=3)
+    rt.write(b0)
+    rng = np.random.default_rng(9)
+    cols = ["c11", "c0", "c15", "c12"]
+    k1 = [f"key{i}" for i in rng.integers(0, 3200, size=900)]
+    k2 = [f"key{i}" for i in rng.integers(0, 3200, size=1000)]
+    assert_same(rt.read(k1, cols), expected([b0], k1, cols))
+    p1 = rt.read_plan(cols, 900)
+    assert_same(rt.read(k2, cols), expected([b0], k2, cols))
+    assert rt.read_plan(cols, 1000) is p1  # same class (1024), same table state: reused
+    # a write (overwrites and new keys) changes the table: a new plan, the new rows
+    b1 = batch_c(1500, start=2500, seed=4)
+    rt.write(b1)
+    k3 = [f"key{i}" for i in rng.integers(0, 4100, size=1000)]
+    assert_same(rt.read(k3, cols), expected([b0, b1], k3, cols))
+    assert rt.read_plan(cols, 1000) is not p1 and p1.h is None  # (the stale plan was freed)
+
+
+def test_plan_keys_as_sliced_arrow_array_and_all_misses(table):
+    rt, b0 = table
+    allk = pa.array([f"key{i}" for i in range(0, 6600, 3)], pa.string())
+    q = allk.slice(100, 500)
+    assert_same(rt.read(q, COLS), expected([b0], q.to_pylist(), COLS))
+    miss = ["nope", "", "key-1", "key99999"]
+    assert_same(rt.read(miss, ["c3", "c11"]), expected([b0], miss, ["c3", "c11"]))
+    assert rt.read([], ["c3", "c11"]).num_rows == 0
+
+
+def test_plan_device_run_equals_unprepared_path(table):
+    # the device variant (keys in HBM, arrays in HBM) against round 5's two-call
+    # path (murr_index_gather + murr_decode_blocks) on the same keys
+    rt, _ = table
+    ctx, L = rt.ctx, rt.ctx.L
+    rng = np.random.default_rng(77)
+    nq = 1000
+    keys = pa.array([f"key{i}" for i in rng.integers(0, 6300, size=nq)], pa.string())
+    qd, qo = _upload_utf8(ctx, keys)
+    plan = rt.read_plan(COLS, nq)
+    dev = plan.run_device(qd.ptr, qo.ptr, nq)
+    blk, _keep = rt.gather(keys.to_pylist())
+    proj = [c.index for c in rt._resolve(COLS)]
+    outs = DecodeOutputs(ctx, rt.segment, proj, [blk])
+    decode_blocks(ctx, rt.segment, proj, [blk], outs)
+    for p, ci in enumerate(proj):
+        dt = int(rt.segment.columns[ci].dtype)
+        a, b = download_array(ctx, dev[p], dt, nq), download_array(ctx, outs.array(0, p), dt, nq)
+        assert a["null_count"] == b["null_count"], p
+        assert a["values"] == b["values"], p
+        if dt == 0:
+            assert np.array_equal(a["offsets"], b["offsets"]), p
+        if a["null_count"]:
+            nb = (nq + 7) // 8
+            assert a["validity"][:nb] == b["validity"][:nb], p

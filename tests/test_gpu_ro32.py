@@ -180,8 +180,19 @@ def test_narrow_equals_host_cast_and_refuses_overflow(ctx, kernel_mode):
     assert np.array_equal(b32.row_off32.download().view(np.uint32), off.astype(np.uint32))
     big = off.copy()
     big[-1] = 1 << 32
-    with pytest.raises(MurrError):
+    with pytest.raises(MurrError, match="overflow"):
         DeviceBlock(ctx.alloc(16), ctx.upload(big), big.size - 1, 0).narrow(ctx)
+    # every offset is checked, not only the last: an interior one
+    # past 2^32 in a malformed block is not truncated into a plausible span
+    mid = off.copy()
+    mid[35000] += 1 << 32
+    with pytest.raises(MurrError, match="overflow"):
+        DeviceBlock(ctx.alloc(16), ctx.upload(mid), mid.size - 1, 0).narrow(ctx)
+    dec = off.copy()
+    dec[50000] = dec[49999] - 1 if dec[49999] else 0
+    dec[49999] += 5
+    with pytest.raises(SegmentError, match="malformed"):
+        DeviceBlock(ctx.alloc(16), ctx.upload(dec), dec.size - 1, 0).narrow(ctx)
 
 
 def test_config_b_block_u32_matches_u64(ctx, kernel_mode):

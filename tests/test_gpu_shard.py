@@ -33,7 +33,7 @@ def _case():
     return schema_c(), batch, keys
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, arrow_keys=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
     from murr_amd.shard import Group, ShardedResidentTable, route_batch
@@ -41,7 +41,8 @@ def _worker(rank, world, port, q):
     ts, batch, keys = _case()
     t = ShardedResidentTable(ts, g)
     t.write_shard(route_batch(batch, "key", world)[rank])  # keys go to their owner shard
-    rb = t.read(keys, COLS, home=1)
+    # (the keys also as a pyarrow array, as a Flight handler hands them over)
+    rb = t.read(pa.array(keys, pa.string()) if arrow_keys else keys, COLS, home=1)
     if rb is None:
         q.put((rank, None))
     else:
@@ -52,12 +53,13 @@ def _worker(rank, world, port, q):
     g.close()
 
 
-def test_two_shards_equal_whole_table():
+@pytest.mark.parametrize("arrow_keys", [False, True])
+def test_two_shards_equal_whole_table(arrow_keys):
     from murr_amd.resident import ResidentTable
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, arrow_keys)) for r in range(2)]
     for p in procs:
         p.start()
     got = [q.get(timeout=100) for _ in procs]

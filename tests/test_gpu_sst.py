@@ -303,3 +303,58 @@ def test_outputs_reused_after_free_never_while_live():
     same(e3)
     same(e2)
     assert ptrs(e3) & old  # (at least one buffer came back from the cache)
+
+
+def test_output_freed_while_another_stream_reads_it():
+    # ADVICE / VERDICT r5: a result freed while a kernel on another context
+    # still reads it must not be handed to the next murr_sst_decode (and
+    # overwritten) before that kernel is done.  The reader: a long decode on
+    # a second context of 2000 copies of the entries' values (row blobs of
+    # the config B schema); then the result is freed and a second SST of the
+    # same sizes but other values is decoded on the first context.  Both
+    # outputs must read as the oracle's.
+    from murr_amd import synth
+    from murr_amd.device import Context, DecodeOutputs, DecodePlan, download_array, encode_batch
+    from murr_amd.schema import SegmentSchema
+
+    n = 20000
+    ctx = default_context()
+    ctx2 = Context(ctx.device)
+
+    def stored_for(scale):
+        cols = synth.config_b(n)
+        cols[0]["values"] = (cols[0]["values"] * scale).astype(np.float32)
+        seg = SegmentSchema([(f"c{i}", c["dtype"]) for i, c in enumerate(cols)])
+        blob, off, blen = encode_batch(ctx, seg, synth.upload_columns(ctx, cols), n)
+        hb, ho = blob.download(blen).tobytes(), off.download(8 * (n + 1)).view(np.uint64)
+        entries = [(b"%08d" % i, 10 + i, G.TYPE_VALUE, hb[ho[i]:ho[i + 1]]) for i in range(n)]
+        return seg, [(G.snappy(b), G.SNAPPY) for b in G.blocks_of(entries)]
+
+    seg, s1 = stored_for(1.0)
+    _, s2 = stored_for(3.0)
+    w1, w2 = oracle_entries(s1), oracle_entries(s2)
+    assert [len(v) for v in w1[1]] == [len(v) for v in w2[1]] and w1[1] != w2[1]
+    b1, h1 = sst.upload_blocks(ctx, s1)
+    b2, h2 = sst.upload_blocks(ctx, s2)
+    e1 = sst.decode(ctx, b1, h1)
+    vblob = np.frombuffer(b"".join(w1[1]), np.uint8)
+    voff = np.concatenate([[0], np.cumsum([len(v) for v in w1[1]])]).astype(np.uint64)
+    want = O.decode_block(O.Segment([int(c.dtype) for c in seg.columns]), [0, 1], vblob, voff)
+    blocks = [e1.block()] * 5000
+    outs = DecodeOutputs(ctx2, seg, [0, 1], blocks)
+    plan = DecodePlan(ctx2, seg, [0, 1], blocks, outs)
+    plan.run_async()  # ctx2's stream reads e1's values ...
+    for buf in (e1.keys, e1.key_offsets, e1.values, e1.value_offsets, e1.seqs, e1.types):
+        buf.free()  # ... while they go back to ctx's reuse cache (murr_dev_free)
+    e2 = sst.decode(ctx, b2, h2)  # of the same sizes: may get e1's buffers back
+    plan.wait()
+    k, v, s, t = e2.to_host()
+    assert k == w2[0] and v == w2[1] and s.tolist() == w2[2] and t.tolist() == w2[3]
+    for b in (0, 2500, 4999):
+        for p in range(2):
+            g = download_array(ctx2, outs.array(b, p), int(seg.columns[p].dtype), n)
+            e = want[p]
+            if e["dtype"] == 0:
+                assert np.array_equal(g["offsets"], e["offsets"]), (b, p)
+            assert bytes(g["values"][: len(e["values"])]) == e["values"], (b, p)
+    plan.close()

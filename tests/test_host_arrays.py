@@ -1,12 +1,14 @@
-"""Host Arrow assembly of a read (murr_amd.row.host_arrays_to_arrow: one copy
-of the output region, zero-copy slices, descriptors read as one numpy view)
-equals the per-column conversion, buffer for buffer (CPU: synthetic
-murr_host_array_t over a host region laid out as the library's)."""
+"""Host Arrow assembly of a read (murr_amd.row.host_arrays_to_arrow: copies of
+the output region's runs, zero-copy slices, descriptors read as one numpy
+view; host_arrays_to_batch: the library's Arrow C Data Interface export,
+murr_arrow_export, imported in one call) equals the per-column conversion,
+buffer for buffer (CPU: synthetic murr_host_array_t over a host region laid
+out as the library's)."""
 import numpy as np
 import pytest
 
 from murr_amd import _abi
-from murr_amd.row import host_array_to_arrow, host_arrays_to_arrow
+from murr_amd.row import c_names, host_array_to_arrow, host_arrays_to_arrow, host_arrays_to_batch
 from murr_amd.schema import DTypeName as D
 
 
@@ -50,6 +52,20 @@ def test_batched_equals_per_column(n, gap):
         else:
             h.validity, h.null_count = None, 0
         h.length = n
+    want = [host_array_to_arrow(outs[i]) for i in range(len(dtypes))]
+    # the Arrow C Data Interface export (murr_arrow_export) imported as one
+    # RecordBatch: the same arrays, named, nullable, buffer for buffer
+    names = [f"col{i}" for i in range(len(dtypes))]
+    rb = host_arrays_to_batch(outs, len(dtypes), c_names(names))
+    rb.validate(full=True)
+    assert rb.schema.names == names and all(f.nullable for f in rb.schema)
+    for i, (x, y) in enumerate(zip(rb.columns, want)):
+        assert x.type == y.type and len(x) == len(y) and x.null_count == y.null_count, i
+        for bx, by in zip(x.buffers(), y.buffers()):
+            assert (bx is None) == (by is None), i
+            if bx is not None:
+                assert bx.to_pybytes() == by.to_pybytes(), i
+    del rb  # (released through the export's callbacks)
     got = host_arrays_to_arrow(outs, len(dtypes))
     for i, (x, y) in enumerate(zip(got, [host_array_to_arrow(outs[i]) for i in range(len(dtypes))])):
         x.validate(full=True)
@@ -58,3 +74,19 @@ def test_batched_equals_per_column(n, gap):
             assert (bx is None) == (by is None)
             if bx is not None:
                 assert bx.to_pybytes() == by.to_pybytes()
+
+
+def test_arrow_export_rejects_mixed_lengths_and_releases():
+    import ctypes as C
+    import gc
+    a = np.arange(10, dtype=np.int32)
+    outs = (_abi.HostArray * 2)()
+    for h, n in zip(outs, (10, 9)):
+        h.values, h.values_len, h.length, h.dtype = a.ctypes.data, 4 * n, n, int(D.Int32)
+    arr, sch = _abi.ArrowArray(), _abi.ArrowSchema()
+    assert _abi.lib().murr_arrow_export(outs, 2, c_names(["a", "b"]), C.byref(arr), C.byref(sch)) == _abi.E_ARGUMENT
+    outs[1].length, outs[1].values_len = 10, 40
+    rbs = [host_arrays_to_batch(outs, 2, c_names(["a", "b"])) for _ in range(200)]
+    assert all(r.column(1).to_pylist() == list(range(10)) for r in rbs)
+    del rbs
+    gc.collect()
