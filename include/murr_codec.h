@@ -651,7 +651,10 @@ int murr_read_plan_new(murr_ctx_t* ctx, const murr_segment_t* seg, const murr_in
                        uint64_t max_row, const uint32_t* proj, uint32_t nproj, uint64_t cap,
                        murr_read_plan_t** out);
 /* Keys in device memory (q_offsets[nq + 1], q_data); outs[nproj] are device
- * arrays in the plan's buffers (n = nq), valid until its next run or free. */
+ * arrays in the plan's buffers (n = nq), valid until its next run or free.
+ * Returns once the decode's counters are in (null counts, lengths, errors):
+ * the arrays are ready for work queued on the context's stream
+ * (murr_ctx_stream); another stream or device waits on that stream first. */
 int murr_read_plan_run_device(murr_read_plan_t* plan, const uint8_t* q_data, const int32_t* q_offsets,
                               uint64_t nq, murr_array_t* outs, murr_error_t* err);
 /* Keys on the host (Arrow utf8 from key_offset); outs[nproj] point into the

@@ -1994,7 +1994,24 @@ int murr_decode_run_async(murr_plan_t* P) {
     return MURR_OK;
 }
 
-int murr_decode_run_wait(murr_plan_t* P, murr_error_t* err) {
+}  // extern "C"
+
+namespace {
+int plan_wait(murr_plan_t* P, murr_error_t* err, bool end_sync);
+}  // namespace
+
+extern "C" {
+
+int murr_decode_run_wait(murr_plan_t* P, murr_error_t* err) { return plan_wait(P, err, true); }
+
+}  // extern "C"
+
+namespace {
+// end_sync: after the done flag, also wait for the kernel's end (its outputs
+// visible beyond the context's stream); a prepared read whose outputs are
+// consumed on that stream (its own D2H kernel, or the caller's work queued on
+// it) skips it: 6 us of a 1000-key read (round 6)
+int plan_wait(murr_plan_t* P, murr_error_t* err, bool end_sync) {
     if (!P) return set_err(err, MURR_E_ARGUMENT);
     murr_ctx* c = P->c;
     if (P->sync_pending) {
@@ -2031,7 +2048,11 @@ int murr_decode_run_wait(murr_plan_t* P, murr_error_t* err) {
     // visible to the host, other streams and peer GPUs when this returns.
     // The kernel is in its last workgroup's epilogue by now; a next run queued
     // behind it keeps the GPU busy meanwhile.
-    if (flagged) HIPC(hipEventSynchronize(R.end));
+#ifdef MURR_TUNING
+    static const bool nosync = std::getenv("MURR_PLAN_NOSYNC") != nullptr;  // A/B: the flag alone
+    if (nosync) end_sync = false;
+#endif
+    if (flagged && end_sync) HIPC(hipEventSynchronize(R.end));
     if (!flagged) {
         if (!R.kargs[set].empty()) c->stats.readback_fallbacks++;
         HIPC(hipMemcpyAsync(R.hrb, set ? R.zb2 : R.dws, R.z_lb, hipMemcpyDeviceToHost, c->stream));
@@ -2059,6 +2080,9 @@ int murr_decode_run_wait(murr_plan_t* P, murr_error_t* err) {
     }
     return finish_counts(c, R.hrb, P->outs, nblocks, nproj, P->n_rows.data(), P->dtypes.data(), err);
 }
+}  // namespace
+
+extern "C" {
 
 int murr_decode_run(murr_plan_t* P, murr_error_t* err) {
     const int st = murr_decode_run_async(P);
@@ -2694,7 +2718,31 @@ struct murr_hstream {
     bool pool_failed = false;        // (no threads: single-threaded copies)
     uint64_t head = 0, tail = 0;  // batches submitted / returned
     murr_hstream_stats_t stats{};
+#ifdef MURR_TUNING
+    // submit phases (MURR_HSTREAM_PHASES=1, printed at free), ms summed over
+    // batches: 0 progress, 1 source / staging, 2 H2D enqueue, 3 output layout,
+    // 4 decode enqueue (descriptors, launch, copy kernels), 5 event record
+    double ph[6] = {0, 0, 0, 0, 0, 0};
+#endif
 };
+
+namespace {
+#ifdef MURR_TUNING
+struct PhaseClock {  // (batches past the first 16 only: first-use allocations and the compile excluded)
+    double* ph;
+    bool on;
+    std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+    void lap(int k) {
+        const auto now = std::chrono::steady_clock::now();
+        if (on) ph[k] += std::chrono::duration<double, std::milli>(now - t).count();
+        t = now;
+    }
+};
+#define HS_LAP(k) pc.lap(k)
+#else
+#define HS_LAP(k) ((void)0)
+#endif
+}  // namespace
 
 namespace {
 
@@ -2730,6 +2778,9 @@ int hstream_enqueue(murr_hstream* h, HSlot& s, const uint8_t* data, const void* 
             c->xout.clear();
         }
     } xreset{c};
+#ifdef MURR_TUNING
+    PhaseClock pc{h->ph, h->head >= 16};
+#endif
     HIPC(hipSetDevice(c->device));
     // row offsets: u64, or u32 (murr_hstream_submit32: half the index bytes over PCIe)
     auto off_at = [&](uint64_t i) -> uint64_t {
@@ -2779,6 +2830,7 @@ int hstream_enqueue(murr_hstream* h, HSlot& s, const uint8_t* data, const void* 
         src_off = s.hin + dbytes;
     }
     uint8_t* doff = s.din + dbytes;
+    HS_LAP(1);
     s.timed = (h->head & 7) == 0;  // every eighth batch carries timing events
     if (engine) {
         // input copies by the copy engine, on the slot stream ahead of the decode
@@ -2797,6 +2849,7 @@ int hstream_enqueue(murr_hstream* h, HSlot& s, const uint8_t* data, const void* 
         HIPC(hipStreamWaitEvent(c->stream, s.e1, 0));
     }
     s.h2d_bytes = head + bytes + obytes;
+    HS_LAP(2);
     // row i of the block is data[row_off[i]..]: the block's data pointer sits
     // row_off[0] & ~15 bytes before the staged bytes (16-B aligned)
     murr_block_t blk{s.din - (b0 - head), w == 8 ? (const uint64_t*)doff : nullptr, n, b1,
@@ -2854,9 +2907,12 @@ int hstream_enqueue(murr_hstream* h, HSlot& s, const uint8_t* data, const void* 
         c->xe[2] = s.e2;
         c->xe[3] = s.e3;
     }
+    HS_LAP(3);
     const int st = murr_decode_enqueue(c, &h->seg, h->proj.data(), np, &blk, 1, o.arr.data());
     if (st) return set_err(err, st, st == MURR_E_HIP ? (int)hipGetLastError() : 0);
+    HS_LAP(4);
     HIPC(hipEventRecord(s.ed, c->stream));  // the decode and its counters' read-back are done
+    HS_LAP(5);
     s.d2h_bytes = fixed_out;  // (the fixed-size part, queued with the utf8 bytes once the counters are in)
     s.n = n;
     s.drained = false;
@@ -2989,7 +3045,11 @@ int hstream_submit(murr_hstream_t* h, const uint8_t* data, const void* row_off, 
         std::chrono::steady_clock::time_point t0;
         ~Clock() { h->stats.host_submit_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(); }
     } clock{h, t0};
+#ifdef MURR_TUNING
+    PhaseClock pc{h->ph, h->head >= 16};
+#endif
     hstream_progress(h);  // D2H of the batches whose decode finished, queued early
+    HS_LAP(0);
     HSlot& s = h->slots[h->head % h->slots.size()];
     s.submit_err = murr_error_t{};
     s.submit_status = hstream_enqueue(h, s, data, row_off, w, n_rows, (flags & MURR_HSTREAM_PINNED) != 0, &s.submit_err);
@@ -3077,6 +3137,15 @@ int murr_hstream_stats(murr_hstream_t* h, murr_hstream_stats_t* out) {
 
 void murr_hstream_free(murr_hstream_t* h) {
     if (!h) return;
+#ifdef MURR_TUNING
+    if (std::getenv("MURR_HSTREAM_PHASES") && h->head > 16)
+        std::fprintf(stderr,
+                     "hstream submit phases (us per batch over %llu): progress %.2f  source %.2f  h2d %.2f  layout %.2f  "
+                     "decode_enqueue %.2f  event %.2f\n",
+                     (unsigned long long)h->head - 16, h->ph[0] * 1e3 / (h->head - 16), h->ph[1] * 1e3 / (h->head - 16),
+                     h->ph[2] * 1e3 / (h->head - 16), h->ph[3] * 1e3 / (h->head - 16), h->ph[4] * 1e3 / (h->head - 16),
+                     h->ph[5] * 1e3 / (h->head - 16));
+#endif
     if (h->owner) (void)hipSetDevice(h->owner->device);
     if (h->s_h2d) (void)hipStreamSynchronize(h->s_h2d);
     if (h->s_d2h) (void)hipStreamSynchronize(h->s_d2h);
@@ -3245,8 +3314,6 @@ void murr_reader_free(murr_reader_t* r) {
 // rows: queries [nq, cap) are misses without a lookup (empty rows), and the
 // arrays are reported at nq rows.
 
-constexpr uint32_t kReadIxStride = 64;  // (the smallest index stride; the decode cuts at whole tiles)
-
 struct murr_read_plan {
     murr_ctx* ctx = nullptr;
     std::vector<murr_column_t> cols;
@@ -3267,14 +3334,35 @@ struct murr_read_plan {
     uint64_t hkeys_cap = 0;
     HostOut out;
     std::vector<CopySeg> d2h;  // the arrays into pinned memory (host runs)
-    bool ix = false;           // the layout has utf8 columns: the gathered block gets a utf8 index
-    Utf8IndexArgs ua{};        //   (murr_utf8_index's kernels over it), so the decode cuts it into
-                               //   virtual blocks of a tile each, one pass, instead of split mode
     murr_plan* dplan = nullptr;
     hipEvent_t ev = nullptr;
+#ifdef MURR_TUNING
+    // run phases (MURR_READ_PHASES=1, printed at free), ms summed over runs:
+    // 0 keys staged, 1 gather (+ index) launches, 2 decode launch, 3 D2H
+    // launch, 4 decode wait, 5 D2H wait
+    double ph[6] = {0, 0, 0, 0, 0, 0};
+    uint64_t runs = 0;
+#endif
 };
 
 namespace {
+#ifdef MURR_TUNING
+struct RunClock {
+    double* ph;
+    std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+    void lap(int k) {
+        const auto now = std::chrono::steady_clock::now();
+        ph[k] += std::chrono::duration<double, std::milli>(now - t).count();
+        t = now;
+    }
+};
+#define RP_CLOCK RunClock rc{r->ph}; r->runs++
+#define RP_LAP(k) rc.lap(k)
+#else
+#define RP_CLOCK ((void)0)
+#define RP_LAP(k) ((void)0)
+#endif
+
 int read_plan_gather(murr_read_plan* r, const uint8_t* q_data, const int32_t* q_off, uint64_t nq) {
     murr_ctx* c = r->ctx;
     murr_error_t* err = nullptr;
@@ -3291,7 +3379,6 @@ int read_plan_gather(murr_read_plan* r, const uint8_t* q_data, const int32_t* q_
     a.needed = r->dneed;
     a.scratch = c->aux;
     HIPC(launch_gather(a, c->stream));
-    if (r->ix) HIPC(launch_utf8_index(r->ua, c->stream));
     return MURR_OK;
 }
 
@@ -3355,37 +3442,14 @@ int murr_read_plan_new(murr_ctx_t* c, const murr_segment_t* seg, const murr_inde
     r->cap = cap;
     r->data_cap = data_cap;
     r->utf8_cap = max_row > fixed ? cap * (max_row - fixed) : 0;
-    // the gathered block's utf8 index (stride kReadIxStride): its string
-    // bytes before every kReadIxStride-th row, per utf8 column
-    Utf8IndexArgs& ua = r->ua;
-    for (uint32_t i = 0; i < seg->ncols; i++) {
-        if (seg->cols[i].dtype != MURR_UTF8 || ua.nu == kMaxUidxCols) continue;
-        ua.col[ua.nu] = seg->cols[i].index;
-        ua.fo[ua.nu] = seg->bitset_size + seg->cols[i].offset;
-        ua.nu++;
-    }
-    uint32_t nu_layout = 0;
-    for (uint32_t i = 0; i < seg->ncols; i++) nu_layout += seg->cols[i].dtype == MURR_UTF8;
-    r->ix = nu_layout && nu_layout == ua.nu;  // (more utf8 columns than the index kernel takes: split mode)
-    const uint64_t nwin = utf8_index_windows(0, cap, kReadIxStride);
-    const uint64_t ix_bytes = r->ix ? 8 * ((cap + kReadIxStride - 1) / kReadIxStride + 1) * ua.nu : 0;
-    const uint64_t part_bytes = r->ix ? 8 * std::max<uint64_t>(nwin, 1) * ua.nu : 0;
-    // device work: offsets | rows | needed | utf8 index | its scratch | gathered rows (16-B aligned)
+    // device work: offsets | rows | needed | gathered rows (16-B aligned)
     const uint64_t o_rows = round_up((cap + 1) * 8, 256), o_need = round_up(o_rows + cap * 4, 256),
-                   o_ix = o_need + 256, o_part = round_up(o_ix + ix_bytes, 256),
-                   o_data = round_up(o_part + part_bytes, 256);
+                   o_data = o_need + 256;
     if (!grow_dev(c, &r->dwork, &r->dwork_cap, o_data + data_cap + 16)) return MURR_E_HIP;
     r->doff = (uint64_t*)r->dwork;
     r->drows = (uint32_t*)(r->dwork + o_rows);
     r->dneed = (uint64_t*)(r->dwork + o_need);
     r->ddata = r->dwork + o_data;
-    ua.data = r->ddata;
-    ua.row_off = r->doff;
-    ua.out = (uint64_t*)(r->dwork + o_ix);
-    ua.part = (uint64_t*)(r->dwork + o_part);
-    ua.n = cap;
-    ua.stride = kReadIxStride;
-    ua.bs = seg->bitset_size;
     // arrays: the fixed-size parts first (values, validity, utf8 offsets), then
     // the utf8 bytes, so the D2H is one segment plus one per utf8 column
     HostOut& o = r->out;
@@ -3429,9 +3493,11 @@ int murr_read_plan_new(murr_ctx_t* c, const murr_segment_t* seg, const murr_inde
     // table's mean row x cap; rows end at doff[cap], never read past)
     const uint64_t mean = x->n ? arena_bytes / x->n : fixed;
     murr_block_t blk{r->ddata, r->doff, cap, std::min<uint64_t>(data_cap, std::max<uint64_t>(16, mean * cap)), nullptr};
-    const uint64_t* ux[1] = {ua.out};
-    int st = murr_decode_plan(c, &r->seg, r->proj.data(), nproj, &blk, 1, r->ix ? ux : nullptr,
-                              r->ix ? kReadIxStride : 0, o.arr.data(), &r->dplan);
+    // (no utf8 index: the decode takes a small block's segments in split
+    // mode; indexing the gathered block -- murr_utf8_index's two kernels, or
+    // a one-workgroup gather that also indexed -- cost more than the single
+    // pass saved)
+    int st = murr_decode_plan(c, &r->seg, r->proj.data(), nproj, &blk, 1, nullptr, 0, o.arr.data(), &r->dplan);
     if (st) return st;
     (void)murr_plan_time_every(r->dplan, 0);  // (no timing events between the run's kernels)
     HIPC(hipEventCreateWithFlags(&r->ev, hipEventDisableTiming));
@@ -3453,12 +3519,16 @@ int murr_read_plan_run_device(murr_read_plan_t* r, const uint8_t* q_data, const 
         return MURR_OK;
     }
     HIPC(hipSetDevice(c->device));
+    RP_CLOCK;
     int st = read_plan_gather(r, q_data, q_offsets, nq);
     if (st) return set_err(err, st);
+    RP_LAP(1);
     st = murr_decode_run_async(r->dplan);
     if (st) return set_err(err, st);
-    st = murr_decode_run_wait(r->dplan, err);
+    RP_LAP(2);
+    st = plan_wait(r->dplan, err, false);  // (its outputs are consumed on c->stream)
     if (st) return st;
+    RP_LAP(4);
     read_plan_report(r, nq, outs, nullptr);
     return MURR_OK;
 }
@@ -3477,6 +3547,7 @@ int murr_read_plan_run(murr_read_plan_t* r, const uint8_t* key_data, const int32
         return MURR_OK;
     }
     HIPC(hipSetDevice(c->device));
+    RP_CLOCK;
     // keys: rebased offsets + bytes in pinned staging, read by the probe in place
     const int32_t k0 = nq ? key_offsets[key_offset] : 0;
     const uint64_t kbytes = nq ? (uint64_t)(key_offsets[key_offset + nq] - k0) : 0;
@@ -3487,19 +3558,25 @@ int murr_read_plan_run(murr_read_plan_t* r, const uint8_t* key_data, const int32
     for (uint64_t i = 1; i <= nq; i++) ho[i] = key_offsets[key_offset + i] - k0;
     if (kbytes) std::memcpy(r->hkeys + offb, key_data + k0, kbytes);
     std::atomic_thread_fence(std::memory_order_seq_cst);
+    RP_LAP(0);
     int st = read_plan_gather(r, r->hkeys + offb, ho, nq);
     if (st) return set_err(err, st);
+    RP_LAP(1);
     st = murr_decode_run_async(r->dplan);
     if (st) return set_err(err, st);
+    RP_LAP(2);
     // the arrays into pinned memory, queued behind the decode on the same stream
     HIPC(launch_copy_segs(r->d2h.data(), (uint32_t)r->d2h.size(), kCopyGridOut, c->stream));
     HIPC(hipEventRecord(r->ev, c->stream));
-    st = murr_decode_run_wait(r->dplan, err);
+    RP_LAP(3);
+    st = plan_wait(r->dplan, err, false);  // (its outputs are consumed on c->stream)
     if (st) {
         (void)hipEventSynchronize(r->ev);
         return st;
     }
+    RP_LAP(4);
     HIPC(hipEventSynchronize(r->ev));
+    RP_LAP(5);
     read_plan_report(r, nq, nullptr, outs);
     return MURR_OK;
 }
@@ -3508,6 +3585,15 @@ uint64_t murr_read_plan_capacity(const murr_read_plan_t* r) { return r ? r->cap 
 
 void murr_read_plan_free(murr_read_plan_t* r) {
     if (!r) return;
+#ifdef MURR_TUNING
+    if (std::getenv("MURR_READ_PHASES") && r->runs)
+        std::fprintf(stderr,
+                     "read plan phases (us per run over %llu, cap %llu): keys %.2f  gather %.2f  decode launch %.2f  "
+                     "d2h launch %.2f  decode wait %.2f  d2h wait %.2f\n",
+                     (unsigned long long)r->runs, (unsigned long long)r->cap, r->ph[0] * 1e3 / r->runs,
+                     r->ph[1] * 1e3 / r->runs, r->ph[2] * 1e3 / r->runs, r->ph[3] * 1e3 / r->runs,
+                     r->ph[4] * 1e3 / r->runs, r->ph[5] * 1e3 / r->runs);
+#endif
     murr_ctx* c = r->ctx;
     if (c) {
         (void)hipSetDevice(c->device);

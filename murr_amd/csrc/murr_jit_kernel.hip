@@ -691,9 +691,14 @@ constexpr uint32_t NBW = (BS + 3) / 4;              // bitset dwords
 // (length after window, string after the tile's prefix wait) and 6 instead of
 // 9 strided dword reads per row on config B (each a 2-way bank conflict at
 // its 18-B row stride).  Other rows (nulls, longer strings, later utf8
-// columns) read the stage as before.
+// columns) read the stage as before.  Measured (round 6, interleaved A/Bs on
+// one box, config B): SQ_LDS_BANK_CONFLICT 31.2 M -> 20.8 M per dispatch and
+// LDS instructions -21 %, but the kernel 0.7225 -> 0.7271 ms and 0.7141 ->
+// 0.7178 ms (4 reps): neutral to 0.5 % slower (more SALU and VALU per chunk),
+// so off by default (tuning: MURR_JIT_DEFS=MJ_XWIN=1; the GPU suite passed
+// on it).  DESIGN.md §7.
 #ifndef MJ_XWIN
-#define MJ_XWIN 1
+#define MJ_XWIN 0
 #endif
 #ifndef MJ_XWMAX
 #define MJ_XWMAX 12

@@ -140,11 +140,26 @@ int main() {
         const int depth = 4, batches = 400;
         hipStream_t ss[4];
         for (int k = 0; k < depth; k++) CK(hipStreamCreateWithFlags(&ss[k], hipStreamNonBlocking));
-        auto stream_shape = [&](const char* name, int mode) {  // 0 engine+kernel, 1 engine+engine, 2 kernel+kernel
+        // 0 engine+kernel, 1 engine+engine, 2 kernel+kernel, 3 engine in two
+        // batches per copy (fewer, larger engine copies) + kernel out
+        auto stream_shape = [&](const char* name, int mode) {
             CK(hipDeviceSynchronize());
             CK(hipEventRecord(e0, ss[0]));
             for (int k = 1; k < depth; k++) CK(hipStreamWaitEvent(ss[k], e0, 0));
-            for (int i = 0; i < batches; i++) {
+            if (mode == 3) {
+                for (int i = 0; i < batches; i += 2) {
+                    hipStream_t st = ss[(i / 2) % depth];
+                    uint8_t* din = (uint8_t*)d1 + (size_t)((i / 2) % depth) * (8u << 20);
+                    uint8_t* dout = (uint8_t*)d2 + (size_t)((i / 2) % depth) * (8u << 20);
+                    uint8_t* hin = (uint8_t*)h1 + (size_t)((i / 2) % depth) * (8u << 20);
+                    uint8_t* hout = (uint8_t*)h2 + (size_t)((i / 2) % depth) * (8u << 20);
+                    CK(hipMemcpyAsync(din, hin, 2 * in_b, hipMemcpyHostToDevice, st));
+                    for (int k = 0; k < 2; k++)
+                        kcopy<<<128, 256, 0, st>>>((const u32x4*)(dout + k * (4u << 20)), (u32x4*)(hout + k * (4u << 20)),
+                                                   (out_b + 15) / 16);
+                }
+            }
+            for (int i = 0; i < (mode == 3 ? 0 : batches); i++) {
                 hipStream_t st = ss[i % depth];
                 uint8_t* din = (uint8_t*)d1 + (size_t)(i % depth) * (4u << 20);
                 uint8_t* dout = (uint8_t*)d2 + (size_t)(i % depth) * (4u << 20);
@@ -171,6 +186,7 @@ int main() {
         stream_shape("engine in + kernel out", 0);
         stream_shape("engine in + engine out", 1);
         stream_shape("kernel in + kernel out", 2);
+        stream_shape("engine in x2 + kernel out", 3);
     }
     return 0;
 }
