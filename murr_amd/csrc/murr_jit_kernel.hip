@@ -712,6 +712,9 @@ constexpr uint32_t NBW = (BS + 3) / 4;              // bitset dwords
 #ifndef MJ_ABL_LOADONLY
 #define MJ_ABL_LOADONLY 0
 #endif
+#ifndef MJ_FULLFAST
+#define MJ_FULLFAST 0
+#endif
 constexpr uint32_t S0 = FIX + 4;         // row byte of the first payload's string (when it is first)
 constexpr uint32_t NRX = S0 / 4 + 3;     // realigned dwords that hold row bytes [0, S0 + 8)
 constexpr bool XW = MJ_XWIN && WIN && NUTF8 >= 1 && NRX <= MJ_XWMAX;
@@ -1250,6 +1253,17 @@ DEV void decode_tile(const Src& src, const Tile& T, const LAS uint32_t* ro, LAS 
 
     Rows<R> W;
     uint32_t badk = 0, partial = 0;
+    // MJ_FULLFAST (tuning A/B): a chunk whose 64 rows are all in the tile
+    // (wave-uniform) stores without the per-lane row guard, so no exec-mask
+    // save / restore per column and chunk
+    bool fullk[R];
+#pragma unroll
+    for (uint32_t k = 0; k < R; k++) fullk[k] = rbase + (k + 1) * 64 <= T.nr;
+#define MJ_IFROW(K, I, ...)                                   \
+    do {                                                      \
+        if (MJ_FULLFAST && fullk[K]) { __VA_ARGS__ }          \
+        else if ((I) < T.nr) { __VA_ARGS__ }                  \
+    } while (0)
 #pragma unroll
     for (uint32_t k = 0; k < R; k++) {
         const uint32_t i = rbase + k * 64 + lane;
@@ -1390,13 +1404,15 @@ DEV void decode_tile(const Src& src, const Tile& T, const LAS uint32_t* ro, LAS 
                 MJ_STASH(C, vlo, vhi, k, (W.vb[k][C / 32] >> (C % 32)) & 1u);                           \
                 if constexpr (W_ == 9) {                                                                \
                     MJ_STASHB(C, k, lo != 0);                                                           \
-                } else if (i < T.nr && !MJ_ABL_NOFIX) {                                                 \
+                } else if (!MJ_ABL_NOFIX) {                                                             \
                     const uint64_t row = T.r0 + i;                                                      \
-                    if constexpr (W_ == 8) ost(gp((uint64_t*)o.values) + row, ((uint64_t)hi << 32) | lo); \
-                    else if constexpr (W_ == 4) ost(gp((uint32_t*)o.values) + row, lo);                 \
-                    else if constexpr (W_ == 2) ost(gp((uint16_t*)o.values) + row, (uint16_t)lo);       \
-                    else if constexpr (MJ_OUT_NT_W1) ost(gp((uint8_t*)o.values) + row, (uint8_t)lo);    \
-                    else gp((uint8_t*)o.values)[row] = (uint8_t)lo;                                     \
+                    MJ_IFROW(k, i, {                                                                    \
+                        if constexpr (W_ == 8) ost(gp((uint64_t*)o.values) + row, ((uint64_t)hi << 32) | lo); \
+                        else if constexpr (W_ == 4) ost(gp((uint32_t*)o.values) + row, lo);             \
+                        else if constexpr (W_ == 2) ost(gp((uint16_t*)o.values) + row, (uint16_t)lo);   \
+                        else if constexpr (MJ_OUT_NT_W1) ost(gp((uint8_t*)o.values) + row, (uint8_t)lo); \
+                        else gp((uint8_t*)o.values)[row] = (uint8_t)lo;                                 \
+                    });                                                                                 \
                 }                                                                                       \
             }                                                                                           \
         }                                                                                               \
@@ -1522,7 +1538,7 @@ DEV void decode_tile(const Src& src, const Tile& T, const LAS uint32_t* ro, LAS 
                 /* XW: the string is in the window's registers (row bytes S0 ..) */                    \
                 const bool inw = XWS && U == 0 && ((xin >> k) & 1u) && n <= 8;                          \
                 if (cend <= 0x7FFFFFFFull && cend <= o.values_cap) { /* wave-uniform fast path */       \
-                    if (act) ost(obf + i, (int32_t)e);                                                  \
+                    MJ_IFROW(k, i, { ost(obf + i, (int32_t)e); });                                     \
                     if (regs) {                                                                         \
                         if (n && !MJ_ABL_NOSTR)                                                         \
                             copy_str_regs(gp(o.values) + (e - n), sw[U][k][0], sw[U][k][1], sw[U][k][2], \
@@ -1553,6 +1569,7 @@ DEV void decode_tile(const Src& src, const Tile& T, const LAS uint32_t* ro, LAS 
     MJ_COLS(MJ_E)
 #undef MJ_E
 #undef MJ_SLOT
+#undef MJ_IFROW
     if (ERS && late) release_slot(rel, lane);
 }
 

@@ -24,7 +24,13 @@ run abC 900 "$PY" tools/ab.py --reps 3 \
   --env base=MURR_LIB=$TL \
   --env lo=MURR_LIB=$TL --env lo=MURR_JIT_DEFS=MJ_ABL_LOADONLY=1 \
   --env nost=MURR_LIB=$TL --env nost=MURR_JIT_DEFS=MJ_ABL_NOSTR=1,MJ_ABL_NOFIX=1 \
+  --env ff=MURR_LIB=$TL --env ff=MURR_JIT_DEFS=MJ_FULLFAST=1 \
   "base::--config C --blocks 10 --extra-lanes 0" "lo::--config C --blocks 10 --extra-lanes 0 --no-verify" \
-  "nost::--config C --blocks 10 --extra-lanes 0 --no-verify"
+  "nost::--config C --blocks 10 --extra-lanes 0 --no-verify" "ff::--config C --blocks 10 --extra-lanes 0"
 cp -r gpurun_out/ab $out/abC
+rm -rf gpurun_out/ab
+run abB 600 "$PY" tools/ab.py --reps 3 \
+  --env base=MURR_LIB=$TL --env ff=MURR_LIB=$TL --env ff=MURR_JIT_DEFS=MJ_FULLFAST=1 \
+  "base::--extra-lanes 0" "ff::--extra-lanes 0"
+cp -r gpurun_out/ab $out/abB
 echo done
