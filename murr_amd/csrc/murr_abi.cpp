@@ -533,11 +533,11 @@ int murr_index_gather(murr_ctx_t* c, const murr_index_t* x, const uint8_t* q_dat
     if (nq >= kMissing || ((uintptr_t)out_data & 15)) return MURR_E_ARGUMENT;
     HIPC(hipSetDevice(c->device));
     // scratch: the scan's group sums, then the rows when the caller wants none
-    const uint64_t groups = gather_scan_groups(nq);
-    const uint64_t need = groups + 1 + (rows ? 0 : (nq + 1) / 2);
+    const uint64_t words = gather_scratch_words(nq);
+    const uint64_t need = words + (rows ? 0 : (nq + 1) / 2);
     if (const int st = ensure_aux(c, need, err)) return st;
     IndexArgs a = index_args(x, q_data, q_offsets, nq);
-    a.rows = rows ? rows : (uint32_t*)(c->aux + groups + 1);
+    a.rows = rows ? rows : (uint32_t*)(c->aux + words);
     a.blob = blob;
     a.row_off = row_off;
     a.sizes = out_row_off;
@@ -3366,8 +3366,7 @@ struct RunClock {
 int read_plan_gather(murr_read_plan* r, const uint8_t* q_data, const int32_t* q_off, uint64_t nq) {
     murr_ctx* c = r->ctx;
     murr_error_t* err = nullptr;
-    const uint64_t groups = gather_scan_groups(r->cap);
-    if (const int st = ensure_aux(c, groups + 1, err)) return st;
+    if (const int st = ensure_aux(c, gather_scratch_words(r->cap), err)) return st;
     IndexArgs a = index_args(r->x, q_data, q_off, r->cap);
     a.nq_live = nq;  // (>= 1: a run of no keys launches nothing)
     a.rows = r->drows;

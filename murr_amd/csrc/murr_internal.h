@@ -318,6 +318,7 @@ hipError_t launch_index_probe(const IndexArgs& a, hipStream_t s);
 hipError_t launch_index_seq(const IndexArgs& a, const uint64_t* seqs, unsigned long long* best,
                             unsigned long long* win, hipStream_t s);
 uint64_t gather_scan_groups(uint64_t nq);
+uint64_t gather_scratch_words(uint64_t nq);  // A.scratch (u64) a launch_gather of nq queries needs
 hipError_t launch_gather(const IndexArgs& a, hipStream_t s);
 hipError_t launch_gather_scan(const IndexArgs& a, hipStream_t s);  // probe + sizes + scan, no copy
 hipError_t launch_gather_copy(const IndexArgs& a, hipStream_t s);  // the copy of a scanned gather

@@ -184,32 +184,39 @@ def test_resident_read_many_keys_three_pass_scan():
     assert_same(t.read(keys, cols), expected([b0], keys, cols))
 
 
-def test_gather_capacity_clamp():
-    # out_cap too small: offsets clamp to the cap, `needed` reports the size
-    import ctypes as C
+@pytest.mark.parametrize("nk,cap,with_rows", [(1500, 5000, True), (700, 5000, True), (1024, 20000, False),
+                                               (1024, 300000, True), (1, 16, False), (64, 100000, False)])
+def test_gather_capacity_clamp(nk, cap, with_rows):
+    # out_cap too small: offsets clamp to the cap, `needed` reports the size.
+    # nk <= 1024 takes the spread probe + per-workgroup scan copy
+    # (gather_probe_wide / gather_scan_copy), above it the one-workgroup scan.
+    # Every fifth key misses; rows NULL puts them in the context's scratch.
     from murr_amd.resident import _upload_utf8
     t = ResidentTable(schema_c())
     t.write(batch_c(2000, seed=4))
     ctx = t.ctx
-    keys = [f"key{i}" for i in range(1500)]
+    want_rows = [i if i % 5 else 10**9 for i in range(nk)]
+    keys = [f"key{r}" for r in want_rows]
     qd, qo = _upload_utf8(ctx, pa.array(keys, pa.string()))
-    cap = 5000
-    data, offs, needed = ctx.alloc(cap + 16), ctx.alloc((len(keys) + 1) * 8), ctx.alloc(8)
-    rows = ctx.alloc(len(keys) * 4)
-    st = ctx.L.murr_index_gather(ctx.h, t.index.h, qd.ptr, qo.ptr, len(keys), t.blob.ptr, t.row_off.ptr,
-                                 data.ptr, cap, offs.ptr, rows.ptr, needed.ptr)
+    data, offs, needed = ctx.alloc(cap + 16), ctx.alloc((nk + 1) * 8), ctx.alloc(8)
+    rows = ctx.alloc(nk * 4) if with_rows else None
+    st = ctx.L.murr_index_gather(ctx.h, t.index.h, qd.ptr, qo.ptr, nk, t.blob.ptr, t.row_off.ptr,
+                                 data.ptr, cap, offs.ptr, rows.ptr if rows else None, needed.ptr)
     assert st == 0
-    off = offs.download((len(keys) + 1) * 8).view(np.uint64)
+    off = offs.download((nk + 1) * 8).view(np.uint64)
     full = t.row_off.download((t.n + 1) * 8).view(np.uint64)
-    sizes = np.diff(full)[:1500].astype(np.uint64)
+    sizes = np.array([int(full[r + 1] - full[r]) if r < t.n else 0 for r in want_rows], np.uint64)
     want = np.concatenate([[0], np.cumsum(sizes)]).astype(np.uint64)
     assert int(needed.download(8).view(np.uint64)[0]) == int(want[-1])
     assert np.array_equal(off, np.minimum(want, cap))
-    assert rows.download(len(keys) * 4).view(np.uint32).tolist() == list(range(1500))
+    if rows:
+        assert rows.download(nk * 4).view(np.uint32).tolist() == \
+            [r if r < t.n else ROW_MISSING for r in want_rows]
     blob = t.blob.download(int(full[-1]))
+    exp = b"".join(blob[int(full[r]):int(full[r + 1])].tobytes() for r in want_rows if r < t.n)
     got = data.download(cap)
     k = int(np.searchsorted(want, cap, side="right")) - 1  # rows wholly inside the cap
-    assert got[:int(want[k])].tobytes() == blob[:int(want[k])].tobytes()
+    assert got[:int(want[k])].tobytes() == exp[:int(want[k])]
 
 
 def test_index_long_duplicate_keys():

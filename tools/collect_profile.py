@@ -48,7 +48,8 @@ for n in ("timeline_D",):
         shutil.copy(f"{src}/{n}.log", f"{dst}/{n}.log")
         print(f"{n}.log")
 for pat, out in [("trace/*kernel_stats.csv", "bench_driver_kernel_stats.csv"),
-                 ("trace/*domain_stats.csv", "bench_driver_domain_stats.csv")]:
+                 ("trace/*domain_stats.csv", "bench_driver_domain_stats.csv"),
+                 ("trace_res_C/*kernel_stats.csv", "resident_C_100reads_kernel_stats.csv")]:
     f = sorted(glob.glob(f"{src}/{pat}"))
     if f:
         shutil.copy(f[0], f"{dst}/{out}")

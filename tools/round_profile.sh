@@ -7,7 +7,7 @@ set -u
 export TMPDIR=/tmp
 # the resolved interpreter after `--` (rocprofv3 execs it; a `python3` on PATH may be a wrapper)
 PY=$(readlink -f "$(command -v python3)")
-R=${R:-r04}
+R=${R:-r06f}
 PART=${PART:-all}  # 1: the headline trace and B/C/D with traffic; 2: the side measurements; all: both
 out=gpurun_out/$R
 mkdir -p $out
@@ -44,6 +44,8 @@ if [ "$PART" != 1 ]; then
   run encode_C 300 "$PY" bench.py --mode encode --enc-config C --steps 10 --warmup 2
   run resident_1000 300 "$PY" bench.py --mode resident --keys 1000 --steps 30 --warmup 5
   run resident_read_plain 300 "$PY" bench.py --mode resident --table ref --rows 10000000 --keys 1000 --steps 200 --warmup 20 --ipc
+  # kernel trace of 100 prepared config-C reads (probe+scan, gather copy, decode)
+  run trace_res_C 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out/trace_res_C -o res -- "$PY" bench.py --mode resident --keys 1000 --steps 100 --warmup 5
   run resident_read_block 400 "$PY" bench.py --mode resident --table ref --rows 100000000 --keys 1000 --steps 200 --warmup 20
   # one-block config D at 2x / 4x the shard: fixed cost per launch (fit over rows)
   run decode_D1x2 300 "$PY" bench.py --config D --rows 2500000 --steps 10 --warmup 2 --no-cpu
