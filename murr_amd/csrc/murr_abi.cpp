@@ -162,8 +162,9 @@ uint32_t nutf8_of(const murr_segment_t* seg) {
     } while (0)
 
 // Caller-owned device outputs through the context's reuse cache: a freed
-// buffer of at least `bytes` (and at most twice that plus 1 MiB) comes back
-// instead of a new hipMalloc; new ones are rounded to 1 MiB.  hipSuccess or
+// buffer of at least `bytes` (and at most twice that plus one granule) comes
+// back instead of a new hipMalloc; new ones are rounded to the granule: 1 MiB,
+// or 4 KiB below 1 MiB (a small SST file's arena stays small).  hipSuccess or
 // the allocation's error (the cache is released and the call retried once).
 constexpr uint64_t kDevCacheMax = 1ull << 30;
 // process-wide: every buffer dev_alloc_cached made, with its context and size
@@ -173,8 +174,9 @@ std::mutex g_dc_mu;
 std::unordered_map<void*, std::pair<murr_ctx*, uint64_t>> g_dcached;
 hipError_t dev_alloc_cached(murr_ctx* c, uint64_t bytes, void** out) {
     std::lock_guard<std::mutex> lk(g_dc_mu);
+    const uint64_t gran = bytes < (1u << 20) ? 4096u : (1u << 20);
     auto it = c->dfree.lower_bound(bytes);
-    if (it != c->dfree.end() && it->first <= 2 * bytes + (1u << 20)) {
+    if (it != c->dfree.end() && it->first <= 2 * bytes + gran) {
         if (c->dfree_unsynced) {
             // every buffer freed so far: its readers queued before the free are done
             const hipError_t se = hipDeviceSynchronize();
@@ -186,7 +188,7 @@ hipError_t dev_alloc_cached(murr_ctx* c, uint64_t bytes, void** out) {
         c->dfree.erase(it);
         return hipSuccess;
     }
-    const uint64_t sz = (bytes + (1u << 20) - 1) & ~(uint64_t)((1u << 20) - 1);
+    const uint64_t sz = std::max<uint64_t>((bytes + gran - 1) & ~(gran - 1), gran);
     hipError_t e = hipMalloc(out, sz);
     if (e != hipSuccess && !c->dfree.empty()) {
         (void)hipGetLastError();
@@ -1308,7 +1310,8 @@ int decode_enqueue_jit(murr_ctx* c, const murr_segment_t* seg, const JitLayout* 
         dout[i] = DecOut{(uint8_t*)outs[i].values, outs[i].validity, outs[i].offsets, outs[i].values_cap};
 
     const uint64_t nbp = (uint64_t)nblocks * nproj;
-    const uint64_t flag_bytes = local || !emit ? 0 : round_up(8 * nu * nseg, 16);  // granules per projection round
+    // granules per projection round, then the round's segment claim word
+    const uint64_t flag_bytes = local || !emit ? 0 : round_up(8 * nu * nseg + 8, 16);
     const uint64_t z_err = 0, z_nulls = kErrBytes, z_lens = z_nulls + 8 * nbp, z_flags = round_up(z_lens + 8 * nbp, 16);
     const uint64_t zbytes = round_up(z_flags + flag_bytes * rounds, 16);
     const uint64_t d_blocks = zbytes;

@@ -150,7 +150,7 @@ struct JitArgsHead {               // = mj::Args without its trailing slot[] (mu
     unsigned long long* nulls;
     unsigned long long* lens;
     unsigned long long* err;
-    unsigned long long* flags;     // split mode: [nseg][max(nutf8, 1)] look-back granules
+    unsigned long long* flags;     // split mode: [nseg][max(nutf8, 1)] look-back granules, then a claim word
     uint8_t* sink;
     uint64_t nseg;
     uint32_t nblocks, nproj, norder, mode;  // mode: 0 local, 1 split

@@ -100,7 +100,7 @@ struct Args {
     unsigned long long* nulls;    // [nblocks][nproj]
     unsigned long long* lens;     // [nblocks][nproj] utf8 data bytes
     unsigned long long* err;      // max of ~key
-    unsigned long long* flags;    // split mode: [nseg][NU] look-back granules
+    unsigned long long* flags;    // split mode: [nseg][NU] look-back granules, then the segment claim word
     uint8_t* sink;
     uint64_t nseg;                // split mode: segments
     uint32_t nblocks, nproj, norder, mode;
@@ -475,7 +475,28 @@ DEV Cur cur_seg(uint32_t k) {
     const uint64_t rb = ok ? sgpr64(sp->r_begin) : 0, re = ok ? sgpr64(sp->r_end) : 0;
     return cur_make(ok, k, ok ? sgpr(sp->b) : 0u, ok ? sgpr(sp->first) : 0u, 1, rb, re, rb);
 }
-template <uint32_t MODE> DEV Cur cur_first() { return MODE == 0 ? cur_local(blockIdx.x) : cur_seg(blockIdx.x); }
+// Split mode with more segments than workgroups: segments are claimed from a
+// counter (the word after the look-back granules, zeroed with them) in the
+// order workgroups actually run, so a segment's predecessors are always held
+// by running workgroups.  A static deal (g, g + G, ...) makes workgroup 0's
+// second segment wait on workgroup G - 1's first, and when other streams'
+// kernels hold CUs that workgroup may not be resident: every resident
+// workgroup waits until the bounded wait aborts the launch (three overlapped
+// split launches measured 21 ms a step instead of 0.43).  One round of
+// segments (nseg <= G) needs no claims: workgroup g's predecessors are
+// workgroups < g, dispatched before it.  Only launches with a second pass
+// wait on other workgroups (emit), so only those claim.
+DEV bool seg_claims() { return args()->emit && args()->nseg > gridDim.x; }
+DEV uint32_t seg_claim() {
+    unsigned int* w = (unsigned int*)(args()->flags + (uint64_t)NU * args()->nseg);
+    uint32_t k = 0;
+    if (lane_id() == 0) k = __hip_atomic_fetch_add(gp(w), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return sgpr(k);
+}
+template <uint32_t MODE> DEV Cur cur_first() {
+    if constexpr (MODE == 0) return cur_local(blockIdx.x);
+    return cur_seg(seg_claims() ? seg_claim() : blockIdx.x);
+}
 // Fast start: the scalar loads behind the first cursors (the segment entries
 // g, g + G, g + 2G, g + 3G, then their block entries) issued side by side, so
 // the dependent chain of cursor loads that follows hits the scalar cache
@@ -520,7 +541,7 @@ template <uint32_t TR> DEV Cur cur_next(const Cur& c) {
         n.r0 = c.r_begin;
         return n;
     }
-    return cur_seg(c.k + gridDim.x);
+    return cur_seg(seg_claims() ? seg_claim() : c.k + gridDim.x);
 }
 template <uint32_t TR> DEV uint32_t cur_nr(const Cur& c) { return (uint32_t)umin64((uint64_t)TR, c.r_end - c.r0); }
 
@@ -1663,7 +1684,7 @@ DEV void kernel_body() {
         // short virtual blocks per workgroup it took the D shard 0.0866 ->
         // 0.0852 ms, while whole-block launches (config B) ran 0.758 -> 0.771.
         const bool fast = ER ? FAST : FAST && args()->fast != 0;
-        if (fast) warm_scalar<MODE>();
+        if (fast && !(MODE == 1 && seg_claims())) warm_scalar<MODE>();  // (claimed segments: unknown yet)
         Cur cs = cur_first<MODE>();  // next tile to announce
         // tiles announced before the first DMA: 0 .. 3, or (fast start) 0 .. 1 / 0
         constexpr uint32_t NPRE_ER = FAST ? 1u : NSLOT + 1;

@@ -158,3 +158,39 @@ def test_two_plans_alternating_async_runs(ctx, kernel_mode):
     plans[0].wait()
     for p in plans:
         p.close()
+
+
+def test_split_plans_overlapped_on_three_streams(kernel_mode):
+    # Three split-mode launches of more segments than one grid round, on three
+    # contexts (streams) at once, so they compete for the CUs.  Segments are
+    # claimed in the order workgroups run (murr_jit_kernel.hip seg_claim):
+    # with the static deal a resident workgroup's look-back waited on a
+    # workgroup of its own launch that other launches kept off the GPU, every
+    # wait ran to its bound and the launch was re-run in local mode
+    # (split_retries; bench.py's C no-index lanes took 21 ms a step).
+    if kernel_mode != "jit":
+        pytest.skip("split mode is the JIT kernel's")
+    rng = np.random.default_rng(606)
+    dtypes = [D.Utf8, D.Int32, D.Utf8]
+    seg = SegmentSchema([(f"c{i}", d) for i, d in enumerate(dtypes)])
+    oseg, data, off = make(rng, dtypes, 400000)
+    proj = [0, 2, 1]
+    ctxs = [Context(0) for _ in range(3)]
+    try:
+        plans = []
+        for c in ctxs:
+            c.set_opts(kernel="jit", mode="split", shape=(3, 1), seg_tiles=1)  # 3125 one-tile segments
+            plans.append(DecodePlan(c, seg, proj, [DeviceBlock.upload(c, data, off)]))
+        for _ in range(3):
+            for p in plans:
+                p.run_async()
+            for p in plans:
+                p.wait()
+        for c, p in zip(ctxs, plans):
+            st = c.stats()
+            assert st["split_retries"] == 0 and st["last_mode"] == "split", st
+            check(c, seg, oseg, proj, [(data, off)], p.outs, "overlapped split")
+            p.close()
+    finally:
+        for c in ctxs:
+            c.close()

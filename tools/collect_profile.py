@@ -54,6 +54,13 @@ for pat, out in [("trace/*kernel_stats.csv", "bench_driver_kernel_stats.csv"),
     if f:
         shutil.copy(f[0], f"{dst}/{out}")
         print(out)
+f = sorted(glob.glob(f"{src}/trace/*kernel_trace.csv"))
+if f:  # the headline's launches apart from the lanes run's overlapped ones
+    import subprocess
+    out = subprocess.run([sys.executable, os.path.join(os.path.dirname(os.path.abspath(__file__)), "trace_split.py"),
+                          f[0]], capture_output=True, text=True).stdout
+    open(f"{dst}/bench_driver_kernel_split.txt", "w").write(out)
+    print("bench_driver_kernel_split.txt")
 for c in ("B", "C"):
     f = sorted(glob.glob(f"gpurun_out/encprof/{c}/*kernel_stats.csv"))
     if f:
