@@ -1111,12 +1111,12 @@ def run_resident(args):
                       "arrow_bytes_out": out_bytes,
                       "us_per_read_device_median": round(med * 1e6, 1),
                       "us_per_read_device_p95": round(float(np.percentile(ts, 95)) * 1e6, 1),
-                      "device_path": "ReadPlan.run_device: probe, scan+gather copy, prepared decode; one wait",
+                      "device_path": "ReadPlan.run_device: fused probe + look-back + gather copy, prepared decode; one wait",
                       "us_per_read_device_unprepared_median": round(float(np.median(tu)) * 1e6, 1),
                       "us_per_read_host_median": round(float(np.median(th)) * 1e6, 1),
                       "GiB_s_arrow_out_device": round(out_bytes / med / GIB, 3),
                       "host_path": "ResidentTable.read: Python keys -> Arrow -> ReadPlan.run -> RecordBatch",
-                      "kernels": "gather_probe_wide, gather_scan_copy, murr_jit_decode (+ copy_segs_kernel on the host path)",
+                      "kernels": "gather_fused, murr_jit_decode (+ copy_segs_kernel on the host path)",
                       **ipc_res}))
 
 

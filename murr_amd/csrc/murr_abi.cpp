@@ -120,6 +120,8 @@ struct murr_ctx {
     std::vector<hipEvent_t> event_pool;
     uint64_t* aux = nullptr;  // device scratch of the gather scan (group sums)
     uint64_t aux_cap = 0;     // entries
+    unsigned long long* glb = nullptr;  // the fused small gather's two look-back word sets
+    uint32_t glb_set = 0;               // the set the next launch uses (zeroed by the one before)
     hipEvent_t xev = nullptr; // multi-GPU reads: this stream's work, awaited by the home stream
     hipEvent_t hev = nullptr; // multi-GPU reads (as home): the work queued before a read, awaited by the shards
     // Fused transfers (the streaming host decode, murr_hstream): the next
@@ -495,6 +497,28 @@ int ensure_aux(murr_ctx* c, uint64_t need, murr_error_t* err) {
     return MURR_OK;
 }
 
+// The fused small gather's words (gather_fused, murr_index.hip): two sets,
+// both zeroed once here; launches alternate between them and each zeroes the
+// other for the next (launches on one context's stream run in order).  Null
+// when the tuning variable MURR_GATHER_TWO picks the two-launch form (A/B).
+int small_gather_words(murr_ctx* c, IndexArgs* a, murr_error_t* err) {
+    a->lb = a->lb_other = nullptr;
+#ifdef MURR_TUNING
+    if (std::getenv("MURR_GATHER_TWO")) return MURR_OK;
+#endif
+    if (a->nq == 0 || a->nq > 64 * kGatherGroups) return MURR_OK;
+    if (!c->glb) {
+        void* p = nullptr;
+        HIPC(hipMalloc(&p, 16 * kGatherGroups));
+        HIPC(hipMemsetAsync(p, 0, 16 * kGatherGroups, c->stream));
+        c->glb = (unsigned long long*)p;
+    }
+    a->lb = c->glb + kGatherGroups * c->glb_set;
+    c->glb_set ^= 1u;
+    a->lb_other = c->glb + kGatherGroups * c->glb_set;
+    return MURR_OK;
+}
+
 IndexArgs index_args(const murr_index_t* x, const uint8_t* q_data, const int32_t* q_offsets, uint64_t nq) {
     IndexArgs a{};
     a.key_data = x->key_data;
@@ -547,6 +571,7 @@ int murr_index_gather(murr_ctx_t* c, const murr_index_t* x, const uint8_t* q_dat
     a.out_cap = out_cap;
     a.needed = needed;
     a.scratch = c->aux;
+    if (const int st = scan_only ? MURR_OK : small_gather_words(c, &a, err)) return st;
     if (scan_only) {
         a.out_cap = ~0ull;
         HIPC(launch_gather_scan(a, c->stream));
@@ -788,6 +813,7 @@ void murr_ctx_destroy(murr_ctx_t* c) {
     }
     if (c->ws) (void)hipFree(c->ws);
     if (c->aux) (void)hipFree(c->aux);
+    if (c->glb) (void)hipFree(c->glb);
     if (c->hs) (void)hipHostFree(c->hs);
     for (const auto& b : c->pool) (void)(b.pinned ? hipHostFree(b.p) : hipFree(b.p));
     for (hipEvent_t e : c->event_pool) (void)hipEventDestroy(e);
@@ -3380,6 +3406,7 @@ int read_plan_gather(murr_read_plan* r, const uint8_t* q_data, const int32_t* q_
     a.out_cap = r->data_cap;
     a.needed = r->dneed;
     a.scratch = c->aux;
+    if (const int st = small_gather_words(c, &a, err)) return st;
     HIPC(launch_gather(a, c->stream));
     return MURR_OK;
 }

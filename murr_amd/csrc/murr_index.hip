@@ -196,7 +196,8 @@ __global__ void __launch_bounds__(256) index_seq(IndexArgs A, const uint64_t* se
 // trip of their own after the compare (query key, slot + location, stored key
 // and row offsets: three dependent round trips, not four).
 template <bool SIZED = false>
-__device__ __forceinline__ uint32_t probe_one(const IndexArgs& A, uint64_t i, uint64_t* size = nullptr) {
+__device__ __forceinline__ uint32_t probe_one(const IndexArgs& A, uint64_t i, uint64_t* size = nullptr,
+                                              uint64_t* start = nullptr) {
     const GAS int32_t* qo = gp(A.q_off);
     const int32_t q0 = qo[i];
     const uint32_t len = (uint32_t)(qo[i + 1] - q0);
@@ -218,7 +219,10 @@ __device__ __forceinline__ uint32_t probe_one(const IndexArgs& A, uint64_t i, ui
             }
             if (key_eq(gp(A.key_data) + (uint32_t)(l >> 32), qc, q, len)) {
                 row = (uint32_t)e;
-                if constexpr (SIZED) *size = o1 - o0;
+                if constexpr (SIZED) {
+                    *size = o1 - o0;
+                    if (start) *start = o0;
+                }
                 break;
             }
         }
@@ -459,6 +463,71 @@ __global__ void __launch_bounds__(256) gather_scan_copy(IndexArgs A) {
     copy_row<kCopyLanes>(gp(A.blob), src, gp(A.out), d0, d1, tid % kCopyLanes);
 }
 
+// A small gather in one launch (nq <= 1024, A.lb set; launch_gather): one
+// workgroup per 64 queries.  Its first wave probes them (rows, sizes and
+// source offsets into LDS) and scans the sizes; lane 0 publishes the group's
+// byte total in lb[g] (bit 63 set), and the group's base is the sum of
+// lb[0 .. g) -- workgroups of lower index are dispatched first and never
+// wait on a later one, so the spin always ends (bounded anyway).  Then all
+// 512 threads copy the group's rows, 8 lanes a row, in one pass.  The words
+// come in two sets used by alternate launches (the host flips A.lb); a
+// launch's workgroup 0 zeroes the other set for the next one, so no launch
+// waits on a ticket at its end.
+constexpr unsigned long long kLbSet = 1ull << 63;
+__global__ void __launch_bounds__(512) gather_fused(IndexArgs A, unsigned long long* other) {
+    __shared__ uint64_t s_off[65], s_src[64];
+    __shared__ uint32_t s_row[64];
+    const uint32_t tid = threadIdx.x, g = blockIdx.x;
+    const uint64_t nq = A.nq, i0 = (uint64_t)g * 64;
+    GAS unsigned long long* lb = (GAS unsigned long long*)A.lb;
+    if (g == 0 && tid >= 64 && tid < 64 + kGatherGroups) gp(other)[tid - 64] = 0ull;
+    if (tid < 64) {
+        const uint64_t i = i0 + tid;
+        uint64_t sz = 0, src = 0;
+        uint32_t row = kMissing;
+        if (i < live_queries(A)) row = probe_one<true>(A, i, &sz, &src);
+        const uint64_t inc = wave_incl_scan64(sz, tid);
+        const uint64_t tot = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(inc >> 32), 63) << 32) |
+                             __builtin_amdgcn_readlane((uint32_t)inc, 63);
+        if (tid == 0) __hip_atomic_store(lb + g, kLbSet | tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // the groups before this one: lane j < g spins on lb[j]
+        uint64_t v = 0;
+        if (tid < g) {
+            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+            for (;;) {
+                v = __hip_atomic_load(lb + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (v & kLbSet) break;
+                if (__builtin_amdgcn_s_memrealtime() - t0 > 5000000ull) {  // 50 ms: cannot happen
+                    if (A.err) __hip_atomic_fetch_max(gp(A.err), ~0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    break;
+                }
+            }
+            v &= ~kLbSet;
+        }
+        const uint64_t base = wave_sum64(v);
+        s_off[tid] = base + inc - sz;
+        s_src[tid] = src;
+        s_row[tid] = row;
+        if (i < nq) {
+            gp(A.rows)[i] = row;
+            gp(A.sizes)[i] = min(base + inc - sz, A.out_cap);
+        }
+        if (tid == 63) {
+            s_off[64] = base + tot;
+            if (i0 + 64 >= nq) {  // the last group: the block's end and the exact size
+                gp(A.sizes)[nq] = min(base + tot, A.out_cap);
+                if (A.needed) gp(A.needed)[0] = base + tot;
+            }
+        }
+    }
+    __syncthreads();
+    const uint32_t r = tid / 8;
+    if (i0 + r < nq && s_row[r] != kMissing) {
+        const uint64_t d0 = min(s_off[r], A.out_cap), d1 = min(s_off[r + 1], A.out_cap);
+        if (d1 > d0) copy_row<8>(gp(A.blob), s_src[r], gp(A.out), d0, d1, tid % 8);
+    }
+}
+
 // ---- one read over a table sharded across GPUs (murr_multi_gather) ----------------
 // The caller's queries are grouped by owner shard (shard s holds grouped
 // positions [q_end[s - 1], q_end[s])); src[i] = grouped position of caller
@@ -582,6 +651,10 @@ uint64_t gather_scratch_words(uint64_t nq) {
 }
 
 hipError_t launch_gather(const IndexArgs& a, hipStream_t s) {
+    if (a.nq && a.nq <= 64 * kGatherGroups && a.lb) {  // (a.lb: this launch's word set; a.lb_other: the next's)
+        hipLaunchKernelGGL(gather_fused, dim3((uint32_t)((a.nq + 63) / 64)), dim3(512), 0, s, a, a.lb_other);
+        return hipGetLastError();
+    }
     if (a.nq && a.nq <= kScanThreads) {  // (A.scratch holds gather_scratch_words(nq))
         hipLaunchKernelGGL(gather_probe_wide, dim3((uint32_t)((a.nq + 63) / 64)), dim3(64), 0, s, a);
         constexpr uint32_t rows_per_wg = 256 / 8;

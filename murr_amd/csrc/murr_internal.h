@@ -301,7 +301,11 @@ struct IndexArgs {
     const uint32_t* src;        // multi-shard gather: caller query -> grouped position
     uint64_t nq_live;           // probe: queries [nq_live, nq) are misses without a lookup (a
                                 //   prepared read's padding to its capacity); 0 = all nq live
+    unsigned long long* lb;     // small gathers (nq <= 1024): the fused kernel's look-back words
+                                //   [kGatherGroups], zero at launch; null = the two-launch form
+    unsigned long long* lb_other;  //   the other word set, zeroed by this launch for the next
 };
+constexpr uint32_t kGatherGroups = 16;  // 64-query groups of a fused small gather
 // Shards of a multi-GPU read (murr_multi_gather): arenas, row offsets and the
 // end of each shard's grouped query range.
 constexpr uint32_t kMaxShards = 16;
