@@ -348,6 +348,15 @@ int murr_utf8_index(murr_ctx_t* ctx, const murr_segment_t* seg, const murr_block
  * from = 0 builds the whole index (= murr_utf8_index).  Enqueued. */
 int murr_utf8_index_update(murr_ctx_t* ctx, const murr_segment_t* seg, const murr_block_t* block,
                            uint64_t from, uint32_t stride, uint64_t* out);
+/* Per-row utf8 string bytes of a block's rows [from, n_rows): out[i * nutf8 +
+ * u] (u32, device) = what row i's u-th utf8 column adds to the decode's utf8
+ * offsets, by the index's cell rules (0 for a null, missing, short or
+ * malformed cell).  A resident table keeps these beside its arena, extended
+ * with every append, so a prepared read (murr_read_plan_new row_ulen) indexes
+ * its gathered block inside the gather.  A layout without utf8 columns
+ * writes nothing.  Enqueued. */
+int murr_utf8_row_lengths(murr_ctx_t* ctx, const murr_segment_t* seg, const murr_block_t* block,
+                          uint64_t from, uint32_t* out);
 /* murr_decode_enqueue / murr_decode_blocks with an index per block (uidx[b]
  * null: block b has none; uidx null: no block has one).  Same outputs. */
 int murr_decode_enqueue_ix(murr_ctx_t* ctx, const murr_segment_t* seg,
@@ -644,12 +653,16 @@ void murr_reader_free(murr_reader_t* r);
  * decodes cap rows (queries past nq are misses) and reports nq.  The table's
  * arena, row offsets and index must not change while the plan lives (a write
  * that appends invalidates it).  Fails with MURR_E_ARGUMENT when cap x
- * max_row passes 64 MiB (murr_reader_read sizes such reads exactly). */
+ * max_row passes 64 MiB (murr_reader_read sizes such reads exactly).
+ * row_ulen (optional, device): the table's per-row utf8 string bytes
+ * (murr_utf8_row_lengths over all its rows).  With it, and a layout of 1 to 4
+ * utf8 columns and cap <= 1024, the gather also writes the gathered block's
+ * utf8 index, and the decode runs in one pass instead of two. */
 typedef struct murr_read_plan murr_read_plan_t;
 int murr_read_plan_new(murr_ctx_t* ctx, const murr_segment_t* seg, const murr_index_t* idx,
-                       const uint8_t* blob, const uint64_t* row_off, uint64_t blob_bytes,
-                       uint64_t max_row, const uint32_t* proj, uint32_t nproj, uint64_t cap,
-                       murr_read_plan_t** out);
+                       const uint8_t* blob, const uint64_t* row_off, const uint32_t* row_ulen,
+                       uint64_t blob_bytes, uint64_t max_row, const uint32_t* proj, uint32_t nproj,
+                       uint64_t cap, murr_read_plan_t** out);
 /* Keys in device memory (q_offsets[nq + 1], q_data); outs[nproj] are device
  * arrays in the plan's buffers (n = nq), valid until its next run or free.
  * Returns once the decode's counters are in (null counts, lengths, errors):

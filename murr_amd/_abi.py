@@ -169,6 +169,7 @@ SIGNATURES = {
     "murr_sst_result_free": (None, [P, C.POINTER(SstResult)]),
     "murr_utf8_index": (I32, [P, C.POINTER(Segment), C.POINTER(Block), U32, P]),
     "murr_utf8_index_update": (I32, [P, C.POINTER(Segment), C.POINTER(Block), U64, U32, P]),
+    "murr_utf8_row_lengths": (I32, [P, C.POINTER(Segment), C.POINTER(Block), U64, P]),
     "murr_encode_batch_ix": (I32, [P, C.POINTER(Segment), C.POINTER(ColIn), U64, P, U64, P, U32, P,
                                    C.POINTER(U64), C.POINTER(Error)]),
     "murr_encode_bound": (U64, [C.POINTER(Segment), U64, C.POINTER(U64)]),
@@ -194,7 +195,7 @@ SIGNATURES = {
     "murr_reader_read": (I32, [P, P, P, P, U64, U64, P, P, U64, U64, C.POINTER(U32), U32,
                                C.POINTER(HostArray), C.POINTER(Error)]),
     "murr_reader_free": (None, [P]),
-    "murr_read_plan_new": (I32, [P, C.POINTER(Segment), P, P, P, U64, U64, C.POINTER(U32), U32, U64, PP]),
+    "murr_read_plan_new": (I32, [P, C.POINTER(Segment), P, P, P, P, U64, U64, C.POINTER(U32), U32, U64, PP]),
     "murr_read_plan_run_device": (I32, [P, P, P, U64, C.POINTER(Array), C.POINTER(Error)]),
     "murr_read_plan_run": (I32, [P, P, P, U64, U64, C.POINTER(HostArray), C.POINTER(Error)]),
     "murr_read_plan_capacity": (U64, [P]),

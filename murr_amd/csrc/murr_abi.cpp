@@ -509,13 +509,13 @@ int small_gather_words(murr_ctx* c, IndexArgs* a, murr_error_t* err) {
     if (a->nq == 0 || a->nq > 64 * kGatherGroups) return MURR_OK;
     if (!c->glb) {
         void* p = nullptr;
-        HIPC(hipMalloc(&p, 16 * kGatherGroups));
-        HIPC(hipMemsetAsync(p, 0, 16 * kGatherGroups, c->stream));
+        HIPC(hipMalloc(&p, 16 * kGatherWords));
+        HIPC(hipMemsetAsync(p, 0, 16 * kGatherWords, c->stream));
         c->glb = (unsigned long long*)p;
     }
-    a->lb = c->glb + kGatherGroups * c->glb_set;
+    a->lb = c->glb + kGatherWords * c->glb_set;
     c->glb_set ^= 1u;
-    a->lb_other = c->glb + kGatherGroups * c->glb_set;
+    a->lb_other = c->glb + kGatherWords * c->glb_set;
     return MURR_OK;
 }
 
@@ -1806,6 +1806,31 @@ int murr_utf8_index_update(murr_ctx_t* c, const murr_segment_t* seg, const murr_
     a.stride = stride;
     a.bs = seg->bitset_size;
     HIPC(launch_utf8_index(a, c->stream));
+    return MURR_OK;
+}
+
+int murr_utf8_row_lengths(murr_ctx_t* c, const murr_segment_t* seg, const murr_block_t* block, uint64_t from,
+                          uint32_t* out) {
+    murr_error_t* err = nullptr;
+    if (!c || !valid_segment(seg) || !block || c->pending || from > block->n_rows) return MURR_E_ARGUMENT;
+    Utf8IndexArgs a{};
+    for (uint32_t i = 0; i < seg->ncols; i++) {
+        if (seg->cols[i].dtype != MURR_UTF8) continue;
+        if (a.nu == kMaxUidxCols) return MURR_E_ARGUMENT;
+        a.col[a.nu] = seg->cols[i].index;
+        a.fo[a.nu] = seg->bitset_size + seg->cols[i].offset;
+        a.nu++;
+    }
+    if (!a.nu || from == block->n_rows) return MURR_OK;
+    if (!out || !block->data || (!block->row_off && !block->row_off32)) return MURR_E_ARGUMENT;
+    HIPC(hipSetDevice(c->device));
+    a.data = block->data;
+    a.row_off = block->row_off;
+    a.row_off32 = block->row_off32;
+    a.from = from;
+    a.n = block->n_rows;
+    a.bs = seg->bitset_size;
+    HIPC(launch_utf8_row_lengths(a, out, c->stream));
     return MURR_OK;
 }
 
@@ -3352,12 +3377,15 @@ struct murr_read_plan {
     const murr_index_t* x = nullptr;
     const uint8_t* blob = nullptr;
     const uint64_t* row_off = nullptr;
+    const uint32_t* row_ulen = nullptr;  // the table's per-row utf8 string bytes (null: none)
+    uint32_t nu = 0;                     // utf8 columns the gather indexes (0: split-mode decode)
     uint64_t cap = 0, data_cap = 0, utf8_cap = 0;
-    uint8_t* dwork = nullptr;  // device: gather offsets (cap+1) | rows (cap) | needed | gathered rows
+    uint8_t* dwork = nullptr;  // device: gather offsets (cap+1) | rows (cap) | needed | utf8 index | gathered rows
     uint64_t dwork_cap = 0;
     uint64_t* doff = nullptr;
     uint32_t* drows = nullptr;
     uint64_t* dneed = nullptr;
+    uint64_t* duidx = nullptr;  // the gathered block's utf8 index, stride 64 (written by the gather)
     uint8_t* ddata = nullptr;
     uint8_t* hkeys = nullptr;  // pinned: rebased key offsets (cap + 1), then the key bytes
     uint64_t hkeys_cap = 0;
@@ -3407,6 +3435,12 @@ int read_plan_gather(murr_read_plan* r, const uint8_t* q_data, const int32_t* q_
     a.needed = r->dneed;
     a.scratch = c->aux;
     if (const int st = small_gather_words(c, &a, err)) return st;
+    if (r->nu) {  // (set only when the fused gather runs: cap <= 1024)
+        if (!a.lb) return MURR_E_INTERNAL;
+        a.ulen = r->row_ulen;
+        a.uidx = r->duidx;
+        a.nu = r->nu;
+    }
     HIPC(launch_gather(a, c->stream));
     return MURR_OK;
 }
@@ -3442,8 +3476,8 @@ void read_plan_report(const murr_read_plan* r, uint64_t nq, murr_array_t* dev, m
 extern "C" {
 
 int murr_read_plan_new(murr_ctx_t* c, const murr_segment_t* seg, const murr_index_t* x, const uint8_t* arena,
-                       const uint64_t* row_off, uint64_t arena_bytes, uint64_t max_row, const uint32_t* proj,
-                       uint32_t nproj, uint64_t cap, murr_read_plan_t** out) {
+                       const uint64_t* row_off, const uint32_t* row_ulen, uint64_t arena_bytes, uint64_t max_row,
+                       const uint32_t* proj, uint32_t nproj, uint64_t cap, murr_read_plan_t** out) {
     murr_error_t* err = nullptr;
     if (!out) return MURR_E_ARGUMENT;
     *out = nullptr;
@@ -3471,13 +3505,25 @@ int murr_read_plan_new(murr_ctx_t* c, const murr_segment_t* seg, const murr_inde
     r->cap = cap;
     r->data_cap = data_cap;
     r->utf8_cap = max_row > fixed ? cap * (max_row - fixed) : 0;
-    // device work: offsets | rows | needed | gathered rows (16-B aligned)
+    // the gathered block's utf8 index, built by the fused gather from the
+    // table's per-row string bytes (§3.4): layouts of 1 .. kGatherMaxU utf8
+    // columns and up to 1024 keys; otherwise the decode takes the block in
+    // split mode
+    uint32_t nu = 0;
+    for (uint32_t i = 0; i < seg->ncols; i++) nu += seg->cols[i].dtype == MURR_UTF8;
+    r->row_ulen = row_ulen;
+    r->nu = row_ulen && nu >= 1 && nu <= kGatherMaxU && cap <= 64 * kGatherGroups ? nu : 0u;
+#ifdef MURR_TUNING
+    if (std::getenv("MURR_READ_NOIDX")) r->nu = 0;
+#endif
+    // device work: offsets | rows | needed | utf8 index | gathered rows (16-B aligned)
     const uint64_t o_rows = round_up((cap + 1) * 8, 256), o_need = round_up(o_rows + cap * 4, 256),
-                   o_data = o_need + 256;
+                   o_uidx = o_need + 256, o_data = round_up(o_uidx + 8 * ((cap + 63) / 64 + 1) * std::max(nu, 1u), 256);
     if (!grow_dev(c, &r->dwork, &r->dwork_cap, o_data + data_cap + 16)) return MURR_E_HIP;
     r->doff = (uint64_t*)r->dwork;
     r->drows = (uint32_t*)(r->dwork + o_rows);
     r->dneed = (uint64_t*)(r->dwork + o_need);
+    r->duidx = (uint64_t*)(r->dwork + o_uidx);
     r->ddata = r->dwork + o_data;
     // arrays: the fixed-size parts first (values, validity, utf8 offsets), then
     // the utf8 bytes, so the D2H is one segment plus one per utf8 column
@@ -3522,11 +3568,14 @@ int murr_read_plan_new(murr_ctx_t* c, const murr_segment_t* seg, const murr_inde
     // table's mean row x cap; rows end at doff[cap], never read past)
     const uint64_t mean = x->n ? arena_bytes / x->n : fixed;
     murr_block_t blk{r->ddata, r->doff, cap, std::min<uint64_t>(data_cap, std::max<uint64_t>(16, mean * cap)), nullptr};
-    // (no utf8 index: the decode takes a small block's segments in split
-    // mode; indexing the gathered block -- murr_utf8_index's two kernels, or
-    // a one-workgroup gather that also indexed -- cost more than the single
-    // pass saved)
-    int st = murr_decode_plan(c, &r->seg, r->proj.data(), nproj, &blk, 1, nullptr, 0, o.arr.data(), &r->dplan);
+    // With the gather's utf8 index the decode cuts the block into one-pass
+    // virtual blocks; without one it takes the block in split mode (two
+    // passes and a look-back).  Indexing the gathered block in kernels of its
+    // own -- murr_utf8_index's two, or a one-workgroup gather that also
+    // indexed -- cost more than the single pass saved.
+    const uint64_t* ux[1] = {r->duidx};
+    int st = murr_decode_plan(c, &r->seg, r->proj.data(), nproj, &blk, 1, r->nu ? ux : nullptr, r->nu ? 64u : 0u,
+                              o.arr.data(), &r->dplan);
     if (st) return st;
     (void)murr_plan_time_every(r->dplan, 0);  // (no timing events between the run's kernels)
     HIPC(hipEventCreateWithFlags(&r->ev, hipEventDisableTiming));

@@ -197,7 +197,7 @@ __global__ void __launch_bounds__(256) index_seq(IndexArgs A, const uint64_t* se
 // and row offsets: three dependent round trips, not four).
 template <bool SIZED = false>
 __device__ __forceinline__ uint32_t probe_one(const IndexArgs& A, uint64_t i, uint64_t* size = nullptr,
-                                              uint64_t* start = nullptr) {
+                                              uint64_t* start = nullptr, uint32_t* ul = nullptr) {
     const GAS int32_t* qo = gp(A.q_off);
     const int32_t q0 = qo[i];
     const uint32_t len = (uint32_t)(qo[i + 1] - q0);
@@ -213,15 +213,25 @@ __device__ __forceinline__ uint32_t probe_one(const IndexArgs& A, uint64_t i, ui
         if (e == kEmpty) break;
         if ((e >> 32) == (h >> 32) && (uint32_t)l == len) {
             uint64_t o0 = 0, o1 = 0;
+            uint32_t u4[kGatherMaxU] = {0, 0, 0, 0};
             if constexpr (SIZED) {
                 o0 = gp(A.row_off)[(uint32_t)e];
                 o1 = gp(A.row_off)[(uint32_t)e + 1];
+                if (ul) {  // (the row's utf8 string bytes, in the same round trip)
+#pragma unroll
+                    for (uint32_t u = 0; u < kGatherMaxU; u++)
+                        if (u < A.nu) u4[u] = gp(A.ulen)[(uint64_t)(uint32_t)e * A.nu + u];
+                }
             }
             if (key_eq(gp(A.key_data) + (uint32_t)(l >> 32), qc, q, len)) {
                 row = (uint32_t)e;
                 if constexpr (SIZED) {
                     *size = o1 - o0;
                     if (start) *start = o0;
+                    if (ul) {
+#pragma unroll
+                        for (uint32_t u = 0; u < kGatherMaxU; u++) ul[u] = u4[u];
+                    }
                 }
                 break;
             }
@@ -466,57 +476,92 @@ __global__ void __launch_bounds__(256) gather_scan_copy(IndexArgs A) {
 // A small gather in one launch (nq <= 1024, A.lb set; launch_gather): one
 // workgroup per 64 queries.  Its first wave probes them (rows, sizes and
 // source offsets into LDS) and scans the sizes; lane 0 publishes the group's
-// byte total in lb[g] (bit 63 set), and the group's base is the sum of
-// lb[0 .. g) -- workgroups of lower index are dispatched first and never
-// wait on a later one, so the spin always ends (bounded anyway).  Then all
-// 512 threads copy the group's rows, 8 lanes a row, in one pass.  The words
-// come in two sets used by alternate launches (the host flips A.lb); a
-// launch's workgroup 0 zeroes the other set for the next one, so no launch
-// waits on a ticket at its end.
+// byte total in its look-back word (bit 63 set), and the group's base is the
+// sum of the words of the groups before it -- workgroups of lower index are
+// dispatched first and never wait on a later one, so the spin always ends
+// (bounded anyway).  Then all 512 threads copy the group's rows, 8 lanes a
+// row, in one pass.  The words come in two sets used by alternate launches
+// (the host flips A.lb); a launch's workgroup 0 zeroes the other set for the
+// next one, so no launch waits on a ticket at its end.
+// With A.ulen (a resident table's per-row utf8 string bytes), the same probe
+// loads each row's string bytes beside its offsets, the look-back carries
+// their group totals too, and the gather writes the gathered block's utf8
+// index at stride 64 (A.uidx): the decode then cuts the block into one-pass
+// virtual blocks instead of split mode's two passes and look-back.
 constexpr unsigned long long kLbSet = 1ull << 63;
+constexpr uint32_t kLbW = 1 + kGatherMaxU;  // words per group: bytes, then each utf8 column's string bytes
 __global__ void __launch_bounds__(512) gather_fused(IndexArgs A, unsigned long long* other) {
     __shared__ uint64_t s_off[65], s_src[64];
     __shared__ uint32_t s_row[64];
     const uint32_t tid = threadIdx.x, g = blockIdx.x;
     const uint64_t nq = A.nq, i0 = (uint64_t)g * 64;
+    const uint32_t nu = A.ulen ? A.nu : 0u;
     GAS unsigned long long* lb = (GAS unsigned long long*)A.lb;
-    if (g == 0 && tid >= 64 && tid < 64 + kGatherGroups) gp(other)[tid - 64] = 0ull;
+    if (g == 0 && tid >= 64 && tid < 64 + kGatherWords) gp(other)[tid - 64] = 0ull;
     if (tid < 64) {
         const uint64_t i = i0 + tid;
         uint64_t sz = 0, src = 0;
+        uint32_t ul[kGatherMaxU] = {0, 0, 0, 0};
         uint32_t row = kMissing;
-        if (i < live_queries(A)) row = probe_one<true>(A, i, &sz, &src);
-        const uint64_t inc = wave_incl_scan64(sz, tid);
-        const uint64_t tot = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(inc >> 32), 63) << 32) |
-                             __builtin_amdgcn_readlane((uint32_t)inc, 63);
-        if (tid == 0) __hip_atomic_store(lb + g, kLbSet | tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        // the groups before this one: lane j < g spins on lb[j]
-        uint64_t v = 0;
+        if (i < live_queries(A)) row = probe_one<true>(A, i, &sz, &src, nu ? ul : nullptr);
+        uint64_t x[kLbW], inc[kLbW];
+        x[0] = sz;
+#pragma unroll
+        for (uint32_t u = 0; u < kGatherMaxU; u++) x[1 + u] = ul[u];
+#pragma unroll
+        for (uint32_t k = 0; k < kLbW; k++) {
+            inc[k] = 0;
+            if (k <= nu) {
+                inc[k] = wave_incl_scan64(x[k], tid);
+                const uint64_t tot = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(inc[k] >> 32), 63) << 32) |
+                                     __builtin_amdgcn_readlane((uint32_t)inc[k], 63);
+                if (tid == 0) __hip_atomic_store(lb + g * kLbW + k, kLbSet | tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        // the groups before this one: lane j < g spins on group j's words,
+        // all of them loaded together each time round
+        uint64_t v[kLbW], base[kLbW];
+#pragma unroll
+        for (uint32_t k = 0; k < kLbW; k++) v[k] = kLbSet;
         if (tid < g) {
             const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
             for (;;) {
-                v = __hip_atomic_load(lb + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (v & kLbSet) break;
+                bool all = true;
+#pragma unroll
+                for (uint32_t k = 0; k < kLbW; k++)
+                    if (k <= nu) v[k] = __hip_atomic_load(lb + tid * kLbW + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+                for (uint32_t k = 0; k < kLbW; k++) all &= !(k <= nu) || (v[k] & kLbSet) != 0;
+                if (all) break;
                 if (__builtin_amdgcn_s_memrealtime() - t0 > 5000000ull) {  // 50 ms: cannot happen
                     if (A.err) __hip_atomic_fetch_max(gp(A.err), ~0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     break;
                 }
             }
-            v &= ~kLbSet;
         }
-        const uint64_t base = wave_sum64(v);
-        s_off[tid] = base + inc - sz;
+#pragma unroll
+        for (uint32_t k = 0; k < kLbW; k++) base[k] = k <= nu ? wave_sum64(tid < g ? v[k] & ~kLbSet : 0ull) : 0;
+        s_off[tid] = base[0] + inc[0] - sz;
         s_src[tid] = src;
         s_row[tid] = row;
         if (i < nq) {
             gp(A.rows)[i] = row;
-            gp(A.sizes)[i] = min(base + inc - sz, A.out_cap);
+            gp(A.sizes)[i] = min(base[0] + inc[0] - sz, A.out_cap);
+        }
+        const bool last = i0 + 64 >= nq;
+        if (tid == 0) {  // utf8 index entry g: the string bytes of the rows before row 64 g
+#pragma unroll
+            for (uint32_t u = 0; u < kGatherMaxU; u++)
+                if (u < nu) gp(A.uidx)[(uint64_t)g * nu + u] = base[1 + u];
         }
         if (tid == 63) {
-            s_off[64] = base + tot;
-            if (i0 + 64 >= nq) {  // the last group: the block's end and the exact size
-                gp(A.sizes)[nq] = min(base + tot, A.out_cap);
-                if (A.needed) gp(A.needed)[0] = base + tot;
+            s_off[64] = base[0] + inc[0];
+            if (last) {  // the block's end, the exact size and the index's last entry
+                gp(A.sizes)[nq] = min(base[0] + inc[0], A.out_cap);
+                if (A.needed) gp(A.needed)[0] = base[0] + inc[0];
+#pragma unroll
+                for (uint32_t u = 0; u < kGatherMaxU; u++)
+                    if (u < nu) gp(A.uidx)[(uint64_t)(g + 1) * nu + u] = base[1 + u] + inc[1 + u];
             }
         }
     }
@@ -728,6 +773,31 @@ __global__ void __launch_bounds__(256) uidx_sums(Utf8IndexArgs A) {
     }
 }
 
+// Per row: out[i * nu + u] = the string bytes row i's u-th utf8 column adds
+// to the decode's offsets, by the same cell rules (rows [from, n)).  A
+// resident table keeps these beside its arena for the fused gather.
+__global__ void __launch_bounds__(256) utf8_row_lengths(Utf8IndexArgs A, uint32_t* out) {
+    const uint64_t i = A.from + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= A.n) return;
+    const uint64_t a = A.row_off32 ? (uint64_t)gp(A.row_off32)[i] : gp(A.row_off)[i];
+    const uint64_t e = A.row_off32 ? (uint64_t)gp(A.row_off32)[i + 1] : gp(A.row_off)[i + 1];
+    const bool span_ok = !(e < a || e - a > 0xFFFFFFFFull);
+    const uint32_t rl = span_ok ? (uint32_t)(e - a) : 0u;
+    const uint8_t* row = A.data + a;
+    for (uint32_t u = 0; u < A.nu; u++) {
+        const uint32_t c = A.col[u], fo = A.fo[u];
+        uint32_t l = 0;
+        if (span_ok && rl >= A.bs && !((row[c >> 3] >> (c & 7)) & 1) && fo + 4 <= rl) {
+            const uint32_t sl = ld32u(row + fo), vlen = rl - A.bs;
+            if (sl <= vlen - 4) {
+                const uint32_t len = ld32u(row + A.bs + sl);
+                if (len <= vlen - 4 - sl) l = len;
+            }
+        }
+        gp(out)[i * A.nu + u] = l;
+    }
+}
+
 // One workgroup: entries k0 + 1 .. k0 + nwin = the total before `from` (the
 // index's old total, entry ceil(from / stride), read before any entry is
 // written) plus the inclusive prefix of the window sums; entry 0 = 0 for a
@@ -768,6 +838,12 @@ __global__ void __launch_bounds__(1024) uidx_scan(uint64_t* out, const uint64_t*
 
 uint64_t utf8_index_windows(uint64_t from, uint64_t n, uint64_t stride) {
     return n > from ? (n + stride - 1) / stride - from / stride : 0;
+}
+
+hipError_t launch_utf8_row_lengths(const Utf8IndexArgs& a, uint32_t* out, hipStream_t s) {
+    if (a.n > a.from)
+        hipLaunchKernelGGL(utf8_row_lengths, dim3((uint32_t)((a.n - a.from + 255) / 256)), dim3(256), 0, s, a, out);
+    return hipGetLastError();
 }
 
 hipError_t launch_utf8_index(const Utf8IndexArgs& a, hipStream_t s) {

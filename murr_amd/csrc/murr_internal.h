@@ -274,6 +274,7 @@ struct Utf8IndexArgs {
     uint32_t fo[kMaxUidxCols];     // its slot's row offset (bitset_size + offset)
 };
 hipError_t launch_utf8_index(const Utf8IndexArgs& a, hipStream_t s);
+hipError_t launch_utf8_row_lengths(const Utf8IndexArgs& a, uint32_t* out, hipStream_t s);  // rows [from, n)
 uint64_t utf8_index_windows(uint64_t from, uint64_t n, uint64_t stride);  // part[] entries per column
 
 // Device key index + row gather (murr_index.hip).
@@ -302,10 +303,17 @@ struct IndexArgs {
     uint64_t nq_live;           // probe: queries [nq_live, nq) are misses without a lookup (a
                                 //   prepared read's padding to its capacity); 0 = all nq live
     unsigned long long* lb;     // small gathers (nq <= 1024): the fused kernel's look-back words
-                                //   [kGatherGroups], zero at launch; null = the two-launch form
+                                //   [kGatherGroups][1 + kGatherMaxU], zero at launch; null = the
+                                //   two-launch form
     unsigned long long* lb_other;  //   the other word set, zeroed by this launch for the next
+    const uint32_t* ulen;       // fused gather (optional): the table's per-row utf8 string bytes
+                                //   [n][nu] (murr_utf8_row_lengths), with them
+    uint64_t* uidx;             //   out: the gathered block's utf8 index at stride 64
+    uint32_t nu;                //   utf8 columns (1 .. kGatherMaxU)
 };
 constexpr uint32_t kGatherGroups = 16;  // 64-query groups of a fused small gather
+constexpr uint32_t kGatherMaxU = 4;     // utf8 columns a fused gather indexes
+constexpr uint32_t kGatherWords = kGatherGroups * (1 + kGatherMaxU);  // look-back words per set
 // Shards of a multi-GPU read (murr_multi_gather): arenas, row offsets and the
 // end of each shard's grouped query range.
 constexpr uint32_t kMaxShards = 16;

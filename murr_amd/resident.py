@@ -165,6 +165,8 @@ TWO_PHASE_BYTES = 64 << 20
 # (profiles/r05/ab_stride.txt), with a quarter of the index.  A table can
 # pick another (uidx_stride).
 UIDX_STRIDE = 512
+# utf8 columns a prepared read's gather indexes (kGatherMaxU, murr_internal.h)
+ROW_ULEN_MAX = 4
 
 
 def read_capacity(nq: int) -> int:
@@ -186,7 +188,8 @@ class ReadPlan:
         pj = (C.c_uint32 * len(proj))(*proj)
         h = C.c_void_p()
         raise_status(L.murr_read_plan_new(self.ctx.h, C.byref(rt.segment.c), rt.index.h, rt.arena.ptr,
-                                          rt.row_off.ptr, rt.used, rt.max_row, pj, len(proj), self.cap,
+                                          rt.row_off.ptr, rt.ulen.ptr if rt.ulen is not None else None,
+                                          rt.used, rt.max_row, pj, len(proj), self.cap,
                                           C.byref(h)), what="murr_read_plan_new")
         self.h = h
         self.host_outs = (_abi.HostArray * len(proj))()
@@ -243,6 +246,12 @@ class ResidentTable:
         self._schemas = {}     # read(): the field names (C strings) per requested column list
         self.uidx = None       # utf8 index of the arena (every self.stride rows), kept with every write
         self.uidx_cap = 0      # entries
+        # per-row utf8 string bytes (murr_utf8_row_lengths, [n][nutf8] u32),
+        # kept with every write for layouts of 1 .. ROW_ULEN_MAX utf8 columns:
+        # a prepared read's gather indexes its block with them (one-pass decode)
+        self.nutf8 = sum(1 for c in self.segment.columns if c.dtype == DTypeName.Utf8)
+        self.ulen = None
+        self.ulen_cap = 0      # rows
         self._scan_plans = {}  # id(outs) (None: the plan's own outputs) -> (key, DecodePlan) of scan_device
         self._read_plans = {}  # (projection, capacity) -> ReadPlan over the table state _rp_state
         self._rp_state = None
@@ -319,8 +328,20 @@ class ResidentTable:
 
     def _index_tail(self, n_old: int):
         """Extend the arena's utf8 index over rows n_old .. n (the written
-        block's index, kept as the table grows: only the new rows are read)."""
+        block's index, kept as the table grows: only the new rows are read),
+        and the per-row utf8 string bytes over the same rows."""
         L, seg = self.ctx.L, self.segment
+        if 1 <= self.nutf8 <= ROW_ULEN_MAX:
+            if self.n > self.ulen_cap:
+                cap = max(self.n, 2 * self.ulen_cap, 1024)
+                buf = self.ctx.alloc(4 * self.nutf8 * cap)
+                if self.ulen is not None and n_old:
+                    buf.copy_from(self.ulen, 4 * self.nutf8 * n_old)
+                    self.ulen.free()
+                self.ulen, self.ulen_cap = buf, cap
+            blk = _abi.Block(self.arena.ptr, self.row_off.ptr, self.n, self.used)
+            raise_status(L.murr_utf8_row_lengths(self.ctx.h, C.byref(seg.c), C.byref(blk), n_old, self.ulen.ptr),
+                         what="murr_utf8_row_lengths")
         need = int(L.murr_utf8_index_len(C.byref(seg.c), self.n, self.stride))
         if need == 0:
             return
@@ -503,7 +524,8 @@ class ResidentTable:
         cap = read_capacity(nq)
         if cap * max(self.max_row, 1) > TWO_PHASE_BYTES:
             return None
-        state = (self.arena.ptr, self.row_off.ptr, self.n, self.used, self.max_row)
+        state = (self.arena.ptr, self.row_off.ptr, self.ulen.ptr if self.ulen is not None else 0, self.n, self.used,
+                 self.max_row)
         if state != self._rp_state:  # a write changed the table: every plan is stale
             for p in self._read_plans.values():
                 p.close()

@@ -121,3 +121,50 @@ def test_plan_device_run_equals_unprepared_path(table):
         if a["null_count"]:
             nb = (nq + 7) // 8
             assert a["validity"][:nb] == b["validity"][:nb], p
+
+
+def test_row_lengths_match_the_written_strings(table):
+    # murr_utf8_row_lengths, kept by ResidentTable beside its arena: per row
+    # and utf8 column, the string bytes the decode's offsets advance by (0 for
+    # a null cell)
+    rt, b0 = table
+    assert rt.nutf8 == 2 and rt.ulen is not None
+    got = rt.ulen.download(4 * 2 * rt.n).view(np.uint32).reshape(rt.n, 2)
+    for u, name in enumerate(["c11", "c12"]):
+        want = [len(s.encode()) if s is not None else 0 for s in b0.column(name).to_pylist()]
+        assert got[:, u].tolist() == want, name
+
+
+@pytest.mark.parametrize("nq,mode", [(1, "cut"), (700, "cut"), (1000, "cut"), (1024, "cut"), (3000, "split")])
+def test_plan_indexes_its_gather_up_to_1024_keys(table, nq, mode):
+    # up to 1024 keys the gather writes the gathered block's utf8 index and
+    # the decode cuts the block (one pass); above, split mode (two passes)
+    rt, b0 = table
+    rng = np.random.default_rng(31 + nq)
+    keys = [f"key{i}" for i in rng.integers(0, 6300, size=nq)]
+    assert_same(rt.read(keys, COLS), expected([b0], keys, COLS))
+    assert rt.ctx.stats()["last_mode"] == mode
+
+
+def test_plan_five_utf8_columns_takes_split_mode():
+    # more utf8 columns than the gather indexes (4): the decode splits the block
+    from murr_amd import ColumnSchema, DTypeName as D, TableSchema
+    cols = {"key": ColumnSchema(D.Utf8, False)}
+    for i in range(5):
+        cols[f"s{i}"] = ColumnSchema(D.Utf8)
+    cols["v"] = ColumnSchema(D.Int32)
+    rt = ResidentTable(TableSchema("key", cols))
+    rng = np.random.default_rng(5)
+    n = 3000
+    arrays = [pa.array([f"key{i}" for i in range(n)], pa.string())]
+    for i in range(5):
+        arrays.append(pa.array([None if rng.random() < 0.2 else "x" * int(rng.integers(0, 40)) for _ in range(n)],
+                               pa.string()))
+    arrays.append(pa.array(rng.integers(-5, 5, size=n).astype(np.int32)))
+    b = pa.RecordBatch.from_arrays(arrays, names=["key"] + [f"s{i}" for i in range(5)] + ["v"])
+    rt.write(b)
+    assert rt.ulen is None
+    names = [f"s{i}" for i in range(5)] + ["v"]
+    keys = [f"key{i}" for i in rng.integers(0, 3100, size=1000)]
+    assert_same(rt.read(keys, names), expected([b], keys, names))
+    assert rt.ctx.stats()["last_mode"] == "split"
