@@ -198,6 +198,8 @@ class ReadPlan:
 
     def run(self, q: pa.Array):
         """Keys as an Arrow utf8/binary array -> the plan's host arrays."""
+        if self.h is None:
+            raise SegmentError("read plan closed (the table was written since it was made)")
         kb = q.buffers()
         nq = len(q)
         st = self.ctx.L.murr_read_plan_run(self.h, kb[2].address if nq and kb[2] is not None else None,
@@ -208,6 +210,8 @@ class ReadPlan:
 
     def run_device(self, q_data: int, q_offsets: int, nq: int):
         """Keys in device memory (Arrow utf8 layout) -> the plan's device arrays (n = nq)."""
+        if self.h is None:
+            raise SegmentError("read plan closed (the table was written since it was made)")
         st = self.ctx.L.murr_read_plan_run_device(self.h, q_data, q_offsets, nq, self.dev_outs, C.byref(self.err))
         raise_status(st, self.err, "murr_read_plan_run_device")
         return self.dev_outs
@@ -298,6 +302,7 @@ class ResidentTable:
         m = batch.num_rows
         if m == 0:
             return
+        self._drop_read_plans()  # (before _grow can free the arena they point at)
         sizes = row_sizes(self.segment, arrays)
         bound = int(sizes.sum())
         self._grow(bound, m)
@@ -368,6 +373,7 @@ class ResidentTable:
         crosses to the host."""
         if self.n:
             raise SegmentError("load_sst rehydrates an empty resident table")
+        self._drop_read_plans()
         n = entries.n
         if n == 0:
             return
@@ -512,6 +518,15 @@ class ResidentTable:
         decode_blocks(self.ctx, self.segment, proj, [blk], outs)
         return req, [download_array(self.ctx, outs.array(0, p), int(c.dtype), nq) for p, c in enumerate(req)]
 
+    def _drop_read_plans(self):
+        """A write changes the arena, offsets and index the prepared reads
+        point at (and may free them): every plan is closed now, so a caller
+        still holding one gets an error from its run, not stale memory."""
+        for p in self._read_plans.values():
+            p.close()
+        self._read_plans = {}
+        self._rp_state = None
+
     def read_plan(self, columns, nq: int) -> ReadPlan | None:
         """The prepared read (ReadPlan) for these columns and nq keys over the
         table as it is now: made at the first read of its key-count class
@@ -526,10 +541,8 @@ class ResidentTable:
             return None
         state = (self.arena.ptr, self.row_off.ptr, self.ulen.ptr if self.ulen is not None else 0, self.n, self.used,
                  self.max_row)
-        if state != self._rp_state:  # a write changed the table: every plan is stale
-            for p in self._read_plans.values():
-                p.close()
-            self._read_plans = {}
+        if state != self._rp_state:  # the table changed since the plans were made: every plan is stale
+            self._drop_read_plans()
             self._rp_state = state
         plan = self._read_plans.pop((proj, cap), None)
         if plan is None:

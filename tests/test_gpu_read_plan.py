@@ -84,6 +84,14 @@ def test_plan_reused_across_key_sets_and_replaced_after_a_write():
     k3 = [f"key{i}" for i in rng.integers(0, 4100, size=1000)]
     assert_same(rt.read(k3, cols), expected([b0, b1], k3, cols))
     assert rt.read_plan(cols, 1000) is not p1 and p1.h is None  # (the stale plan was freed)
+    # a plan held across a write is closed by the write itself: running it
+    # raises instead of reading the arena the write may have moved
+    p2 = rt.read_plan(cols, 1000)
+    rt.write(batch_c(10, start=9000, seed=5))
+    assert p2.h is None
+    from murr_amd import SegmentError
+    with pytest.raises(SegmentError):
+        p2.run(pa.array(k3[:1000], pa.string()))
 
 
 def test_plan_keys_as_sliced_arrow_array_and_all_misses(table):
