@@ -1071,6 +1071,23 @@ def run_resident(args):
         rb = rt.read(qsets[i % 4], names)
         th.append(time.perf_counter() - t0)
     out_bytes = sum(sum(b.size for b in col.buffers() if b is not None) for col in rb.columns)
+    # the same reads with the keys already an Arrow array (what an Arrow-native
+    # caller -- the Rust binding of INTEGRATION.md -- hands over): the library
+    # run + the RecordBatch, without Python's list -> Arrow conversion
+    qarr = [pa.array(q, pa.string()) for q in qsets]
+    for i in range(args.warmup):
+        rt.read(qarr[i % 4], names)
+    ta = []
+    for i in range(args.steps):
+        t0 = time.perf_counter()
+        rt.read(qarr[i % 4], names)
+        ta.append(time.perf_counter() - t0)
+    hplan = rt.read_plan(names, nq)  # the library call alone (arrays left in pinned memory)
+    tr = []
+    for i in range(args.steps):
+        t0 = time.perf_counter()
+        hplan.run(qarr[i % 4])
+        tr.append(time.perf_counter() - t0)
     ipc_res = {}
     if args.ipc:
         # + Arrow IPC record-batch message packed in HBM (murr_ipc_batch_device)
@@ -1114,6 +1131,8 @@ def run_resident(args):
                       "device_path": "ReadPlan.run_device: fused probe + look-back + gather copy, prepared decode; one wait",
                       "us_per_read_device_unprepared_median": round(float(np.median(tu)) * 1e6, 1),
                       "us_per_read_host_median": round(float(np.median(th)) * 1e6, 1),
+                      "us_per_read_host_arrow_keys_median": round(float(np.median(ta)) * 1e6, 1),
+                      "us_per_read_host_plan_run_median": round(float(np.median(tr)) * 1e6, 1),
                       "GiB_s_arrow_out_device": round(out_bytes / med / GIB, 3),
                       "host_path": "ResidentTable.read: Python keys -> Arrow -> ReadPlan.run -> RecordBatch",
                       "kernels": "gather_fused, murr_jit_decode (+ copy_segs_kernel on the host path)",

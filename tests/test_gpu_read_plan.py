@@ -176,3 +176,46 @@ def test_plan_five_utf8_columns_takes_split_mode():
     keys = [f"key{i}" for i in rng.integers(0, 3100, size=1000)]
     assert_same(rt.read(keys, names), expected([b], keys, names))
     assert rt.ctx.stats()["last_mode"] == "split"
+
+
+@pytest.mark.parametrize("nu", [1, 3, 4])
+def test_plan_index_from_row_lengths_any_utf8_count(nu):
+    # layouts of 1, 3 and 4 utf8 columns (with empty, null and long strings,
+    # some over 1 KiB) between fixed-width ones: the gather's utf8 index from
+    # the per-row string bytes, a one-pass decode, the MemoryStore's answer;
+    # then an append (the row lengths extend) and a read over both batches
+    from murr_amd import ColumnSchema, DTypeName as D, TableSchema
+    rng = np.random.default_rng(70 + nu)
+    cols = {"key": ColumnSchema(D.Utf8, False), "a": ColumnSchema(D.Int64)}
+    for i in range(nu):
+        cols[f"s{i}"] = ColumnSchema(D.Utf8)
+    cols["b"] = ColumnSchema(D.Bool)
+    rt = ResidentTable(TableSchema("key", cols))
+    names = ["a"] + [f"s{i}" for i in range(nu)] + ["b"]
+
+    def batch(start, n):
+        arrays = [pa.array([f"key{start + i}" for i in range(n)], pa.string()),
+                  pa.array(rng.integers(-10**12, 10**12, size=n).astype(np.int64))]
+        for _ in range(nu):
+            vals = []
+            for _ in range(n):
+                r = rng.random()
+                vals.append(None if r < 0.15 else "" if r < 0.25 else
+                            "y" * int(rng.integers(1000, 3000)) if r < 0.27 else
+                            "é" * int(rng.integers(1, 20)))
+            arrays.append(pa.array(vals, pa.string()))
+        arrays.append(pa.array([None if rng.random() < 0.1 else bool(rng.random() < 0.5) for _ in range(n)]))
+        return pa.RecordBatch.from_arrays(arrays, names=["key"] + names)
+
+    b0 = batch(0, 4000)
+    rt.write(b0)
+    assert rt.ulen is not None
+    for nq in (1, 333, 1000):
+        keys = [f"key{i}" for i in rng.integers(0, 4200, size=nq)]
+        assert_same(rt.read(keys, names), expected([b0], keys, names))
+        assert rt.ctx.stats()["last_mode"] == "cut"
+    b1 = batch(3500, 2000)  # overwrites 500 keys, adds 1500
+    rt.write(b1)
+    keys = [f"key{i}" for i in rng.integers(0, 5600, size=1000)]
+    assert_same(rt.read(keys, names), expected([b0, b1], keys, names))
+    assert rt.ctx.stats()["last_mode"] == "cut"
