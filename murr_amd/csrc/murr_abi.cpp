@@ -499,13 +499,9 @@ int ensure_aux(murr_ctx* c, uint64_t need, murr_error_t* err) {
 
 // The fused small gather's words (gather_fused, murr_index.hip): two sets,
 // both zeroed once here; launches alternate between them and each zeroes the
-// other for the next (launches on one context's stream run in order).  Null
-// when the tuning variable MURR_GATHER_TWO picks the two-launch form (A/B).
+// other for the next (launches on one context's stream run in order).
 int small_gather_words(murr_ctx* c, IndexArgs* a, murr_error_t* err) {
     a->lb = a->lb_other = nullptr;
-#ifdef MURR_TUNING
-    if (std::getenv("MURR_GATHER_TWO")) return MURR_OK;
-#endif
     if (a->nq == 0 || a->nq > 64 * kGatherGroups) return MURR_OK;
     if (!c->glb) {
         void* p = nullptr;

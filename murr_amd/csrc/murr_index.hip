@@ -354,22 +354,6 @@ __global__ void __launch_bounds__(kScanThreads) gather_probe_scan(IndexArgs A) {
     }
 }
 
-// A small gather's other form (nq <= kScanThreads, launch_gather): the probe
-// spread over one wave per 64 queries instead of one workgroup's 16 waves on
-// one CU (its ~12 scattered loads per query go through that CU's address unit
-// alone), raw sizes into A.scratch.  The copy workgroups then each scan all
-// nq sizes themselves (8 KiB from L2, gather_scan_copy): no workgroup waits
-// on another's scan, and the number of launches stays two.
-__global__ void __launch_bounds__(64) gather_probe_wide(IndexArgs A) {
-    const uint64_t i = (uint64_t)blockIdx.x * 64 + threadIdx.x;
-    if (i >= A.nq) return;
-    uint64_t sz = 0;
-    uint32_t row = kMissing;
-    if (i < live_queries(A)) row = probe_one<true>(A, i, &sz);
-    gp(A.rows)[i] = row;
-    gp(A.scratch)[i] = sz;
-}
-
 // Eight lanes per query row, eight rows per wave: copy the row's blob bytes
 // to the block (rows clamped by the scan copy only what fits).  A lane owns
 // 16-B destination blocks b = lane%8, +8, ... aligned to the block buffer; it
@@ -423,54 +407,6 @@ __global__ void __launch_bounds__(256) gather_copy(IndexArgs A) {
     const uint64_t d0 = gp(A.sizes)[i], d1 = gp(A.sizes)[i + 1];
     if (d1 <= d0) return;
     copy_row<kCopyLanes>(gp(A.blob), gp(A.row_off)[row], gp(A.out), d0, d1, j);
-}
-
-// gather_probe_wide's second launch: every workgroup scans A.scratch[0, nq)
-// (exclusive, clamped to out_cap like gather_scan) into LDS and copies its
-// 256 / kCopyLanes rows; workgroup 0 also writes the offsets (A.sizes[0..nq])
-// and the total (*A.needed).
-template <uint32_t kCopyLanes>
-__global__ void __launch_bounds__(256) gather_scan_copy(IndexArgs A) {
-    constexpr uint32_t kT = 256, kPer = kScanThreads / kT;
-    __shared__ uint64_t s_off[kScanThreads + 1];
-    __shared__ uint64_t s_t[kT / 64];
-    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const uint64_t nq = A.nq;
-    const uint64_t i = (uint64_t)blockIdx.x * (kT / kCopyLanes) + tid / kCopyLanes;
-    const uint32_t row = i < nq ? gp(A.rows)[i] : kMissing;  // (issued beside the sizes' loads)
-    const uint64_t src = row != kMissing ? gp(A.row_off)[row] : 0;
-    uint64_t x[kPer], s = 0;
-#pragma unroll
-    for (uint32_t q = 0; q < kPer; q++) {
-        const uint64_t j = (uint64_t)tid * kPer + q;
-        x[q] = j < nq ? gp(A.scratch)[j] : 0;
-        s += x[q];
-    }
-    const uint64_t inc = wave_incl_scan64(s, lane);
-    if (lane == 63) s_t[wave] = inc;
-    __syncthreads();
-    uint64_t run = inc - s, all = 0;
-#pragma unroll
-    for (uint32_t w = 0; w < kT / 64; w++) {
-        run += w < wave ? s_t[w] : 0u;
-        all += s_t[w];
-    }
-#pragma unroll
-    for (uint32_t q = 0; q < kPer; q++) {
-        const uint64_t j = (uint64_t)tid * kPer + q;
-        if (j < nq) s_off[j] = min(run, A.out_cap);
-        run += x[q];
-    }
-    if (tid == 0) s_off[nq] = min(all, A.out_cap);
-    __syncthreads();
-    if (blockIdx.x == 0) {
-        for (uint64_t j = tid; j <= nq; j += kT) gp(A.sizes)[j] = s_off[j];
-        if (tid == 0 && A.needed) gp(A.needed)[0] = all;
-    }
-    if (row == kMissing) return;
-    const uint64_t d0 = s_off[i], d1 = s_off[i + 1];
-    if (d1 <= d0) return;
-    copy_row<kCopyLanes>(gp(A.blob), src, gp(A.out), d0, d1, tid % kCopyLanes);
 }
 
 // A small gather in one launch (nq <= 1024, A.lb set; launch_gather): one
@@ -690,21 +626,11 @@ hipError_t launch_multi_copy(const IndexArgs& a, const MultiTab& t, hipStream_t 
     return hipGetLastError();
 }
 
-uint64_t gather_scratch_words(uint64_t nq) {
-    const uint64_t g = gather_scan_groups(nq) + 1;
-    return nq <= kScanThreads ? (nq > g ? nq : g) : g;
-}
+uint64_t gather_scratch_words(uint64_t nq) { return gather_scan_groups(nq) + 1; }
 
 hipError_t launch_gather(const IndexArgs& a, hipStream_t s) {
     if (a.nq && a.nq <= 64 * kGatherGroups && a.lb) {  // (a.lb: this launch's word set; a.lb_other: the next's)
         hipLaunchKernelGGL(gather_fused, dim3((uint32_t)((a.nq + 63) / 64)), dim3(512), 0, s, a, a.lb_other);
-        return hipGetLastError();
-    }
-    if (a.nq && a.nq <= kScanThreads) {  // (A.scratch holds gather_scratch_words(nq))
-        hipLaunchKernelGGL(gather_probe_wide, dim3((uint32_t)((a.nq + 63) / 64)), dim3(64), 0, s, a);
-        constexpr uint32_t rows_per_wg = 256 / 8;
-        hipLaunchKernelGGL(gather_scan_copy<8>, dim3((uint32_t)((a.nq + rows_per_wg - 1) / rows_per_wg)), dim3(256), 0,
-                           s, a);
         return hipGetLastError();
     }
     const hipError_t e = launch_gather_scan(a, s);
