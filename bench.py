@@ -996,6 +996,49 @@ def ref_keys(kind: str, rows: int, nq: int, k: int):
     return [f"key{int(i)}" for i in ids]
 
 
+def resident_cpu_baseline(rt, kind: str, n: int, names, qarr, reads: int):
+    """CPU baseline of a resident read: the oracle's MemoryStore restatement
+    (src/io/store/memory.rs:28-45: a key map, then ReadBatchBuilder add_row /
+    add_empty per key and build) over the same table's keys and blobs (the
+    arena downloaded), the same key sets, one host thread.  None above 20 M
+    rows (the host key map of read_block's 100 M rows is not a bounded
+    sample)."""
+    if n > 20_000_000:
+        return None
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    import pyarrow as pa
+    blob = rt.arena.download(max(rt.used, 1))
+    off = rt.row_off.download(8 * (rt.n + 1)).view(np.uint64)
+    keys = pa.array([str(i) for i in range(n)] if kind == "ref" else [f"key{i}" for i in range(n)], pa.string())
+    store = O.MemStore(keys, blob, off)
+    seg = O.Segment([int(c.dtype) for c in rt.segment.columns])
+    proj = [c.index for c in rt._resolve(names)]
+    pj = (C.c_uint32 * len(proj))(*proj)
+    outs = (O.OcArray * len(proj))()
+    err = O.OcError()
+    bufs = [(q.buffers(), len(q)) for q in qarr]
+
+    def once(i):
+        qb, nq = bufs[i % len(bufs)]
+        t0 = time.perf_counter()
+        st = store.read_raw(seg, pj, len(proj), qb[2].address, qb[1].address, nq, outs, err)
+        dt = time.perf_counter() - t0
+        assert st == 0, st
+        for p in range(len(proj)):
+            O.lib().oc_array_free(C.byref(outs[p]))
+        return dt
+
+    for i in range(5):
+        once(i)
+    ts = [once(i) for i in range(reads)]
+    store.close()
+    return {"us_per_read_median": round(float(np.median(ts)) * 1e6, 1), "cores": 1, "kind": "port",
+            "cpu_model": cpu_model(),
+            "sample": f"{reads} reads of the same key sets through oracle/libmurr_oracle.so oc_memstore_read "
+                      f"(MemoryStore restatement, FNV map in place of SipHash) over the table's {n} rows"}
+
+
 def run_resident(args):
     """Device-resident Table::read (SURVEY.md §8(f) rank 1) on a table of
     args.rows rows in HBM: `--table C` (config C) or `--table ref` (the
@@ -1082,6 +1125,7 @@ def run_resident(args):
         t0 = time.perf_counter()
         rt.read(qarr[i % 4], names)
         ta.append(time.perf_counter() - t0)
+    cpu_read = None if args.no_cpu else resident_cpu_baseline(rt, args.table, n, names, qarr, min(args.steps, 200))
     hplan = rt.read_plan(names, nq)  # the library call alone (arrays left in pinned memory)
     tr = []
     for i in range(args.steps):
@@ -1133,6 +1177,7 @@ def run_resident(args):
                       "us_per_read_host_median": round(float(np.median(th)) * 1e6, 1),
                       "us_per_read_host_arrow_keys_median": round(float(np.median(ta)) * 1e6, 1),
                       "us_per_read_host_plan_run_median": round(float(np.median(tr)) * 1e6, 1),
+                      "cpu_baseline": cpu_read,
                       "GiB_s_arrow_out_device": round(out_bytes / med / GIB, 3),
                       "host_path": "ResidentTable.read: Python keys -> Arrow -> ReadPlan.run -> RecordBatch",
                       "kernels": "gather_fused, murr_jit_decode (+ copy_segs_kernel on the host path)",

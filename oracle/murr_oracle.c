@@ -486,6 +486,87 @@ int oc_encode_batch(const oc_segment* seg, const oc_col_in* cols, uint64_t n,
     return OC_OK;
 }
 
+/* ---- MemoryStore restatement (src/io/store/memory.rs) ---------------------- */
+struct oc_memstore {
+    const uint8_t* key_data;
+    const int32_t* key_off;
+    const uint8_t* blob;
+    const uint64_t* row_off;
+    uint64_t* slot;  /* row + 1, 0 = empty */
+    uint64_t mask;
+};
+
+static uint64_t oc_fnv1a(const uint8_t* p, uint64_t n) {
+    uint64_t h = 0xcbf29ce484222325ull;
+    for (uint64_t i = 0; i < n; i++) h = (h ^ p[i]) * 0x100000001b3ull;
+    return h;
+}
+
+oc_memstore* oc_memstore_new(const uint8_t* key_data, const int32_t* key_off, uint64_t n,
+                             const uint8_t* blob, const uint64_t* row_off) {
+    oc_memstore* m = (oc_memstore*)calloc(1, sizeof *m);
+    if (!m) return NULL;
+    uint64_t cap = 16;
+    while (cap < 2 * n) cap <<= 1;
+    m->slot = (uint64_t*)calloc(cap, sizeof(uint64_t));
+    if (!m->slot) {
+        free(m);
+        return NULL;
+    }
+    m->key_data = key_data, m->key_off = key_off, m->blob = blob, m->row_off = row_off, m->mask = cap - 1;
+    for (uint64_t r = 0; r < n; r++) {  /* entries.insert(key, value): a later key replaces */
+        const uint8_t* k = key_data + key_off[r];
+        const uint64_t len = (uint64_t)(key_off[r + 1] - key_off[r]);
+        for (uint64_t s = oc_fnv1a(k, len) & m->mask;; s = (s + 1) & m->mask) {
+            const uint64_t e = m->slot[s];
+            if (!e) {
+                m->slot[s] = r + 1;
+                break;
+            }
+            const uint64_t o = e - 1, olen = (uint64_t)(key_off[o + 1] - key_off[o]);
+            if (olen == len && memcmp(key_data + key_off[o], k, len) == 0) {
+                m->slot[s] = r + 1;
+                break;
+            }
+        }
+    }
+    return m;
+}
+
+int oc_memstore_read(const oc_memstore* m, const oc_segment* seg, const uint32_t* proj, uint32_t nproj,
+                     const uint8_t* q_data, const int32_t* q_off, uint64_t nq, oc_array* outs, oc_error* err) {
+    oc_builder* b = oc_builder_new(seg, proj, nproj, nq);
+    if (!b) return OC_E_ARGUMENT;
+    for (uint64_t i = 0; i < nq; i++) {  /* memory.rs:38-43 */
+        const uint8_t* k = q_data + q_off[i];
+        const uint64_t len = (uint64_t)(q_off[i + 1] - q_off[i]);
+        uint64_t row = ~0ull;
+        for (uint64_t s = oc_fnv1a(k, len) & m->mask; m->slot[s]; s = (s + 1) & m->mask) {
+            const uint64_t o = m->slot[s] - 1, olen = (uint64_t)(m->key_off[o + 1] - m->key_off[o]);
+            if (olen == len && memcmp(m->key_data + m->key_off[o], k, len) == 0) {
+                row = o;
+                break;
+            }
+        }
+        int st;
+        if (row == ~0ull) st = oc_builder_add_empty(b);
+        else st = oc_builder_add_row(b, m->blob + m->row_off[row], m->row_off[row + 1] - m->row_off[row], err);
+        if (st) {
+            oc_builder_free(b);
+            return st;
+        }
+    }
+    const int st = oc_builder_build(b, outs, err);
+    oc_builder_free(b);
+    return st;
+}
+
+void oc_memstore_free(oc_memstore* m) {
+    if (!m) return;
+    free(m->slot);
+    free(m);
+}
+
 void oc_array_free(oc_array* a) {
     if (!a) return;
     free(a->values); free(a->validity); free(a->offsets);

@@ -101,6 +101,21 @@ int  oc_decode_block(const oc_segment* seg, const uint32_t* proj, uint32_t nproj
 int  oc_encode_batch(const oc_segment* seg, const oc_col_in* cols, uint64_t n,
                      uint8_t** blob, uint64_t* blob_len, uint64_t* row_off, oc_error* err);
 
+/* MemoryStore (src/io/store/memory.rs): a key -> row blob map over n keys
+ * (Arrow utf8: key_data, key_off[n+1]) and their blobs (blob, row_off[n+1]);
+ * a key given twice maps to its later row (HashMap::insert, memory.rs:55-57).
+ * The map is FNV-1a open addressing in place of Rust's SipHash HashMap: the
+ * same lookup semantics, a different hash.  The pointers are kept, not
+ * copied. */
+typedef struct oc_memstore oc_memstore;
+oc_memstore* oc_memstore_new(const uint8_t* key_data, const int32_t* key_off, uint64_t n,
+                             const uint8_t* blob, const uint64_t* row_off);
+/* Store::read (memory.rs:28-45): per key add_row of its blob or add_empty,
+ * then build() -> outs[nproj] (owned, oc_array_free). */
+int  oc_memstore_read(const oc_memstore* m, const oc_segment* seg, const uint32_t* proj, uint32_t nproj,
+                      const uint8_t* q_data, const int32_t* q_off, uint64_t nq, oc_array* outs,
+                      oc_error* err);
+void oc_memstore_free(oc_memstore* m);
 /* core::str::from_utf8: 1 valid, 0 invalid (valid_up_to / error_len like Utf8Error). */
 int  oc_utf8_valid(const uint8_t* s, uint64_t len, uint64_t* valid_up_to, int* error_len);
 

@@ -81,6 +81,11 @@ def lib():
                                      C.POINTER(C.c_uint64)]
         L.oc_block_decode.argtypes = [C.c_char_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                       C.c_void_p, C.c_void_p]
+        L.oc_memstore_new.restype = C.c_void_p
+        L.oc_memstore_new.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p]
+        L.oc_memstore_read.argtypes = [C.c_void_p, C.POINTER(OcSegment), C.POINTER(C.c_uint32), C.c_uint32,
+                                       C.c_void_p, C.c_void_p, C.c_uint64, C.POINTER(OcArray), C.POINTER(OcError)]
+        L.oc_memstore_free.argtypes = [C.c_void_p]
         _lib = L
     return _lib
 
@@ -145,6 +150,67 @@ def decode_block(seg: Segment, proj, data: bytes | np.ndarray, row_off: np.ndarr
         res.append(_take_array(outs[p]))
         lib().oc_array_free(C.byref(outs[p]))
     return res
+
+
+class MemStore:
+    """MemoryStore (src/io/store/memory.rs) restated over host buffers: keys as
+    an Arrow utf8/binary array (row i = key i; a repeated key maps to its
+    later row), blobs back to back with row_off[n+1].  read() is Store::read:
+    per key its blob into the ReadBatchBuilder or add_empty, then build()."""
+
+    def __init__(self, keys, blob, row_off):
+        import pyarrow as pa
+        keys = keys if isinstance(keys, pa.Array) else pa.array(keys, pa.string())
+        if keys.offset:
+            keys = pa.concat_arrays([keys])
+        b = keys.buffers()
+        self._keys = keys  # (the store keeps pointers into these buffers)
+        self._blob = np.ascontiguousarray(np.frombuffer(blob, np.uint8) if isinstance(blob, (bytes, bytearray))
+                                          else blob, dtype=np.uint8)
+        if self._blob.size == 0:
+            self._blob = np.zeros(1, np.uint8)
+        self._off = np.ascontiguousarray(row_off, dtype=np.uint64)
+        n = len(keys)
+        self.h = lib().oc_memstore_new(b[2].address if b[2] is not None else None, b[1].address, n,
+                                       self._blob.ctypes.data, self._off.ctypes.data)
+        if not self.h:
+            raise MemoryError("oc_memstore_new")
+
+    def read_raw(self, seg: Segment, proj, nproj: int, q_data: int, q_off: int, nq: int, outs, err) -> int:
+        """The timed call: keys as raw Arrow buffers; outs[nproj] owned by the caller."""
+        return lib().oc_memstore_read(self.h, C.byref(seg.seg), proj, nproj, q_data, q_off, nq, outs,
+                                      C.byref(err))
+
+    def read(self, seg: Segment, proj, keys):
+        import pyarrow as pa
+        q = keys if isinstance(keys, pa.Array) else pa.array(keys, pa.string())
+        if q.offset:
+            q = pa.concat_arrays([q])
+        qb = q.buffers()
+        proj = list(proj)
+        pj = (C.c_uint32 * max(len(proj), 1))(*proj)
+        outs = (OcArray * max(len(proj), 1))()
+        err = OcError()
+        st = self.read_raw(seg, pj, len(proj), qb[2].address if qb[2] is not None and len(q) else None,
+                           qb[1].address if len(q) else None, len(q), outs, err)
+        if st:
+            raise OracleError(st, err.row, err.column, err.message.decode(errors="replace"))
+        res = []
+        for p in range(len(proj)):
+            res.append(_take_array(outs[p]))
+            lib().oc_array_free(C.byref(outs[p]))
+        return res
+
+    def close(self):
+        if self.h:
+            lib().oc_memstore_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def encode_batch(seg: Segment, cols, n: int):
