@@ -1,9 +1,12 @@
-// Host-only check of murr_arrow_export under AddressSanitizer /
-// UndefinedBehaviorSanitizer (no GPU): exports of every dtype with and
-// without nulls, empty and zero-column batches, a mixed-length rejection,
-// then reads every exported buffer back and releases parent and schema.
+// Host-only check of the library's host code under AddressSanitizer /
+// UndefinedBehaviorSanitizer (no GPU): murr_arrow_export with every dtype,
+// with and without nulls, empty and zero-column batches, a mixed-length
+// rejection (every exported byte read back, the export released); and the
+// Arrow IPC framing of murr_ipc.cpp (schema and record-batch messages at
+// several alignments, the size query, a short buffer).
 //   hipcc -O1 -g -std=c++17 -Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined \
-//     -I../../include tools/asan/arrow_export_check.cpp murr_amd/csrc/murr_arrow.cpp -o /tmp/arrow_export_check
+//     -Iinclude -Imurr_amd/csrc tools/asan/arrow_export_check.cpp murr_amd/csrc/murr_arrow.cpp \
+//     murr_amd/csrc/murr_ipc.cpp -o /tmp/arrow_export_check
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -96,6 +99,45 @@ int main() {
         CHECK(murr_arrow_export(nullptr, 0, nullptr, &arr, &sch) == MURR_OK);
         arr.release(&arr);
         sch.release(&sch);
+    }
+    {  // IPC framing of the same arrays (host): schema + record batch
+        murr_column_t cols[5];
+        uint32_t off = 0;
+        for (uint32_t k = 0; k < 5; k++) {
+            const uint32_t sz = dts[k] == MURR_UTF8 ? 4 : dts[k] == MURR_UINT8 || dts[k] == MURR_BOOL ? 1 : 8;
+            cols[k] = murr_column_t{k, dts[k], off, sz};
+            off += sz;
+        }
+        murr_segment_t seg{5, 1, off, 0, cols};
+        const uint32_t proj[] = {2, 0, 1, 4, 3, 2};
+        const char* names[] = {"c", "a", "b", "e", "d", "c2"};
+        std::vector<murr_host_array_t> a(6);
+        for (int p = 0; p < 6; p++) {
+            murr_host_array_t& h = a[p];
+            std::memset(&h, 0, sizeof h);
+            const uint32_t dt = dts[proj[p]];
+            h.dtype = dt;
+            h.length = n;
+            h.null_count = p % 2 ? 4 : 0;
+            h.validity = p % 2 ? validity.data() : nullptr;
+            if (dt == MURR_UTF8) h.values = (const uint8_t*)bytes.data(), h.offsets = offs.data(), h.values_len = bytes.size();
+            else if (dt == MURR_BOOL) h.values = bools.data(), h.values_len = (n + 7) / 8;
+            else h.values = (const uint8_t*)i64.data(), h.values_len = n * (dt == MURR_UINT8 ? 1 : 8);
+        }
+        for (uint32_t align : {8u, 64u, 4096u}) {
+            uint64_t len = 0;
+            CHECK(murr_ipc_schema(&seg, proj, 6, names, align, nullptr, 0, &len) == MURR_OK && len > 0);
+            std::vector<uint8_t> sm(len);
+            CHECK(murr_ipc_schema(&seg, proj, 6, names, align, sm.data(), len, &len) == MURR_OK);
+            CHECK(murr_ipc_batch_host(&seg, proj, 6, a.data(), n, align, nullptr, 0, &len) == MURR_OK && len > 0);
+            std::vector<uint8_t> bm(len);
+            CHECK(murr_ipc_batch_host(&seg, proj, 6, a.data(), n, align, bm.data(), len, &len) == MURR_OK);
+            CHECK(*(const uint32_t*)bm.data() == 0xFFFFFFFFu);
+            uint64_t need = 0;
+            CHECK(murr_ipc_batch_host(&seg, proj, 6, a.data(), n, align, bm.data(), len - 1, &need) == MURR_E_CAPACITY);
+        }
+        uint8_t eos[8];
+        CHECK(murr_ipc_eos(eos) == 8);
     }
     std::printf("arrow_export_check: %s\n", fails ? "FAILED" : "ok");
     return fails ? 1 : 0;
