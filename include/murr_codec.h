@@ -817,7 +817,10 @@ struct ArrowArray {
  * arrow::ffi::from_ffi / pyarrow RecordBatch._import_from_c in one call.
  * The export owns a compacted copy of the bytes (the arrays' pinned memory is
  * reused by the next read); its release callbacks free it.  Validity is
- * exported only when null_count > 0.  Host only. */
+ * exported only when null_count > 0.  out_schema may be NULL: a caller that
+ * reads the same columns again keeps the schema of its first export (the
+ * schema depends only on names and dtypes) and imports the array against it.
+ * Host only. */
 int murr_arrow_export(const murr_host_array_t* arrays, uint32_t n, const char* const* names,
                       struct ArrowArray* out_array, struct ArrowSchema* out_schema);
 

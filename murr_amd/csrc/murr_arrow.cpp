@@ -71,9 +71,9 @@ extern "C" {
 
 int murr_arrow_export(const murr_host_array_t* arrays, uint32_t n, const char* const* names, ArrowArray* out_array,
                       ArrowSchema* out_schema) {
-    if (!out_array || !out_schema || (n && (!arrays || !names))) return MURR_E_ARGUMENT;
+    if (!out_array || (n && (!arrays || !names))) return MURR_E_ARGUMENT;
     std::memset(out_array, 0, sizeof *out_array);
-    std::memset(out_schema, 0, sizeof *out_schema);
+    if (out_schema) std::memset(out_schema, 0, sizeof *out_schema);
     uint64_t length = n ? arrays[0].length : 0;
     for (uint32_t i = 0; i < n; i++)
         if (arrays[i].length != length || !arrow_format(arrays[i].dtype) || !names[i]) return MURR_E_ARGUMENT;
@@ -135,7 +135,9 @@ int murr_arrow_export(const murr_host_array_t* arrays, uint32_t n, const char* c
     out_array->dictionary = nullptr;
     out_array->release = release_array;
     out_array->private_data = A;
-    // ---- schema side: "+s" with one nullable field per column
+    // ---- schema side: "+s" with one nullable field per column (unless the
+    // caller keeps the schema of an earlier export)
+    if (!out_schema) return MURR_OK;
     uint64_t names_len = 0;
     for (uint32_t i = 0; i < n; i++) names_len += std::strlen(names[i]) + 1;
     const uint64_t s_kids = 0, s_ptrs = s_kids + sizeof(ArrowSchema) * n, s_names = s_ptrs + sizeof(ArrowSchema*) * n;

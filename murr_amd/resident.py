@@ -247,7 +247,7 @@ class ResidentTable:
         self.n = 0
         self.max_row = 0
         self._reader = None    # murr_reader_t: scratch of the one-call host read
-        self._schemas = {}     # read(): the field names (C strings) per requested column list
+        self._schemas = {}     # read(): per requested column list, its names (C strings) and batch schema
         self.uidx = None       # utf8 index of the arena (every self.stride rows), kept with every write
         self.uidx_cap = 0      # entries
         # per-row utf8 string bytes (murr_utf8_row_lengths, [n][nutf8] u32),
@@ -584,10 +584,13 @@ class ResidentTable:
         # copies the arrays out of its pinned memory into an export pyarrow
         # imports in one call (one Array.from_buffers per column cost ~4x more)
         key = tuple(c.name for c in req)
-        names = self._schemas.get(key)
-        if names is None:  # (the field names as C strings, once per column list)
-            names = self._schemas[key] = c_names(list(key))
-        return host_arrays_to_batch(outs, len(req), names)
+        ent = self._schemas.get(key)
+        if ent is None:  # (the field names as C strings, and the first batch's schema, once per column list)
+            names = c_names(list(key))
+            rb = host_arrays_to_batch(outs, len(req), names)
+            self._schemas[key] = (names, rb.schema)
+            return rb
+        return host_arrays_to_batch(outs, len(req), ent[0], ent[1])
 
     def read_ipc(self, keys, columns, alignment: int = 64) -> bytes:
         """read() as the Arrow IPC stream of the HTTP fetch handler's StreamWriter

@@ -189,12 +189,17 @@ def host_arrays_to_batch(outs, k: int, names, schema: pa.Schema | None = None) -
     Data Interface (murr_arrow_export: the library copies the bytes out of its
     pinned region into an export it owns; pyarrow imports it in one call).
     `names`: a ctypes array of k c_char_p (built once per column list).
-    `schema`: the batch's schema, when the caller has it (checked equal)."""
-    arr, sch = _abi.ArrowArray(), _abi.ArrowSchema()
+    `schema`: the schema of an earlier batch of the same columns (names and
+    dtypes): the export then carries no schema and the array is imported
+    against this one (saves the schema's export and parse on every read)."""
+    arr = _abi.ArrowArray()
     L = _abi.lib()
+    if schema is not None:
+        raise_status(L.murr_arrow_export(outs, k, names, C.byref(arr), None), what="murr_arrow_export")
+        return pa.RecordBatch._import_from_c(C.addressof(arr), schema)
+    sch = _abi.ArrowSchema()
     raise_status(L.murr_arrow_export(outs, k, names, C.byref(arr), C.byref(sch)), what="murr_arrow_export")
-    rb = pa.RecordBatch._import_from_c(C.addressof(arr), C.addressof(sch))
-    return rb
+    return pa.RecordBatch._import_from_c(C.addressof(arr), C.addressof(sch))
 
 
 def c_names(names) -> "C.Array":
@@ -289,7 +294,10 @@ class HostStream:
                 fields.append(pa.field(seg_col.name, seg_col.dtype.arrow_dtype(), True))
             self._arrow_schema = pa.schema(fields)
             self._cnames = c_names(self._arrow_schema.names)
-        return host_arrays_to_batch(outs, self._nproj, self._cnames)
+            rb = host_arrays_to_batch(outs, self._nproj, self._cnames)
+            self._batch_schema = rb.schema  # (the later batches import against it)
+            return rb
+        return host_arrays_to_batch(outs, self._nproj, self._cnames, self._batch_schema)
 
     @property
     def pending(self) -> int:

@@ -65,7 +65,14 @@ def test_batched_equals_per_column(n, gap):
             assert (bx is None) == (by is None), i
             if bx is not None:
                 assert bx.to_pybytes() == by.to_pybytes(), i
-    del rb  # (released through the export's callbacks)
+    # against the schema of an earlier export (no schema side exported): the same batch
+    rb2 = host_arrays_to_batch(outs, len(dtypes), c_names(names), rb.schema)
+    rb2.validate(full=True)
+    assert rb2.schema == rb.schema and rb2.num_rows == rb.num_rows  # (random floats: NaNs, so bytes below)
+    for x, y in zip(rb2.columns, rb.columns):
+        for bx, by in zip(x.buffers(), y.buffers()):
+            assert (bx is None) == (by is None) and (bx is None or bx.to_pybytes() == by.to_pybytes())
+    del rb, rb2  # (released through the export's callbacks)
     got = host_arrays_to_arrow(outs, len(dtypes))
     for i, (x, y) in enumerate(zip(got, [host_array_to_arrow(outs[i]) for i in range(len(dtypes))])):
         x.validate(full=True)

@@ -93,6 +93,19 @@ int main() {
         ArrowSchema sch;
         CHECK(murr_arrow_export(a, 2, names, &arr, &sch) == MURR_E_ARGUMENT);
     }
+    {  // no schema side (a caller that keeps an earlier export's schema)
+        murr_host_array_t a;
+        std::memset(&a, 0, sizeof a);
+        a.dtype = MURR_INT64;
+        a.length = 10;
+        a.values = (const uint8_t*)i64.data();
+        a.values_len = 80;
+        const char* names[] = {"x"};
+        ArrowArray arr;
+        CHECK(murr_arrow_export(&a, 1, names, &arr, nullptr) == MURR_OK);
+        CHECK(arr.n_children == 1 && ((const int64_t*)arr.children[0]->buffers[1])[9] == 63);
+        arr.release(&arr);
+    }
     {  // no columns
         ArrowArray arr;
         ArrowSchema sch;
