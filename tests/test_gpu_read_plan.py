@@ -219,3 +219,30 @@ def test_plan_index_from_row_lengths_any_utf8_count(nu):
     keys = [f"key{i}" for i in rng.integers(0, 5600, size=1000)]
     assert_same(rt.read(keys, names), expected([b0, b1], keys, names))
     assert rt.ctx.stats()["last_mode"] == "cut"
+
+
+def test_plan_soak_reads_between_appends():
+    # many prepared reads of random sizes (every capacity class up to 2048,
+    # so both gather forms and both decode modes) between appends that
+    # overwrite and add keys, each checked against the MemoryStore
+    # restatement: the fused gather's alternating look-back word sets, the
+    # plans' reuse and their invalidation by a write, over many cycles
+    rt = ResidentTable(schema_c())
+    rng = np.random.default_rng(2026)
+    batches = []
+    start = 0
+    for cycle in range(5):
+        m = int(rng.integers(500, 2500))
+        keys = [f"key{start + i}" for i in range(m)]
+        for i in rng.choice(m, size=m // 4, replace=False):  # overwrites of earlier keys
+            if start:
+                keys[i] = f"key{int(rng.integers(0, start))}"
+        b = batch_c(m, start=start, seed=cycle, keys=keys)
+        rt.write(b)
+        batches.append(b)
+        start += m
+        cols = [f"c{i}" for i in rng.permutation(16)[:int(rng.integers(1, 17))]]
+        for _ in range(40):
+            nq = int(rng.choice([1, 2, 63, 64, 65, 200, 511, 700, 1000, 1024, 1025, 2048]))
+            q = [f"key{int(x)}" for x in rng.integers(0, int(start * 1.05) + 1, size=nq)]
+            assert_same(rt.read(q, cols), expected(batches, q, cols))
