@@ -588,6 +588,17 @@ int murr_multi_gather(murr_ctx_t* home, const murr_shard_read_t* shards, uint32_
 int murr_multi_gather_copy(murr_ctx_t* home, const murr_shard_read_t* shards, uint32_t nshards,
                            const uint32_t* src, uint64_t nq, const uint32_t* rows,
                            const uint64_t* out_row_off, uint8_t* out_data, murr_error_t* err);
+/* The slot cache of a resident table's index: beside each slot, the row
+ * offset and size of the row it holds (row_off, the table's n + 1 offsets)
+ * and, for a layout of 1 to 4 utf8 columns, the row's string bytes (row_ulen,
+ * murr_utf8_row_lengths' [n][nutf8]; NULL and 0 otherwise).  With every row
+ * cached, a prepared read's probe resolves a key of up to 16 bytes in the
+ * round trip that loads its slot (murr_read_plan_*).  Caches the rows added
+ * since the last call (every row after a rehash or murr_index_prefer_seq);
+ * call it after each append, once the table's offsets (and string bytes) hold
+ * the new rows.  Enqueued. */
+int murr_index_cache_rows(murr_ctx_t* ctx, murr_index_t* idx, const uint64_t* row_off,
+                          const uint32_t* row_ulen, uint32_t nutf8, murr_error_t* err);
 /* Rows indexed (n at build) and hash-table slots. */
 int murr_index_info(const murr_index_t* idx, uint64_t* n, uint64_t* slots);
 

@@ -170,6 +170,7 @@ SIGNATURES = {
     "murr_utf8_index": (I32, [P, C.POINTER(Segment), C.POINTER(Block), U32, P]),
     "murr_utf8_index_update": (I32, [P, C.POINTER(Segment), C.POINTER(Block), U64, U32, P]),
     "murr_utf8_row_lengths": (I32, [P, C.POINTER(Segment), C.POINTER(Block), U64, P]),
+    "murr_index_cache_rows": (I32, [P, P, P, P, U32, C.POINTER(Error)]),
     "murr_encode_batch_ix": (I32, [P, C.POINTER(Segment), C.POINTER(ColIn), U64, P, U64, P, U32, P,
                                    C.POINTER(U64), C.POINTER(Error)]),
     "murr_encode_bound": (U64, [C.POINTER(Segment), U64, C.POINTER(U64)]),

@@ -142,6 +142,11 @@ struct murr_index {
     int32_t* key_off = nullptr;     // n + 1 offsets into key_data (grows by doubling)
     uint64_t* slots = nullptr;
     uint64_t* loc = nullptr;
+    uint64_t* kp = nullptr;         // per slot: the key's first 16 bytes
+    uint64_t* rc = nullptr;         // slot cache: per slot {row offset, row bytes} (murr_index_cache_rows)
+    uint32_t* ru = nullptr;         //   and the row's utf8 string bytes [rc_nu]
+    uint32_t rc_nu = 0;
+    uint64_t cached = 0;            // rows [0, cached) are in the slot cache (0 after a rehash)
     unsigned long long* err = nullptr;
     uint64_t n = 0, mask = 0;
     uint64_t key_bytes = 0, key_cap = 0, off_cap = 0;
@@ -369,7 +374,8 @@ extern "C" {
 void murr_index_free(murr_index_t* x) {
     if (!x) return;
     (void)hipSetDevice(x->device);
-    for (void* p : {(void*)x->key_data, (void*)x->key_off, (void*)x->slots, (void*)x->loc, (void*)x->err})
+    for (void* p : {(void*)x->key_data, (void*)x->key_off, (void*)x->slots, (void*)x->loc, (void*)x->kp,
+                    (void*)x->rc, (void*)x->ru, (void*)x->err})
         if (p) (void)hipFree(p);
     delete x;
 }
@@ -425,12 +431,14 @@ int murr_index_append(murr_ctx_t* c, murr_index_t* x, const uint8_t* key_data, c
         // rehash: a table of >= 2 * total slots, every key inserted again
         slots = 64;
         while (slots < 2 * total) slots <<= 1;
-        if (x->slots) HIPC(hipFree(x->slots));
-        if (x->loc) HIPC(hipFree(x->loc));
-        x->slots = nullptr;
-        x->loc = nullptr;
+        for (void** p : {(void**)&x->slots, (void**)&x->loc, (void**)&x->kp, (void**)&x->rc, (void**)&x->ru}) {
+            if (*p) HIPC(hipFree(*p));
+            *p = nullptr;
+        }
+        x->cached = 0;  // (the slot cache is rebuilt over the new table by the next murr_index_cache_rows)
         HIPC(hipMalloc(&x->slots, 8 * slots));
         HIPC(hipMalloc(&x->loc, 8 * slots));
+        HIPC(hipMalloc(&x->kp, 16 * slots));
         HIPC(hipMemsetAsync(x->slots, 0xFF, 8 * slots, c->stream));
         x->mask = slots - 1;
         a.base = 0;
@@ -441,6 +449,7 @@ int murr_index_append(murr_ctx_t* c, murr_index_t* x, const uint8_t* key_data, c
     }
     a.slots = x->slots;
     a.loc = x->loc;
+    a.kp = x->kp;
     a.mask = x->mask;
     HIPC(launch_index_insert(a, c->stream));
     unsigned long long word = 0;
@@ -470,10 +479,44 @@ int murr_index_prefer_seq(murr_ctx_t* c, murr_index_t* x, const uint64_t* seqs, 
     a.n = x->n;
     a.err = x->err;
     HIPC(launch_index_seq(a, seqs, tmp, tmp + slots, c->stream));
+    x->cached = 0;  // (rows moved between slots)
     unsigned long long word = 0;
     HIPC(hipMemcpyAsync(&word, x->err, 8, hipMemcpyDeviceToHost, c->stream));
     HIPC(hipStreamSynchronize(c->stream));
     if (word) return set_err(err, MURR_E_INTERNAL);
+    return MURR_OK;
+}
+
+int murr_index_cache_rows(murr_ctx_t* c, murr_index_t* x, const uint64_t* row_off, const uint32_t* row_ulen,
+                          uint32_t nutf8, murr_error_t* err) {
+    if (!c || !x || x->device != c->device || c->pending || (x->n && !row_off) || (nutf8 && !row_ulen) ||
+        nutf8 > kGatherMaxU)
+        return set_err(err, MURR_E_ARGUMENT);
+    if (!x->n) return MURR_OK;
+    HIPC(hipSetDevice(c->device));
+    const uint64_t slots = x->mask + 1;
+    if (!x->rc || nutf8 != x->rc_nu) {
+        if (x->rc) HIPC(hipFree(x->rc));
+        if (x->ru) HIPC(hipFree(x->ru));
+        x->rc = nullptr;
+        x->ru = nullptr;
+        HIPC(hipMalloc(&x->rc, 16 * slots));
+        if (nutf8) HIPC(hipMalloc(&x->ru, 4ull * nutf8 * slots));
+        x->rc_nu = nutf8;
+        x->cached = 0;
+    }
+    IndexArgs a{};
+    a.key_data = x->key_data;
+    a.key_off = x->key_off;
+    a.slots = x->slots;
+    a.loc = x->loc;
+    a.mask = x->mask;
+    a.n = x->n;
+    a.rc = x->rc;
+    a.ru = x->ru;
+    a.nu_rc = nutf8;
+    HIPC(launch_index_cache_rows(a, row_off, row_ulen, x->cached, c->stream));
+    x->cached = x->n;
     return MURR_OK;
 }
 
@@ -3436,6 +3479,13 @@ int read_plan_gather(murr_read_plan* r, const uint8_t* q_data, const int32_t* q_
         a.ulen = r->row_ulen;
         a.uidx = r->duidx;
         a.nu = r->nu;
+    }
+    const murr_index* x = r->x;
+    if (x->rc && x->cached == x->n && (!r->nu || x->rc_nu == r->nu)) {  // the slot cache holds every row
+        a.kp = x->kp;
+        a.rc = x->rc;
+        a.ru = x->ru;
+        a.nu_rc = x->rc_nu;
     }
     HIPC(launch_gather(a, c->stream));
     return MURR_OK;

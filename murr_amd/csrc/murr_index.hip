@@ -125,6 +125,10 @@ __global__ void __launch_bounds__(256) index_insert(IndexArgs A) {
                 // where a probe finds the key bytes; equal keys share them, so
                 // the row a later atomicMax installs needs no update here
                 gp(A.loc)[s] = ((uint64_t)(uint32_t)k0 << 32) | len;
+                if (A.kp) {  // the key's first 16 bytes (a key of <= 16 compares here alone)
+                    gp(A.kp)[2 * s] = ((uint64_t)kc.w[1] << 32) | kc.w[0];
+                    gp(A.kp)[2 * s + 1] = ((uint64_t)kc.w[3] << 32) | kc.w[2];
+                }
                 return;
             }
             e = want;  // another key took it first
@@ -190,6 +194,21 @@ __global__ void __launch_bounds__(256) index_seq(IndexArgs A, const uint64_t* se
         __hip_atomic_fetch_max(gp(win) + s, (unsigned long long)(i + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// The slot cache of row i (i in [from, n)): its slot's row offset, size and
+// utf8 string bytes, written only when the slot holds row i (a key written
+// again: its later row is the one in the slot, and that row's thread writes).
+__global__ void __launch_bounds__(256) index_cache_rows(IndexArgs A, const uint64_t* row_off, const uint32_t* ulen,
+                                                        uint64_t from) {
+    const uint64_t i = from + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= A.n) return;
+    const uint64_t s = slot_of(A, i);
+    if (s == kEmpty || (uint32_t)gp(A.slots)[s] != (uint32_t)i) return;
+    const uint64_t o0 = gp(row_off)[i], o1 = gp(row_off)[i + 1];
+    gp(A.rc)[2 * s] = o0;
+    gp(A.rc)[2 * s + 1] = o1 - o0;
+    for (uint32_t u = 0; u < A.nu_rc; u++) gp(A.ru)[s * A.nu_rc + u] = gp(ulen)[i * A.nu_rc + u];
+}
+
 // Row of query i, or kMissing.  With `size` (a gather): the row's blob
 // length too, its two row offsets loaded beside the candidate's key bytes --
 // a tag match is the row with near certainty, so the lengths need no round
@@ -208,6 +227,38 @@ __device__ __forceinline__ uint32_t probe_one(const IndexArgs& A, uint64_t i, ui
     const GAS uint64_t* loc = gp(A.loc);
     uint32_t row = kMissing;
     uint64_t s = h & A.mask;
+    if constexpr (SIZED) {
+        if (A.rc) {
+            // slot cache (murr_index_cache_rows): the slot's key prefix, row
+            // offset, size and string bytes come with the slot, so a key of
+            // <= 16 bytes resolves in this round trip
+            const uint64_t q0 = ((uint64_t)qc.w[1] << 32) | qc.w[0], q1 = ((uint64_t)qc.w[3] << 32) | qc.w[2];
+            for (uint64_t probe = 0; probe <= A.mask; probe++, s = (s + 1) & A.mask) {
+                const uint64_t e = slots[s], l = loc[s];  // independent loads
+                const uint64_t p0 = gp(A.kp)[2 * s], p1 = gp(A.kp)[2 * s + 1];
+                const uint64_t c0 = gp(A.rc)[2 * s], c1 = gp(A.rc)[2 * s + 1];
+                uint32_t u4[kGatherMaxU] = {0, 0, 0, 0};
+                if (ul) {
+#pragma unroll
+                    for (uint32_t u = 0; u < kGatherMaxU; u++)
+                        if (u < A.nu_rc) u4[u] = gp(A.ru)[s * A.nu_rc + u];
+                }
+                if (e == kEmpty) break;
+                if ((e >> 32) == (h >> 32) && (uint32_t)l == len && p0 == q0 && p1 == q1 &&
+                    (len <= 16 || key_eq(gp(A.key_data) + (uint32_t)(l >> 32), qc, q, len))) {
+                    row = (uint32_t)e;
+                    *size = c1;
+                    if (start) *start = c0;
+                    if (ul) {
+#pragma unroll
+                        for (uint32_t u = 0; u < kGatherMaxU; u++) ul[u] = u4[u];
+                    }
+                    break;
+                }
+            }
+            return row;
+        }
+    }
     for (uint64_t probe = 0; probe <= A.mask; probe++, s = (s + 1) & A.mask) {
         const uint64_t e = slots[s], l = loc[s];  // independent loads
         if (e == kEmpty) break;
@@ -549,6 +600,14 @@ __global__ void __launch_bounds__(256) multi_copy(IndexArgs A, MultiTab T) {
 hipError_t launch_index_insert(const IndexArgs& a, hipStream_t s) {
     if (!a.n) return hipSuccess;
     hipLaunchKernelGGL(index_insert, dim3((uint32_t)((a.n + 255) / 256)), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_index_cache_rows(const IndexArgs& a, const uint64_t* row_off, const uint32_t* ulen, uint64_t from,
+                                   hipStream_t s) {
+    if (a.n > from)
+        hipLaunchKernelGGL(index_cache_rows, dim3((uint32_t)((a.n - from + 255) / 256)), dim3(256), 0, s, a, row_off,
+                           ulen, from);
     return hipGetLastError();
 }
 

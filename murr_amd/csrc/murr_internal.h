@@ -310,6 +310,10 @@ struct IndexArgs {
                                 //   [n][nu] (murr_utf8_row_lengths), with them
     uint64_t* uidx;             //   out: the gathered block's utf8 index at stride 64
     uint32_t nu;                //   utf8 columns (1 .. kGatherMaxU)
+    uint32_t nu_rc;             // slot cache: utf8 columns of ru (murr_index_cache_rows)
+    uint64_t* kp;               // per slot: the key's first 16 bytes, zero-padded (written by insert)
+    uint64_t* rc;               // slot cache (optional, probe): per slot {row offset, row bytes}
+    uint32_t* ru;               //   and the row's utf8 string bytes [nu_rc]
 };
 constexpr uint32_t kGatherGroups = 16;  // 64-query groups of a fused small gather
 constexpr uint32_t kGatherMaxU = 4;     // utf8 columns a fused gather indexes
@@ -326,6 +330,10 @@ struct MultiTab {
 hipError_t launch_multi_gather(const IndexArgs& a, const MultiTab& t, bool copy, hipStream_t s);
 hipError_t launch_multi_copy(const IndexArgs& a, const MultiTab& t, hipStream_t s);
 hipError_t launch_index_insert(const IndexArgs& a, hipStream_t s);
+// the slot cache of rows [from, a.n): rc / ru of each row's slot when the
+// slot holds that row (a.rc, a.ru, a.nu_rc; row_off / ulen of the table)
+hipError_t launch_index_cache_rows(const IndexArgs& a, const uint64_t* row_off, const uint32_t* ulen, uint64_t from,
+                                   hipStream_t s);
 hipError_t launch_index_probe(const IndexArgs& a, hipStream_t s);
 hipError_t launch_index_seq(const IndexArgs& a, const uint64_t* seqs, unsigned long long* best,
                             unsigned long long* win, hipStream_t s);

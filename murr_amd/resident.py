@@ -100,6 +100,14 @@ class DeviceIndex:
         data.free()
         offs.free()
 
+    def cache_rows(self, row_off, row_ulen, nutf8: int):
+        """murr_index_cache_rows: the rows added since the last call into the
+        slot cache (row offsets and sizes, and utf8 string bytes)."""
+        err = _abi.Error()
+        st = self.ctx.L.murr_index_cache_rows(self.ctx.h, self.h, row_off.ptr,
+                                              row_ulen.ptr if row_ulen is not None else None, nutf8, C.byref(err))
+        raise_status(st, err, "murr_index_cache_rows")
+
     def info(self):
         n, slots = C.c_uint64(), C.c_uint64()
         raise_status(self.ctx.L.murr_index_info(self.h, C.byref(n), C.byref(slots)), what="murr_index_info")
@@ -347,6 +355,8 @@ class ResidentTable:
             blk = _abi.Block(self.arena.ptr, self.row_off.ptr, self.n, self.used)
             raise_status(L.murr_utf8_row_lengths(self.ctx.h, C.byref(seg.c), C.byref(blk), n_old, self.ulen.ptr),
                          what="murr_utf8_row_lengths")
+        # the index's slot cache: each slot's row offset, size (and string bytes)
+        self.index.cache_rows(self.row_off, self.ulen, self.nutf8 if self.ulen is not None else 0)
         need = int(L.murr_utf8_index_len(C.byref(seg.c), self.n, self.stride))
         if need == 0:
             return

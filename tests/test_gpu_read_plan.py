@@ -246,3 +246,29 @@ def test_plan_soak_reads_between_appends():
             nq = int(rng.choice([1, 2, 63, 64, 65, 200, 511, 700, 1000, 1024, 1025, 2048]))
             q = [f"key{int(x)}" for x in rng.integers(0, int(start * 1.05) + 1, size=nq)]
             assert_same(rt.read(q, cols), expected(batches, q, cols))
+
+
+def test_plan_slot_cache_long_and_short_keys():
+    # the index's slot cache (murr_index_cache_rows, kept by every write):
+    # keys of <= 16 bytes resolve on the slot's key prefix, longer ones
+    # compare their remaining bytes; overwrites move a key's slot to its new
+    # row, a rehash rebuilds the cache; all against the MemoryStore restatement
+    rt = ResidentTable(schema_c())
+    rng = np.random.default_rng(616)
+
+    def key(i):
+        return f"key{i}" if i % 3 else f"a-longer-key-of-the-table-{i:08d}"  # 4-10 or 34 bytes
+
+    batches, start = [], 0
+    for w, m in enumerate([700, 1500, 5000]):  # the third append rehashes
+        keys = [key(start + i) for i in range(m)]
+        if start:
+            for i in rng.choice(m, size=m // 5, replace=False):
+                keys[i] = key(int(rng.integers(0, start)))
+        b = batch_c(m, start=start, seed=w, keys=keys)
+        rt.write(b)
+        batches.append(b)
+        start += m
+        for nq in (1, 100, 1000):
+            q = [key(int(x)) for x in rng.integers(0, int(start * 1.05), size=nq)] + ["a-longer-key-of-the-table-x"]
+            assert_same(rt.read(q, COLS), expected(batches, q, COLS))
