@@ -3481,7 +3481,11 @@ int read_plan_gather(murr_read_plan* r, const uint8_t* q_data, const int32_t* q_
         a.nu = r->nu;
     }
     const murr_index* x = r->x;
-    if (x->rc && x->cached == x->n && (!r->nu || x->rc_nu == r->nu)) {  // the slot cache holds every row
+    bool use_rc = x->rc && x->cached == x->n && (!r->nu || x->rc_nu == r->nu);  // the slot cache holds every row
+#ifdef MURR_TUNING
+    if (std::getenv("MURR_INDEX_NOCACHE")) use_rc = false;  // (A/B)
+#endif
+    if (use_rc) {
         a.kp = x->kp;
         a.rc = x->rc;
         a.ru = x->ru;
