@@ -272,3 +272,31 @@ def test_plan_slot_cache_long_and_short_keys():
         for nq in (1, 100, 1000):
             q = [key(int(x)) for x in rng.integers(0, int(start * 1.05), size=nq)] + ["a-longer-key-of-the-table-x"]
             assert_same(rt.read(q, COLS), expected(batches, q, COLS))
+
+
+def test_plan_keys_at_their_length_bounds():
+    # keys of every length 1 .. 40 around the probe's bounds (the slot
+    # cache's 16-byte key prefix, the 32-byte key chunk; 28 bytes: the 32-B
+    # key record of EXPERIMENTS #30), multi-byte text, a 28-byte miss and the
+    # empty key, each read against the MemoryStore restatement
+    rt = ResidentTable(schema_c())
+    rng = np.random.default_rng(28)
+
+    def key(i):
+        n = i % 41
+        return ("é" * (n // 2) + "k" * (n % 2)) if i % 7 == 0 else (f"{i:x}" * 41)[:n]
+
+    keys = sorted({key(i) for i in range(4000)} - {""}, key=lambda s: (len(s.encode()), s))
+    keys = [k for k in keys if len(k.encode()) <= 40]
+    b = batch_c(len(keys), seed=6, keys=keys)
+    rt.write(b)
+    short = [k for k in keys if len(k.encode()) <= 28]
+    assert any(len(k.encode()) == 28 for k in short) and any(len(k.encode()) == 17 for k in short)
+    for nq in (1, 64, 1000):
+        q = [short[int(x)] for x in rng.integers(0, len(short), size=nq)]
+        q[-1] = "k" * 28 if nq > 1 else q[-1]  # (a 28-byte miss)
+        assert_same(rt.read(q, COLS), expected([b], q, COLS))
+        q2 = q[:-1] + [keys[-1]]  # (one key of 40 bytes: two key chunks)
+        assert len(keys[-1].encode()) > 28
+        assert_same(rt.read(q2, COLS), expected([b], q2, COLS))
+    assert_same(rt.read([""], COLS), expected([b], [""], COLS))
