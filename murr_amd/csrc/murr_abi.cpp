@@ -3438,6 +3438,13 @@ struct murr_read_plan {
     // launch, 4 decode wait, 5 D2H wait
     double ph[6] = {0, 0, 0, 0, 0, 0};
     uint64_t runs = 0;
+    // gather_fused's phase clocks (MURR_GATHER_STAMPS=1), us summed over runs:
+    // 0 dispatch skew, 1 probe, 2 look-back, 3 publish, 4 copy (means over
+    // groups), 5 span, 6 the slowest group's look-back; [0] device runs, [1]
+    // host runs (keys read over PCIe)
+    uint64_t* dstamps = nullptr;
+    double gs[2][7] = {};
+    uint64_t gruns[2] = {0, 0};
 #endif
 };
 
@@ -3491,9 +3498,44 @@ int read_plan_gather(murr_read_plan* r, const uint8_t* q_data, const int32_t* q_
         a.ru = x->ru;
         a.nu_rc = x->rc_nu;
     }
+#ifdef MURR_TUNING
+    if (a.lb && std::getenv("MURR_GATHER_STAMPS")) {
+        if (!r->dstamps) HIPC(hipMalloc(&r->dstamps, 8 * kGatherGroups * kGatherStamps));
+        a.stamps = r->dstamps;
+    }
+#endif
     HIPC(launch_gather(a, c->stream));
     return MURR_OK;
 }
+
+#ifdef MURR_TUNING
+// One run's gather phase clocks (after its wait), into r->gs.
+void read_plan_stamps(murr_read_plan* r, int host) {
+    if (!r->dstamps) return;
+    const uint32_t G = (uint32_t)((r->cap + 63) / 64);
+    uint64_t t[kGatherGroups * kGatherStamps];
+    if (hipMemcpy(t, r->dstamps, 8 * G * kGatherStamps, hipMemcpyDeviceToHost) != hipSuccess) return;
+    uint64_t b = ~0ull, e = 0, s0 = 0, lbmax = 0;
+    double ph[4] = {0, 0, 0, 0};
+    for (uint32_t g = 0; g < G; g++) {
+        const uint64_t* x = t + g * kGatherStamps;
+        b = std::min(b, x[0]);
+        s0 = std::max(s0, x[0]);
+        e = std::max(e, x[4]);
+        lbmax = std::max(lbmax, x[2] - x[1]);
+        for (uint32_t k = 0; k < 4; k++) ph[k] += (double)(x[k + 1] - x[k]);
+    }
+    double* gs = r->gs[host];
+    gs[0] += (s0 - b) * 0.01;  // (100 MHz ticks -> us)
+    for (uint32_t k = 0; k < 4; k++) gs[1 + k] += ph[k] / G * 0.01;
+    gs[5] += (e - b) * 0.01;
+    gs[6] += lbmax * 0.01;
+    r->gruns[host]++;
+}
+#define RP_STAMPS(host) read_plan_stamps(r, host)
+#else
+#define RP_STAMPS(host) ((void)0)
+#endif
 
 // The plan's arrays at nq rows (padding rows are misses: null in every column).
 void read_plan_report(const murr_read_plan* r, uint64_t nq, murr_array_t* dev, murr_host_array_t* host) {
@@ -3657,6 +3699,7 @@ int murr_read_plan_run_device(murr_read_plan_t* r, const uint8_t* q_data, const 
     st = plan_wait(r->dplan, err, false);  // (its outputs are consumed on c->stream)
     if (st) return st;
     RP_LAP(4);
+    RP_STAMPS(0);
     read_plan_report(r, nq, outs, nullptr);
     return MURR_OK;
 }
@@ -3705,6 +3748,7 @@ int murr_read_plan_run(murr_read_plan_t* r, const uint8_t* key_data, const int32
     RP_LAP(4);
     HIPC(hipEventSynchronize(r->ev));
     RP_LAP(5);
+    RP_STAMPS(1);
     read_plan_report(r, nq, nullptr, outs);
     return MURR_OK;
 }
@@ -3721,6 +3765,18 @@ void murr_read_plan_free(murr_read_plan_t* r) {
                      (unsigned long long)r->runs, (unsigned long long)r->cap, r->ph[0] * 1e3 / r->runs,
                      r->ph[1] * 1e3 / r->runs, r->ph[2] * 1e3 / r->runs, r->ph[3] * 1e3 / r->runs,
                      r->ph[4] * 1e3 / r->runs, r->ph[5] * 1e3 / r->runs);
+    for (int h = 0; h < 2; h++)
+        if (r->gruns[h]) {
+            const double* gs = r->gs[h];
+            const double n = (double)r->gruns[h];
+            std::fprintf(stderr,
+                         "gather stamps, %s runs (us per run over %llu, %llu groups; means over groups): dispatch skew "
+                         "%.2f  probe %.2f  look-back %.2f (slowest %.2f)  publish %.2f  copy %.2f  span %.2f\n",
+                         h ? "host" : "device", (unsigned long long)r->gruns[h],
+                         (unsigned long long)((r->cap + 63) / 64), gs[0] / n, gs[1] / n, gs[2] / n, gs[6] / n,
+                         gs[3] / n, gs[4] / n, gs[5] / n);
+        }
+    if (r->dstamps) (void)hipFree(r->dstamps);
 #endif
     murr_ctx* c = r->ctx;
     if (c) {

@@ -476,6 +476,18 @@ __global__ void __launch_bounds__(256) gather_copy(IndexArgs A) {
 // index at stride 64 (A.uidx): the decode then cuts the block into one-pass
 // virtual blocks instead of split mode's two passes and look-back.
 constexpr unsigned long long kLbSet = 1ull << 63;
+// Phase clocks of tuning builds (100 MHz s_memrealtime, workgroup's thread 0,
+// after a wait for every memory operation in flight; murr_abi.cpp prints them
+// with MURR_GATHER_STAMPS=1).
+#ifdef MURR_TUNING
+#define GF_STAMP(k)                                                                                 \
+    if (A.stamps) {                                                                                 \
+        __builtin_amdgcn_s_waitcnt(0); /* (the phase's loads land before its clock) */              \
+        if (tid == 0) gp(A.stamps)[(uint64_t)g * kGatherStamps + (k)] = __builtin_amdgcn_s_memrealtime(); \
+    }
+#else
+#define GF_STAMP(k)
+#endif
 constexpr uint32_t kLbW = 1 + kGatherMaxU;  // words per group: bytes, then each utf8 column's string bytes
 __global__ void __launch_bounds__(512) gather_fused(IndexArgs A, unsigned long long* other) {
     __shared__ uint64_t s_off[65], s_src[64];
@@ -484,6 +496,7 @@ __global__ void __launch_bounds__(512) gather_fused(IndexArgs A, unsigned long l
     const uint64_t nq = A.nq, i0 = (uint64_t)g * 64;
     const uint32_t nu = A.ulen ? A.nu : 0u;
     GAS unsigned long long* lb = (GAS unsigned long long*)A.lb;
+    GF_STAMP(0);
     if (g == 0 && tid >= 64 && tid < 64 + kGatherWords) gp(other)[tid - 64] = 0ull;
     if (tid < 64) {
         const uint64_t i = i0 + tid;
@@ -491,6 +504,7 @@ __global__ void __launch_bounds__(512) gather_fused(IndexArgs A, unsigned long l
         uint32_t ul[kGatherMaxU] = {0, 0, 0, 0};
         uint32_t row = kMissing;
         if (i < live_queries(A)) row = probe_one<true>(A, i, &sz, &src, nu ? ul : nullptr);
+        GF_STAMP(1);
         uint64_t x[kLbW], inc[kLbW];
         x[0] = sz;
 #pragma unroll
@@ -526,6 +540,7 @@ __global__ void __launch_bounds__(512) gather_fused(IndexArgs A, unsigned long l
                 }
             }
         }
+        GF_STAMP(2);
 #pragma unroll
         for (uint32_t k = 0; k < kLbW; k++) base[k] = k <= nu ? wave_sum64(tid < g ? v[k] & ~kLbSet : 0ull) : 0;
         s_off[tid] = base[0] + inc[0] - sz;
@@ -553,11 +568,18 @@ __global__ void __launch_bounds__(512) gather_fused(IndexArgs A, unsigned long l
         }
     }
     __syncthreads();
+    GF_STAMP(3);
     const uint32_t r = tid / 8;
     if (i0 + r < nq && s_row[r] != kMissing) {
         const uint64_t d0 = min(s_off[r], A.out_cap), d1 = min(s_off[r + 1], A.out_cap);
         if (d1 > d0) copy_row<8>(gp(A.blob), s_src[r], gp(A.out), d0, d1, tid % 8);
     }
+#ifdef MURR_TUNING
+    if (A.stamps) {
+        __syncthreads();
+        GF_STAMP(4);
+    }
+#endif
 }
 
 // ---- one read over a table sharded across GPUs (murr_multi_gather) ----------------

@@ -314,7 +314,9 @@ struct IndexArgs {
     uint64_t* kp;               // per slot: the key's first 16 bytes, zero-padded (written by insert)
     uint64_t* rc;               // slot cache (optional, probe): per slot {row offset, row bytes}
     uint32_t* ru;               //   and the row's utf8 string bytes [nu_rc]
+    uint64_t* stamps;           // tuning builds: gather_fused's phase clocks [group][kGatherStamps]
 };
+constexpr uint32_t kGatherStamps = 5;  // entry, probed, look-back done, published, copied
 constexpr uint32_t kGatherGroups = 16;  // 64-query groups of a fused small gather
 constexpr uint32_t kGatherMaxU = 4;     // utf8 columns a fused gather indexes
 constexpr uint32_t kGatherWords = kGatherGroups * (1 + kGatherMaxU);  // look-back words per set
