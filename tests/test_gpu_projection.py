@@ -5,8 +5,9 @@ Table::read takes an arbitrary column list per request
 segment layout only (murr_jit_kernel.hip); the table compiles it once at open
 (murr_segment_prepare) and every projection -- subsets, permutations,
 duplicates -- runs the same code object.  A never-seen projection's first read
-must therefore cost what a repeated one costs (a hiprtc compile takes
-seconds), and must decode exactly like the builder path over MemoryStore."""
+must therefore cost about what a repeated one costs (a hiprtc compile takes
+seconds; preparing the projection's read plan, a millisecond at most), and must
+decode exactly like the builder path over MemoryStore."""
 import time
 
 import numpy as np
@@ -43,6 +44,8 @@ def test_new_projection_first_read_costs_no_compile():
         got = rt.read(keys, cols)
         first = time.perf_counter() - t0
         assert_same(got, expected([batch], keys, cols))
-        # no compile: within 1 ms of a warm read of every column
-        assert first < warm_s + 1e-3, (cols, first, warm_s)
+        # no compile (seconds): within 20 ms of a warm read of every column --
+        # the first read of a projection prepares its read plan, whose pinned
+        # and device buffers may be new allocations (~1 ms on some boxes)
+        assert first < warm_s + 20e-3, (cols, first, warm_s)
     ctx.set_opts()
