@@ -544,7 +544,7 @@ void murr_index_free(murr_index_t* idx);
  * already holds rows, src/io/table/mod.rs:54-112 -> Store::write,
  * src/io/store/memory.rs:47-60): a key written again now maps to its new
  * row (later write wins).  The key copy grows by doubling and the slot table
- * is rehashed only when the load would pass 1/2, so an append costs in
+ * is rehashed only when the load would pass 1/3, so an append costs in
  * proportion to the batch (amortised).  Synchronous. */
 int murr_index_append(murr_ctx_t* ctx, murr_index_t* idx, const uint8_t* key_data,
                       const int32_t* key_offsets, uint64_t key_offset, uint64_t n,

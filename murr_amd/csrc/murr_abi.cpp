@@ -427,10 +427,18 @@ int murr_index_append(murr_ctx_t* c, murr_index_t* x, const uint8_t* key_data, c
     a.key_off = x->key_off;
     a.err = x->err;
     uint64_t slots = x->mask + 1;
-    if (!x->slots || 2 * total > slots) {
-        // rehash: a table of >= 2 * total slots, every key inserted again
+    // slots per key at least: load factor <= 1/3.  At 1/2 (round 5) a
+    // config C table sat at 0.48 and every 64-key group of a read walked a
+    // 6-9 slot chain for its slowest key; at 1/3 (0.24 there) its reads took
+    // 28.7-29.5 us instead of 31.2-33.2 (tools/r06/EXPERIMENTS.md #34).
+    uint64_t spread = 3;
+#ifdef MURR_TUNING
+    if (const char* v = std::getenv("MURR_INDEX_SPREAD")) spread = std::max<uint64_t>(2, std::strtoull(v, nullptr, 10));  // (A/B)
+#endif
+    if (!x->slots || spread * total > slots) {
+        // rehash: a table of >= spread * total slots, every key inserted again
         slots = 64;
-        while (slots < 2 * total) slots <<= 1;
+        while (slots < spread * total) slots <<= 1;
         for (void** p : {(void**)&x->slots, (void**)&x->loc, (void**)&x->kp, (void**)&x->rc, (void**)&x->ru}) {
             if (*p) HIPC(hipFree(*p));
             *p = nullptr;

@@ -10,7 +10,7 @@
 // follow put semantics: of equal keys the later row wins (memory.rs:47-56,
 // RocksDB's newest sequence number).
 //
-// Table: capacity = 2^k >= 2n slots of u64 {hash tag (32) | row (32)}, empty
+// Table: capacity = 2^k >= 3n slots of u64 {hash tag (32) | row (32)}, empty
 // = ~0, and beside each slot the key's {start (32) | length (32)} in the
 // index's key copy, so a probe reads slot and key location together and then
 // the key bytes.  Insert is lock-free: CAS into the first empty slot of the linear
@@ -143,7 +143,7 @@ __global__ void __launch_bounds__(256) index_insert(IndexArgs A) {
             }
         }
     }
-    report(A.err, err_key(0, i, 0, kStInternal));  // table full: cannot happen at load <= 1/2
+    report(A.err, err_key(0, i, 0, kStInternal));  // table full: cannot happen at load <= 1/3
 }
 
 // Slot holding stored key i (inserted already): index_probe's walk over the

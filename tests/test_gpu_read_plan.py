@@ -260,7 +260,7 @@ def test_plan_slot_cache_long_and_short_keys():
         return f"key{i}" if i % 3 else f"a-longer-key-of-the-table-{i:08d}"  # 4-10 or 34 bytes
 
     batches, start = [], 0
-    for w, m in enumerate([700, 1500, 5000]):  # the third append rehashes
+    for w, m in enumerate([700, 1500, 5000]):  # the second and third appends rehash
         keys = [key(start + i) for i in range(m)]
         if start:
             for i in rng.choice(m, size=m // 5, replace=False):
